@@ -1,0 +1,439 @@
+// index_capi.hip — extern "C" boundary of the flat index (declared in include/ragmi.h).
+//
+// Host side of the Qdrant replacement: handle lifetime, capacity growth, workspace ring,
+// kernel launch sequence of one search (qprep -> scan -> merge1 -> merge2). No compute runs
+// on the host; every entry point either enqueues on the caller's stream or (for *_host)
+// stages through device memory and synchronises.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/ragmi.h"
+#include "common_host.hpp"
+#include "scan_kernels.hip"
+
+using ragmi::half8;
+
+namespace {
+
+constexpr int kRing = 4;            // workspace slots (concurrent searches in flight)
+constexpr int kMergeGroup = 64;     // wave lists per merge-1 wave
+
+struct Workspace {
+  float* qn = nullptr;
+  half8* qfrag = nullptr;
+  uint32_t* filt = nullptr;
+  float* part_s = nullptr;
+  int* part_i = nullptr;
+  float* mid_s = nullptr;
+  int* mid_i = nullptr;
+  hipEvent_t done = nullptr;
+};
+
+struct ProfPair {
+  hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct rag_index {
+  int dim = 0;
+  int device = 0;
+  int64_t cap_rows = 0;   // multiple of 16
+  int64_t count = 0;
+  half8* corpus = nullptr;
+  uint32_t* tags = nullptr;
+  int max_wgs = 0;        // scan workgroups at full occupancy
+  std::mutex mu;
+  Workspace ws[kRing];
+  int ws_next = 0;
+  // host staging for *_host entry points
+  void* stage = nullptr;
+  size_t stage_bytes = 0;
+  // profiling
+  bool prof = false;
+  std::vector<ProfPair> prof_pairs;
+};
+
+namespace {
+
+int64_t round16(int64_t n) { return (n + 15) & ~int64_t(15); }
+
+int alloc_corpus(rag_index* h, int64_t cap_rows, half8** corpus, uint32_t** tags) {
+  const size_t cbytes = (size_t)cap_rows * h->dim * 2;
+  RAG_HIP(hipMalloc(reinterpret_cast<void**>(corpus), std::max<size_t>(cbytes, 16)));
+  if (hipMalloc(reinterpret_cast<void**>(tags), std::max<size_t>(cap_rows * 4, 16)) !=
+      hipSuccess) {
+    (void)hipFree(*corpus);
+    return ragmi::fail(RAG_ENOMEM, "hipMalloc(tags) failed");
+  }
+  RAG_HIP(hipMemset(*corpus, 0, std::max<size_t>(cbytes, 16)));
+  RAG_HIP(hipMemset(*tags, 0, std::max<size_t>(cap_rows * 4, 16)));
+  return RAG_OK;
+}
+
+int ensure_stage(rag_index* h, size_t bytes) {
+  if (h->stage_bytes >= bytes) return RAG_OK;
+  if (h->stage) (void)hipFree(h->stage);
+  h->stage = nullptr;
+  h->stage_bytes = 0;
+  RAG_HIP(hipMalloc(&h->stage, bytes));
+  h->stage_bytes = bytes;
+  return RAG_OK;
+}
+
+template <int D>
+void launch_upsert(rag_index* h, const float* v, const int64_t* rows, const uint32_t* tags,
+                   int64_t n, hipStream_t st) {
+  ragmi::upsert_kernel<D><<<dim3((unsigned)n), dim3(64), 0, st>>>(v, rows, tags, h->corpus,
+                                                                  h->tags, n, h->cap_rows);
+}
+
+template <int D>
+int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k,
+                       const uint32_t* filt, int64_t id_offset, float* out_s, int64_t* out_i,
+                       hipStream_t st) {
+  using namespace ragmi;
+  qprep_kernel<D><<<dim3(kQ), dim3(64), 0, st>>>(q, Bq, filt, w.qn, w.qfrag, w.filt);
+  const int64_t n_tiles = (h->count + 15) / 16;
+  int grid = (int)std::min<int64_t>(h->max_wgs, std::max<int64_t>(1, (n_tiles + 3) / 4));
+  ProfPair pp{};
+  if (h->prof) {
+    RAG_HIP(hipEventCreate(&pp.a));
+    RAG_HIP(hipEventCreate(&pp.b));
+    RAG_HIP(hipEventRecord(pp.a, st));
+  }
+  if (filt)
+    scan_kernel<D, true><<<dim3(grid), dim3(256), 0, st>>>(
+        h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, (int)n_tiles, w.part_s, w.part_i);
+  else
+    scan_kernel<D, false><<<dim3(grid), dim3(256), 0, st>>>(
+        h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, (int)n_tiles, w.part_s, w.part_i);
+  if (h->prof) {
+    RAG_HIP(hipEventRecord(pp.b, st));
+    h->prof_pairs.push_back(pp);
+  }
+  const int n_lists = grid * kWavesPerWG;
+  const int n_groups = (n_lists + kMergeGroup - 1) / kMergeGroup;
+  merge1_kernel<<<dim3(n_groups, Bq), dim3(64), 0, st>>>(w.part_s, w.part_i, n_lists,
+                                                         kMergeGroup, w.mid_s, w.mid_i);
+  merge2_kernel<D><<<dim3(Bq), dim3(64), 0, st>>>(w.mid_s, w.mid_i, n_groups, h->corpus, w.qn,
+                                                  k, id_offset, out_s, out_i);
+  RAG_HIP(hipGetLastError());
+  return RAG_OK;
+}
+
+template <int D>
+void launch_export(rag_index* h, int64_t row0, int64_t n, half8* out, hipStream_t st) {
+  const int64_t total = n * (D / 8);
+  const int blocks = (int)((total + 255) / 256);
+  ragmi::export_kernel<D><<<dim3(blocks), dim3(256), 0, st>>>(h->corpus, row0, n, out);
+}
+
+#define RAG_DISPATCH_DIM(dim, FN, ...)                                   \
+  do {                                                                   \
+    if ((dim) == 384)                                                    \
+      FN<384>(__VA_ARGS__);                                              \
+    else if ((dim) == 1024)                                              \
+      FN<1024>(__VA_ARGS__);                                             \
+    else                                                                 \
+      return ragmi::fail(RAG_EINVAL, "unsupported dim (built: 384, 1024)"); \
+  } while (0)
+
+int upsert_locked(rag_index* h, const float* vecs, const int64_t* rows, const uint32_t* tags,
+                  int64_t n, int64_t new_count, hipStream_t st) {
+  if (n < 0 || (n > 0 && (!vecs || !rows))) return ragmi::fail(RAG_EINVAL, "bad upsert args");
+  if (new_count < 0 || new_count > h->cap_rows)
+    return ragmi::fail(RAG_ERANGE, "new_count exceeds capacity (call rag_index_reserve)");
+  if (n > 0x7fffffff) return ragmi::fail(RAG_ERANGE, "n too large for one upsert");
+  RAG_HIP(hipSetDevice(h->device));
+  if (n > 0) {
+    RAG_DISPATCH_DIM(h->dim, launch_upsert, h, vecs, rows, tags, n, st);
+    RAG_HIP(hipGetLastError());
+  }
+  h->count = new_count;
+  return RAG_OK;
+}
+
+int search_locked(rag_index* h, const float* q, int B, int k, const uint32_t* filt,
+                  int64_t id_offset, float* out_s, int64_t* out_i, hipStream_t st) {
+  if (B < 0 || (B > 0 && (!q || !out_s || !out_i))) return ragmi::fail(RAG_EINVAL, "bad search args");
+  if (k < 1 || k > RAG_MAX_K) return ragmi::fail(RAG_ERANGE, "k must be in [1, RAG_MAX_K=32]");
+  RAG_HIP(hipSetDevice(h->device));
+  for (int b0 = 0; b0 < B; b0 += ragmi::kQ) {
+    const int Bq = std::min(ragmi::kQ, B - b0);
+    Workspace& w = h->ws[h->ws_next];
+    h->ws_next = (h->ws_next + 1) % kRing;
+    RAG_HIP(hipStreamWaitEvent(st, w.done, 0));
+    int rc;
+    if (h->dim == 384)
+      rc = launch_search_pass<384>(h, w, q + (int64_t)b0 * h->dim, Bq, k,
+                                   filt ? filt + 2 * b0 : nullptr, id_offset,
+                                   out_s + (int64_t)b0 * k, out_i + (int64_t)b0 * k, st);
+    else
+      rc = launch_search_pass<1024>(h, w, q + (int64_t)b0 * h->dim, Bq, k,
+                                    filt ? filt + 2 * b0 : nullptr, id_offset,
+                                    out_s + (int64_t)b0 * k, out_i + (int64_t)b0 * k, st);
+    if (rc) return rc;
+    RAG_HIP(hipEventRecord(w.done, st));
+  }
+  return RAG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* rag_last_error(void) { return ragmi::last_error().c_str(); }
+const char* rag_version(void) { return "ragmi 0.1.0 (gfx950)"; }
+
+int rag_index_create(int dim, int64_t capacity_rows, int device, rag_index_t** out) {
+  ragmi::clear_error();
+  if (!out) return ragmi::fail(RAG_EINVAL, "out is NULL");
+  *out = nullptr;
+  if (dim != 384 && dim != 1024) return ragmi::fail(RAG_EINVAL, "dim must be 384 or 1024");
+  if (capacity_rows < 0 || capacity_rows > (int64_t(1) << 31) - 16)
+    return ragmi::fail(RAG_ERANGE, "capacity_rows out of range [0, 2^31-16]");
+  RAG_HIP(hipSetDevice(device));
+  auto* h = new rag_index();
+  h->dim = dim;
+  h->device = device;
+  h->cap_rows = round16(std::max<int64_t>(capacity_rows, 16));
+  int rc = alloc_corpus(h, h->cap_rows, &h->corpus, &h->tags);
+  if (rc) {
+    delete h;
+    return rc;
+  }
+  int n_cu = 0;
+  if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) !=
+          hipSuccess ||
+      n_cu <= 0)
+    n_cu = 256;
+  h->max_wgs = n_cu * 2;  // 2 x 256-thread workgroups per CU (__launch_bounds__(256, 2))
+  const int max_lists = h->max_wgs * ragmi::kWavesPerWG;
+  const int max_groups = (max_lists + kMergeGroup - 1) / kMergeGroup;
+  for (auto& w : h->ws) {
+    bool ok = hipMalloc(reinterpret_cast<void**>(&w.qn), ragmi::kQ * dim * 4) == hipSuccess &&
+              hipMalloc(reinterpret_cast<void**>(&w.qfrag), 2 * (dim / 32) * 64 * 16) ==
+                  hipSuccess &&
+              hipMalloc(reinterpret_cast<void**>(&w.filt), ragmi::kQ * 2 * 4) == hipSuccess &&
+              hipMalloc(reinterpret_cast<void**>(&w.part_s),
+                        (size_t)max_lists * ragmi::kQ * ragmi::kKS * 4) == hipSuccess &&
+              hipMalloc(reinterpret_cast<void**>(&w.part_i),
+                        (size_t)max_lists * ragmi::kQ * ragmi::kKS * 4) == hipSuccess &&
+              hipMalloc(reinterpret_cast<void**>(&w.mid_s),
+                        (size_t)max_groups * ragmi::kQ * ragmi::kKS * 4) == hipSuccess &&
+              hipMalloc(reinterpret_cast<void**>(&w.mid_i),
+                        (size_t)max_groups * ragmi::kQ * ragmi::kKS * 4) == hipSuccess &&
+              hipEventCreateWithFlags(&w.done, hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+      rag_index_destroy(h);
+      return ragmi::fail(RAG_ENOMEM, "workspace allocation failed");
+    }
+  }
+  *out = h;
+  return RAG_OK;
+}
+
+int rag_index_destroy(rag_index_t* h) {
+  ragmi::clear_error();
+  if (!h) return RAG_OK;
+  (void)hipSetDevice(h->device);
+  (void)hipDeviceSynchronize();
+  for (auto& w : h->ws) {
+    if (w.qn) (void)hipFree(w.qn);
+    if (w.qfrag) (void)hipFree(w.qfrag);
+    if (w.filt) (void)hipFree(w.filt);
+    if (w.part_s) (void)hipFree(w.part_s);
+    if (w.part_i) (void)hipFree(w.part_i);
+    if (w.mid_s) (void)hipFree(w.mid_s);
+    if (w.mid_i) (void)hipFree(w.mid_i);
+    if (w.done) (void)hipEventDestroy(w.done);
+  }
+  for (auto& p : h->prof_pairs) {
+    (void)hipEventDestroy(p.a);
+    (void)hipEventDestroy(p.b);
+  }
+  if (h->corpus) (void)hipFree(h->corpus);
+  if (h->tags) (void)hipFree(h->tags);
+  if (h->stage) (void)hipFree(h->stage);
+  delete h;
+  return RAG_OK;
+}
+
+int rag_index_reserve(rag_index_t* h, int64_t capacity_rows) {
+  ragmi::clear_error();
+  if (!h) return ragmi::fail(RAG_EINVAL, "index is NULL");
+  if (capacity_rows > (int64_t(1) << 31) - 16)
+    return ragmi::fail(RAG_ERANGE, "capacity_rows out of range");
+  std::lock_guard<std::mutex> lk(h->mu);
+  const int64_t cap = round16(capacity_rows);
+  if (cap <= h->cap_rows) return RAG_OK;
+  RAG_HIP(hipSetDevice(h->device));
+  half8* nc = nullptr;
+  uint32_t* nt = nullptr;
+  int rc = alloc_corpus(h, cap, &nc, &nt);
+  if (rc) return rc;
+  RAG_HIP(hipDeviceSynchronize());
+  RAG_HIP(hipMemcpy(nc, h->corpus, (size_t)h->cap_rows * h->dim * 2, hipMemcpyDeviceToDevice));
+  RAG_HIP(hipMemcpy(nt, h->tags, (size_t)h->cap_rows * 4, hipMemcpyDeviceToDevice));
+  (void)hipFree(h->corpus);
+  (void)hipFree(h->tags);
+  h->corpus = nc;
+  h->tags = nt;
+  h->cap_rows = cap;
+  return RAG_OK;
+}
+
+int64_t rag_index_capacity(const rag_index_t* h) { return h ? h->cap_rows : -1; }
+int64_t rag_index_count(const rag_index_t* h) { return h ? h->count : -1; }
+int rag_index_dim(const rag_index_t* h) { return h ? h->dim : -1; }
+
+int rag_index_upsert(rag_index_t* h, const float* vecs, const int64_t* rows,
+                     const uint32_t* tags, int64_t n, int64_t new_count, void* stream) {
+  ragmi::clear_error();
+  if (!h) return ragmi::fail(RAG_EINVAL, "index is NULL");
+  std::lock_guard<std::mutex> lk(h->mu);
+  return upsert_locked(h, vecs, rows, tags, n, new_count, static_cast<hipStream_t>(stream));
+}
+
+int rag_index_upsert_host(rag_index_t* h, const float* vecs, const int64_t* rows,
+                          const uint32_t* tags, int64_t n, int64_t new_count) {
+  ragmi::clear_error();
+  if (!h) return ragmi::fail(RAG_EINVAL, "index is NULL");
+  if (n < 0 || (n > 0 && (!vecs || !rows))) return ragmi::fail(RAG_EINVAL, "bad upsert args");
+  for (int64_t i = 0; i < n; ++i)
+    if (rows[i] < 0 || rows[i] >= h->cap_rows)
+      return ragmi::fail(RAG_ERANGE, "row slot beyond capacity (call rag_index_reserve)");
+  std::lock_guard<std::mutex> lk(h->mu);
+  RAG_HIP(hipSetDevice(h->device));
+  const size_t vb = (size_t)n * h->dim * 4, rb = (size_t)n * 8, tb = (size_t)n * 4;
+  int rc = ensure_stage(h, vb + rb + tb + 64);
+  if (rc) return rc;
+  char* base = static_cast<char*>(h->stage);
+  RAG_HIP(hipDeviceSynchronize());
+  if (n > 0) {
+    RAG_HIP(hipMemcpy(base, vecs, vb, hipMemcpyHostToDevice));
+    RAG_HIP(hipMemcpy(base + vb, rows, rb, hipMemcpyHostToDevice));
+    if (tags) RAG_HIP(hipMemcpy(base + vb + rb, tags, tb, hipMemcpyHostToDevice));
+  }
+  rc = upsert_locked(h, reinterpret_cast<float*>(base), reinterpret_cast<int64_t*>(base + vb),
+                     tags ? reinterpret_cast<uint32_t*>(base + vb + rb) : nullptr, n, new_count,
+                     nullptr);
+  if (rc) return rc;
+  RAG_HIP(hipDeviceSynchronize());
+  return RAG_OK;
+}
+
+int rag_index_search(rag_index_t* h, const float* q, int B, int k, const uint32_t* filters,
+                     int64_t id_offset, float* out_s, int64_t* out_i, void* stream) {
+  ragmi::clear_error();
+  if (!h) return ragmi::fail(RAG_EINVAL, "index is NULL");
+  std::lock_guard<std::mutex> lk(h->mu);
+  return search_locked(h, q, B, k, filters, id_offset, out_s, out_i,
+                       static_cast<hipStream_t>(stream));
+}
+
+int rag_index_search_host(rag_index_t* h, const float* q, int B, int k,
+                          const uint32_t* filters, int64_t id_offset, float* out_s,
+                          int64_t* out_i) {
+  ragmi::clear_error();
+  if (!h) return ragmi::fail(RAG_EINVAL, "index is NULL");
+  if (B < 0 || (B > 0 && (!q || !out_s || !out_i))) return ragmi::fail(RAG_EINVAL, "bad search args");
+  if (k < 1 || k > RAG_MAX_K) return ragmi::fail(RAG_ERANGE, "k must be in [1, RAG_MAX_K=32]");
+  if (B == 0) return RAG_OK;
+  std::lock_guard<std::mutex> lk(h->mu);
+  RAG_HIP(hipSetDevice(h->device));
+  const size_t qb = (size_t)B * h->dim * 4, sb = (size_t)B * k * 4, ib = (size_t)B * k * 8;
+  const size_t fb = (size_t)B * 8;
+  int rc = ensure_stage(h, qb + sb + ib + fb + 64);
+  if (rc) return rc;
+  char* base = static_cast<char*>(h->stage);
+  RAG_HIP(hipDeviceSynchronize());
+  RAG_HIP(hipMemcpy(base, q, qb, hipMemcpyHostToDevice));
+  if (filters) RAG_HIP(hipMemcpy(base + qb + sb + ib, filters, fb, hipMemcpyHostToDevice));
+  rc = search_locked(h, reinterpret_cast<float*>(base), B, k,
+                     filters ? reinterpret_cast<uint32_t*>(base + qb + sb + ib) : nullptr,
+                     id_offset, reinterpret_cast<float*>(base + qb),
+                     reinterpret_cast<int64_t*>(base + qb + sb), nullptr);
+  if (rc) return rc;
+  RAG_HIP(hipDeviceSynchronize());
+  RAG_HIP(hipMemcpy(out_s, base + qb, sb, hipMemcpyDeviceToHost));
+  RAG_HIP(hipMemcpy(out_i, base + qb + sb, ib, hipMemcpyDeviceToHost));
+  return RAG_OK;
+}
+
+int rag_index_export_rows(rag_index_t* h, int64_t row0, int64_t n, uint16_t* out) {
+  ragmi::clear_error();
+  if (!h || !out || row0 < 0 || n < 0 || row0 + n > h->cap_rows)
+    return ragmi::fail(RAG_EINVAL, "bad export range");
+  if (n == 0) return RAG_OK;
+  std::lock_guard<std::mutex> lk(h->mu);
+  RAG_HIP(hipSetDevice(h->device));
+  const size_t bytes = (size_t)n * h->dim * 2;
+  int rc = ensure_stage(h, bytes);
+  if (rc) return rc;
+  RAG_HIP(hipDeviceSynchronize());
+  RAG_DISPATCH_DIM(h->dim, launch_export, h, row0, n, static_cast<half8*>(h->stage), nullptr);
+  RAG_HIP(hipGetLastError());
+  RAG_HIP(hipDeviceSynchronize());
+  RAG_HIP(hipMemcpy(out, h->stage, bytes, hipMemcpyDeviceToHost));
+  return RAG_OK;
+}
+
+int rag_index_export_tags(rag_index_t* h, int64_t row0, int64_t n, uint32_t* out) {
+  ragmi::clear_error();
+  if (!h || !out || row0 < 0 || n < 0 || row0 + n > h->cap_rows)
+    return ragmi::fail(RAG_EINVAL, "bad export range");
+  if (n == 0) return RAG_OK;
+  std::lock_guard<std::mutex> lk(h->mu);
+  RAG_HIP(hipSetDevice(h->device));
+  RAG_HIP(hipDeviceSynchronize());
+  RAG_HIP(hipMemcpy(out, h->tags + row0, (size_t)n * 4, hipMemcpyDeviceToHost));
+  return RAG_OK;
+}
+
+int rag_merge_topk(const float* in_s, const int64_t* in_i, int n_lists, int B, int k,
+                   float* out_s, int64_t* out_i, void* stream) {
+  ragmi::clear_error();
+  if (n_lists < 1 || B < 0 || k < 1 || k > RAG_MAX_K)
+    return ragmi::fail(RAG_EINVAL, "bad merge args");
+  if (B == 0) return RAG_OK;
+  ragmi::merge_exact_kernel<<<dim3(B), dim3(64), 0, static_cast<hipStream_t>(stream)>>>(
+      in_s, in_i, n_lists, B, k, out_s, out_i);
+  RAG_HIP(hipGetLastError());
+  return RAG_OK;
+}
+
+int rag_profile_enable(rag_index_t* h, int enable) {
+  ragmi::clear_error();
+  if (!h) return ragmi::fail(RAG_EINVAL, "index is NULL");
+  std::lock_guard<std::mutex> lk(h->mu);
+  h->prof = enable != 0;
+  return RAG_OK;
+}
+
+int rag_profile_scan_ms(rag_index_t* h, double* total_ms, int64_t* launches) {
+  ragmi::clear_error();
+  if (!h || !total_ms || !launches) return ragmi::fail(RAG_EINVAL, "bad args");
+  std::lock_guard<std::mutex> lk(h->mu);
+  double tot = 0.0;
+  for (auto& p : h->prof_pairs) {
+    RAG_HIP(hipEventSynchronize(p.b));
+    float ms = 0.f;
+    RAG_HIP(hipEventElapsedTime(&ms, p.a, p.b));
+    tot += ms;
+    (void)hipEventDestroy(p.a);
+    (void)hipEventDestroy(p.b);
+  }
+  *launches = (int64_t)h->prof_pairs.size();
+  *total_ms = tot;
+  h->prof_pairs.clear();
+  return RAG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,59 @@
+"""Build libragmi.so in-tree with hipcc for gfx950 (no JIT cache, so the .so travels with
+the repo snapshot to the GPU box)."""
+from __future__ import annotations
+
+import os
+import subprocess
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG_DIR)                      # financial-rag-system_amd/
+CSRC = os.path.join(ROOT, "csrc")
+LIB_PATH = os.path.join(PKG_DIR, "libragmi.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+
+# translation units of libragmi.so
+SOURCES = ["index_capi.hip", "bert_capi.hip"]
+HEADERS = ["device_common.hpp", "common_host.hpp", "scan_kernels.hip", "bert_kernels.hip"]
+
+
+def _inputs():
+    files = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
+    files.append(os.path.join(os.path.dirname(ROOT), "include", "ragmi.h"))
+    files.append(os.path.join(os.path.dirname(ROOT), "include", "ragmi_bert.h"))
+    return [f for f in files if os.path.exists(f)]
+
+
+def needs_build() -> bool:
+    if not os.path.exists(LIB_PATH):
+        return True
+    t = os.path.getmtime(LIB_PATH)
+    return any(os.path.getmtime(f) > t for f in _inputs())
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not needs_build():
+        return LIB_PATH
+    srcs = [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
+    objs = []
+    for src in srcs:
+        obj = os.path.join(CSRC, os.path.basename(src) + ".o")
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
+               "-fno-strict-aliasing", "-Wall", "-Wno-unused-function", "-c", src, "-o", obj]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.check_call(cmd)
+        objs.append(obj)
+    tmp = LIB_PATH + ".tmp"
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd)
+    os.replace(tmp, LIB_PATH)
+    for o in objs:
+        os.remove(o)
+    return LIB_PATH
+
+
+if __name__ == "__main__":
+    print(build(force=True, verbose=True))

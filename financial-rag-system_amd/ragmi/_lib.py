@@ -1,0 +1,102 @@
+"""ctypes binding of libragmi.so (the C ABI declared in include/ragmi.h).
+
+torch is imported first on purpose: libragmi.so links libamdhip64.so.7, and loading torch
+first makes the dynamic loader reuse torch's HIP runtime (same SONAME) so tensors, streams
+and our kernels share one runtime in the process.
+
+There is no fallback: if libragmi.so is missing or fails to load, every product entry point
+raises RagmiUnavailable.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+from ._build import LIB_PATH
+
+_lock = threading.Lock()
+_lib = None
+
+
+class RagmiUnavailable(RuntimeError):
+    """libragmi.so is not built or cannot be loaded (no CPU fallback exists)."""
+
+
+class RagmiError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"libragmi error {code}: {msg}")
+        self.code = code
+
+
+c_f32p = ctypes.POINTER(ctypes.c_float)
+c_i64p = ctypes.POINTER(ctypes.c_int64)
+c_u32p = ctypes.POINTER(ctypes.c_uint32)
+c_u16p = ctypes.POINTER(ctypes.c_uint16)
+c_i32p = ctypes.POINTER(ctypes.c_int32)
+c_vp = ctypes.c_void_p
+
+# name -> (restype, argtypes); the single source of truth for the exported C ABI.
+INDEX_API = {
+    "rag_last_error": (ctypes.c_char_p, []),
+    "rag_version": (ctypes.c_char_p, []),
+    "rag_index_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, ctypes.c_int,
+                                        ctypes.POINTER(c_vp)]),
+    "rag_index_destroy": (ctypes.c_int, [c_vp]),
+    "rag_index_reserve": (ctypes.c_int, [c_vp, ctypes.c_int64]),
+    "rag_index_capacity": (ctypes.c_int64, [c_vp]),
+    "rag_index_count": (ctypes.c_int64, [c_vp]),
+    "rag_index_dim": (ctypes.c_int, [c_vp]),
+    "rag_index_upsert": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, ctypes.c_int64, ctypes.c_int64,
+                                        c_vp]),
+    "rag_index_upsert_host": (ctypes.c_int, [c_vp, c_f32p, c_i64p, c_u32p, ctypes.c_int64,
+                                             ctypes.c_int64]),
+    "rag_index_search": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, ctypes.c_int, c_vp,
+                                        ctypes.c_int64, c_vp, c_vp, c_vp]),
+    "rag_index_search_host": (ctypes.c_int, [c_vp, c_f32p, ctypes.c_int, ctypes.c_int, c_u32p,
+                                             ctypes.c_int64, c_f32p, c_i64p]),
+    "rag_index_export_rows": (ctypes.c_int, [c_vp, ctypes.c_int64, ctypes.c_int64, c_u16p]),
+    "rag_index_export_tags": (ctypes.c_int, [c_vp, ctypes.c_int64, ctypes.c_int64, c_u32p]),
+    "rag_merge_topk": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                      c_vp, c_vp, c_vp]),
+    "rag_profile_enable": (ctypes.c_int, [c_vp, ctypes.c_int]),
+    "rag_profile_scan_ms": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_double), c_i64p]),
+}
+
+BERT_API: dict = {}   # filled by ragmi.encoders when the encoder ABI is present
+
+
+def load():
+    """Load libragmi.so (raises RagmiUnavailable; never falls back)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise RagmiUnavailable(
+                f"{LIB_PATH} is not built; run `python -c 'import __graft_entry__ as g; "
+                f"g.build()'` (hipcc --offload-arch=gfx950)")
+        try:
+            L = ctypes.CDLL(LIB_PATH)
+        except OSError as e:
+            raise RagmiUnavailable(f"cannot load {LIB_PATH}: {e}") from e
+        for name, (res, args) in {**INDEX_API, **BERT_API}.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+        return L
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        msg = load().rag_last_error()
+        raise RagmiError(rc, msg.decode() if msg else "")
+
+
+def require_gpu() -> None:
+    if not torch.cuda.is_available():
+        raise RagmiUnavailable("no HIP device visible: the ragmi hot path runs only on MI355X "
+                               "(gfx950); there is no CPU fallback")

@@ -1,0 +1,188 @@
+"""FlatIndex — Python handle over the in-HBM flat cosine index of libragmi.so.
+
+This is the storage + search engine that replaces the Qdrant server's COSINE collection
+(reference main.py:92-95 get_qdrant, main.py:215-239 retrieve_from_qdrant, ingest.py:86-96
+ensure_collection, ingest.py:148-175 upsert). Vectors live in HBM as fp16 in the MFMA
+"tile16" layout; search runs the HIP scan + top-k + exact-rescoring merge on
+the caller's current torch stream. Inputs may be numpy arrays (copied to the device) or cuda
+torch tensors (used in place).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check
+
+MAX_K = 32          # RAG_MAX_K in include/ragmi.h
+QUERY_TILE = 32     # RAG_QUERY_TILE
+
+
+def _stream_ptr(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _as_dev(x, dtype, device) -> torch.Tensor:
+    if isinstance(x, torch.Tensor):
+        t = x.to(device=device, dtype=dtype)
+    else:
+        t = torch.from_numpy(np.ascontiguousarray(np.asarray(x))).to(dtype=dtype)
+        t = t.to(device=device, non_blocking=False)
+    return t.contiguous()
+
+
+class FlatIndex:
+    """In-HBM fp16 flat index with exact (score desc, row asc) top-k search."""
+
+    def __init__(self, dim: int = 384, capacity: int = 0, device=None):
+        _lib.require_gpu()
+        self._L = _lib.load()
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        device = torch.device(device)
+        if device.type != "cuda":
+            raise ValueError("FlatIndex lives on a HIP device (torch 'cuda' device)")
+        self.device = torch.device("cuda", device.index if device.index is not None
+                                   else torch.cuda.current_device())
+        self.dim = int(dim)
+        h = ctypes.c_void_p()
+        check(self._L.rag_index_create(self.dim, int(capacity), self.device.index,
+                                       ctypes.byref(h)))
+        self._h = h
+
+    # ---------------------------------------------------------------- lifetime
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._L.rag_index_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---------------------------------------------------------------- properties
+    @property
+    def capacity(self) -> int:
+        return int(self._L.rag_index_capacity(self._h))
+
+    @property
+    def count(self) -> int:
+        return int(self._L.rag_index_count(self._h))
+
+    def reserve(self, capacity: int) -> None:
+        check(self._L.rag_index_reserve(self._h, int(capacity)))
+
+    # ---------------------------------------------------------------- writes
+    def upsert(self, vectors, rows, tags=None, new_count: int | None = None) -> None:
+        """Normalise + store vectors [n, dim] at row slots `rows` [n] (overwrite allowed)."""
+        v = _as_dev(vectors, torch.float32, self.device)
+        if v.dim() != 2 or v.shape[1] != self.dim:
+            raise ValueError(f"vectors must be [n, {self.dim}]")
+        r = _as_dev(rows, torch.int64, self.device)
+        n = v.shape[0]
+        if r.shape != (n,):
+            raise ValueError("rows must be [n]")
+        if n and (int(r.min()) < 0 or int(r.max()) >= self.capacity):
+            raise IndexError("row slot outside capacity; reserve() first")
+        t = None
+        if tags is not None:
+            t = _as_dev(np.asarray(tags, dtype=np.uint32).view(np.int32)
+                        if not isinstance(tags, torch.Tensor) else tags, torch.int32,
+                        self.device)
+        if new_count is None:
+            new_count = max(self.count, int(r.max()) + 1 if n else 0)
+        check(self._L.rag_index_upsert(self._h, v.data_ptr(), r.data_ptr(),
+                                       t.data_ptr() if t is not None else None, n,
+                                       int(new_count), _stream_ptr(self.device)))
+        # staging tensors are released to the stream-ordered caching allocator (safe reuse).
+
+    def set_count(self, new_count: int) -> None:
+        check(self._L.rag_index_upsert(self._h, None, None, None, 0, int(new_count),
+                                       _stream_ptr(self.device)))
+
+    # ---------------------------------------------------------------- search
+    def search(self, queries, k: int, filters=None, id_offset: int = 0,
+               out: tuple[torch.Tensor, torch.Tensor] | None = None):
+        """Top-k of each query row. Returns (scores fp32 [B,k], ids int64 [B,k]) as cuda
+        tensors, enqueued on the current stream (ids -1 where fewer than k rows match).
+        `filters`: None, or per-query (tag_mask, tag_value) pairs [B, 2] (uint32)."""
+        if not 1 <= k <= MAX_K:
+            raise ValueError(f"k must be in [1, {MAX_K}]")
+        q = _as_dev(queries, torch.float32, self.device)
+        if q.dim() == 1:
+            q = q.unsqueeze(0)
+        if q.shape[-1] != self.dim:
+            raise ValueError(f"query dim {q.shape[-1]} != index dim {self.dim}")
+        B = q.shape[0]
+        if out is None:
+            out_s = torch.empty((B, k), dtype=torch.float32, device=self.device)
+            out_i = torch.empty((B, k), dtype=torch.int64, device=self.device)
+        else:
+            out_s, out_i = out
+        f = None
+        if filters is not None:
+            if isinstance(filters, torch.Tensor):
+                f = filters.to(device=self.device, dtype=torch.int32).contiguous()
+            else:
+                f = torch.from_numpy(np.ascontiguousarray(
+                    np.asarray(filters, dtype=np.uint32).reshape(B, 2)).view(np.int32))
+                f = f.to(self.device)
+            if f.shape != (B, 2):
+                raise ValueError("filters must be [B, 2] (tag_mask, tag_value)")
+        check(self._L.rag_index_search(self._h, q.data_ptr(), B, int(k),
+                                       f.data_ptr() if f is not None else None,
+                                       int(id_offset), out_s.data_ptr(), out_i.data_ptr(),
+                                       _stream_ptr(self.device)))
+        # staging tensors (q, f) go back to torch's stream-ordered caching allocator: any
+        # reuse is enqueued on this same stream after our kernels, so no sync is needed.
+        return out_s, out_i
+
+    # ---------------------------------------------------------------- introspection
+    def export_rows(self, row0: int = 0, n: int | None = None) -> np.ndarray:
+        """Stored fp16 rows (uint16 bits) [n, dim], row-major."""
+        if n is None:
+            n = self.count - row0
+        out = np.empty((n, self.dim), dtype=np.uint16)
+        torch.cuda.current_stream(self.device).synchronize()
+        check(self._L.rag_index_export_rows(self._h, int(row0), int(n),
+                                            out.ctypes.data_as(_lib.c_u16p)))
+        return out
+
+    def export_tags(self, row0: int = 0, n: int | None = None) -> np.ndarray:
+        if n is None:
+            n = self.count - row0
+        out = np.empty((n,), dtype=np.uint32)
+        torch.cuda.current_stream(self.device).synchronize()
+        check(self._L.rag_index_export_tags(self._h, int(row0), int(n),
+                                            out.ctypes.data_as(_lib.c_u32p)))
+        return out
+
+    # ---------------------------------------------------------------- profiling
+    def profile(self, enable: bool) -> None:
+        check(self._L.rag_profile_enable(self._h, int(bool(enable))))
+
+    def profile_scan_ms(self) -> tuple[float, int]:
+        tot = ctypes.c_double()
+        n = ctypes.c_int64()
+        check(self._L.rag_profile_scan_ms(self._h, ctypes.byref(tot), ctypes.byref(n)))
+        return float(tot.value), int(n.value)
+
+
+def merge_topk(scores: torch.Tensor, ids: torch.Tensor, k: int):
+    """Merge per-shard exact lists [n_lists, B, k] -> global [B, k] on the GPU."""
+    L = _lib.load()
+    n_lists, B, kk = scores.shape
+    if kk != k:
+        raise ValueError("list length must equal k")
+    scores = scores.contiguous()
+    ids = ids.contiguous()
+    out_s = torch.empty((B, k), dtype=torch.float32, device=scores.device)
+    out_i = torch.empty((B, k), dtype=torch.int64, device=scores.device)
+    check(L.rag_merge_topk(scores.data_ptr(), ids.data_ptr(), n_lists, B, k, out_s.data_ptr(),
+                           out_i.data_ptr(), _stream_ptr(scores.device)))
+    return out_s, out_i

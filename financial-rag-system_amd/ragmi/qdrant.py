@@ -1,0 +1,311 @@
+"""QdrantClient-shaped front end of the in-HBM flat index.
+
+Drop-in for the calls the reference makes on `qdrant_client.QdrantClient`:
+  get_collections()                       main.py:135, main2.py:337 (/ready)
+  collection_exists(name)                 ingest.py:87, database.py:121
+  create_collection(name, vectors_config) ingest.py:89-95, database.py:122-128
+  upsert(name, points=[PointStruct])      ingest.py:171-175
+  query_points(name, query, limit, query_filter) -> .points[i].{id,score,payload}
+                                          main.py:232-237, main2.py:163
+plus query_batch_points (one GPU scan for a whole micro-batch; main2.py:281-295 stage 2),
+count, retrieve and delete_collection.
+
+`url` is accepted and ignored: the collection lives in this process's GPU memory (the
+Qdrant service of docker-compose.yml:22 is replaced, not contacted). Payloads stay host-side
+keyed by row; the keyword payload fields used by the reference's `must` filter (`ticker`,
+`document_type`, main.py:218-230) are dictionary-coded into a per-row uint32 tag in HBM
+(16 bits per field) so filtering runs inside the scan kernel.
+"""
+from __future__ import annotations
+
+import threading
+import uuid
+from typing import Any, Iterable
+
+import numpy as np
+import torch
+
+from . import qdrant_models as models
+from .index import MAX_K, FlatIndex
+
+DEFAULT_TAG_FIELDS = ("ticker", "document_type")
+
+
+def _norm_id(pid):
+    """Qdrant point ids are unsigned ints or UUIDs; 32-hex md5 digests (ingest.py:151-154)
+    are accepted as UUIDs and reported back in canonical dashed form."""
+    if isinstance(pid, bool):
+        raise ValueError("point id must be int or UUID string")
+    if isinstance(pid, (int, np.integer)):
+        if pid < 0:
+            raise ValueError("integer point ids must be unsigned")
+        return int(pid)
+    if isinstance(pid, uuid.UUID):
+        return str(pid)
+    if isinstance(pid, str):
+        return str(uuid.UUID(pid))
+    raise ValueError(f"unsupported point id type {type(pid)!r}")
+
+
+class UnsupportedFilter(NotImplementedError):
+    pass
+
+
+class Collection:
+    """One COSINE collection: FlatIndex in HBM + host-side id/payload maps."""
+
+    def __init__(self, name: str, dim: int, device, tag_fields=DEFAULT_TAG_FIELDS,
+                 capacity: int = 1024):
+        if len(tag_fields) > 2:
+            raise ValueError("at most two indexed keyword payload fields (16 bits each)")
+        self.name = name
+        self.dim = dim
+        self.index = FlatIndex(dim=dim, capacity=capacity, device=device)
+        self.tag_fields = tuple(tag_fields)
+        self.codes: list[dict[Any, int]] = [dict() for _ in self.tag_fields]
+        self.id_to_row: dict[Any, int] = {}
+        self.row_ids: list[Any] = []
+        self.payloads: list[dict | None] = []
+        self.versions: list[int] = []
+        self.op = 0
+        self.lock = threading.RLock()
+
+    # ---------------------------------------------------------------- tags / filters
+    def _code(self, f: int, value, create: bool) -> int | None:
+        if isinstance(value, (list, dict)) or value is None:
+            return None
+        table = self.codes[f]
+        c = table.get(value)
+        if c is None and create:
+            if len(table) >= 0xFFFF:
+                raise OverflowError(f"more than 65535 distinct values for {self.tag_fields[f]}")
+            c = len(table) + 1          # 0 = field absent
+            table[value] = c
+        return c
+
+    def _tag(self, payload: dict | None) -> int:
+        tag = 0
+        if payload:
+            for f, key in enumerate(self.tag_fields):
+                if key in payload:
+                    c = self._code(f, payload[key], create=True)
+                    if c:
+                        tag |= c << (16 * f)
+        return tag
+
+    def compile_filter(self, flt: models.Filter | None):
+        """Filter(must=[FieldCondition(key, MatchValue(v))...]) -> (mask, value), or None for
+        "matches nothing" (a value never ingested), or (0, 0) for no filter."""
+        if flt is None:
+            return (0, 0)
+        if flt.should or flt.must_not:
+            raise UnsupportedFilter("only `must` conditions are supported (main.py:218-236)")
+        mask = value = 0
+        for cond in flt.must or []:
+            if not isinstance(cond, models.FieldCondition) or cond.range is not None:
+                raise UnsupportedFilter("only FieldCondition(key, match=MatchValue) is supported")
+            if cond.key not in self.tag_fields:
+                raise UnsupportedFilter(
+                    f"payload key {cond.key!r} is not an indexed keyword field "
+                    f"{self.tag_fields}; create the collection with payload_tag_fields")
+            if not isinstance(cond.match, models.MatchValue):
+                raise UnsupportedFilter("only MatchValue matches are supported")
+            f = self.tag_fields.index(cond.key)
+            c = self._code(f, cond.match.value, create=False)
+            if c is None:
+                return None
+            m = 0xFFFF << (16 * f)
+            if mask & m and (value & m) != (c << (16 * f)):
+                return None             # two different values for one field
+            mask |= m
+            value |= c << (16 * f)
+        return (mask, value)
+
+    # ---------------------------------------------------------------- writes
+    def upsert(self, ids: list, vectors, payloads: list) -> int:
+        with self.lock:
+            self.op += 1
+            vec = np.asarray(vectors, dtype=np.float32) if not isinstance(
+                vectors, torch.Tensor) else vectors
+            if vec.ndim != 2 or vec.shape[1] != self.dim:
+                raise ValueError(f"vectors must be [n, {self.dim}]")
+            # last write wins for duplicate ids inside one batch (Qdrant semantics)
+            last: dict[Any, int] = {}
+            for i, pid in enumerate(ids):
+                last[_norm_id(pid)] = i
+            rows, sel, tags = [], [], []
+            new_count = len(self.row_ids)
+            for pid, i in last.items():
+                r = self.id_to_row.get(pid)
+                if r is None:
+                    r = new_count
+                    new_count += 1
+                    self.id_to_row[pid] = r
+                    self.row_ids.append(pid)
+                    self.payloads.append(None)
+                    self.versions.append(0)
+                p = payloads[i] if payloads is not None else None
+                self.payloads[r] = dict(p) if p is not None else None
+                self.versions[r] = self.op
+                rows.append(r)
+                sel.append(i)
+                tags.append(self._tag(p))
+            if new_count > self.index.capacity:
+                self.index.reserve(max(new_count, 2 * self.index.capacity))
+            if rows:
+                sel_t = vec[sel] if isinstance(vec, torch.Tensor) else vec[np.asarray(sel)]
+                self.index.upsert(sel_t, np.asarray(rows, dtype=np.int64),
+                                  np.asarray(tags, dtype=np.uint32), new_count=new_count)
+            return self.op
+
+    # ---------------------------------------------------------------- reads
+    def search(self, queries, limit: int, filters: list):
+        """queries [B, dim]; filters: per query compiled filter ((mask, value) or None)."""
+        with self.lock:
+            B = len(filters)
+            if limit < 1:
+                return [[] for _ in range(B)]
+            k = min(limit, MAX_K)
+            if limit > MAX_K:
+                raise ValueError(f"limit > {MAX_K} is not supported by the GPU top-k")
+            live = [i for i, f in enumerate(filters) if f is not None]
+            out = [[] for _ in range(B)]
+            if not live or self.index.count == 0:
+                return out
+            q = queries if isinstance(queries, torch.Tensor) else np.asarray(queries, np.float32)
+            q = q[live] if len(live) != B else q
+            fl = np.asarray([filters[i] for i in live], dtype=np.uint32).reshape(-1, 2)
+            use = fl if fl.any() else None
+            s, ids = self.index.search(q, k, filters=use)
+            s = s.cpu().numpy()
+            ids = ids.cpu().numpy()
+            for j, i in enumerate(live):
+                out[i] = [(int(r), float(sc)) for r, sc in zip(ids[j], s[j]) if r >= 0]
+            return out
+
+    def point(self, row: int, score: float, with_payload=True, with_vectors=False):
+        payload = self.payloads[row] if with_payload else None
+        vec = None
+        if with_vectors:
+            vec = self.index.export_rows(row, 1)[0].view(np.float16).astype(np.float32).tolist()
+        return models.ScoredPoint(id=self.row_ids[row], version=self.versions[row],
+                                  score=score, payload=payload, vector=vec)
+
+
+class QdrantClient:
+    """In-process, GPU-resident replacement for qdrant_client.QdrantClient."""
+
+    def __init__(self, url: str | None = None, *args, device=None, **kwargs):
+        self.url = url
+        self.device = device
+        self._collections: dict[str, Collection] = {}
+        self._lock = threading.Lock()
+
+    # ---------------------------------------------------------------- collections
+    def get_collections(self) -> models.CollectionsResponse:
+        with self._lock:
+            return models.CollectionsResponse(
+                collections=[models.CollectionDescription(name=n) for n in self._collections])
+
+    def collection_exists(self, collection_name: str) -> bool:
+        with self._lock:
+            return collection_name in self._collections
+
+    def create_collection(self, collection_name: str, vectors_config: models.VectorParams,
+                          payload_tag_fields: Iterable[str] = DEFAULT_TAG_FIELDS,
+                          capacity: int = 1024, **kwargs) -> bool:
+        if vectors_config.distance != models.Distance.COSINE:
+            raise NotImplementedError("only Distance.COSINE collections (database.py:126)")
+        with self._lock:
+            if collection_name in self._collections:
+                raise ValueError(f"collection {collection_name!r} already exists")
+            self._collections[collection_name] = Collection(
+                collection_name, int(vectors_config.size), self.device,
+                tuple(payload_tag_fields), capacity)
+        return True
+
+    def recreate_collection(self, collection_name: str, vectors_config, **kwargs) -> bool:
+        self.delete_collection(collection_name)
+        return self.create_collection(collection_name, vectors_config, **kwargs)
+
+    def delete_collection(self, collection_name: str, **kwargs) -> bool:
+        with self._lock:
+            col = self._collections.pop(collection_name, None)
+        if col is not None:
+            col.index.close()
+        return col is not None
+
+    def _col(self, name: str) -> Collection:
+        with self._lock:
+            col = self._collections.get(name)
+        if col is None:
+            raise ValueError(f"Collection `{name}` doesn't exist!")
+        return col
+
+    # ---------------------------------------------------------------- points
+    def upsert(self, collection_name: str, points, wait: bool = True, **kwargs):
+        col = self._col(collection_name)
+        if isinstance(points, models.Batch):
+            ids, vecs, pls = points.ids, points.vectors, points.payloads
+        else:
+            points = list(points)
+            ids = [p.id for p in points]
+            vecs = [p.vector for p in points]
+            pls = [p.payload for p in points]
+        if not ids:
+            return models.UpdateResult(operation_id=col.op, status=models.UpdateStatus.COMPLETED)
+        op = col.upsert(ids, vecs, pls)
+        return models.UpdateResult(operation_id=op, status=models.UpdateStatus.COMPLETED)
+
+    def count(self, collection_name: str, **kwargs) -> models.CountResult:
+        return models.CountResult(count=len(self._col(collection_name).row_ids))
+
+    def retrieve(self, collection_name: str, ids, with_payload=True, with_vectors=False,
+                 **kwargs):
+        col = self._col(collection_name)
+        out = []
+        for pid in ids:
+            r = col.id_to_row.get(_norm_id(pid))
+            if r is not None:
+                p = col.point(r, 0.0, with_payload, with_vectors)
+                out.append(models.Record(id=p.id, payload=p.payload, vector=p.vector))
+        return out
+
+    def query_points(self, collection_name: str, query=None, limit: int = 10,
+                     query_filter: models.Filter | None = None, with_payload=True,
+                     with_vectors=False, **kwargs) -> models.QueryResponse:
+        col = self._col(collection_name)
+        q = query if isinstance(query, torch.Tensor) else np.asarray(query, dtype=np.float32)
+        q = q.reshape(1, -1)
+        hits = col.search(q, int(limit), [col.compile_filter(query_filter)])[0]
+        return models.QueryResponse(points=[col.point(r, s, with_payload, with_vectors)
+                                            for r, s in hits])
+
+    def query_batch_points(self, collection_name: str, requests: list,
+                           **kwargs) -> list[models.QueryResponse]:
+        """One GPU scan for the whole batch (per-query filters ride along in the kernel)."""
+        col = self._col(collection_name)
+        if not requests:
+            return []
+        limit = max(int(r.limit) for r in requests)
+        qs = [r.query for r in requests]
+        Q = torch.stack([x if isinstance(x, torch.Tensor) else
+                         torch.as_tensor(np.asarray(x, np.float32)) for x in qs]) \
+            if any(isinstance(x, torch.Tensor) for x in qs) else np.asarray(qs, np.float32)
+        hits = col.search(Q, limit, [col.compile_filter(r.filter) for r in requests])
+        return [models.QueryResponse(points=[col.point(i, s, r.with_payload)
+                                             for i, s in h[:int(r.limit)]])
+                for r, h in zip(requests, hits)]
+
+    def search(self, collection_name: str, query_vector, limit: int = 10,
+               query_filter=None, with_payload=True, **kwargs):
+        """Legacy qdrant_client.search: list[ScoredPoint]."""
+        return self.query_points(collection_name, query_vector, limit, query_filter,
+                                 with_payload).points
+
+    def close(self) -> None:
+        with self._lock:
+            cols = list(self._collections.values())
+            self._collections.clear()
+        for c in cols:
+            c.index.close()

@@ -1,0 +1,126 @@
+/*
+ * ragmi.h — C ABI of libragmi.so, the MI355X-native (gfx950) two-stage retrieval hot path.
+ *
+ * This is the drop-in boundary that replaces, for the reference
+ * (pythonmailer/financial-rag-system, read-only at /root/reference):
+ *   - the Qdrant server behind `QdrantClient.query_points` / `upsert` / `create_collection`
+ *       main.py:92-95    get_qdrant()            -> rag_index_create
+ *       main.py:215-239  retrieve_from_qdrant()  -> rag_index_search (one query per call, B=1)
+ *       main2.py:160-163 retrieve_from_qdrant()  -> rag_index_search
+ *       main2.py:281-295 batch_processor()       -> rag_index_search (B=32 in one call)
+ *       ingest.py:86-96  ensure_collection()     -> rag_index_create (dim=384, COSINE)
+ *       ingest.py:148-175 PointStruct + upsert   -> rag_index_upsert (row slots assigned by host)
+ *       database.py:111-143 init_qdrant()        -> rag_index_create
+ *   - the sentence-transformers encoders (see ragmi_bert.h).
+ *
+ * Conventions
+ *   - All functions return 0 on success and a negative RAG_E* code on failure;
+ *     rag_last_error() returns a thread-local message for the last failure on this thread.
+ *   - "_dev" pointers are HIP device pointers (e.g. torch.Tensor.data_ptr() of a cuda tensor);
+ *     "_host" pointers are host memory. Host buffers are caller-owned; device storage made by
+ *     rag_index_create is handle-owned.
+ *   - `stream` is a hipStream_t (torch.cuda.current_stream().cuda_stream); NULL = default stream.
+ *     Device-pointer calls are asynchronous on `stream`; *_host calls are synchronous.
+ *   - Handles are re-entrant: calls on one handle from several threads are serialised
+ *     internally and each search uses its own workspace slot guarded by a HIP event, so
+ *     concurrent searches on different streams are safe (main2.py runs up to 25 requests
+ *     in flight through asyncio.to_thread, main2.py:52-53,218,228).
+ *
+ * Semantics (Qdrant COSINE collection, restated; see DESIGN.md §2 and oracle/scan_ref.c)
+ *   - upsert: every vector is L2-normalised (canonical fp64 norm) to fp32,
+ *     rounded to fp16 (RNE) and stored at its row slot; an existing slot is overwritten
+ *     (md5 point ids make re-ingest idempotent, ingest.py:151-154).
+ *   - search: the query is normalised the same way; score(row) = fp32(sum_k fp64(c_k)*fp64(q_k))
+ *     accumulated sequentially in k with fp64 fma; result = top-k rows by
+ *     (score desc, row asc), optionally restricted per query to rows whose tag satisfies
+ *     (tag & tag_mask) == tag_value (the payload `must` filter, main.py:218-236).
+ *     Missing results (fewer than k matching rows) are reported as id -1, score -inf.
+ */
+#ifndef RAGMI_H
+#define RAGMI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  RAG_OK = 0,
+  RAG_EINVAL = -1,   /* bad argument */
+  RAG_EHIP = -2,     /* HIP runtime error */
+  RAG_ENOMEM = -3,   /* device allocation failed */
+  RAG_ERANGE = -4,   /* row slot beyond capacity, k too large, ... */
+};
+
+/* Largest k a single search may ask for (the reference uses limit=15, main.py:215). */
+#define RAG_MAX_K 32
+/* Queries handled per scan pass; larger batches run ceil(B/32) passes. */
+#define RAG_QUERY_TILE 32
+
+typedef struct rag_index rag_index_t;
+
+/* Last error message of the calling thread ("" if none). */
+const char* rag_last_error(void);
+/* Library version string. */
+const char* rag_version(void);
+
+/* Create an empty flat index of `dim`-dimensional vectors (dim % 32 == 0; 384 and 1024 are
+ * built) with room for `capacity_rows` rows on HIP device `device`.
+ * Replaces QdrantClient.create_collection(vectors_config=VectorParams(size, COSINE)),
+ * ingest.py:86-96. */
+int rag_index_create(int dim, int64_t capacity_rows, int device, rag_index_t** out);
+int rag_index_destroy(rag_index_t* index);
+
+/* Grow capacity (keeps contents). */
+int rag_index_reserve(rag_index_t* index, int64_t capacity_rows);
+int64_t rag_index_capacity(const rag_index_t* index);
+int64_t rag_index_count(const rag_index_t* index);
+int rag_index_dim(const rag_index_t* index);
+
+/* Write n vectors (fp32 [n][dim], device) into the row slots rows_dev[i] (int64, device);
+ * tags_dev (uint32 [n], device) may be NULL (tag 0). `new_count` is the number of valid rows
+ * after this upsert (rows >= new_count are ignored by search). Replaces qdrant.upsert,
+ * ingest.py:171-175. */
+int rag_index_upsert(rag_index_t* index, const float* vecs_dev, const int64_t* rows_dev,
+                     const uint32_t* tags_dev, int64_t n, int64_t new_count, void* stream);
+/* Same, host pointers, synchronous. */
+int rag_index_upsert_host(rag_index_t* index, const float* vecs_host, const int64_t* rows_host,
+                          const uint32_t* tags_host, int64_t n, int64_t new_count);
+
+/* Top-k search of B queries (fp32 [B][dim], device). Outputs: out_scores_dev fp32 [B][k],
+ * out_ids_dev int64 [B][k] (row + id_offset, or -1). filters_dev is NULL (no filter) or
+ * uint32 [B][2] = (tag_mask, tag_value) per query: row r qualifies for query b iff
+ * (tag[r] & tag_mask) == tag_value ((0,0) = every row). One scan serves a whole micro-batch
+ * whose requests filter on different tickers (main2.py:228 per request).
+ * Replaces QdrantClient.query_points, main.py:232-237. */
+int rag_index_search(rag_index_t* index, const float* queries_dev, int B, int k,
+                     const uint32_t* filters_dev, int64_t id_offset,
+                     float* out_scores_dev, int64_t* out_ids_dev, void* stream);
+/* Same, host pointers (filters_host may be NULL), synchronous. */
+int rag_index_search_host(rag_index_t* index, const float* queries_host, int B, int k,
+                          const uint32_t* filters_host, int64_t id_offset,
+                          float* out_scores_host, int64_t* out_ids_host);
+
+/* Copy stored rows [row0, row0+n) out as row-major fp16 bits ([n][dim] uint16, host). */
+int rag_index_export_rows(rag_index_t* index, int64_t row0, int64_t n, uint16_t* out_host);
+/* Copy stored tags of rows [row0, row0+n) to host. */
+int rag_index_export_tags(rag_index_t* index, int64_t row0, int64_t n, uint32_t* out_host);
+
+/* Merge n_lists per-shard result lists (each [B][k] sorted by (score desc, id asc), device;
+ * laid out [n_lists][B][k]) into the global top-k [B][k] (device). Used after the RCCL
+ * all-gather of per-shard results. */
+int rag_merge_topk(const float* in_scores_dev, const int64_t* in_ids_dev, int n_lists, int B,
+                   int k, float* out_scores_dev, int64_t* out_ids_dev, void* stream);
+
+/* Kernel timing hook for bench.py: average device time (ms) of the last `rag_index_search`
+ * scan-kernel launches measured with HIP events on the launch stream. enable != 0 turns on
+ * event recording around the scan kernel (adds two event records per pass). */
+int rag_profile_enable(rag_index_t* index, int enable);
+int rag_profile_scan_ms(rag_index_t* index, double* total_ms, int64_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RAGMI_H */

@@ -1,0 +1,166 @@
+"""oracle/oracle_scan.py — numpy + ctypes front end of the CPU search restatement.
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg as the checker. The product path (ragmi / libragmi.so) never imports it.
+
+Restates the reference's COSINE search (reference main.py:215-239 query_points with
+limit=15 and the ticker/document_type `must` filter; ingest.py:86-96,148-175 collection +
+upsert; Qdrant COSINE = normalise at insert, dot product) with the canonical arithmetic of
+oracle/scan_ref.c (see its header). Parity against the reference itself is UNPINNED: the
+reference's only test file (tests.py) runs TESTING stubs (main.py:216) and pins no numbers,
+and neither Qdrant nor sentence-transformers is installed here.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_SO = os.path.join(_HERE, "liboracle_scan.so")
+_lib = None
+
+
+def build() -> str:
+    """Compile scan_ref.c -> liboracle_scan.so (gcc; no reference sources involved)."""
+    src = os.path.join(_HERE, "scan_ref.c")
+    if not os.path.exists(_SO) or os.path.getmtime(_SO) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", _HERE, "liboracle_scan.so"])
+    return _SO
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(_SO)
+        f32p = ctypes.POINTER(ctypes.c_float)
+        u16p = ctypes.POINTER(ctypes.c_uint16)
+        u32p = ctypes.POINTER(ctypes.c_uint32)
+        i64p = ctypes.POINTER(ctypes.c_int64)
+        L.orc_canon_sumsq.restype = ctypes.c_double
+        L.orc_canon_sumsq.argtypes = [f32p, ctypes.c_int]
+        L.orc_encode_rows.argtypes = [f32p, ctypes.c_int64, ctypes.c_int, u16p]
+        L.orc_normalize.argtypes = [f32p, ctypes.c_int, f32p, u16p]
+        L.orc_search.argtypes = [u16p, u32p, ctypes.c_int64, ctypes.c_int, f32p, ctypes.c_int,
+                                 ctypes.c_int, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32,
+                                 f32p, i64p]
+        L.orc_rescore.argtypes = [u16p, ctypes.c_int, f32p, ctypes.c_int, i64p, ctypes.c_int,
+                                  f32p]
+        L.orc_f32_to_f16.restype = ctypes.c_uint16
+        L.orc_f32_to_f16.argtypes = [ctypes.c_float]
+        _lib = L
+    return _lib
+
+
+def _p(a, ct):
+    return a.ctypes.data_as(ctypes.POINTER(ct))
+
+
+def encode_rows(x: np.ndarray) -> np.ndarray:
+    """fp32 [n, D] input vectors -> stored fp16 rows (as uint16 bits), canonical normalise."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    n, d = x.shape
+    out = np.empty((n, d), dtype=np.uint16)
+    lib().orc_encode_rows(_p(x, ctypes.c_float), n, d, _p(out, ctypes.c_uint16))
+    return out
+
+
+def normalize(x: np.ndarray) -> np.ndarray:
+    """Canonical fp32 normalisation of each row of x [n, D]."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    out = np.empty_like(x)
+    for i in range(x.shape[0]):
+        lib().orc_normalize(_p(x[i], ctypes.c_float), x.shape[1], _p(out[i], ctypes.c_float),
+                            None)
+    return out
+
+
+def search(corpus16: np.ndarray, queries: np.ndarray, k: int, tags: np.ndarray | None = None,
+           mask: int = 0, value: int = 0, use_filter: bool = False):
+    """Exact top-k by (score desc, row asc). corpus16: uint16 fp16 bits [N, D]."""
+    corpus16 = np.ascontiguousarray(corpus16, dtype=np.uint16)
+    queries = np.ascontiguousarray(queries, dtype=np.float32)
+    n, d = corpus16.shape
+    b = queries.shape[0]
+    if tags is None:
+        tags = np.zeros(max(n, 1), dtype=np.uint32)
+    tags = np.ascontiguousarray(tags, dtype=np.uint32)
+    out_s = np.empty((b, k), dtype=np.float32)
+    out_i = np.empty((b, k), dtype=np.int64)
+    lib().orc_search(_p(corpus16, ctypes.c_uint16), _p(tags, ctypes.c_uint32), n, d,
+                     _p(queries, ctypes.c_float), b, k, int(use_filter), mask, value,
+                     _p(out_s, ctypes.c_float), _p(out_i, ctypes.c_int64))
+    return out_s, out_i
+
+
+def rescore(corpus16: np.ndarray, qn: np.ndarray, cand: np.ndarray) -> np.ndarray:
+    corpus16 = np.ascontiguousarray(corpus16, dtype=np.uint16)
+    qn = np.ascontiguousarray(qn, dtype=np.float32)
+    cand = np.ascontiguousarray(cand, dtype=np.int64)
+    b, m = cand.shape
+    sc = np.empty((b, m), dtype=np.float32)
+    lib().orc_rescore(_p(corpus16, ctypes.c_uint16), corpus16.shape[1], _p(qn, ctypes.c_float),
+                      b, _p(cand, ctypes.c_int64), m, _p(sc, ctypes.c_float))
+    return sc
+
+
+def search_fast(corpus16: np.ndarray, queries: np.ndarray, k: int, margin: int = 64,
+                chunk: int = 1 << 20, tags: np.ndarray | None = None, mask: int = 0,
+                value: int = 0, use_filter: bool = False):
+    """Same result as search() for large corpora: numpy fp32 BLAS shortlist of k+margin
+    candidates per query (chunked), then canonical exact rescoring and (score desc, row asc)
+    ordering. Exact unless more than `margin` rows lie within fp32-BLAS error of the k-th."""
+    queries = np.ascontiguousarray(queries, dtype=np.float32)
+    qn = normalize(queries)
+    n, d = corpus16.shape
+    b = qn.shape[0]
+    m = min(k + margin, n)
+    best_s = np.full((b, 0), -np.inf, dtype=np.float32)
+    best_i = np.zeros((b, 0), dtype=np.int64)
+    for r0 in range(0, n, chunk):
+        c = corpus16[r0:r0 + chunk].view(np.float16).astype(np.float32)
+        s = qn @ c.T  # [b, chunk]
+        if use_filter:
+            t = tags[r0:r0 + chunk]
+            s[:, (t & mask) != value] = -np.inf
+        mm = min(m, s.shape[1])
+        part = np.argpartition(-s, mm - 1, axis=1)[:, :mm]
+        ps = np.take_along_axis(s, part, axis=1)
+        best_s = np.concatenate([best_s, ps], axis=1)
+        best_i = np.concatenate([best_i, part + r0], axis=1)
+        if best_s.shape[1] > m:
+            sel = np.argpartition(-best_s, m - 1, axis=1)[:, :m]
+            best_s = np.take_along_axis(best_s, sel, axis=1)
+            best_i = np.take_along_axis(best_i, sel, axis=1)
+    cand = np.where(np.isfinite(best_s), best_i, -1)
+    ex = rescore(corpus16, qn, cand)
+    out_s = np.full((b, k), -np.inf, dtype=np.float32)
+    out_i = np.full((b, k), -1, dtype=np.int64)
+    for q in range(b):
+        valid = cand[q] >= 0
+        ids, sc = cand[q][valid], ex[q][valid]
+        order = np.lexsort((ids, -sc.astype(np.float64)))[:k]
+        out_s[q, :len(order)] = sc[order]
+        out_i[q, :len(order)] = ids[order]
+    return out_s, out_i
+
+
+def search_f64_reference(corpus16: np.ndarray, queries: np.ndarray, k: int):
+    """Independent numpy formulation used to pin the C oracle in tests: float64 matmul on
+    the fp16 corpus against canonically normalised queries, rounded to fp32, full lexsort.
+    (Summation order differs from the canonical one; equal to it whenever no fp32 rounding
+    boundary is straddled, which the tests check on fixtures.)"""
+    qn = normalize(queries).astype(np.float64)
+    c = corpus16.view(np.float16).astype(np.float64)
+    s = (qn @ c.T).astype(np.float32)
+    out_s = np.empty((qn.shape[0], k), dtype=np.float32)
+    out_i = np.empty((qn.shape[0], k), dtype=np.int64)
+    ids = np.arange(c.shape[0])
+    for q in range(qn.shape[0]):
+        order = np.lexsort((ids, -s[q].astype(np.float64)))[:k]
+        out_s[q] = s[q][order]
+        out_i[q] = order
+    return out_s, out_i

@@ -1,0 +1,33 @@
+"""pytest configuration: `gpu` marker, import paths for the product package (ragmi, under
+financial-rag-system_amd/) and the test-only oracle (oracle/)."""
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "financial-rag-system_amd")
+for p in (ROOT, PKG, os.path.join(ROOT, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device); run with -m gpu")
+
+
+@pytest.fixture(scope="session")
+def gpu():
+    import torch
+    assert torch.cuda.is_available(), "GPU test run without a HIP device"
+    from ragmi import _lib
+    _lib.load()   # fail loudly if libragmi.so is missing
+    return torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="session")
+def golden_scan():
+    import numpy as np
+    return dict(np.load(os.path.join(GOLDEN, "scan_golden.npz")))
