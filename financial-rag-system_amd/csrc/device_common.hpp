@@ -88,6 +88,14 @@ __device__ __forceinline__ double canon_sumsq(const float* __restrict__ x, int l
   return __shfl(acc, 0, 64);
 }
 
+// fp32 -> fp16 RNE of an fp32 value. The empty asm makes `y` opaque: without it LLVM folds
+// (half)(float)(double) into one direct f64->f16 rounding, which differs from the canonical
+// double rounding (fp64 -> fp32 -> fp16) in ~1/8192 of the elements.
+__device__ __forceinline__ _Float16 f32_to_f16(float y) {
+  asm volatile("" : "+v"(y));
+  return (_Float16)y;
+}
+
 // y = fp32(x / sqrt(sumsq)) with fp64 division; zero vector stays zero.
 __device__ __forceinline__ float canon_scale(float x, double norm) {
   return norm > 0.0 ? (float)((double)x / norm) : 0.0f;

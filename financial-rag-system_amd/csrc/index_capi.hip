@@ -1,7 +1,7 @@
 // index_capi.hip — extern "C" boundary of the flat index (declared in include/ragmi.h).
 //
 // Host side of the Qdrant replacement: handle lifetime, capacity growth, workspace ring,
-// kernel launch sequence of one search (qprep -> scan -> merge1 -> merge2). No compute runs
+// kernel launch sequence of one search (qprep -> scan -> select). No compute runs
 // on the host; every entry point either enqueues on the caller's stream or (for *_host)
 // stages through device memory and synchronises.
 #include <hip/hip_runtime.h>
@@ -21,16 +21,15 @@ using ragmi::half8;
 namespace {
 
 constexpr int kRing = 4;            // workspace slots (concurrent searches in flight)
-constexpr int kMergeGroup = 64;     // wave lists per merge-1 wave
 
 struct Workspace {
   float* qn = nullptr;
   half8* qfrag = nullptr;
   uint32_t* filt = nullptr;
+  float* smax = nullptr;      // [kMaxLists][32] per-sample-wave maxima
+  float* seed = nullptr;      // [32] seed thresholds
   float* part_s = nullptr;
   int* part_i = nullptr;
-  float* mid_s = nullptr;
-  int* mid_i = nullptr;
   hipEvent_t done = nullptr;
 };
 
@@ -93,14 +92,33 @@ void launch_upsert(rag_index* h, const float* v, const int64_t* rows, const uint
                                                                   h->tags, n, h->cap_rows);
 }
 
+// sample + thresh: seed thresholds for the scan (see sample_kernel). ~0.8% of the shard's
+// tiles, spread evenly, at least 256 tiles (all of them for small shards).
+template <int D, bool FILTER>
+void launch_seed(rag_index* h, Workspace& w, hipStream_t st) {
+  using namespace ragmi;
+  const int n_tiles = (int)((h->count + 15) / 16);
+  if (n_tiles == 0) return;   // the scan visits no tile; seeds are never read
+  const int n_sample = std::min(n_tiles, std::max(256, n_tiles / 128));
+  const int nsw = std::min(kMaxLists, (n_sample + 3) & ~3);
+  sample_kernel<D, FILTER><<<dim3(nsw / 4), dim3(256), 0, st>>>(
+      h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, n_tiles, n_sample, w.smax);
+  thresh_kernel<<<dim3(kQ), dim3(256), 0, st>>>(w.smax, nsw, w.seed);
+}
+
 template <int D>
 int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k,
                        const uint32_t* filt, int64_t id_offset, float* out_s, int64_t* out_i,
                        hipStream_t st) {
   using namespace ragmi;
   qprep_kernel<D><<<dim3(kQ), dim3(64), 0, st>>>(q, Bq, filt, w.qn, w.qfrag, w.filt);
+  if (filt)
+    launch_seed<D, true>(h, w, st);
+  else
+    launch_seed<D, false>(h, w, st);
   const int64_t n_tiles = (h->count + 15) / 16;
   int grid = (int)std::min<int64_t>(h->max_wgs, std::max<int64_t>(1, (n_tiles + 3) / 4));
+  grid = std::min(grid, kMaxLists / kWavesPerWG);
   ProfPair pp{};
   if (h->prof) {
     RAG_HIP(hipEventCreate(&pp.a));
@@ -109,20 +127,19 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
   }
   if (filt)
     scan_kernel<D, true><<<dim3(grid), dim3(256), 0, st>>>(
-        h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, (int)n_tiles, w.part_s, w.part_i);
+        h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, (int)n_tiles, w.seed, w.part_s,
+        w.part_i);
   else
     scan_kernel<D, false><<<dim3(grid), dim3(256), 0, st>>>(
-        h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, (int)n_tiles, w.part_s, w.part_i);
+        h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, (int)n_tiles, w.seed, w.part_s,
+        w.part_i);
   if (h->prof) {
     RAG_HIP(hipEventRecord(pp.b, st));
     h->prof_pairs.push_back(pp);
   }
   const int n_lists = grid * kWavesPerWG;
-  const int n_groups = (n_lists + kMergeGroup - 1) / kMergeGroup;
-  merge1_kernel<<<dim3(n_groups, Bq), dim3(64), 0, st>>>(w.part_s, w.part_i, n_lists,
-                                                         kMergeGroup, w.mid_s, w.mid_i);
-  merge2_kernel<D><<<dim3(Bq), dim3(64), 0, st>>>(w.mid_s, w.mid_i, n_groups, h->corpus, w.qn,
-                                                  k, id_offset, out_s, out_i);
+  select_kernel<D><<<dim3(Bq), dim3(256), 0, st>>>(w.part_s, w.part_i, n_lists, h->corpus,
+                                                   w.qn, k, id_offset, out_s, out_i);
   RAG_HIP(hipGetLastError());
   return RAG_OK;
 }
@@ -184,6 +201,62 @@ int search_locked(rag_index* h, const float* q, int B, int k, const uint32_t* fi
   return RAG_OK;
 }
 
+
+// Diagnostic A/B of scan variants (see scan_kernel's knobs). Returns avg device ms/launch.
+template <int D, int V>
+void launch_variant(rag_index* h, Workspace& w, int grid, hipStream_t st) {
+  using namespace ragmi;
+  const int n_tiles = (int)((h->count + 15) / 16);
+  // 0 prod (seeded) | 1 unseeded | 2 contiguous | 3 mfma-only | 4 loads-only | 5 no-nt
+  // 6 no-sb
+  constexpr int MODE = V == 3 ? 1 : (V == 4 ? 2 : 0);
+  constexpr bool STRIDED = V != 2;
+  constexpr bool NT = V != 5;
+  constexpr bool SB = V != 6;
+  scan_kernel<D, false, MODE, STRIDED, NT, SB><<<dim3(grid), dim3(256), 0, st>>>(
+      h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, n_tiles, V == 1 ? nullptr : w.seed,
+      w.part_s, w.part_i);
+}
+
+template <int D>
+int bench_scan(rag_index* h, const float* q, int B, int variant, int reps, double* avg_ms) {
+  using namespace ragmi;
+  Workspace& w = h->ws[0];
+  RAG_HIP(hipDeviceSynchronize());
+  qprep_kernel<D><<<dim3(kQ), dim3(64), 0, nullptr>>>(q, std::min(B, kQ), nullptr, w.qn,
+                                                      w.qfrag, w.filt);
+  launch_seed<D, false>(h, w, nullptr);
+  const int64_t n_tiles = (h->count + 15) / 16;
+  int grid = (int)std::min<int64_t>(h->max_wgs, std::max<int64_t>(1, (n_tiles + 3) / 4));
+  grid = std::min(grid, kMaxLists / kWavesPerWG);
+  hipEvent_t a, b;
+  RAG_HIP(hipEventCreate(&a));
+  RAG_HIP(hipEventCreate(&b));
+  auto one = [&]() {
+    switch (variant) {
+      case 0: launch_variant<D, 0>(h, w, grid, nullptr); break;
+      case 1: launch_variant<D, 1>(h, w, grid, nullptr); break;
+      case 2: launch_variant<D, 2>(h, w, grid, nullptr); break;
+      case 3: launch_variant<D, 3>(h, w, grid, nullptr); break;
+      case 4: launch_variant<D, 4>(h, w, grid, nullptr); break;
+      case 5: launch_variant<D, 5>(h, w, grid, nullptr); break;
+      default: launch_variant<D, 6>(h, w, grid, nullptr); break;
+    }
+  };
+  one();  // warm
+  RAG_HIP(hipEventRecord(a, nullptr));
+  for (int r = 0; r < reps; ++r) one();
+  RAG_HIP(hipEventRecord(b, nullptr));
+  RAG_HIP(hipEventSynchronize(b));
+  float ms = 0.f;
+  RAG_HIP(hipEventElapsedTime(&ms, a, b));
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  RAG_HIP(hipGetLastError());
+  *avg_ms = ms / reps;
+  return RAG_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -214,21 +287,19 @@ int rag_index_create(int dim, int64_t capacity_rows, int device, rag_index_t** o
       n_cu <= 0)
     n_cu = 256;
   h->max_wgs = n_cu * 2;  // 2 x 256-thread workgroups per CU (__launch_bounds__(256, 2))
-  const int max_lists = h->max_wgs * ragmi::kWavesPerWG;
-  const int max_groups = (max_lists + kMergeGroup - 1) / kMergeGroup;
+  const int max_lists = std::min(h->max_wgs * ragmi::kWavesPerWG, ragmi::kMaxLists);
   for (auto& w : h->ws) {
     bool ok = hipMalloc(reinterpret_cast<void**>(&w.qn), ragmi::kQ * dim * 4) == hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&w.qfrag), 2 * (dim / 32) * 64 * 16) ==
                   hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&w.filt), ragmi::kQ * 2 * 4) == hipSuccess &&
+              hipMalloc(reinterpret_cast<void**>(&w.smax),
+                        (size_t)ragmi::kMaxLists * ragmi::kQ * 4) == hipSuccess &&
+              hipMalloc(reinterpret_cast<void**>(&w.seed), ragmi::kQ * 4) == hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&w.part_s),
                         (size_t)max_lists * ragmi::kQ * ragmi::kKS * 4) == hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&w.part_i),
                         (size_t)max_lists * ragmi::kQ * ragmi::kKS * 4) == hipSuccess &&
-              hipMalloc(reinterpret_cast<void**>(&w.mid_s),
-                        (size_t)max_groups * ragmi::kQ * ragmi::kKS * 4) == hipSuccess &&
-              hipMalloc(reinterpret_cast<void**>(&w.mid_i),
-                        (size_t)max_groups * ragmi::kQ * ragmi::kKS * 4) == hipSuccess &&
               hipEventCreateWithFlags(&w.done, hipEventDisableTiming) == hipSuccess;
     if (!ok) {
       rag_index_destroy(h);
@@ -248,10 +319,10 @@ int rag_index_destroy(rag_index_t* h) {
     if (w.qn) (void)hipFree(w.qn);
     if (w.qfrag) (void)hipFree(w.qfrag);
     if (w.filt) (void)hipFree(w.filt);
+    if (w.smax) (void)hipFree(w.smax);
+    if (w.seed) (void)hipFree(w.seed);
     if (w.part_s) (void)hipFree(w.part_s);
     if (w.part_i) (void)hipFree(w.part_i);
-    if (w.mid_s) (void)hipFree(w.mid_s);
-    if (w.mid_i) (void)hipFree(w.mid_i);
     if (w.done) (void)hipEventDestroy(w.done);
   }
   for (auto& p : h->prof_pairs) {
@@ -407,6 +478,17 @@ int rag_merge_topk(const float* in_s, const int64_t* in_i, int n_lists, int B, i
       in_s, in_i, n_lists, B, k, out_s, out_i);
   RAG_HIP(hipGetLastError());
   return RAG_OK;
+}
+
+int rag_bench_scan(rag_index_t* h, const float* queries_dev, int B, int variant, int reps,
+                   double* avg_ms) {
+  ragmi::clear_error();
+  if (!h || !queries_dev || B < 1 || reps < 1 || !avg_ms || variant < 0 || variant > 6)
+    return ragmi::fail(RAG_EINVAL, "bad bench args");
+  std::lock_guard<std::mutex> lk(h->mu);
+  RAG_HIP(hipSetDevice(h->device));
+  if (h->dim != 384) return ragmi::fail(RAG_EINVAL, "bench variants built for dim 384");
+  return bench_scan<384>(h, queries_dev, B, variant, reps, avg_ms);
 }
 
 int rag_profile_enable(rag_index_t* h, int enable) {

@@ -20,6 +20,7 @@ constexpr int kQ = 32;            // queries per pass
 constexpr int kKS = 32;           // candidates kept per (wave, query)
 constexpr int kP = 8;             // pending slots per (lane, query tile)
 constexpr int kWavesPerWG = 4;
+constexpr int kMaxLists = 2048;   // max scan waves (= per-wave lists) per pass
 constexpr int kLdsPerWave = 4096; // dwords: keep_s[32][32] keep_i[32][32] pend_s[2][8][64] pend_i[2][8][64]
 
 template <int D>
@@ -47,7 +48,7 @@ __global__ __launch_bounds__(64) void upsert_kernel(const float* __restrict__ ve
   for (int c = lane; c < D / 8; c += 64) {
     half8 h;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) h[j] = (_Float16)canon_scale(x[8 * c + j], norm);
+    for (int j = 0; j < 8; ++j) h[j] = f32_to_f16(canon_scale(x[8 * c + j], norm));
     const int s = c >> 2, hh = c & 3;
     corpus[t * (steps<D>() * 64) + s * 64 + hh * 16 + r] = h;
   }
@@ -84,7 +85,7 @@ __global__ __launch_bounds__(64) void qprep_kernel(const float* __restrict__ q, 
     for (int j = 0; j < 8; ++j) {
       const float y = live ? canon_scale(q[(int64_t)b * D + 8 * c + j], norm) : 0.0f;
       qn[b * D + 8 * c + j] = y;
-      h[j] = (_Float16)y;
+      h[j] = f32_to_f16(y);
     }
     const int s = c >> 2, hh = c & 3;
     qfrag[(qt * steps<D>() + s) * 64 + hh * 16 + c16] = h;
@@ -148,10 +149,10 @@ __device__ __forceinline__ void flush_query(const WaveTopK& w, int q, int lane, 
   const float nt = __shfl(s, 31, 64);
   if ((lane & 15) == c) {
     if (qt == 0) {
-      thr0 = nt;
+      thr0 = fmaxf(thr0, nt);
       cnt0 = 0;
     } else {
-      thr1 = nt;
+      thr1 = fmaxf(thr1, nt);
       cnt1 = 0;
     }
   }
@@ -167,11 +168,18 @@ __device__ __forceinline__ void flush_mask(const WaveTopK& w, uint64_t b, int qt
   }
 }
 
-template <int D, bool FILTER>
+// Variant knobs (A/B'd by rag_bench_scan; the production instance is scan_kernel<D, F>):
+//   MODE 0 full scan + top-k; 1 MFMA only (running max, no top-k); 2 loads only
+//   STRIDED tile order gw, gw+nw, ... (the chip sweeps one window) vs contiguous ranges
+//   NT non-temporal corpus loads (the corpus is read once per search; MI355X_MICROARCH
+//      'nt-weights': once-read streams)
+//   SB sched_barrier after each tile's load batch, so the scheduler cannot sink the next
+//      tile's loads below the current tile's wait (which leaves one tile in flight)
+template <int D, bool FILTER, int MODE = 0, bool STRIDED = true, bool NT = true, bool SB = true>
 __global__ __launch_bounds__(256, 2) void scan_kernel(
     const half8* __restrict__ corpus, const uint32_t* __restrict__ tags,
     const uint32_t* __restrict__ filt, const half8* __restrict__ qfrag, int n_rows, int n_tiles,
-    float* __restrict__ part_s, int* __restrict__ part_i) {
+    const float* __restrict__ seed_thr, float* __restrict__ part_s, int* __restrict__ part_i) {
   constexpr int S = steps<D>();
   __shared__ int lds[kWavesPerWG * kLdsPerWave];
   const int lane = threadIdx.x & 63;
@@ -190,10 +198,20 @@ __global__ __launch_bounds__(256, 2) void scan_kernel(
   }
   lds_fence();
 
-  const int gw = blockIdx.x * kWavesPerWG + wid;
+  const int gw = blockIdx.x * kWavesPerWG + __builtin_amdgcn_readfirstlane(wid);
   const int nw = gridDim.x * kWavesPerWG;
-  const int t_begin = (int)((int64_t)n_tiles * gw / nw);
-  const int t_end = (int)((int64_t)n_tiles * (gw + 1) / nw);
+  // tile sequence of this wave: t_j = t_first + j * t_step, j < n_mine (always increasing,
+  // which the strict `> thr` tie rule relies on)
+  int t_first, t_step, n_mine;
+  if constexpr (STRIDED) {
+    t_first = gw;
+    t_step = nw;
+    n_mine = gw < n_tiles ? (n_tiles - 1 - gw) / nw + 1 : 0;
+  } else {
+    t_first = (int)((int64_t)n_tiles * gw / nw);
+    t_step = 1;
+    n_mine = (int)((int64_t)n_tiles * (gw + 1) / nw) - t_first;
+  }
 
   half8 q0[S], q1[S];
 #pragma unroll
@@ -202,7 +220,15 @@ __global__ __launch_bounds__(256, 2) void scan_kernel(
     q1[s] = qfrag[(S + s) * 64 + lane];
   }
 
+  // Seed thresholds: seed_thr[q] is a lower bound of the global 32nd-best score (32 rows
+  // scoring >= it exist, sample_kernel), so rows scoring below it can never be in the top-32.
+  // `> pred(T)` == `>= T`; thresholds only ever rise.
   float thr0 = kNegInf, thr1 = kNegInf;
+  if (seed_thr) {
+    const float T0 = seed_thr[lane & 15], T1 = seed_thr[16 + (lane & 15)];
+    thr0 = T0 == kNegInf ? kNegInf : nextafterf(T0, kNegInf);
+    thr1 = T1 == kNegInf ? kNegInf : nextafterf(T1, kNegInf);
+  }
   int cnt0 = 0, cnt1 = 0;
   const int rsub = 4 * (lane >> 4);
   uint32_t fm0 = 0, fv0 = 0, fm1 = 0, fv1 = 0;
@@ -261,24 +287,61 @@ __global__ __launch_bounds__(256, 2) void scan_kernel(
     }
   };
 
-  if (t_begin < t_end) {
-    half8 a0[S], a1[S];
-    const half8* base = corpus + lane;
-    auto load = [&](half8(&a)[S], int t) {
-      const half8* p = base + (int64_t)t * (S * 64);
+  float vmax = kNegInf;   // MODE 1/2: keeps the work alive
+  auto process_v = [&](const half8(&a)[S], int t) {
+    if constexpr (MODE == 0) {
+      process(a, t);
+    } else if constexpr (MODE == 1) {
+      floatx4 acc0 = {0.f, 0.f, 0.f, 0.f};
+      floatx4 acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < S; ++s) a[s] = p[s * 64];
-    };
-    load(a0, t_begin);
-    int t = t_begin;
-    while (true) {
-      load(a1, min(t + 1, t_end - 1));
-      process(a0, t);
-      if (++t >= t_end) break;
-      load(a0, min(t + 1, t_end - 1));
-      process(a1, t);
-      if (++t >= t_end) break;
+      for (int s = 0; s < S; ++s) {
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[s], q0[s], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[s], q1[s], acc1, 0, 0, 0);
+      }
+      vmax = fmaxf(vmax, fmaxf(fmaxf(fmaxf(acc0[0], acc0[1]), fmaxf(acc0[2], acc0[3])),
+                               fmaxf(fmaxf(acc1[0], acc1[1]), fmaxf(acc1[2], acc1[3]))));
+    } else {
+      half8 x = a[0];
+#pragma unroll
+      for (int s = 1; s < S; ++s) x += a[s];
+      vmax = fmaxf(vmax, (float)(x[0] + x[1] + x[2] + x[3] + x[4] + x[5] + x[6] + x[7]));
     }
+  };
+
+  if (n_mine > 0) {
+    half8 a0[S], a1[S];
+    // Buffer loads off a wave-uniform per-tile descriptor: the address lives in SGPRs and the
+    // per-lane part is one VGPR (lane*16), so no 64-bit address VGPRs are live across the
+    // loop (their reuse as load destinations forced a vmcnt(0) at the loop head).
+    const char* cbase = reinterpret_cast<const char*>(corpus);
+    const int voff = lane * 16;
+    auto load = [&](half8(&a)[S], int j) {
+      const int t = __builtin_amdgcn_readfirstlane(t_first + j * t_step);
+      const char* tp = cbase + (int64_t)t * (S * 1024);
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(tp), 0, S * 1024, 0x00020000);
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, s * 1024, NT ? 2 : 0);
+        a[s] = __builtin_bit_cast(half8, v);
+      }
+      if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
+    };
+    load(a0, 0);
+    int j = 0;
+    while (true) {
+      load(a1, min(j + 1, n_mine - 1));
+      process_v(a0, t_first + j * t_step);
+      if (++j >= n_mine) break;
+      load(a0, min(j + 1, n_mine - 1));
+      process_v(a1, t_first + j * t_step);
+      if (++j >= n_mine) break;
+    }
+  }
+  if constexpr (MODE != 0) {
+    if (vmax == 12345.0f) part_s[gw] = vmax;   // never true in practice; defeats DCE
+    return;
   }
 
   // final flush of every query with pending entries
@@ -298,87 +361,313 @@ __global__ __launch_bounds__(256, 2) void scan_kernel(
 }
 
 // ----------------------------------------------------------------------------------------
-// merge stage 1: grid (groups, Bq); one wave merges up to `per_group` sorted wave lists of
-// one query into its top-32 (approximate MFMA scores).
+// sample: seed thresholds for the scan. Sample wave w scores the corpus tiles
+//   t = (j * n_tiles) / n_sample, j = w, w + n_waves, ...   (spread over the shard)
+// and writes, per query, the max score over its (valid, filter-passing) rows to
+// smax[w][q]. The 32nd largest of these per-wave maxima comes from 32 distinct rows, so it
+// is a lower bound of the global 32nd-best score: thresh_kernel turns it into seed_thr.
 // ----------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void merge1_kernel(const float* __restrict__ part_s,
-                                                    const int* __restrict__ part_i,
-                                                    int n_lists, int per_group,
-                                                    float* __restrict__ mid_s,
-                                                    int* __restrict__ mid_i) {
-  const int g = blockIdx.x, b = blockIdx.y, lane = threadIdx.x;
-  const int l0 = g * per_group;
-  const int l1 = min(l0 + per_group, n_lists);
-  float s = kNegInf;
-  int id = kIdNone32;
-  if (lane < 32 && l0 < n_lists) {
-    s = part_s[((int64_t)l0 * kQ + b) * kKS + lane];
-    id = part_i[((int64_t)l0 * kQ + b) * kKS + lane];
+template <int D, bool FILTER>
+__global__ __launch_bounds__(256) void sample_kernel(const half8* __restrict__ corpus,
+                                                     const uint32_t* __restrict__ tags,
+                                                     const uint32_t* __restrict__ filt,
+                                                     const half8* __restrict__ qfrag,
+                                                     int n_rows, int n_tiles, int n_sample,
+                                                     float* __restrict__ smax) {
+  constexpr int S = steps<D>();
+  const int lane = threadIdx.x & 63;
+  const int w = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nw = gridDim.x * 4;
+  uint32_t fm0 = 0, fv0 = 0, fm1 = 0, fv1 = 0;
+  if constexpr (FILTER) {
+    fm0 = filt[2 * (lane & 15)];
+    fv0 = filt[2 * (lane & 15) + 1];
+    fm1 = filt[2 * (16 + (lane & 15))];
+    fv1 = filt[2 * (16 + (lane & 15)) + 1];
   }
-  for (int l = l0 + 1; l < l1; ++l) {
-    if (lane >= 32) {
-      s = part_s[((int64_t)l * kQ + b) * kKS + (63 - lane)];
-      id = part_i[((int64_t)l * kQ + b) * kKS + (63 - lane)];
+  float m0 = kNegInf, m1 = kNegInf;
+  const int rsub = 4 * (lane >> 4);
+  for (int j = w; j < n_sample; j += nw) {
+    const int t = (int)(((int64_t)j * n_tiles) / n_sample);
+    const half8* p = corpus + (int64_t)t * (S * 64) + lane;
+    floatx4 acc0 = {0.f, 0.f, 0.f, 0.f};
+    floatx4 acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const half8 a = __builtin_nontemporal_load(p + s * 64);
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, qfrag[s * 64 + lane], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, qfrag[(S + s) * 64 + lane], acc1, 0, 0, 0);
     }
-    bitonic_merge64(s, id, lane);
+    const int rbase = t * kTileRows + rsub;
+    uint4 tg = {0u, 0u, 0u, 0u};
+    if constexpr (FILTER) tg = *reinterpret_cast<const uint4*>(tags + rbase);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const bool ok = (rbase + r) < n_rows;
+      bool ok0 = ok, ok1 = ok;
+      if constexpr (FILTER) {
+        const uint32_t tr = r == 0 ? tg.x : r == 1 ? tg.y : r == 2 ? tg.z : tg.w;
+        ok0 = ok0 && ((tr & fm0) == fv0);
+        ok1 = ok1 && ((tr & fm1) == fv1);
+      }
+      if (ok0) m0 = fmaxf(m0, acc0[r]);
+      if (ok1) m1 = fmaxf(m1, acc1[r]);
+    }
   }
-  if (lane < 32) {
-    mid_s[((int64_t)g * kQ + b) * kKS + lane] = s;
-    mid_i[((int64_t)g * kQ + b) * kKS + lane] = id;
+  // lanes l, l^16, l^32, l^48 hold the same queries
+  m0 = fmaxf(m0, __shfl_xor(m0, 16, 64));
+  m0 = fmaxf(m0, __shfl_xor(m0, 32, 64));
+  m1 = fmaxf(m1, __shfl_xor(m1, 16, 64));
+  m1 = fmaxf(m1, __shfl_xor(m1, 32, 64));
+  if (lane < 16) {
+    smax[(int64_t)w * kQ + lane] = m0;
+    smax[(int64_t)w * kQ + 16 + lane] = m1;
+  }
+}
+
+// thresh: one 256-thread workgroup per query slot: seed_thr[q] = 32nd largest of
+// smax[0..n_waves)[q] (-inf if fewer than 32 are finite). MFMA-rounded scores are used only
+// to prune, never to rank, so their rounding is harmless... except that a pruning bound must
+// not exceed an exact score it stands for: the bound is lowered by kSeedMargin (relative +
+// absolute) to cover the MFMA-vs-exact difference (fp16 query rounding, fp32 accumulation).
+constexpr float kSeedMargin = 1e-3f;
+
+__global__ __launch_bounds__(256) void thresh_kernel(const float* __restrict__ smax,
+                                                     int n_waves, float* __restrict__ seed_thr) {
+  __shared__ float w_s[4][32];
+  const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  constexpr int kCols = kMaxLists / 256;
+  float cs = kNegInf;
+  int ci = kIdNone32;
+#pragma unroll
+  for (int j = 0; j < kCols; ++j) {
+    const int w = (j * 4 + wid) * 64 + lane;
+    float s = w < n_waves ? smax[(int64_t)w * kQ + q] : kNegInf;
+    if (!__ballot(s != kNegInf)) continue;
+    int id = w;
+    bitonic_sort64(s, id, lane);
+    const float rs = __shfl(s, 63 - lane, 64);
+    const int ri = __shfl(id, 63 - lane, 64);
+    if (lane >= 32) {
+      cs = rs;
+      ci = ri;
+    }
+    bitonic_merge64(cs, ci, lane);
+    if (lane >= 32) {
+      cs = kNegInf;
+      ci = kIdNone32;
+    }
+  }
+  if (lane < 32) w_s[wid][lane] = cs;
+  __syncthreads();
+  if (wid == 0) {
+    float s = lane < 32 ? w_s[0][lane] : kNegInf;
+    int id = lane;
+    for (int v = 1; v < 4; ++v) {
+      if (lane >= 32) {
+        s = w_s[v][63 - lane];
+        id = 64 * v + lane;
+      }
+      bitonic_merge64(s, id, lane);
+    }
+    const float t32 = __shfl(s, 31, 64);
+    if (lane == 0)
+      seed_thr[q] = t32 == kNegInf ? kNegInf : t32 - kSeedMargin * (1.0f + fabsf(t32));
   }
 }
 
 // ----------------------------------------------------------------------------------------
-// merge stage 2: one wave per query. Merge the group lists -> approximate top-32, then
-// rescore each candidate exactly: fp32( sequential fp64 fma over k of fp16 row x fp32
-// normalised query ), sort by (exact score desc, row asc) and emit the top k.
+// canonical exact score of one stored row against a normalised fp32 query, by one wave:
+// lane l accumulates the 8-element chunks c = l, l+64, ... with fp64 fma in order, then a
+// xor butterfly (32..1) in fp64; lane 0's sum rounded to fp32. oracle/scan_ref.c
+// (orc_exact_score) restates this order bit for bit.
 // ----------------------------------------------------------------------------------------
 template <int D>
-__global__ __launch_bounds__(64) void merge2_kernel(const float* __restrict__ mid_s,
-                                                    const int* __restrict__ mid_i,
-                                                    int n_groups,
-                                                    const half8* __restrict__ corpus,
-                                                    const float* __restrict__ qn, int k,
-                                                    int64_t id_offset,
-                                                    float* __restrict__ out_s,
-                                                    int64_t* __restrict__ out_i) {
+__device__ __forceinline__ float exact_score_wave(const half8* __restrict__ corpus, int row,
+                                                  const float* __restrict__ qq, int lane) {
   constexpr int S = steps<D>();
-  const int b = blockIdx.x, lane = threadIdx.x;
-  float s = kNegInf;
-  int id = kIdNone32;
-  if (lane < 32) {
-    s = mid_s[(int64_t)b * kKS + lane];
-    id = mid_i[(int64_t)b * kKS + lane];
+  const int64_t t = row >> 4;
+  const int r = row & 15;
+  const half8* rp = corpus + t * (S * 64) + r;
+  double acc = 0.0;
+  for (int c = lane; c < D / 8; c += 64) {
+    const half8 h = rp[(c >> 2) * 64 + (c & 3) * 16];
+    const float4 qa = *reinterpret_cast<const float4*>(qq + 8 * c);
+    const float4 qb = *reinterpret_cast<const float4*>(qq + 8 * c + 4);
+    acc = fma((double)h[0], (double)qa.x, acc);
+    acc = fma((double)h[1], (double)qa.y, acc);
+    acc = fma((double)h[2], (double)qa.z, acc);
+    acc = fma((double)h[3], (double)qa.w, acc);
+    acc = fma((double)h[4], (double)qb.x, acc);
+    acc = fma((double)h[5], (double)qb.y, acc);
+    acc = fma((double)h[6], (double)qb.z, acc);
+    acc = fma((double)h[7], (double)qb.w, acc);
   }
-  for (int g = 1; g < n_groups; ++g) {
-    if (lane >= 32) {
-      s = mid_s[((int64_t)g * kQ + b) * kKS + (63 - lane)];
-      id = mid_i[((int64_t)g * kQ + b) * kKS + (63 - lane)];
-    }
-    bitonic_merge64(s, id, lane);
-  }
-  // exact rescoring of the approximate top-32
-  float es = kNegInf;
-  int eid = kIdNone32;
-  if (lane < 32 && s != kNegInf) {
-    const int64_t t = id >> 4;
-    const int r = id & 15;
-    const half8* row = corpus + t * (S * 64) + r;
-    const float* qq = qn + b * D;
-    double acc = 0.0;
-    for (int c = 0; c < D / 8; ++c) {
-      const half8 h = row[(c >> 2) * 64 + (c & 3) * 16];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc = fma((double)h[j], (double)qq[8 * c + j], acc);
+  for (int d = 32; d > 0; d >>= 1) acc = acc + __shfl_xor(acc, d, 64);
+  return (float)__shfl(acc, 0, 64);
+}
+
+// ----------------------------------------------------------------------------------------
+// select: one 256-thread workgroup per query merges the n_lists sorted per-wave top-32
+// lists (approximate MFMA scores) into the exact top-k.
+//  1. top-32 of the list HEADS (each wave sorts 64-head columns, merges into its top-32).
+//     Any entry of a list whose head is not among the 32 best heads is beaten by those 32
+//     heads, so the global top-32 lies inside the 32 selected lists.
+//  2. each wave merges 8 of the selected lists (prefetched) -> wave 0 merges the 4 results.
+//  3. exact rescoring of the 32 candidates (exact_score_wave), 8 per wave.
+//  4. sort by (exact score desc, row asc), emit k.
+// ----------------------------------------------------------------------------------------
+template <int D>
+__global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ part_s,
+                                                     const int* __restrict__ part_i,
+                                                     int n_lists,
+                                                     const half8* __restrict__ corpus,
+                                                     const float* __restrict__ qn, int k,
+                                                     int64_t id_offset,
+                                                     float* __restrict__ out_s,
+                                                     int64_t* __restrict__ out_i) {
+  __shared__ float w_s[4][32];
+  __shared__ int64_t w_k[4][32];
+  __shared__ int sel[32];
+  __shared__ float c_s[4][32];
+  __shared__ int c_i[4][32];
+  __shared__ float e_s[32];
+  __shared__ int e_i[32];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  auto at = [&](int l, int pos) { return ((int64_t)l * kQ + b) * kKS + pos; };
+
+  // ---- 1. top-32 heads; key = row * 4096 + list (rows unique => row order preserved)
+  constexpr int kCols = kMaxLists / 256;
+  float hs[kCols];
+  int64_t hk[kCols];
+#pragma unroll
+  for (int j = 0; j < kCols; ++j) {
+    const int l = (j * 4 + wid) * 64 + lane;
+    hs[j] = kNegInf;
+    hk[j] = INT64_MAX;
+    if (l < n_lists) {
+      const float s = part_s[at(l, 0)];
+      if (s != kNegInf) {
+        hs[j] = s;
+        hk[j] = (int64_t)part_i[at(l, 0)] * 4096 + l;
+      }
     }
-    es = (float)acc;
-    eid = id;
   }
-  bitonic_sort64(es, eid, lane);
-  if (lane < k) {
-    const bool ok = es != kNegInf;
-    out_s[(int64_t)b * k + lane] = es;
-    out_i[(int64_t)b * k + lane] = ok ? (int64_t)eid + id_offset : (int64_t)-1;
+  float cs = kNegInf;
+  int64_t ck = INT64_MAX;
+#pragma unroll
+  for (int j = 0; j < kCols; ++j) {
+    if (!__ballot(hs[j] != kNegInf)) continue;   // wave-uniform: empty column
+    float s = hs[j];
+    int64_t key = hk[j];
+    bitonic_sort64(s, key, lane);
+    const float rs = __shfl(s, 63 - lane, 64);
+    const int64_t rk = (int64_t)(((uint64_t)(uint32_t)__shfl((int)(key >> 32), 63 - lane, 64) << 32) |
+                                 (uint32_t)__shfl((int)key, 63 - lane, 64));
+    if (lane >= 32) {
+      cs = rs;
+      ck = rk;
+    }
+    bitonic_merge64(cs, ck, lane);
+    if (lane >= 32) {
+      cs = kNegInf;
+      ck = INT64_MAX;
+    }
+  }
+  if (lane < 32) {
+    w_s[wid][lane] = cs;
+    w_k[wid][lane] = ck;
+  }
+  __syncthreads();
+  if (wid == 0) {
+    float s = lane < 32 ? w_s[0][lane] : kNegInf;
+    int64_t key = lane < 32 ? w_k[0][lane] : INT64_MAX;
+    for (int v = 1; v < 4; ++v) {
+      if (lane >= 32) {
+        s = w_s[v][63 - lane];
+        key = w_k[v][63 - lane];
+      }
+      bitonic_merge64(s, key, lane);
+    }
+    if (lane < 32) sel[lane] = (s != kNegInf) ? (int)(key & 4095) : -1;
+  }
+  __syncthreads();
+
+  // ---- 2. merge the selected lists: wave w takes lists sel[8w .. 8w+7]
+  {
+    float ls[8];
+    int li[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int l = sel[wid * 8 + j];
+      const int pos = j == 0 ? lane : 63 - lane;   // lanes 32..63 hold lists reversed
+      const bool use = (j == 0) ? lane < 32 : lane >= 32;
+      ls[j] = kNegInf;
+      li[j] = kIdNone32;
+      if (l >= 0 && use && pos < kKS) {
+        ls[j] = part_s[at(l, pos)];
+        li[j] = part_i[at(l, pos)];
+      }
+    }
+    float s = ls[0];
+    int id = li[0];
+#pragma unroll
+    for (int j = 1; j < 8; ++j) {
+      if (lane >= 32) {
+        s = ls[j];
+        id = li[j];
+      }
+      bitonic_merge64(s, id, lane);
+    }
+    if (lane < 32) {
+      c_s[wid][lane] = s;
+      c_i[wid][lane] = id;
+    }
+  }
+  __syncthreads();
+  if (wid == 0) {
+    float s = lane < 32 ? c_s[0][lane] : kNegInf;
+    int id = lane < 32 ? c_i[0][lane] : kIdNone32;
+    for (int v = 1; v < 4; ++v) {
+      if (lane >= 32) {
+        s = c_s[v][63 - lane];
+        id = c_i[v][63 - lane];
+      }
+      bitonic_merge64(s, id, lane);
+    }
+    if (lane < 32) {
+      c_s[0][lane] = s;
+      c_i[0][lane] = id;
+    }
+  }
+  __syncthreads();
+
+  // ---- 3. exact rescoring, 8 candidates per wave
+  const float* qq = qn + b * D;
+  for (int j = 0; j < 8; ++j) {
+    const int c = wid * 8 + j;
+    const float as = c_s[0][c];
+    const int row = c_i[0][c];
+    float es = kNegInf;
+    if (as != kNegInf) es = exact_score_wave<D>(corpus, row, qq, lane);
+    if (lane == 0) {
+      e_s[c] = es;
+      e_i[c] = as != kNegInf ? row : kIdNone32;
+    }
+  }
+  __syncthreads();
+
+  // ---- 4. final order by exact score
+  if (wid == 0) {
+    float s = lane < 32 ? e_s[lane] : kNegInf;
+    int id = lane < 32 ? e_i[lane] : kIdNone32;
+    bitonic_sort64(s, id, lane);
+    if (lane < k) {
+      const bool ok = s != kNegInf;
+      out_s[(int64_t)b * k + lane] = s;
+      out_i[(int64_t)b * k + lane] = ok ? (int64_t)id + id_offset : (int64_t)-1;
+    }
   }
 }
 

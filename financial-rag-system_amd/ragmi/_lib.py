@@ -61,6 +61,8 @@ INDEX_API = {
     "rag_index_export_tags": (ctypes.c_int, [c_vp, ctypes.c_int64, ctypes.c_int64, c_u32p]),
     "rag_merge_topk": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                       c_vp, c_vp, c_vp]),
+    "rag_bench_scan": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                      ctypes.POINTER(ctypes.c_double)]),
     "rag_profile_enable": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "rag_profile_scan_ms": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_double), c_i64p]),
 }

@@ -166,6 +166,15 @@ class FlatIndex:
     def profile(self, enable: bool) -> None:
         check(self._L.rag_profile_enable(self._h, int(bool(enable))))
 
+    def bench_scan(self, queries: torch.Tensor, variant: int, reps: int = 10) -> float:
+        """Diagnostic: avg device ms per launch of scan variant `variant` (rag_bench_scan)."""
+        q = _as_dev(queries, torch.float32, self.device)
+        ms = ctypes.c_double()
+        torch.cuda.synchronize(self.device)
+        check(self._L.rag_bench_scan(self._h, q.data_ptr(), q.shape[0], int(variant),
+                                     int(reps), ctypes.byref(ms)))
+        return float(ms.value)
+
     def profile_scan_ms(self) -> tuple[float, int]:
         tot = ctypes.c_double()
         n = ctypes.c_int64()

@@ -31,7 +31,7 @@
  *     rounded to fp16 (RNE) and stored at its row slot; an existing slot is overwritten
  *     (md5 point ids make re-ingest idempotent, ingest.py:151-154).
  *   - search: the query is normalised the same way; score(row) = fp32(sum_k fp64(c_k)*fp64(q_k))
- *     accumulated sequentially in k with fp64 fma; result = top-k rows by
+ *     with the canonical fp64 summation order (oracle/scan_ref.c); result = top-k rows by
  *     (score desc, row asc), optionally restricted per query to rows whose tag satisfies
  *     (tag & tag_mask) == tag_value (the payload `must` filter, main.py:218-236).
  *     Missing results (fewer than k matching rows) are reported as id -1, score -inf.
@@ -118,6 +118,13 @@ int rag_merge_topk(const float* in_scores_dev, const int64_t* in_ids_dev, int n_
  * event recording around the scan kernel (adds two event records per pass). */
 int rag_profile_enable(rag_index_t* index, int enable);
 int rag_profile_scan_ms(rag_index_t* index, double* total_ms, int64_t* launches);
+
+/* Diagnostic: average device ms of `reps` launches of scan variant `variant` on the current
+ * corpus with the first min(B,32) queries (dim 384 only). Variants: 0 production (seeded
+ * thresholds), 1 unseeded, 2 contiguous per-wave tile ranges, 3 MFMA without top-k,
+ * 4 loads only, 5 without non-temporal loads, 6 without the load sched-barrier. */
+int rag_bench_scan(rag_index_t* index, const float* queries_dev, int B, int variant, int reps,
+                   double* avg_ms);
 
 #ifdef __cplusplus
 }

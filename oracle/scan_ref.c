@@ -23,7 +23,8 @@
  *   norm    : sqrt(sumsq) (fp64, correctly rounded)
  *   y_k     : fp32(fp64(x_k) / norm), 0 if norm == 0
  *   stored  : fp16_rne(y_k)
- *   score   : fp32( sequential fp64 fma over k of fp64(c16_k) * fp64(qn_k) )
+ *   score   : fp32( canonical fp64 sum of fp64(c16_k) * fp64(qn_k) ): 64 lane partials
+ *             (chunks of 8, fp64 fma in order) + xor-butterfly, exactly as for sumsq
  *   order   : score desc, row asc; rows with (tag & mask) != value are excluded when filtering.
  */
 #include <math.h>
@@ -121,10 +122,24 @@ ORC_API void orc_encode_rows(const float* x, int64_t n, int D, uint16_t* out16) 
   free(y);
 }
 
+/* Canonical exact score: 64 lane partials (lane l: chunks c = l, l+64, ... of 8 elements,
+ * fp64 fma in order), xor-butterfly d = 32..1, v[0] rounded to fp32 — the order of the HIP
+ * select kernel's exact_score_wave. */
 ORC_API float orc_exact_score(const uint16_t* c16, const float* qn, int D) {
-  double acc = 0.0;
-  for (int k = 0; k < D; ++k) acc = fma((double)orc_f16_to_f32(c16[k]), (double)qn[k], acc);
-  return (float)acc;
+  double v[64];
+  for (int l = 0; l < 64; ++l) {
+    double acc = 0.0;
+    for (int c = l; c < D / 8; c += 64)
+      for (int j = 0; j < 8; ++j)
+        acc = fma((double)orc_f16_to_f32(c16[8 * c + j]), (double)qn[8 * c + j], acc);
+    v[l] = acc;
+  }
+  for (int d = 32; d > 0; d >>= 1) {
+    double w[64];
+    for (int i = 0; i < 64; ++i) w[i] = v[i] + v[i ^ d];
+    memcpy(v, w, sizeof(v));
+  }
+  return (float)v[0];
 }
 
 static int better(float as, int64_t ai, float bs, int64_t bi) {
