@@ -17,51 +17,91 @@ constexpr float kNegInf = -__builtin_inff();
 constexpr int kIdNone32 = 0x7fffffff;
 
 // Total order used everywhere for ranking: score descending, then id ascending
-// ("sorted by (score desc, row id asc)").
+// ("sorted by (score desc, row id asc)"). Bitwise ops, no short-circuit: the
+// comparator must compile to v_cmp + mask logic, not exec-masked branches.
 template <typename IdT>
 __device__ __forceinline__ bool better(float as, IdT ai, float bs, IdT bi) {
-  return (as > bs) || (as == bs && ai < bi);
+  return (as > bs) | ((as == bs) & (ai < bi));
 }
 
-template <typename IdT>
-__device__ __forceinline__ IdT shfl_xor_id(IdT v, int mask) {
-  if constexpr (sizeof(IdT) == 8) {
-    int lo = __shfl_xor((int)(uint32_t)((uint64_t)v), mask, 64);
-    int hi = __shfl_xor((int)(uint32_t)((uint64_t)v >> 32), mask, 64);
-    return (IdT)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+// Lane exchange v[lane ^ J] for a compile-time J. J = 1, 2 (quad_perm), 4, 8 (two DPP mirror
+// steps: i^4 = half_mirror(i^3), i^8 = mirror(half_mirror)) stay in the VALU; 16 and 32 use
+// ds_bpermute.
+template <int J>
+__device__ __forceinline__ int xor_lane(int v) {
+  if constexpr (J == 1) {
+    return __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+  } else if constexpr (J == 2) {
+    return __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+  } else if constexpr (J == 4) {
+    const int t = __builtin_amdgcn_update_dpp(0, v, 0x1B, 0xF, 0xF, false);  // [3,2,1,0]
+    return __builtin_amdgcn_update_dpp(0, t, 0x141, 0xF, 0xF, false);        // row_half_mirror
+  } else if constexpr (J == 8) {
+    const int t = __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false); // row_half_mirror
+    return __builtin_amdgcn_update_dpp(0, t, 0x140, 0xF, 0xF, false);        // row_mirror
   } else {
-    return (IdT)__shfl_xor((int)v, mask, 64);
+    return __shfl_xor(v, J, 64);
   }
 }
 
-// One compare-exchange stage across lanes (lane, lane ^ j). `asc` = this lane's block is
+template <int J>
+__device__ __forceinline__ float xor_lane_f(float v) {
+  return __builtin_bit_cast(float, xor_lane<J>(__builtin_bit_cast(int, v)));
+}
+
+template <int J, typename IdT>
+__device__ __forceinline__ IdT xor_lane_id(IdT v) {
+  if constexpr (sizeof(IdT) == 8) {
+    const uint64_t u = (uint64_t)v;
+    const int lo = xor_lane<J>((int)(uint32_t)u);
+    const int hi = xor_lane<J>((int)(uint32_t)(u >> 32));
+    return (IdT)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+  } else {
+    return (IdT)xor_lane<J>((int)v);
+  }
+}
+
+// One compare-exchange stage across lanes (lane, lane ^ J). `asc` = this lane's block is
 // sorted best-first.
-template <typename IdT>
-__device__ __forceinline__ void cas_stage(float& s, IdT& id, int lane, int j, bool asc) {
-  const float os = __shfl_xor(s, j, 64);
-  const IdT oi = shfl_xor_id(id, j);
-  const bool lower = (lane & j) == 0;
-  const bool take = (asc == lower) ? better(os, oi, s, id) : better(s, id, os, oi);
+template <int J, typename IdT>
+__device__ __forceinline__ void cas_stage(float& s, IdT& id, int lane, bool asc) {
+  const float os = xor_lane_f<J>(s);
+  const IdT oi = xor_lane_id<J>(id);
+  const bool lower = (lane & J) == 0;
+  const bool ob = better(os, oi, s, id);
+  const bool sb = better(s, id, os, oi);
+  const bool take = (asc == lower) ? ob : sb;
   s = take ? os : s;
   id = take ? oi : id;
+}
+
+template <int K, int J, typename IdT>
+__device__ __forceinline__ void bitonic_steps(float& s, IdT& id, int lane) {
+  if constexpr (J > 0) {
+    cas_stage<J>(s, id, lane, K == 64 ? true : (lane & K) == 0);
+    bitonic_steps<K, J / 2>(s, id, lane);
+  }
+}
+
+template <int K, typename IdT>
+__device__ __forceinline__ void bitonic_sort_from(float& s, IdT& id, int lane) {
+  if constexpr (K <= 64) {
+    bitonic_steps<K, K / 2>(s, id, lane);
+    bitonic_sort_from<K * 2>(s, id, lane);
+  }
 }
 
 // Full bitonic sort of the 64 (score, id) pairs held one per lane; lane 0 ends best.
 template <typename IdT>
 __device__ __forceinline__ void bitonic_sort64(float& s, IdT& id, int lane) {
-#pragma unroll
-  for (int k = 2; k <= 64; k <<= 1) {
-#pragma unroll
-    for (int j = k >> 1; j > 0; j >>= 1) cas_stage(s, id, lane, j, (lane & k) == 0);
-  }
+  bitonic_sort_from<2>(s, id, lane);
 }
 
 // Bitonic merge: lanes 0..31 sorted best-first, lanes 32..63 sorted worst-first
 // -> all 64 sorted best-first.
 template <typename IdT>
 __device__ __forceinline__ void bitonic_merge64(float& s, IdT& id, int lane) {
-#pragma unroll
-  for (int j = 32; j > 0; j >>= 1) cas_stage(s, id, lane, j, true);
+  bitonic_steps<64, 32>(s, id, lane);
 }
 
 // Canonical L2 norm of a D-vector held in global memory, computed by one wave.

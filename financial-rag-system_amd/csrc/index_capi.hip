@@ -30,6 +30,8 @@ struct Workspace {
   float* seed = nullptr;      // [32] seed thresholds
   float* part_s = nullptr;
   int* part_i = nullptr;
+  float* heads_s = nullptr;   // [32][n_lists]
+  int* heads_i = nullptr;
   hipEvent_t done = nullptr;
 };
 
@@ -99,11 +101,10 @@ void launch_seed(rag_index* h, Workspace& w, hipStream_t st) {
   using namespace ragmi;
   const int n_tiles = (int)((h->count + 15) / 16);
   if (n_tiles == 0) return;   // the scan visits no tile; seeds are never read
-  const int n_sample = std::min(n_tiles, std::max(256, n_tiles / 128));
-  const int nsw = std::min(kMaxLists, (n_sample + 3) & ~3);
-  sample_kernel<D, FILTER><<<dim3(nsw / 4), dim3(256), 0, st>>>(
+  const int n_sample = std::min({n_tiles, std::max(256, n_tiles / 128), kMaxSample});
+  sample_kernel<D, FILTER><<<dim3((n_sample + 7) / 8), dim3(256), 0, st>>>(
       h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, n_tiles, n_sample, w.smax);
-  thresh_kernel<<<dim3(kQ), dim3(256), 0, st>>>(w.smax, nsw, w.seed);
+  thresh_kernel<<<dim3(kQ), dim3(256), 0, st>>>(w.smax, n_sample, w.seed);
 }
 
 template <int D>
@@ -128,18 +129,19 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
   if (filt)
     scan_kernel<D, true><<<dim3(grid), dim3(256), 0, st>>>(
         h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, (int)n_tiles, w.seed, w.part_s,
-        w.part_i);
+        w.part_i, w.heads_s, w.heads_i);
   else
     scan_kernel<D, false><<<dim3(grid), dim3(256), 0, st>>>(
         h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, (int)n_tiles, w.seed, w.part_s,
-        w.part_i);
+        w.part_i, w.heads_s, w.heads_i);
   if (h->prof) {
     RAG_HIP(hipEventRecord(pp.b, st));
     h->prof_pairs.push_back(pp);
   }
   const int n_lists = grid * kWavesPerWG;
-  select_kernel<D><<<dim3(Bq), dim3(256), 0, st>>>(w.part_s, w.part_i, n_lists, h->corpus,
-                                                   w.qn, k, id_offset, out_s, out_i);
+  select_kernel<D><<<dim3(Bq), dim3(256), 0, st>>>(w.part_s, w.part_i, w.heads_s, w.heads_i,
+                                                   n_lists, h->corpus, w.qn, k, id_offset,
+                                                   out_s, out_i);
   RAG_HIP(hipGetLastError());
   return RAG_OK;
 }
@@ -215,7 +217,7 @@ void launch_variant(rag_index* h, Workspace& w, int grid, hipStream_t st) {
   constexpr bool SB = V != 6;
   scan_kernel<D, false, MODE, STRIDED, NT, SB><<<dim3(grid), dim3(256), 0, st>>>(
       h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, n_tiles, V == 1 ? nullptr : w.seed,
-      w.part_s, w.part_i);
+      w.part_s, w.part_i, w.heads_s, w.heads_i);
 }
 
 template <int D>
@@ -294,6 +296,10 @@ int rag_index_create(int dim, int64_t capacity_rows, int device, rag_index_t** o
                   hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&w.filt), ragmi::kQ * 2 * 4) == hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&w.smax),
+                        (size_t)ragmi::kMaxSample * ragmi::kQ * 4) == hipSuccess &&
+              hipMalloc(reinterpret_cast<void**>(&w.heads_s),
+                        (size_t)ragmi::kMaxLists * ragmi::kQ * 4) == hipSuccess &&
+              hipMalloc(reinterpret_cast<void**>(&w.heads_i),
                         (size_t)ragmi::kMaxLists * ragmi::kQ * 4) == hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&w.seed), ragmi::kQ * 4) == hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&w.part_s),
@@ -320,6 +326,8 @@ int rag_index_destroy(rag_index_t* h) {
     if (w.qfrag) (void)hipFree(w.qfrag);
     if (w.filt) (void)hipFree(w.filt);
     if (w.smax) (void)hipFree(w.smax);
+    if (w.heads_s) (void)hipFree(w.heads_s);
+    if (w.heads_i) (void)hipFree(w.heads_i);
     if (w.seed) (void)hipFree(w.seed);
     if (w.part_s) (void)hipFree(w.part_s);
     if (w.part_i) (void)hipFree(w.part_i);

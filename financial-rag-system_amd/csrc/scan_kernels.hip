@@ -179,7 +179,8 @@ template <int D, bool FILTER, int MODE = 0, bool STRIDED = true, bool NT = true,
 __global__ __launch_bounds__(256, 2) void scan_kernel(
     const half8* __restrict__ corpus, const uint32_t* __restrict__ tags,
     const uint32_t* __restrict__ filt, const half8* __restrict__ qfrag, int n_rows, int n_tiles,
-    const float* __restrict__ seed_thr, float* __restrict__ part_s, int* __restrict__ part_i) {
+    const float* __restrict__ seed_thr, float* __restrict__ part_s, int* __restrict__ part_i,
+    float* __restrict__ heads_s, int* __restrict__ heads_i) {
   constexpr int S = steps<D>();
   __shared__ int lds[kWavesPerWG * kLdsPerWave];
   const int lane = threadIdx.x & 63;
@@ -358,6 +359,11 @@ __global__ __launch_bounds__(256, 2) void scan_kernel(
     ps[lane + 64 * j] = w.keep_s[lane + 64 * j];
     pi[lane + 64 * j] = w.keep_i[lane + 64 * j];
   }
+  // compact list heads [query][wave] for the select kernel's first step
+  if (lane < kQ) {
+    heads_s[lane * nw + gw] = w.keep_s[lane * kKS];
+    heads_i[lane * nw + gw] = w.keep_i[lane * kKS];
+  }
 }
 
 // ----------------------------------------------------------------------------------------
@@ -377,7 +383,22 @@ __global__ __launch_bounds__(256) void sample_kernel(const half8* __restrict__ c
   constexpr int S = steps<D>();
   const int lane = threadIdx.x & 63;
   const int w = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int nw = gridDim.x * 4;
+  // two sample tiles per wave (j = 2w, 2w+1), all loads in flight at once
+  const int j0 = 2 * w;
+  if (j0 >= n_sample) return;
+  const bool two = j0 + 1 < n_sample;
+  const int t0 = (int)(((int64_t)j0 * n_tiles) / n_sample);
+  const int t1 = two ? (int)(((int64_t)(j0 + 1) * n_tiles) / n_sample) : t0;
+  const half8* p0 = corpus + (int64_t)t0 * (S * 64) + lane;
+  const half8* p1 = corpus + (int64_t)t1 * (S * 64) + lane;
+  half8 a0[S], a1[S], b0[S], b1[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    a0[s] = __builtin_nontemporal_load(p0 + s * 64);
+    a1[s] = __builtin_nontemporal_load(p1 + s * 64);
+    b0[s] = qfrag[s * 64 + lane];
+    b1[s] = qfrag[(S + s) * 64 + lane];
+  }
   uint32_t fm0 = 0, fv0 = 0, fm1 = 0, fv1 = 0;
   if constexpr (FILTER) {
     fm0 = filt[2 * (lane & 15)];
@@ -385,22 +406,22 @@ __global__ __launch_bounds__(256) void sample_kernel(const half8* __restrict__ c
     fm1 = filt[2 * (16 + (lane & 15))];
     fv1 = filt[2 * (16 + (lane & 15)) + 1];
   }
-  float m0 = kNegInf, m1 = kNegInf;
-  const int rsub = 4 * (lane >> 4);
-  for (int j = w; j < n_sample; j += nw) {
-    const int t = (int)(((int64_t)j * n_tiles) / n_sample);
-    const half8* p = corpus + (int64_t)t * (S * 64) + lane;
+  float mx[2][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const half8(&a)[S] = u == 0 ? a0 : a1;
+    const int t = u == 0 ? t0 : t1;
     floatx4 acc0 = {0.f, 0.f, 0.f, 0.f};
     floatx4 acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      const half8 a = __builtin_nontemporal_load(p + s * 64);
-      acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, qfrag[s * 64 + lane], acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, qfrag[(S + s) * 64 + lane], acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[s], b0[s], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[s], b1[s], acc1, 0, 0, 0);
     }
-    const int rbase = t * kTileRows + rsub;
+    const int rbase = t * kTileRows + 4 * (lane >> 4);
     uint4 tg = {0u, 0u, 0u, 0u};
     if constexpr (FILTER) tg = *reinterpret_cast<const uint4*>(tags + rbase);
+    float m0 = kNegInf, m1 = kNegInf;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const bool ok = (rbase + r) < n_rows;
@@ -410,18 +431,24 @@ __global__ __launch_bounds__(256) void sample_kernel(const half8* __restrict__ c
         ok0 = ok0 && ((tr & fm0) == fv0);
         ok1 = ok1 && ((tr & fm1) == fv1);
       }
-      if (ok0) m0 = fmaxf(m0, acc0[r]);
-      if (ok1) m1 = fmaxf(m1, acc1[r]);
+      m0 = ok0 ? fmaxf(m0, acc0[r]) : m0;
+      m1 = ok1 ? fmaxf(m1, acc1[r]) : m1;
     }
+    // lanes l, l^16, l^32, l^48 hold the same queries
+    m0 = fmaxf(m0, __shfl_xor(m0, 16, 64));
+    m0 = fmaxf(m0, __shfl_xor(m0, 32, 64));
+    m1 = fmaxf(m1, __shfl_xor(m1, 16, 64));
+    m1 = fmaxf(m1, __shfl_xor(m1, 32, 64));
+    mx[u][0] = m0;
+    mx[u][1] = m1;
   }
-  // lanes l, l^16, l^32, l^48 hold the same queries
-  m0 = fmaxf(m0, __shfl_xor(m0, 16, 64));
-  m0 = fmaxf(m0, __shfl_xor(m0, 32, 64));
-  m1 = fmaxf(m1, __shfl_xor(m1, 16, 64));
-  m1 = fmaxf(m1, __shfl_xor(m1, 32, 64));
   if (lane < 16) {
-    smax[(int64_t)w * kQ + lane] = m0;
-    smax[(int64_t)w * kQ + 16 + lane] = m1;
+    smax[(int64_t)lane * n_sample + j0] = mx[0][0];
+    smax[(int64_t)(16 + lane) * n_sample + j0] = mx[0][1];
+    if (two) {
+      smax[(int64_t)lane * n_sample + j0 + 1] = mx[1][0];
+      smax[(int64_t)(16 + lane) * n_sample + j0 + 1] = mx[1][1];
+    }
   }
 }
 
@@ -431,44 +458,36 @@ __global__ __launch_bounds__(256) void sample_kernel(const half8* __restrict__ c
 // not exceed an exact score it stands for: the bound is lowered by kSeedMargin (relative +
 // absolute) to cover the MFMA-vs-exact difference (fp16 query rounding, fp32 accumulation).
 constexpr float kSeedMargin = 1e-3f;
+constexpr int kMaxSample = 4096;
+constexpr int kCandCap = 256;   // select: compacted heads at/above the lane-max threshold
 
 __global__ __launch_bounds__(256) void thresh_kernel(const float* __restrict__ smax,
-                                                     int n_waves, float* __restrict__ seed_thr) {
+                                                     int n_sample, float* __restrict__ seed_thr) {
+  // Each lane takes the max over its group of sample tiles (disjoint groups), each wave
+  // sorts its 64 group maxima, wave 0 merges the four top-32s: the 32nd best of the group
+  // maxima is attained by 32 distinct rows, so it is a valid lower bound.
   __shared__ float w_s[4][32];
   const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  constexpr int kCols = kMaxLists / 256;
-  float cs = kNegInf;
-  int ci = kIdNone32;
+  const float* v = smax + (int64_t)q * n_sample;
+  float m = kNegInf;
+  float x[kMaxSample / 256];
 #pragma unroll
-  for (int j = 0; j < kCols; ++j) {
-    const int w = (j * 4 + wid) * 64 + lane;
-    float s = w < n_waves ? smax[(int64_t)w * kQ + q] : kNegInf;
-    if (!__ballot(s != kNegInf)) continue;
-    int id = w;
-    bitonic_sort64(s, id, lane);
-    const float rs = __shfl(s, 63 - lane, 64);
-    const int ri = __shfl(id, 63 - lane, 64);
-    if (lane >= 32) {
-      cs = rs;
-      ci = ri;
-    }
-    bitonic_merge64(cs, ci, lane);
-    if (lane >= 32) {
-      cs = kNegInf;
-      ci = kIdNone32;
-    }
-  }
-  if (lane < 32) w_s[wid][lane] = cs;
+  for (int i = 0; i < kMaxSample / 256; ++i) x[i] = v[min(tid + 256 * i, n_sample - 1)];
+#pragma unroll
+  for (int i = 0; i < kMaxSample / 256; ++i) m = (tid + 256 * i < n_sample) ? fmaxf(m, x[i]) : m;
+  int id = tid;
+  bitonic_sort64(m, id, lane);
+  if (lane < 32) w_s[wid][lane] = m;
   __syncthreads();
   if (wid == 0) {
     float s = lane < 32 ? w_s[0][lane] : kNegInf;
-    int id = lane;
-    for (int v = 1; v < 4; ++v) {
+    int i2 = lane;
+    for (int w = 1; w < 4; ++w) {
       if (lane >= 32) {
-        s = w_s[v][63 - lane];
-        id = 64 * v + lane;
+        s = w_s[w][63 - lane];
+        i2 = 64 * w + lane;
       }
-      bitonic_merge64(s, id, lane);
+      bitonic_merge64(s, i2, lane);
     }
     const float t32 = __shfl(s, 31, 64);
     if (lane == 0)
@@ -482,38 +501,57 @@ __global__ __launch_bounds__(256) void thresh_kernel(const float* __restrict__ s
 // xor butterfly (32..1) in fp64; lane 0's sum rounded to fp32. oracle/scan_ref.c
 // (orc_exact_score) restates this order bit for bit.
 // ----------------------------------------------------------------------------------------
-template <int D>
-__device__ __forceinline__ float exact_score_wave(const half8* __restrict__ corpus, int row,
-                                                  const float* __restrict__ qq, int lane) {
+template <int D, int NC>
+__device__ __forceinline__ void exact_scores_wave(const half8* __restrict__ corpus,
+                                                  const int (&rows)[NC],
+                                                  const float* __restrict__ qq, int lane,
+                                                  float (&out)[NC]) {
+  // NC candidates at once: every row chunk is loaded before any arithmetic, so the wave pays
+  // one memory round trip instead of NC dependent ones. rows[i] < 0 => out[i] = -inf.
   constexpr int S = steps<D>();
-  const int64_t t = row >> 4;
-  const int r = row & 15;
-  const half8* rp = corpus + t * (S * 64) + r;
-  double acc = 0.0;
+  double acc[NC];
+#pragma unroll
+  for (int i = 0; i < NC; ++i) acc[i] = 0.0;
   for (int c = lane; c < D / 8; c += 64) {
-    const half8 h = rp[(c >> 2) * 64 + (c & 3) * 16];
+    half8 h[NC];
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+      const int row = rows[i] < 0 ? 0 : rows[i];
+      h[i] = corpus[(int64_t)(row >> 4) * (S * 64) + (c >> 2) * 64 + (c & 3) * 16 + (row & 15)];
+    }
     const float4 qa = *reinterpret_cast<const float4*>(qq + 8 * c);
     const float4 qb = *reinterpret_cast<const float4*>(qq + 8 * c + 4);
-    acc = fma((double)h[0], (double)qa.x, acc);
-    acc = fma((double)h[1], (double)qa.y, acc);
-    acc = fma((double)h[2], (double)qa.z, acc);
-    acc = fma((double)h[3], (double)qa.w, acc);
-    acc = fma((double)h[4], (double)qb.x, acc);
-    acc = fma((double)h[5], (double)qb.y, acc);
-    acc = fma((double)h[6], (double)qb.z, acc);
-    acc = fma((double)h[7], (double)qb.w, acc);
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+      double x = acc[i];
+      x = fma((double)h[i][0], (double)qa.x, x);
+      x = fma((double)h[i][1], (double)qa.y, x);
+      x = fma((double)h[i][2], (double)qa.z, x);
+      x = fma((double)h[i][3], (double)qa.w, x);
+      x = fma((double)h[i][4], (double)qb.x, x);
+      x = fma((double)h[i][5], (double)qb.y, x);
+      x = fma((double)h[i][6], (double)qb.z, x);
+      x = fma((double)h[i][7], (double)qb.w, x);
+      acc[i] = x;
+    }
   }
 #pragma unroll
-  for (int d = 32; d > 0; d >>= 1) acc = acc + __shfl_xor(acc, d, 64);
-  return (float)__shfl(acc, 0, 64);
+  for (int d = 32; d > 0; d >>= 1) {
+#pragma unroll
+    for (int i = 0; i < NC; ++i) acc[i] = acc[i] + __shfl_xor(acc[i], d, 64);
+  }
+#pragma unroll
+  for (int i = 0; i < NC; ++i)
+    out[i] = rows[i] < 0 ? kNegInf : (float)__shfl(acc[i], 0, 64);
 }
 
 // ----------------------------------------------------------------------------------------
 // select: one 256-thread workgroup per query merges the n_lists sorted per-wave top-32
 // lists (approximate MFMA scores) into the exact top-k.
-//  1. top-32 of the list HEADS (each wave sorts 64-head columns, merges into its top-32).
-//     Any entry of a list whose head is not among the 32 best heads is beaten by those 32
-//     heads, so the global top-32 lies inside the 32 selected lists.
+//  1. top-32 of the list HEADS. Any entry of a list whose head is not among the 32 best
+//     heads is beaten by those 32 heads, so the global top-32 lies inside the 32 selected
+//     lists. (Threshold from lane maxima -> compaction -> small sort; exact column-sort
+//     fallback when ties push more than kCandCap heads past the threshold.)
 //  2. each wave merges 8 of the selected lists (prefetched) -> wave 0 merges the 4 results.
 //  3. exact rescoring of the 32 candidates (exact_score_wave), 8 per wave.
 //  4. sort by (exact score desc, row asc), emit k.
@@ -521,6 +559,8 @@ __device__ __forceinline__ float exact_score_wave(const half8* __restrict__ corp
 template <int D>
 __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ part_s,
                                                      const int* __restrict__ part_i,
+                                                     const float* __restrict__ heads_s,
+                                                     const int* __restrict__ heads_i,
                                                      int n_lists,
                                                      const half8* __restrict__ corpus,
                                                      const float* __restrict__ qn, int k,
@@ -528,8 +568,12 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
                                                      float* __restrict__ out_s,
                                                      int64_t* __restrict__ out_i) {
   __shared__ float w_s[4][32];
-  __shared__ int64_t w_k[4][32];
+  __shared__ int w_i[4][32];
   __shared__ int sel[32];
+  __shared__ float cand_s[kCandCap];
+  __shared__ int cand_i[kCandCap];
+  __shared__ int n_cand;
+  __shared__ float head_t;
   __shared__ float c_s[4][32];
   __shared__ int c_i[4][32];
   __shared__ float e_s[32];
@@ -537,60 +581,120 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   auto at = [&](int l, int pos) { return ((int64_t)l * kQ + b) * kKS + pos; };
 
-  // ---- 1. top-32 heads; key = row * 4096 + list (rows unique => row order preserved)
+  // ---- 1. the 32 best list heads (a list = one scan wave; under the interleaved tile order
+  //      the wave of row r is (r >> 4) % n_lists, so the row alone identifies the list).
   constexpr int kCols = kMaxLists / 256;
   float hs[kCols];
-  int64_t hk[kCols];
+  int hr[kCols];
+  // unconditional (clamped) loads, selects afterwards: a load under a data-dependent branch
+  // makes hipcc wait vmcnt(0) per element (one round trip each)
+#pragma unroll
+  for (int j = 0; j < kCols; ++j) {
+    const int l = min((j * 4 + wid) * 64 + lane, n_lists - 1);
+    hs[j] = heads_s[(int64_t)b * n_lists + l];
+    hr[j] = heads_i[(int64_t)b * n_lists + l];
+  }
+  float lmax = kNegInf;
 #pragma unroll
   for (int j = 0; j < kCols; ++j) {
     const int l = (j * 4 + wid) * 64 + lane;
-    hs[j] = kNegInf;
-    hk[j] = INT64_MAX;
-    if (l < n_lists) {
-      const float s = part_s[at(l, 0)];
-      if (s != kNegInf) {
-        hs[j] = s;
-        hk[j] = (int64_t)part_i[at(l, 0)] * 4096 + l;
+    const bool ok = l < n_lists && hs[j] != kNegInf;
+    hs[j] = ok ? hs[j] : kNegInf;
+    hr[j] = ok ? hr[j] : kIdNone32;
+    lmax = fmaxf(lmax, hs[j]);
+  }
+  // 1a. T = 32nd largest lane maximum (the maxima of 32 distinct lanes are 32 distinct heads,
+  //     so at least 32 heads score >= T and every top-32 head scores >= T)
+  {
+    float m = lmax;
+    int id = tid;
+    bitonic_sort64(m, id, lane);
+    if (lane < 32) w_s[wid][lane] = m;
+  }
+  if (tid == 0) n_cand = 0;
+  __syncthreads();
+  if (wid == 0) {
+    float m = lane < 32 ? w_s[0][lane] : kNegInf;
+    int id = lane;
+    for (int v = 1; v < 4; ++v) {
+      if (lane >= 32) {
+        m = w_s[v][63 - lane];
+        id = 64 * v + lane;
+      }
+      bitonic_merge64(m, id, lane);
+    }
+    const float t32 = __shfl(m, 31, 64);
+    if (lane == 0) head_t = t32;
+  }
+  __syncthreads();
+  // 1b. compact the heads scoring >= T (typically ~35) into LDS
+  {
+    const float T = head_t;
+#pragma unroll
+    for (int j = 0; j < kCols; ++j) {
+      if (hs[j] != kNegInf && hs[j] >= T) {
+        const int p = atomicAdd(&n_cand, 1);
+        if (p < kCandCap) {
+          cand_s[p] = hs[j];
+          cand_i[p] = hr[j];
+        }
       }
     }
   }
-  float cs = kNegInf;
-  int64_t ck = INT64_MAX;
+  __syncthreads();
+  const int nc = n_cand;
+  if (nc <= kCandCap) {
+    // 1c. top-32 of the compacted heads: each wave sorts 64 of them, wave 0 merges
+    float m = kNegInf;
+    int id = kIdNone32;
+    if (64 * wid + lane < nc) {
+      m = cand_s[64 * wid + lane];
+      id = cand_i[64 * wid + lane];
+    }
+    if (64 * wid < nc) bitonic_sort64(m, id, lane);
+    if (lane < 32) {
+      w_s[wid][lane] = m;
+      w_i[wid][lane] = id;
+    }
+  } else {
+    // 1c'. adversarial ties (more than kCandCap heads at the threshold): exact column sort
+    float cs = kNegInf;
+    int ci = kIdNone32;
 #pragma unroll
-  for (int j = 0; j < kCols; ++j) {
-    if (!__ballot(hs[j] != kNegInf)) continue;   // wave-uniform: empty column
-    float s = hs[j];
-    int64_t key = hk[j];
-    bitonic_sort64(s, key, lane);
-    const float rs = __shfl(s, 63 - lane, 64);
-    const int64_t rk = (int64_t)(((uint64_t)(uint32_t)__shfl((int)(key >> 32), 63 - lane, 64) << 32) |
-                                 (uint32_t)__shfl((int)key, 63 - lane, 64));
-    if (lane >= 32) {
-      cs = rs;
-      ck = rk;
+    for (int j = 0; j < kCols; ++j) {
+      if (!__ballot(hs[j] != kNegInf)) continue;   // wave-uniform: empty column
+      float x = hs[j];
+      int id = hr[j];
+      bitonic_sort64(x, id, lane);
+      const float rx = __shfl(x, 63 - lane, 64);
+      const int ri = __shfl(id, 63 - lane, 64);
+      if (lane >= 32) {
+        cs = rx;
+        ci = ri;
+      }
+      bitonic_merge64(cs, ci, lane);
+      if (lane >= 32) {
+        cs = kNegInf;
+        ci = kIdNone32;
+      }
     }
-    bitonic_merge64(cs, ck, lane);
-    if (lane >= 32) {
-      cs = kNegInf;
-      ck = INT64_MAX;
+    if (lane < 32) {
+      w_s[wid][lane] = cs;
+      w_i[wid][lane] = ci;
     }
-  }
-  if (lane < 32) {
-    w_s[wid][lane] = cs;
-    w_k[wid][lane] = ck;
   }
   __syncthreads();
   if (wid == 0) {
-    float s = lane < 32 ? w_s[0][lane] : kNegInf;
-    int64_t key = lane < 32 ? w_k[0][lane] : INT64_MAX;
+    float x = lane < 32 ? w_s[0][lane] : kNegInf;
+    int id = lane < 32 ? w_i[0][lane] : kIdNone32;
     for (int v = 1; v < 4; ++v) {
       if (lane >= 32) {
-        s = w_s[v][63 - lane];
-        key = w_k[v][63 - lane];
+        x = w_s[v][63 - lane];
+        id = w_i[v][63 - lane];
       }
-      bitonic_merge64(s, key, lane);
+      bitonic_merge64(x, id, lane);
     }
-    if (lane < 32) sel[lane] = (s != kNegInf) ? (int)(key & 4095) : -1;
+    if (lane < 32) sel[lane] = (x != kNegInf) ? (int)(((uint32_t)id >> 4) % (uint32_t)n_lists) : -1;
   }
   __syncthreads();
 
@@ -601,14 +705,16 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int l = sel[wid * 8 + j];
-      const int pos = j == 0 ? lane : 63 - lane;   // lanes 32..63 hold lists reversed
-      const bool use = (j == 0) ? lane < 32 : lane >= 32;
-      ls[j] = kNegInf;
-      li[j] = kIdNone32;
-      if (l >= 0 && use && pos < kKS) {
-        ls[j] = part_s[at(l, pos)];
-        li[j] = part_i[at(l, pos)];
-      }
+      const int pos = (j == 0 ? lane : 63 - lane) & (kKS - 1);  // lanes 32..63: reversed
+      const int64_t off = at(l < 0 ? 0 : l, pos);
+      ls[j] = part_s[off];
+      li[j] = part_i[off];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const bool use = sel[wid * 8 + j] >= 0 && ((j == 0) ? lane < 32 : lane >= 32);
+      ls[j] = use ? ls[j] : kNegInf;
+      li[j] = use ? li[j] : kIdNone32;
     }
     float s = ls[0];
     int id = li[0];
@@ -643,17 +749,23 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
   }
   __syncthreads();
 
-  // ---- 3. exact rescoring, 8 candidates per wave
-  const float* qq = qn + b * D;
-  for (int j = 0; j < 8; ++j) {
-    const int c = wid * 8 + j;
-    const float as = c_s[0][c];
-    const int row = c_i[0][c];
-    float es = kNegInf;
-    if (as != kNegInf) es = exact_score_wave<D>(corpus, row, qq, lane);
+  // ---- 3. exact rescoring, 8 candidates per wave (one round trip)
+  {
+    const float* qq = qn + b * D;
+    int rows[8];
+    float es[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = wid * 8 + j;
+      rows[j] = c_s[0][c] != kNegInf ? c_i[0][c] : -1;
+    }
+    exact_scores_wave<D, 8>(corpus, rows, qq, lane, es);
     if (lane == 0) {
-      e_s[c] = es;
-      e_i[c] = as != kNegInf ? row : kIdNone32;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        e_s[wid * 8 + j] = es[j];
+        e_i[wid * 8 + j] = rows[j] >= 0 ? rows[j] : kIdNone32;
+      }
     }
   }
   __syncthreads();

@@ -81,6 +81,21 @@ def test_many_duplicates_tie_break_by_row(gpu):
     np.testing.assert_array_equal(i[0], np.sort(dup_rows)[:32])
 
 
+def test_massive_ties_take_exact_fallback(gpu):
+    """> kCandCap (256) list heads tie at the threshold: select's exact column-sort fallback."""
+    rng = np.random.default_rng(17)
+    base = rng.standard_normal((1, 384)).astype(np.float32)
+    x = rng.standard_normal((12000, 384)).astype(np.float32)
+    x[::2] = base                                 # 6000 identical rows in every tile
+    q = base + 0.02 * rng.standard_normal((3, 384)).astype(np.float32)
+    idx = make_index(gpu, x)
+    s, i = search(idx, q, 32)
+    np.testing.assert_array_equal(i, np.tile(np.arange(0, 64, 2), (3, 1)))
+    s2, i2 = O.search(O.encode_rows(x), q, 32)
+    np.testing.assert_array_equal(i, i2)
+    np.testing.assert_array_equal(s, s2)
+
+
 def test_empty_and_sparse_filters(gpu):
     rng = np.random.default_rng(5)
     x = rng.standard_normal((2000, 384)).astype(np.float32)
