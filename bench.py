@@ -149,33 +149,27 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
+    torch.cuda.set_device(dev)
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
+        backend = os.environ.get("RAGMI_DIST_BACKEND", "nccl")   # nccl = RCCL over xGMI
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
-    from ragmi.index import FlatIndex, merge_topk
+    from ragmi.dist import ShardedIndex
 
     n_total = args.rows
-    lo = n_total * rank // world
-    hi = n_total * (rank + 1) // world
-    idx = FlatIndex(D, hi - lo, dev)
+    sh = ShardedIndex(n_total, dim=D, device=dev)
+    idx, lo, hi = sh.local, sh.lo, sh.hi
     build_shard(idx, lo, hi, n_total, dev)
     nb = args.warmup + args.steps
     qs, _ = make_queries(nb, n_total, dev)
 
-    ag_s = torch.empty((world, B, K_TOP), dtype=torch.float32, device=dev)
-    ag_i = torch.empty((world, B, K_TOP), dtype=torch.int64, device=dev)
-
     def step(q):
-        s, i = idx.search(q, K_TOP, id_offset=lo)
-        if world > 1:
-            dist.all_gather_into_tensor(ag_s, s)
-            dist.all_gather_into_tensor(ag_i, i)
-            s, i = merge_topk(ag_s, ag_i, K_TOP)
-        return s, i
+        return sh.search(q, K_TOP)
 
     for w in range(args.warmup):
         step(qs[w])
@@ -243,7 +237,8 @@ def main():
             "data": "synthetic (torch randn corpus, 1M-row chunks seeded 1000+c; planted "
                     "queries = corpus row + 0.05 N(0,1), every 4th batch pure random)",
             "config": {"workload": f"cosine top-{K_TOP} over {n_total}x{D} fp16 corpus, "
-                                   f"batch={B}, {world} shard(s) + RCCL all-gather merge",
+                                   f"batch={B}, {world} shard(s)" +
+                                   (" + RCCL all-gather merge" if world > 1 else ""),
                        "corpus_rows": n_total, "dim": D, "batch": B, "k": K_TOP,
                        "rows_per_gpu": local_rows, "parallelism": f"corpus-shard{world}"},
             "recall_at_5": recall5,

@@ -97,6 +97,23 @@ __device__ __forceinline__ void bitonic_sort64(float& s, IdT& id, int lane) {
   bitonic_sort_from<2>(s, id, lane);
 }
 
+template <int K, typename IdT>
+__device__ __forceinline__ void bitonic_sort32_from(float& s, IdT& id, int lane) {
+  if constexpr (K <= 32) {
+    if constexpr (K == 32)
+      bitonic_steps<64, 16>(s, id, lane);   // final pass: both halves best-first
+    else
+      bitonic_steps<K, K / 2>(s, id, lane);
+    bitonic_sort32_from<K * 2>(s, id, lane);
+  }
+}
+
+// Two independent 32-element bitonic sorts (lanes 0..31 and 32..63), each best-first.
+template <typename IdT>
+__device__ __forceinline__ void bitonic_sort32x2(float& s, IdT& id, int lane) {
+  bitonic_sort32_from<2>(s, id, lane);
+}
+
 // Bitonic merge: lanes 0..31 sorted best-first, lanes 32..63 sorted worst-first
 // -> all 64 sorted best-first.
 template <typename IdT>

@@ -32,6 +32,7 @@ struct Workspace {
   int* part_i = nullptr;
   float* heads_s = nullptr;   // [32][n_lists]
   int* heads_i = nullptr;
+  int* heads_n = nullptr;
   hipEvent_t done = nullptr;
 };
 
@@ -129,18 +130,18 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
   if (filt)
     scan_kernel<D, true><<<dim3(grid), dim3(256), 0, st>>>(
         h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, (int)n_tiles, w.seed, w.part_s,
-        w.part_i, w.heads_s, w.heads_i);
+        w.part_i, w.heads_s, w.heads_i, w.heads_n);
   else
     scan_kernel<D, false><<<dim3(grid), dim3(256), 0, st>>>(
         h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, (int)n_tiles, w.seed, w.part_s,
-        w.part_i, w.heads_s, w.heads_i);
+        w.part_i, w.heads_s, w.heads_i, w.heads_n);
   if (h->prof) {
     RAG_HIP(hipEventRecord(pp.b, st));
     h->prof_pairs.push_back(pp);
   }
   const int n_lists = grid * kWavesPerWG;
   select_kernel<D><<<dim3(Bq), dim3(256), 0, st>>>(w.part_s, w.part_i, w.heads_s, w.heads_i,
-                                                   n_lists, h->corpus, w.qn, k, id_offset,
+                                                   w.heads_n, n_lists, h->corpus, w.qn, k, id_offset,
                                                    out_s, out_i);
   RAG_HIP(hipGetLastError());
   return RAG_OK;
@@ -217,7 +218,7 @@ void launch_variant(rag_index* h, Workspace& w, int grid, hipStream_t st) {
   constexpr bool SB = V != 6;
   scan_kernel<D, false, MODE, STRIDED, NT, SB><<<dim3(grid), dim3(256), 0, st>>>(
       h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, n_tiles, V == 1 ? nullptr : w.seed,
-      w.part_s, w.part_i, w.heads_s, w.heads_i);
+      w.part_s, w.part_i, w.heads_s, w.heads_i, w.heads_n);
 }
 
 template <int D>
@@ -301,6 +302,8 @@ int rag_index_create(int dim, int64_t capacity_rows, int device, rag_index_t** o
                         (size_t)ragmi::kMaxLists * ragmi::kQ * 4) == hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&w.heads_i),
                         (size_t)ragmi::kMaxLists * ragmi::kQ * 4) == hipSuccess &&
+              hipMalloc(reinterpret_cast<void**>(&w.heads_n),
+                        (size_t)ragmi::kMaxLists * ragmi::kQ * 4) == hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&w.seed), ragmi::kQ * 4) == hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&w.part_s),
                         (size_t)max_lists * ragmi::kQ * ragmi::kKS * 4) == hipSuccess &&
@@ -328,6 +331,7 @@ int rag_index_destroy(rag_index_t* h) {
     if (w.smax) (void)hipFree(w.smax);
     if (w.heads_s) (void)hipFree(w.heads_s);
     if (w.heads_i) (void)hipFree(w.heads_i);
+    if (w.heads_n) (void)hipFree(w.heads_n);
     if (w.seed) (void)hipFree(w.seed);
     if (w.part_s) (void)hipFree(w.part_s);
     if (w.part_i) (void)hipFree(w.part_i);

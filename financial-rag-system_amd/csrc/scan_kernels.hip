@@ -180,7 +180,7 @@ __global__ __launch_bounds__(256, 2) void scan_kernel(
     const half8* __restrict__ corpus, const uint32_t* __restrict__ tags,
     const uint32_t* __restrict__ filt, const half8* __restrict__ qfrag, int n_rows, int n_tiles,
     const float* __restrict__ seed_thr, float* __restrict__ part_s, int* __restrict__ part_i,
-    float* __restrict__ heads_s, int* __restrict__ heads_i) {
+    float* __restrict__ heads_s, int* __restrict__ heads_i, int* __restrict__ heads_n) {
   constexpr int S = steps<D>();
   __shared__ int lds[kWavesPerWG * kLdsPerWave];
   const int lane = threadIdx.x & 63;
@@ -345,24 +345,64 @@ __global__ __launch_bounds__(256, 2) void scan_kernel(
     return;
   }
 
-  // final flush of every query with pending entries
+  // ---- final flush. With seeded thresholds most queries never flushed during the scan:
+  // their keep list is empty and their <= 32 pending entries (4 lanes x 8 slots) only need a
+  // 32-wide sort, two queries per pass. Queries with a non-empty keep list take flush_query.
   {
     const uint64_t b0 = __ballot(cnt0 > 0);
     const uint64_t b1 = __ballot(cnt1 > 0);
-    if (b0) flush_mask(w, b0, 0, lane, thr0, cnt0, thr1, cnt1);
-    if (b1) flush_mask(w, b1, 1, lane, thr0, cnt0, thr1, cnt1);
+    const uint32_t p0 = (uint32_t)((b0 | (b0 >> 16) | (b0 >> 32) | (b0 >> 48)) & 0xffffu);
+    const uint32_t p1 = (uint32_t)((b1 | (b1 >> 16) | (b1 >> 32) | (b1 >> 48)) & 0xffffu);
+    const uint32_t pend = p0 | (p1 << 16);
+    const uint32_t kept =
+        (uint32_t)__ballot(lane < kQ && w.keep_s[(lane & 31) * kKS] != kNegInf);
+    uint32_t full = pend & kept;
+    uint32_t only = pend & ~kept;
+    while (full) {
+      const int q = __builtin_ctz(full);
+      full &= full - 1;
+      flush_query(w, q, lane, thr0, cnt0, thr1, cnt1);
+    }
+    while (only) {
+      const int qa = __builtin_ctz(only);
+      only &= only - 1;
+      const int qb = only ? __builtin_ctz(only) : -1;
+      if (only) only &= only - 1;
+      const int q = lane < 32 ? qa : qb;
+      const int j = lane & 31;
+      float s = kNegInf;
+      int id = kIdNone32;
+      if (q >= 0) {
+        const int pidx = (((q >> 4) * kP + (j & 7)) * 64) + (q & 15) + 16 * (j >> 3);
+        s = w.pend_s[pidx];
+        id = w.pend_i[pidx];
+      }
+      lds_fence();
+      bitonic_sort32x2(s, id, lane);
+      if (q >= 0) {
+        w.keep_s[q * kKS + j] = s;
+        w.keep_i[q * kKS + j] = id;
+      }
+      lds_fence();
+    }
   }
+  // ---- outputs: finite entries of each sorted keep list, list heads and lengths
   float* ps = part_s + (int64_t)gw * (kQ * kKS);
   int* pi = part_i + (int64_t)gw * (kQ * kKS);
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
-    ps[lane + 64 * j] = w.keep_s[lane + 64 * j];
-    pi[lane + 64 * j] = w.keep_i[lane + 64 * j];
+    const float v = w.keep_s[lane + 64 * j];
+    if (v != kNegInf) {
+      ps[lane + 64 * j] = v;
+      pi[lane + 64 * j] = w.keep_i[lane + 64 * j];
+    }
   }
-  // compact list heads [query][wave] for the select kernel's first step
   if (lane < kQ) {
+    int n = 0;
+    for (int j = 0; j < kKS; ++j) n += w.keep_s[lane * kKS + j] != kNegInf;
     heads_s[lane * nw + gw] = w.keep_s[lane * kKS];
-    heads_i[lane * nw + gw] = w.keep_i[lane * kKS];
+    heads_i[lane * nw + gw] = n > 0 ? w.keep_i[lane * kKS] : kIdNone32;
+    heads_n[lane * nw + gw] = n;
   }
 }
 
@@ -561,6 +601,7 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
                                                      const int* __restrict__ part_i,
                                                      const float* __restrict__ heads_s,
                                                      const int* __restrict__ heads_i,
+                                                     const int* __restrict__ heads_n,
                                                      int n_lists,
                                                      const half8* __restrict__ corpus,
                                                      const float* __restrict__ qn, int k,
@@ -570,6 +611,7 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
   __shared__ float w_s[4][32];
   __shared__ int w_i[4][32];
   __shared__ int sel[32];
+  __shared__ int sel_n[32];
   __shared__ float cand_s[kCandCap];
   __shared__ int cand_i[kCandCap];
   __shared__ int n_cand;
@@ -694,7 +736,11 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
       }
       bitonic_merge64(x, id, lane);
     }
-    if (lane < 32) sel[lane] = (x != kNegInf) ? (int)(((uint32_t)id >> 4) % (uint32_t)n_lists) : -1;
+    if (lane < 32) {
+      const int l = (x != kNegInf) ? (int)(((uint32_t)id >> 4) % (uint32_t)n_lists) : -1;
+      sel[lane] = l;
+      sel_n[lane] = l >= 0 ? heads_n[(int64_t)b * n_lists + l] : 0;
+    }
   }
   __syncthreads();
 
@@ -712,7 +758,10 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const bool use = sel[wid * 8 + j] >= 0 && ((j == 0) ? lane < 32 : lane >= 32);
+      // entries past a list's length were not written this search (stale memory)
+      const int pos = (j == 0 ? lane : 63 - lane) & (kKS - 1);
+      const bool use = sel[wid * 8 + j] >= 0 && ((j == 0) ? lane < 32 : lane >= 32) &&
+                       pos < sel_n[wid * 8 + j];
       ls[j] = use ? ls[j] : kNegInf;
       li[j] = use ? li[j] : kIdNone32;
     }

@@ -1,0 +1,108 @@
+"""Corpus sharded over the GPUs of one node.
+
+One process per GPU. Rank r holds the contiguous global rows [lo_r, hi_r) of the collection
+in its own in-HBM FlatIndex. A search is:
+  local scan + per-wave top-k + exact-rescoring select   (libragmi.so, this rank's stream)
+  -> all-gather of the per-shard exact top-k (score f32, global id i64: B*k*12 bytes/rank)
+     over RCCL/xGMI (torch.distributed backend "nccl" = RCCL on ROCm)
+  -> GPU merge of world lists by (score desc, id asc)  (rag_merge_topk)
+Because every shard reports canonical exact scores, the merged result equals the unsharded
+one id-for-id (tests/test_scan_gpu.py::test_sharded_merge_equals_unsharded).
+
+This replaces the per-request HTTP hop to the Qdrant service (reference main.py:232-237);
+the reference itself has no multi-GPU component.
+"""
+from __future__ import annotations
+
+from typing import Callable
+
+import torch
+import torch.distributed as dist
+
+
+def shard_bounds(n_total: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous row range [lo, hi) of `rank` (sizes differ by at most one row)."""
+    if not 0 <= rank < world:
+        raise ValueError("rank out of range")
+    return n_total * rank // world, n_total * (rank + 1) // world
+
+
+def owner_of(row: int, n_total: int, world: int) -> int:
+    """Rank holding global row `row` under shard_bounds."""
+    r = (row * world) // max(n_total, 1)
+    while shard_bounds(n_total, r, world)[0] > row:
+        r -= 1
+    while shard_bounds(n_total, r, world)[1] <= row:
+        r += 1
+    return r
+
+
+def all_gather_lists(scores: torch.Tensor, ids: torch.Tensor, group=None):
+    """[B, k] per rank -> [world, B, k] on every rank (RCCL all-gather on GPU tensors,
+    gloo list all-gather on CPU tensors)."""
+    world = dist.get_world_size(group)
+    if scores.is_cuda and dist.get_backend(group) == "nccl":
+        out_s = torch.empty((world,) + tuple(scores.shape), dtype=scores.dtype,
+                            device=scores.device)
+        out_i = torch.empty((world,) + tuple(ids.shape), dtype=ids.dtype, device=ids.device)
+        dist.all_gather_into_tensor(out_s, scores.contiguous(), group=group)
+        dist.all_gather_into_tensor(out_i, ids.contiguous(), group=group)
+        return out_s, out_i
+    dev = scores.device
+    sc, ic = scores.detach().cpu().contiguous(), ids.detach().cpu().contiguous()   # gloo: host
+    ls = [torch.empty_like(sc) for _ in range(world)]
+    li = [torch.empty_like(ic) for _ in range(world)]
+    dist.all_gather(ls, sc, group=group)
+    dist.all_gather(li, ic, group=group)
+    return torch.stack(ls).to(dev), torch.stack(li).to(dev)
+
+
+def _gpu_merge(s, i, k):
+    from .index import merge_topk
+    return merge_topk(s, i, k)
+
+
+class ShardedIndex:
+    """A collection of n_total rows sharded over the process group's ranks.
+
+    `local` is this rank's index object: anything with
+        search(queries, k, filters=None, id_offset=0) -> (scores [B,k], ids [B,k])
+    (a ragmi.index.FlatIndex in production). `merge` combines [world, B, k] lists into the
+    global [B, k] (the rag_merge_topk GPU kernel by default).
+    """
+
+    def __init__(self, n_total: int, local=None, dim: int = 384, device=None, group=None,
+                 merge: Callable | None = None):
+        self.group = group
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.n_total = int(n_total)
+        self.lo, self.hi = shard_bounds(self.n_total, self.rank, self.world)
+        if local is None:
+            from .index import FlatIndex
+            local = FlatIndex(dim=dim, capacity=max(self.hi - self.lo, 16), device=device)
+        self.local = local
+        self.merge = merge or _gpu_merge
+
+    @property
+    def rows(self) -> int:
+        return self.hi - self.lo
+
+    def owns(self, global_rows: torch.Tensor) -> torch.Tensor:
+        return (global_rows >= self.lo) & (global_rows < self.hi)
+
+    def upsert_global(self, vectors: torch.Tensor, global_rows: torch.Tensor, tags=None):
+        """Keep the rows this rank owns (vectors/rows may be the full batch on every rank)."""
+        m = self.owns(global_rows)
+        if bool(m.any()):
+            rows = (global_rows[m] - self.lo).to(torch.int64)
+            t = tags[m] if tags is not None else None
+            cnt = max(getattr(self.local, "count", 0), int(rows.max()) + 1)
+            self.local.upsert(vectors[m], rows, t, new_count=cnt)
+
+    def search(self, queries, k: int, filters=None):
+        s, i = self.local.search(queries, k, filters=filters, id_offset=self.lo)
+        if self.world == 1:
+            return s, i
+        gs, gi = all_gather_lists(s, i, self.group)
+        return self.merge(gs, gi, k)
