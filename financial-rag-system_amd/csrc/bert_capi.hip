@@ -1,0 +1,284 @@
+// bert_capi.hip — extern "C" boundary of the encoders (include/ragmi_bert.h): weight upload
+// (fp32 HF layout -> fp16 GEMM weights with fused Q|K|V), workspace, forward launch sequence.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <mutex>
+#include <vector>
+
+#include "../../include/ragmi_bert.h"
+#include "bert_kernels.hip"
+#include "common_host.hpp"
+
+namespace {
+
+using namespace ragmi::bert;
+
+struct Layer {
+  _Float16 *wqkv = nullptr, *wo = nullptr, *w1 = nullptr, *w2 = nullptr;
+  float *bqkv = nullptr, *bo = nullptr, *g1 = nullptr, *be1 = nullptr, *bi1 = nullptr,
+        *bi2 = nullptr, *g2 = nullptr, *be2 = nullptr;
+};
+
+__global__ void f32_to_f16_kernel(const float* __restrict__ in, _Float16* __restrict__ out,
+                                  int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (_Float16)in[i];
+}
+
+}  // namespace
+
+struct rag_encoder {
+  rag_bert_config cfg{};
+  int device = 0;
+  std::mutex mu;
+  std::vector<void*> allocs;
+  float *wemb = nullptr, *pemb = nullptr, *temb = nullptr, *eg = nullptr, *eb = nullptr;
+  std::vector<Layer> layers;
+  float *wp = nullptr, *bp = nullptr, *wc = nullptr, *bc = nullptr;
+  // workspace (grown on demand)
+  int64_t cap_t = 0;
+  float *x = nullptr, *y = nullptr;
+  _Float16 *xh = nullptr, *qkv = nullptr, *ctx = nullptr, *ff = nullptr;
+  // host-entry staging
+  void* stage = nullptr;
+  size_t stage_bytes = 0;
+};
+
+namespace {
+
+template <typename T>
+int dalloc(rag_encoder* e, T** p, size_t n) {
+  RAG_HIP(hipMalloc(reinterpret_cast<void**>(p), std::max<size_t>(n * sizeof(T), 16)));
+  e->allocs.push_back(*p);
+  return RAG_OK;
+}
+
+int up_f32(rag_encoder* e, float** dst, const float* src, size_t n) {
+  int rc = dalloc(e, dst, n);
+  if (rc) return rc;
+  RAG_HIP(hipMemcpy(*dst, src, n * 4, hipMemcpyHostToDevice));
+  return RAG_OK;
+}
+
+// fp16 copy of one or more host fp32 blocks laid end to end ([rows][K] each)
+int up_f16(rag_encoder* e, _Float16** dst, std::initializer_list<std::pair<const float*, size_t>> parts) {
+  size_t n = 0;
+  for (auto& p : parts) n += p.second;
+  int rc = dalloc(e, dst, n);
+  if (rc) return rc;
+  float* tmp = nullptr;
+  RAG_HIP(hipMalloc(reinterpret_cast<void**>(&tmp), n * 4));
+  size_t off = 0;
+  for (auto& p : parts) {
+    if (hipMemcpy(tmp + off, p.first, p.second * 4, hipMemcpyHostToDevice) != hipSuccess) {
+      (void)hipFree(tmp);
+      return ragmi::fail(RAG_EHIP, "weight upload failed");
+    }
+    off += p.second;
+  }
+  f32_to_f16_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256)>>>(tmp, *dst, (int64_t)n);
+  RAG_HIP(hipDeviceSynchronize());
+  (void)hipFree(tmp);
+  return RAG_OK;
+}
+
+int ensure_ws(rag_encoder* e, int64_t T) {
+  if (T <= e->cap_t) return RAG_OK;
+  const int64_t cap = std::max<int64_t>(T, std::max<int64_t>(2 * e->cap_t, 1024));
+  for (void* p : {(void*)e->x, (void*)e->y, (void*)e->xh, (void*)e->qkv, (void*)e->ctx,
+                  (void*)e->ff})
+    if (p) (void)hipFree(p);
+  e->x = e->y = nullptr;
+  e->xh = e->qkv = e->ctx = e->ff = nullptr;
+  e->cap_t = 0;
+  RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->x), cap * H * 4));
+  RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->y), cap * H * 4));
+  RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->xh), cap * H * 2));
+  RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->qkv), cap * 3 * H * 2));
+  RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->ctx), cap * H * 2));
+  RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->ff), cap * FF * 2));
+  e->cap_t = cap;
+  return RAG_OK;
+}
+
+template <int EPI>
+void gemm(const _Float16* A, const _Float16* W, const float* bias, int M, int N, int K, void* C,
+          hipStream_t st) {
+  gemm_kernel<EPI><<<dim3(N / BN, (M + BM - 1) / BM), dim3(256), 0, st>>>(A, W, bias, M, N, K,
+                                                                          C);
+}
+
+int forward_locked(rag_encoder* e, const int32_t* ids, const int32_t* types, const int32_t* cu,
+                   int B, int T, int max_len, float* out, hipStream_t st) {
+  const rag_bert_config& c = e->cfg;
+  int rc = ensure_ws(e, T);
+  if (rc) return rc;
+  embed_ln_kernel<<<dim3((max_len + 3) / 4, B), dim3(256), 0, st>>>(
+      ids, types, cu, e->wemb, e->pemb, e->temb, e->eg, e->eb, c.layer_norm_eps, c.vocab,
+      c.type_vocab, c.max_position, e->x, e->xh);
+  const float scale = 1.0f / sqrtf((float)HD);
+  const unsigned ln_grid = (unsigned)((T + 3) / 4);
+  for (const Layer& L : e->layers) {
+    gemm<kEpiF16>(e->xh, L.wqkv, L.bqkv, T, 3 * H, H, e->qkv, st);
+    attn_kernel<<<dim3((max_len + 63) / 64, NH, B), dim3(256), 0, st>>>(e->qkv, cu, scale,
+                                                                        e->ctx);
+    gemm<kEpiF32>(e->ctx, L.wo, L.bo, T, H, H, e->y, st);
+    add_ln_kernel<<<dim3(ln_grid), dim3(256), 0, st>>>(e->x, e->y, L.g1, L.be1,
+                                                       c.layer_norm_eps, e->xh, T);
+    gemm<kEpiGeluF16>(e->xh, L.w1, L.bi1, T, FF, H, e->ff, st);
+    gemm<kEpiF32>(e->ff, L.w2, L.bi2, T, H, FF, e->y, st);
+    add_ln_kernel<<<dim3(ln_grid), dim3(256), 0, st>>>(e->x, e->y, L.g2, L.be2,
+                                                       c.layer_norm_eps, e->xh, T);
+  }
+  if (c.head == RAG_HEAD_CLS_L2)
+    cls_normalize_kernel<<<dim3(B), dim3(64), 0, st>>>(e->x, cu, out);
+  else
+    ce_head_kernel<<<dim3(B), dim3(256), 0, st>>>(e->x, cu, e->wp, e->bp, e->wc, e->bc, out);
+  RAG_HIP(hipGetLastError());
+  return RAG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rag_encoder_num_weights(const rag_bert_config* cfg) {
+  if (!cfg) return -1;
+  return 5 + 16 * cfg->layers + (cfg->head == RAG_HEAD_POOLER_CLS ? 4 : 0);
+}
+
+int rag_encoder_create(const rag_bert_config* cfg, const float* const* w, int n_weights,
+                       int device, rag_encoder_t** out) {
+  ragmi::clear_error();
+  if (!cfg || !w || !out) return ragmi::fail(RAG_EINVAL, "NULL argument");
+  *out = nullptr;
+  if (cfg->hidden != H || cfg->heads != NH || cfg->intermediate != FF)
+    return ragmi::fail(RAG_EINVAL, "built for hidden 384, 12 heads, intermediate 1536");
+  if (cfg->layers < 1 || cfg->layers > 64 || cfg->vocab < 1 || cfg->type_vocab < 1 ||
+      cfg->max_position < 1 || cfg->max_position > 4096)
+    return ragmi::fail(RAG_EINVAL, "bad config");
+  if (cfg->head != RAG_HEAD_CLS_L2 && cfg->head != RAG_HEAD_POOLER_CLS)
+    return ragmi::fail(RAG_EINVAL, "unknown head");
+  if (n_weights != rag_encoder_num_weights(cfg))
+    return ragmi::fail(RAG_EINVAL, "wrong number of weight tensors");
+  for (int i = 0; i < n_weights; ++i)
+    if (!w[i]) return ragmi::fail(RAG_EINVAL, "NULL weight tensor");
+  RAG_HIP(hipSetDevice(device));
+  auto* e = new rag_encoder();
+  e->cfg = *cfg;
+  e->device = device;
+  int rc = RAG_OK;
+  auto chk = [&](int r) {
+    if (r && !rc) rc = r;
+  };
+  const size_t Hs = H;
+  chk(up_f32(e, &e->wemb, w[0], (size_t)cfg->vocab * Hs));
+  chk(up_f32(e, &e->pemb, w[1], (size_t)cfg->max_position * Hs));
+  chk(up_f32(e, &e->temb, w[2], (size_t)cfg->type_vocab * Hs));
+  chk(up_f32(e, &e->eg, w[3], Hs));
+  chk(up_f32(e, &e->eb, w[4], Hs));
+  e->layers.resize(cfg->layers);
+  for (int l = 0; l < cfg->layers && !rc; ++l) {
+    const float* const* p = w + 5 + 16 * l;
+    Layer& L = e->layers[l];
+    chk(up_f16(e, &L.wqkv, {{p[0], Hs * H}, {p[2], Hs * H}, {p[4], Hs * H}}));
+    {
+      std::vector<float> b(3 * H);
+      std::copy(p[1], p[1] + H, b.begin());
+      std::copy(p[3], p[3] + H, b.begin() + H);
+      std::copy(p[5], p[5] + H, b.begin() + 2 * H);
+      chk(up_f32(e, &L.bqkv, b.data(), 3 * Hs));
+    }
+    chk(up_f16(e, &L.wo, {{p[6], Hs * H}}));
+    chk(up_f32(e, &L.bo, p[7], Hs));
+    chk(up_f32(e, &L.g1, p[8], Hs));
+    chk(up_f32(e, &L.be1, p[9], Hs));
+    chk(up_f16(e, &L.w1, {{p[10], (size_t)FF * H}}));
+    chk(up_f32(e, &L.bi1, p[11], FF));
+    chk(up_f16(e, &L.w2, {{p[12], Hs * FF}}));
+    chk(up_f32(e, &L.bi2, p[13], Hs));
+    chk(up_f32(e, &L.g2, p[14], Hs));
+    chk(up_f32(e, &L.be2, p[15], Hs));
+  }
+  if (cfg->head == RAG_HEAD_POOLER_CLS && !rc) {
+    const float* const* p = w + 5 + 16 * cfg->layers;
+    chk(up_f32(e, &e->wp, p[0], Hs * H));
+    chk(up_f32(e, &e->bp, p[1], Hs));
+    chk(up_f32(e, &e->wc, p[2], Hs));
+    chk(up_f32(e, &e->bc, p[3], 1));
+  }
+  if (rc) {
+    rag_encoder_destroy(e);
+    return rc;
+  }
+  *out = e;
+  return RAG_OK;
+}
+
+int rag_encoder_destroy(rag_encoder_t* e) {
+  ragmi::clear_error();
+  if (!e) return RAG_OK;
+  (void)hipSetDevice(e->device);
+  (void)hipDeviceSynchronize();
+  for (void* p : e->allocs) (void)hipFree(p);
+  for (void* p : {(void*)e->x, (void*)e->y, (void*)e->xh, (void*)e->qkv, (void*)e->ctx,
+                  (void*)e->ff, e->stage})
+    if (p) (void)hipFree(p);
+  delete e;
+  return RAG_OK;
+}
+
+int rag_encoder_forward(rag_encoder_t* e, const int32_t* ids, const int32_t* types,
+                        const int32_t* cu, int B, int T, int max_len, float* out, void* stream) {
+  ragmi::clear_error();
+  if (!e || !ids || !types || !cu || !out) return ragmi::fail(RAG_EINVAL, "NULL argument");
+  if (B < 1 || T < B || max_len < 1 || max_len > e->cfg.max_position)
+    return ragmi::fail(RAG_EINVAL, "bad batch shape (max_len must be <= max_position)");
+  std::lock_guard<std::mutex> lk(e->mu);
+  RAG_HIP(hipSetDevice(e->device));
+  return forward_locked(e, ids, types, cu, B, T, max_len, out, static_cast<hipStream_t>(stream));
+}
+
+int rag_encoder_forward_host(rag_encoder_t* e, const int32_t* ids, const int32_t* types,
+                             const int32_t* cu, int B, int T, float* out) {
+  ragmi::clear_error();
+  if (!e || !ids || !types || !cu || !out || B < 1) return ragmi::fail(RAG_EINVAL, "bad args");
+  if (cu[0] != 0 || cu[B] != T) return ragmi::fail(RAG_EINVAL, "cu_seqlens must span [0, T]");
+  int max_len = 0;
+  for (int b = 0; b < B; ++b) {
+    const int L = cu[b + 1] - cu[b];
+    if (L < 1) return ragmi::fail(RAG_EINVAL, "empty sequence");
+    max_len = std::max(max_len, L);
+  }
+  if (max_len > e->cfg.max_position) return ragmi::fail(RAG_EINVAL, "sequence longer than max_position");
+  for (int t = 0; t < T; ++t)
+    if (ids[t] < 0 || ids[t] >= e->cfg.vocab || types[t] < 0 || types[t] >= e->cfg.type_vocab)
+      return ragmi::fail(RAG_EINVAL, "token id / type out of range");
+  const size_t ob = (size_t)B * (e->cfg.head == RAG_HEAD_CLS_L2 ? H : 1) * 4;
+  const size_t need = (size_t)T * 8 + (size_t)(B + 1) * 4 + ob + 64;
+  std::lock_guard<std::mutex> lk(e->mu);
+  RAG_HIP(hipSetDevice(e->device));
+  if (e->stage_bytes < need) {
+    if (e->stage) (void)hipFree(e->stage);
+    e->stage = nullptr;
+    e->stage_bytes = 0;
+    RAG_HIP(hipMalloc(&e->stage, need));
+    e->stage_bytes = need;
+  }
+  char* s = static_cast<char*>(e->stage);
+  int32_t* d_ids = reinterpret_cast<int32_t*>(s);
+  int32_t* d_ty = d_ids + T;
+  int32_t* d_cu = d_ty + T;
+  float* d_out = reinterpret_cast<float*>(s + (((size_t)T * 8 + (size_t)(B + 1) * 4 + 15) & ~size_t(15)));
+  RAG_HIP(hipMemcpy(d_ids, ids, (size_t)T * 4, hipMemcpyHostToDevice));
+  RAG_HIP(hipMemcpy(d_ty, types, (size_t)T * 4, hipMemcpyHostToDevice));
+  RAG_HIP(hipMemcpy(d_cu, cu, (size_t)(B + 1) * 4, hipMemcpyHostToDevice));
+  int rc = forward_locked(e, d_ids, d_ty, d_cu, B, T, max_len, d_out, nullptr);
+  if (rc) return rc;
+  RAG_HIP(hipDeviceSynchronize());
+  RAG_HIP(hipMemcpy(out, d_out, ob, hipMemcpyDeviceToHost));
+  return RAG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,381 @@
+// bert_kernels.hip — BERT-small encoder forward for gfx950 (bge-small-en-v1.5 and
+// ms-marco-MiniLM-L-6-v2 cross-encoder).
+//
+// Replaces the torch CPU forward behind sentence-transformers' SentenceTransformer.encode
+// (reference main.py:80-84, 144-149, 211-213; main2.py:170-171) and CrossEncoder.predict
+// (main.py:86-90, 241-247). Arithmetic follows transformers modeling_bert.py (post-LN,
+// erf-GELU, softmax(QK^T/sqrt(d) + mask)V); see oracle/bert_ref.py.
+//
+// Numerics: GEMM operands fp16 (weights and activations), fp32 MFMA accumulation, fp32
+// residual stream, fp32 LayerNorm/softmax statistics.
+// Layout: sequences are PACKED (no padding): token t of sequence b sits at row cu[b] + pos.
+// Right padding never changes a valid token's output (masked keys contribute exp(-inf) = 0),
+// so packing is exact w.r.t. the padded reference.
+#include "device_common.hpp"
+
+namespace ragmi {
+namespace bert {
+
+constexpr int H = 384;      // hidden
+constexpr int NH = 12;      // heads
+constexpr int HD = 32;      // head dim
+constexpr int FF = 1536;    // intermediate
+
+typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float gelu_erf(float x) {
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
+}
+
+// ----------------------------------------------------------------------------------------
+// embeddings: x = LN(word[id] + type[tt] + pos[p]); one wave per token, grid (ceil(L/4), B)
+// ----------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void embed_ln_kernel(
+    const int* __restrict__ ids, const int* __restrict__ types, const int* __restrict__ cu,
+    const float* __restrict__ wemb, const float* __restrict__ pemb, const float* __restrict__ temb,
+    const float* __restrict__ g, const float* __restrict__ bt, float eps, int vocab,
+    int type_vocab, int max_pos, float* __restrict__ x, _Float16* __restrict__ xh) {
+  const int b = blockIdx.y;
+  const int pos = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int len = cu[b + 1] - cu[b];
+  if (pos >= len) return;
+  const int64_t t = cu[b] + pos;
+  // clamp: a bad id must never become an out-of-bounds gather
+  const int id = min(max(ids[t], 0), vocab - 1);
+  const int ty = min(max(types[t], 0), type_vocab - 1);
+  const int pp = min(pos, max_pos - 1);
+  float v[H / 64];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < H / 64; ++j) {
+    const int c = lane + 64 * j;
+    v[j] = wemb[(int64_t)id * H + c] + temb[ty * H + c] + pemb[pp * H + c];
+    s += v[j];
+  }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) s += __shfl_xor(s, d, 64);
+  const float mu = s * (1.0f / H);
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < H / 64; ++j) q += (v[j] - mu) * (v[j] - mu);
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) q += __shfl_xor(q, d, 64);
+  const float rs = rsqrtf(q * (1.0f / H) + eps);
+#pragma unroll
+  for (int j = 0; j < H / 64; ++j) {
+    const int c = lane + 64 * j;
+    const float y = (v[j] - mu) * rs * g[c] + bt[c];
+    x[t * H + c] = y;
+    xh[t * H + c] = (_Float16)y;
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// residual + LayerNorm: x = LN(x + y) (fp32, in place), xh = fp16(x); one wave per row
+// ----------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void add_ln_kernel(float* __restrict__ x,
+                                                     const float* __restrict__ y,
+                                                     const float* __restrict__ g,
+                                                     const float* __restrict__ bt, float eps,
+                                                     _Float16* __restrict__ xh, int T) {
+  const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (t >= T) return;
+  float v[H / 64];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < H / 64; ++j) {
+    const int c = lane + 64 * j;
+    v[j] = x[t * H + c] + y[t * H + c];
+    s += v[j];
+  }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) s += __shfl_xor(s, d, 64);
+  const float mu = s * (1.0f / H);
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < H / 64; ++j) q += (v[j] - mu) * (v[j] - mu);
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) q += __shfl_xor(q, d, 64);
+  const float rs = rsqrtf(q * (1.0f / H) + eps);
+#pragma unroll
+  for (int j = 0; j < H / 64; ++j) {
+    const int c = lane + 64 * j;
+    const float o = (v[j] - mu) * rs * g[c] + bt[c];
+    x[t * H + c] = o;
+    xh[t * H + c] = (_Float16)o;
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// GEMM: C[M,N] = A[M,K] . W[N,K]^T + bias[N]   (A fp16 row-major, W fp16 [N][K] = HF Linear)
+// 128x128 tile, BK = 64, 256 threads = 2x2 waves of 64x64, v_mfma_f32_16x16x32_f16.
+// Register-staged double-buffered LDS (one barrier per K step), XOR-swizzled 16-B chunks.
+// ----------------------------------------------------------------------------------------
+enum Epi { kEpiF16 = 0, kEpiGeluF16 = 1, kEpiF32 = 2 };
+
+constexpr int BM = 128, BN = 128, BK = 64;
+
+__device__ __forceinline__ int swz(int row, int chunk) { return row * 8 + (chunk ^ (row & 7)); }
+
+template <int EPI>
+__global__ __launch_bounds__(256) void gemm_kernel(const _Float16* __restrict__ A,
+                                                   const _Float16* __restrict__ W,
+                                                   const float* __restrict__ bias, int M, int N,
+                                                   int K, void* __restrict__ Cout) {
+  __shared__ half8 lds[2 * 2 * BM * (BK / 8)];   // [buf][A|B][row][8 chunks]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int nk = K / BK;
+
+  half8 ra[4], rb[4];
+  auto gload = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + 256 * i;
+      const int row = c >> 3, ch = c & 7;
+      const int am = min(m0 + row, M - 1);
+      ra[i] = *reinterpret_cast<const half8*>(A + (int64_t)am * K + kt * BK + ch * 8);
+      rb[i] = *reinterpret_cast<const half8*>(W + (int64_t)(n0 + row) * K + kt * BK + ch * 8);
+    }
+  };
+  auto lstore = [&](int buf) {
+    half8* la = lds + buf * (2 * BM * 8);
+    half8* lb = la + BM * 8;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + 256 * i;
+      const int row = c >> 3, ch = c & 7;
+      la[swz(row, ch)] = ra[i];
+      lb[swz(row, ch)] = rb[i];
+    }
+  };
+
+  floatx4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) gload(kt + 1);
+    const half8* la = lds + buf * (2 * BM * 8);
+    const half8* lb = la + BM * 8;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      half8 af[4], bf[4];
+      const int ch = ks * 4 + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = la[swz(wr * 64 + i * 16 + (lane & 15), ch)];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bf[j] = lb[swz(wc * 64 + j * 16 + (lane & 15), ch)];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) lstore(buf ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: lane holds C[rows 4(l>>4)+r][col l&15] of each 16x16 tile
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = n0 + wc * 64 + j * 16 + (lane & 15);
+    const float bn = bias[n];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wr * 64 + i * 16 + 4 * (lane >> 4) + r;
+        if (m < M) {
+          float v = acc[i][j][r] + bn;
+          if constexpr (EPI == kEpiF32) {
+            static_cast<float*>(Cout)[(int64_t)m * N + n] = v;
+          } else {
+            if constexpr (EPI == kEpiGeluF16) v = gelu_erf(v);
+            static_cast<_Float16*>(Cout)[(int64_t)m * N + n] = (_Float16)v;
+          }
+        }
+      }
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// attention (flash style, varlen): grid (ceil(maxlen/64), NH, B), 256 threads; wave w owns
+// query rows qb*64 + 16w .. +15 of sequence b, head h. Key blocks of 32 staged in LDS
+// (K as [key][dim], V transposed as [dim][key]); S = Q K^T and O += P V on
+// v_mfma_f32_16x16x32_f16 (head_dim 32 = one K step); online softmax in fp32.
+// qkv: fp16 [T][3H] (Q | K | V, head h = columns h*32 .. +31 of each); ctx: fp16 [T][H].
+// ----------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void attn_kernel(const _Float16* __restrict__ qkv,
+                                                   const int* __restrict__ cu, float scale,
+                                                   _Float16* __restrict__ ctx) {
+  __shared__ _Float16 kl[32][HD + 8];     // [key][dim] (+8 pad: 80-B rows)
+  __shared__ _Float16 vt[HD][32 + 8];     // [dim][key]
+  __shared__ _Float16 pl[4][16][32 + 8];  // per wave P tile [row][key]
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int base = cu[b], len = cu[b + 1] - cu[b];
+  const int q0 = blockIdx.x * 64 + wid * 16;
+  if (blockIdx.x * 64 >= len) return;
+  const int qrow = q0 + (lane & 15);
+
+  half8 qf;
+  {
+    const int r = min(qrow, len - 1);
+    qf = *reinterpret_cast<const half8*>(qkv + (int64_t)(base + r) * (3 * H) + h * HD +
+                                         8 * (lane >> 4));
+  }
+  floatx4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = {0.f, 0.f, 0.f, 0.f};
+  float mrow[4], lrow[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    mrow[i] = kNegInf;
+    lrow[i] = 0.f;
+  }
+
+  for (int kb = 0; kb < len; kb += 32) {
+    // stage K and V^T of keys kb .. kb+31 (zeros past the end)
+    {
+      const int key = tid >> 3, dc = (tid & 7) * 4;
+      half4 kv = {0, 0, 0, 0}, vv = {0, 0, 0, 0};
+      if (kb + key < len) {
+        const _Float16* src = qkv + (int64_t)(base + kb + key) * (3 * H) + h * HD + dc;
+        kv = *reinterpret_cast<const half4*>(src + H);
+        vv = *reinterpret_cast<const half4*>(src + 2 * H);
+      }
+      *reinterpret_cast<half4*>(&kl[key][dc]) = kv;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) vt[dc + e][key] = vv[e];
+    }
+    __syncthreads();
+    // S = Q K^T for two 16-key tiles
+    floatx4 s[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const half8 kf = *reinterpret_cast<const half8*>(&kl[16 * j + (lane & 15)][8 * (lane >> 4)]);
+      s[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(qf, kf, floatx4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    }
+    // lane: rows 4(l>>4)+i, keys kb + 16j + (l&15)
+    float p[2][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float mx = kNegInf;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const bool ok = kb + 16 * j + (lane & 15) < len;
+        s[j][i] = ok ? s[j][i] * scale : kNegInf;
+        mx = fmaxf(mx, s[j][i]);
+      }
+      mx = fmaxf(mx, xor_lane_f<1>(mx));
+      mx = fmaxf(mx, xor_lane_f<2>(mx));
+      mx = fmaxf(mx, xor_lane_f<4>(mx));
+      mx = fmaxf(mx, xor_lane_f<8>(mx));
+      const float mnew = fmaxf(mrow[i], mx);
+      const float corr = __expf(mrow[i] - mnew);
+      float rsum = 0.f;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const float e = (float)(_Float16)__expf(s[j][i] - mnew);   // P as MFMA sees it
+        p[j][i] = e;
+        rsum += e;
+      }
+      rsum += xor_lane_f<1>(rsum);
+      rsum += xor_lane_f<2>(rsum);
+      rsum += xor_lane_f<4>(rsum);
+      rsum += xor_lane_f<8>(rsum);
+      lrow[i] = lrow[i] * corr + rsum;
+      mrow[i] = mnew;
+      o0[i] *= corr;
+      o1[i] *= corr;
+    }
+    // P -> LDS (this wave's tile) -> A fragment
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) pl[wid][4 * (lane >> 4) + i][16 * j + (lane & 15)] = (_Float16)p[j][i];
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const half8 pf = *reinterpret_cast<const half8*>(&pl[wid][lane & 15][8 * (lane >> 4)]);
+    const half8 v0 = *reinterpret_cast<const half8*>(&vt[lane & 15][8 * (lane >> 4)]);
+    const half8 v1 = *reinterpret_cast<const half8*>(&vt[16 + (lane & 15)][8 * (lane >> 4)]);
+    o0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(pf, v0, o0, 0, 0, 0);
+    o1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(pf, v1, o1, 0, 0, 0);
+    __syncthreads();
+  }
+  // O: lane rows 4(l>>4)+i, dims (l&15) and 16 + (l&15)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = q0 + 4 * (lane >> 4) + i;
+    if (r < len) {
+      const float inv = 1.0f / lrow[i];
+      _Float16* dst = ctx + (int64_t)(base + r) * H + h * HD;
+      dst[lane & 15] = (_Float16)(o0[i] * inv);
+      dst[16 + (lane & 15)] = (_Float16)(o1[i] * inv);
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// heads
+// ----------------------------------------------------------------------------------------
+// bge (sentence-transformers Pooling(cls) + Normalize): out[b] = x[cls] / max(||x[cls]||, 1e-12)
+__global__ __launch_bounds__(64) void cls_normalize_kernel(const float* __restrict__ x,
+                                                           const int* __restrict__ cu,
+                                                           float* __restrict__ out) {
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const float* r = x + (int64_t)cu[b] * H;
+  float v[H / 64];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < H / 64; ++j) {
+    v[j] = r[lane + 64 * j];
+    s += v[j] * v[j];
+  }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) s += __shfl_xor(s, d, 64);
+  const float inv = 1.0f / fmaxf(sqrtf(s), 1e-12f);
+#pragma unroll
+  for (int j = 0; j < H / 64; ++j) out[(int64_t)b * H + lane + 64 * j] = v[j] * inv;
+}
+
+// cross-encoder: pooled = tanh(Wp x[cls] + bp); logit = Wc pooled + bc (num_labels = 1)
+__global__ __launch_bounds__(256) void ce_head_kernel(const float* __restrict__ x,
+                                                      const int* __restrict__ cu,
+                                                      const float* __restrict__ wp,
+                                                      const float* __restrict__ bp,
+                                                      const float* __restrict__ wc,
+                                                      const float* __restrict__ bc,
+                                                      float* __restrict__ out) {
+  __shared__ float cls[H];
+  __shared__ float part[4];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  for (int c = tid; c < H; c += 256) cls[c] = x[(int64_t)cu[b] * H + c];
+  __syncthreads();
+  float acc = 0.f;
+  for (int o = tid; o < H; o += 256) {
+    const float* wr = wp + (int64_t)o * H;
+    float d = 0.f;
+    for (int c = 0; c < H; c += 4) {
+      const float4 w4 = *reinterpret_cast<const float4*>(wr + c);
+      d += w4.x * cls[c] + w4.y * cls[c + 1] + w4.z * cls[c + 2] + w4.w * cls[c + 3];
+    }
+    acc += tanhf(d + bp[o]) * wc[o];
+  }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) acc += __shfl_xor(acc, d, 64);
+  if (lane == 0) part[wid] = acc;
+  __syncthreads();
+  if (tid == 0) out[b] = part[0] + part[1] + part[2] + part[3] + bc[0];
+}
+
+}  // namespace bert
+}  // namespace ragmi

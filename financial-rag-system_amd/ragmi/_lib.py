@@ -67,7 +67,26 @@ INDEX_API = {
     "rag_profile_scan_ms": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_double), c_i64p]),
 }
 
-BERT_API: dict = {}   # filled by ragmi.encoders when the encoder ABI is present
+class RagBertConfig(ctypes.Structure):
+    """rag_bert_config (include/ragmi_bert.h)."""
+    _fields_ = [("vocab", ctypes.c_int), ("hidden", ctypes.c_int), ("layers", ctypes.c_int),
+                ("heads", ctypes.c_int), ("intermediate", ctypes.c_int),
+                ("max_position", ctypes.c_int), ("type_vocab", ctypes.c_int),
+                ("layer_norm_eps", ctypes.c_float), ("head", ctypes.c_int)]
+
+
+c_i32p_ = ctypes.POINTER(ctypes.c_int32)
+BERT_API = {
+    "rag_encoder_num_weights": (ctypes.c_int, [ctypes.POINTER(RagBertConfig)]),
+    "rag_encoder_create": (ctypes.c_int, [ctypes.POINTER(RagBertConfig),
+                                          ctypes.POINTER(ctypes.POINTER(ctypes.c_float)),
+                                          ctypes.c_int, ctypes.c_int, ctypes.POINTER(c_vp)]),
+    "rag_encoder_destroy": (ctypes.c_int, [c_vp]),
+    "rag_encoder_forward": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_int, c_vp, c_vp]),
+    "rag_encoder_forward_host": (ctypes.c_int, [c_vp, c_i32p_, c_i32p_, c_i32p_, ctypes.c_int,
+                                                ctypes.c_int, c_f32p]),
+}
 
 
 def load():

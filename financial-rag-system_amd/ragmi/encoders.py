@@ -1,0 +1,239 @@
+"""Encoders on MI355X: bge-small-en-v1.5 embedder and ms-marco-MiniLM-L-6-v2 cross-encoder.
+
+Drop-ins for the two sentence-transformers objects the reference builds in its lazy loaders:
+  get_embedder() -> SentenceTransformer("BAAI/bge-small-en-v1.5")       main.py:80-84, main2.py:88-96
+      .encode(str) -> float32 [384]; .encode(list[str]) -> float32 [n, 384]
+      (main.py:144-149 /embed, 211-213 embed_query; main2.py:170-171 embed_query_batch)
+  get_reranker() -> CrossEncoder("cross-encoder/ms-marco-MiniLM-L-6-v2")  main.py:86-90
+      .predict([[query, text], ...]) -> float32 [n]   (main.py:241-247 rerank_documents)
+The transformer forward runs in libragmi.so (csrc/bert_kernels.hip); tokenisation is host-side
+WordPiece (`tokenizers`) from the checkpoint's own vocab.txt. Models load from LOCAL
+directories in the HF layout (config.json + model.safetensors + vocab.txt): there is no hub
+access, and no CPU forward to fall back to.
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check
+
+HEAD_CLS_L2 = 0        # sentence-transformers: Pooling(cls) + Normalize  (bge)
+HEAD_POOLER_CLS = 1    # BertForSequenceClassification, num_labels = 1   (cross-encoder)
+
+
+# ------------------------------------------------------------------ weights
+def weight_order(layers: int, head: int) -> list[str]:
+    """HF state-dict names in the order rag_encoder_create expects (include/ragmi_bert.h)."""
+    names = ["embeddings.word_embeddings.weight", "embeddings.position_embeddings.weight",
+             "embeddings.token_type_embeddings.weight", "embeddings.LayerNorm.weight",
+             "embeddings.LayerNorm.bias"]
+    for l in range(layers):
+        p = f"encoder.layer.{l}."
+        for n in ("attention.self.query", "attention.self.key", "attention.self.value",
+                  "attention.output.dense"):
+            names += [p + n + ".weight", p + n + ".bias"]
+        names += [p + "attention.output.LayerNorm.weight", p + "attention.output.LayerNorm.bias",
+                  p + "intermediate.dense.weight", p + "intermediate.dense.bias",
+                  p + "output.dense.weight", p + "output.dense.bias",
+                  p + "output.LayerNorm.weight", p + "output.LayerNorm.bias"]
+    if head == HEAD_POOLER_CLS:
+        names += ["pooler.dense.weight", "pooler.dense.bias", "classifier.weight",
+                  "classifier.bias"]
+    return names
+
+
+def _lookup(w: dict, name: str):
+    for k in (name, "bert." + name, "model." + name):
+        if k in w:
+            return w[k]
+    raise KeyError(f"weight {name!r} not found")
+
+
+def load_safetensors(path: str) -> dict:
+    """Tensors of a local .safetensors file as fp32 numpy (safe loader: executes nothing)."""
+    from safetensors.numpy import load_file
+    return {k: np.asarray(v, dtype=np.float32) for k, v in load_file(path).items()}
+
+
+def config_from_hf(cfg: dict) -> dict:
+    return dict(vocab=cfg["vocab_size"], hidden=cfg["hidden_size"],
+                layers=cfg["num_hidden_layers"], heads=cfg["num_attention_heads"],
+                inter=cfg["intermediate_size"], max_pos=cfg["max_position_embeddings"],
+                type_vocab=cfg.get("type_vocab_size", 2), eps=cfg.get("layer_norm_eps", 1e-12))
+
+
+# ------------------------------------------------------------------ device encoder
+class BertEncoder:
+    """One encoder instance in HBM (fp16 GEMM weights, fp32 norms/embeddings)."""
+
+    def __init__(self, cfg: dict, weights: dict, head: int, device=None):
+        _lib.require_gpu()
+        self._L = _lib.load()
+        self.device = torch.device(device if device is not None else
+                                   torch.device("cuda", torch.cuda.current_device()))
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        self.cfg, self.head = dict(cfg), head
+        c = _lib.RagBertConfig(cfg["vocab"], cfg["hidden"], cfg["layers"], cfg["heads"],
+                               cfg["inter"], cfg["max_pos"], cfg["type_vocab"], cfg["eps"], head)
+        names = weight_order(cfg["layers"], head)
+        if self._L.rag_encoder_num_weights(ctypes.byref(c)) != len(names):
+            raise RuntimeError("weight order / ABI mismatch")
+        arrs = [np.ascontiguousarray(_lookup(weights, n), dtype=np.float32) for n in names]
+        ptrs = (ctypes.POINTER(ctypes.c_float) * len(arrs))(
+            *[a.ctypes.data_as(ctypes.POINTER(ctypes.c_float)) for a in arrs])
+        h = ctypes.c_void_p()
+        check(self._L.rag_encoder_create(ctypes.byref(c), ptrs, len(arrs), self.device.index,
+                                         ctypes.byref(h)))
+        self._h = h
+        self.out_dim = cfg["hidden"] if head == HEAD_CLS_L2 else 1
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._L.rag_encoder_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def forward_packed(self, ids: np.ndarray, types: np.ndarray, cu: np.ndarray,
+                       out: torch.Tensor | None = None) -> torch.Tensor:
+        """ids/types int32 [T], cu int32 [B+1] (host) -> cuda fp32 [B, out_dim] (or [B])."""
+        ids = np.ascontiguousarray(ids, np.int32)
+        types = np.ascontiguousarray(types, np.int32)
+        cu = np.ascontiguousarray(cu, np.int32)
+        B = len(cu) - 1
+        T = int(cu[-1])
+        lens = np.diff(cu)
+        if B < 1 or cu[0] != 0 or (lens < 1).any() or ids.shape != (T,) or types.shape != (T,):
+            raise ValueError("bad packed batch")
+        if int(lens.max()) > self.cfg["max_pos"]:
+            raise ValueError("sequence longer than max_position_embeddings")
+        if ids.min() < 0 or ids.max() >= self.cfg["vocab"] or types.min() < 0 or \
+                types.max() >= self.cfg["type_vocab"]:
+            raise ValueError("token id / type out of range")
+        dev = self.device
+        t_ids = torch.from_numpy(ids).to(dev)
+        t_ty = torch.from_numpy(types).to(dev)
+        t_cu = torch.from_numpy(cu).to(dev)
+        if out is None:
+            shape = (B, self.out_dim) if self.head == HEAD_CLS_L2 else (B,)
+            out = torch.empty(shape, dtype=torch.float32, device=dev)
+        check(self._L.rag_encoder_forward(self._h, t_ids.data_ptr(), t_ty.data_ptr(),
+                                          t_cu.data_ptr(), B, T, int(lens.max()),
+                                          out.data_ptr(),
+                                          torch.cuda.current_stream(dev).cuda_stream))
+        return out
+
+    def forward_padded(self, ids: np.ndarray, types: np.ndarray, mask: np.ndarray):
+        """HF-style right-padded [B, S] batch -> same outputs as the padded reference."""
+        lens = mask.sum(1).astype(np.int32)
+        cu = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+        sel = mask.astype(bool)
+        return self.forward_packed(ids[sel], types[sel], cu)
+
+
+# ------------------------------------------------------------------ tokenisation
+class WordPiece:
+    """BERT uncased WordPiece from a local vocab.txt ([CLS] a [SEP] (b [SEP]); truncation
+    'longest_first' to max_length; token types 0/1)."""
+
+    def __init__(self, vocab_file: str, max_length: int = 512, lowercase: bool = True):
+        from tokenizers import BertWordPieceTokenizer
+        self.tok = BertWordPieceTokenizer(vocab_file, lowercase=lowercase)
+        self.tok.enable_truncation(max_length=max_length, strategy="longest_first")
+        self.max_length = max_length
+
+    def encode_packed(self, texts, pairs=None):
+        encs = (self.tok.encode_batch(list(texts)) if pairs is None else
+                self.tok.encode_batch(list(zip(texts, pairs))))
+        ids = np.concatenate([np.asarray(e.ids, np.int32) for e in encs])
+        types = np.concatenate([np.asarray(e.type_ids, np.int32) for e in encs])
+        cu = np.concatenate([[0], np.cumsum([len(e.ids) for e in encs])]).astype(np.int32)
+        return ids, types, cu
+
+
+def _load_dir(model_dir: str):
+    with open(os.path.join(model_dir, "config.json")) as f:
+        hf = json.load(f)
+    st = os.path.join(model_dir, "model.safetensors")
+    if not os.path.exists(st):
+        raise FileNotFoundError(f"{st}: only safetensors checkpoints are loaded")
+    return config_from_hf(hf), load_safetensors(st), os.path.join(model_dir, "vocab.txt")
+
+
+# ------------------------------------------------------------------ reference-shaped APIs
+class SentenceTransformer:
+    """`SentenceTransformer(model_dir).encode(...)` for bge-small-en-v1.5 (CLS + L2 norm)."""
+
+    def __init__(self, model_dir: str | None = None, device=None, *, cfg=None, weights=None,
+                 vocab_file=None, max_seq_length: int = 512):
+        if model_dir is not None:
+            cfg, weights, vocab_file = _load_dir(model_dir)
+        if cfg is None or weights is None:
+            raise ValueError("need a local model_dir or cfg + weights (no hub access)")
+        self.encoder = BertEncoder(cfg, weights, HEAD_CLS_L2, device)
+        self.tokenizer = WordPiece(vocab_file, max_seq_length) if vocab_file else None
+        self.max_seq_length = max_seq_length
+
+    def encode(self, sentences, batch_size: int = 32, convert_to_numpy: bool = True,
+               show_progress_bar=None, **kwargs):
+        single = isinstance(sentences, str)
+        texts = [sentences] if single else list(sentences)
+        if not texts:
+            return np.zeros((0, self.encoder.out_dim), np.float32)
+        if self.tokenizer is None:
+            raise RuntimeError("no vocab.txt: use encode_ids with token ids")
+        outs = []
+        for i in range(0, len(texts), max(batch_size, 1)):
+            ids, types, cu = self.tokenizer.encode_packed(texts[i:i + batch_size])
+            outs.append(self.encoder.forward_packed(ids, types, cu))
+        emb = torch.cat(outs)
+        if not convert_to_numpy:
+            return emb[0] if single else emb
+        emb = emb.cpu().numpy()
+        return emb[0] if single else emb
+
+    def encode_ids(self, ids, types, cu) -> np.ndarray:
+        return self.encoder.forward_packed(ids, types, cu).cpu().numpy()
+
+
+class CrossEncoder:
+    """`CrossEncoder(model_dir).predict([[q, t], ...])` for ms-marco-MiniLM-L-6-v2: raw logits
+    (identity activation, num_labels = 1)."""
+
+    def __init__(self, model_dir: str | None = None, device=None, *, cfg=None, weights=None,
+                 vocab_file=None, max_length: int = 512):
+        if model_dir is not None:
+            cfg, weights, vocab_file = _load_dir(model_dir)
+        if cfg is None or weights is None:
+            raise ValueError("need a local model_dir or cfg + weights (no hub access)")
+        self.encoder = BertEncoder(cfg, weights, HEAD_POOLER_CLS, device)
+        self.tokenizer = WordPiece(vocab_file, max_length) if vocab_file else None
+
+    def predict(self, sentences, batch_size: int = 32, convert_to_numpy: bool = True, **kwargs):
+        pairs = [list(p) for p in sentences]
+        if not pairs:
+            return np.zeros((0,), np.float32)
+        if self.tokenizer is None:
+            raise RuntimeError("no vocab.txt: use predict_ids with token ids")
+        outs = []
+        for i in range(0, len(pairs), max(batch_size, 1)):
+            chunk = pairs[i:i + batch_size]
+            ids, types, cu = self.tokenizer.encode_packed([p[0] for p in chunk],
+                                                          [p[1] for p in chunk])
+            outs.append(self.encoder.forward_packed(ids, types, cu))
+        s = torch.cat(outs)
+        return s.cpu().numpy() if convert_to_numpy else s
+
+    def predict_ids(self, ids, types, cu) -> np.ndarray:
+        return self.encoder.forward_packed(ids, types, cu).cpu().numpy()

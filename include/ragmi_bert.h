@@ -1,0 +1,68 @@
+/*
+ * ragmi_bert.h — C ABI of the two BERT-small encoders on the retrieval hot path (libragmi.so).
+ *
+ * Replaces, for the reference (pythonmailer/financial-rag-system):
+ *   main.py:80-84 / main2.py:88-96  get_embedder() -> SentenceTransformer("BAAI/bge-small-en-v1.5")
+ *       .encode(str | list[str])  (main.py:144-149 /embed, 211-213 embed_query; main2.py:170-171
+ *       embed_query_batch)                                   -> rag_encoder_create(head = RAG_HEAD_CLS_L2)
+ *                                                              + rag_encoder_forward
+ *   main.py:86-90 / main2.py:98-103 get_reranker() -> CrossEncoder("cross-encoder/ms-marco-MiniLM-L-6-v2")
+ *       .predict([[q, t], ...])  (main.py:241-247 rerank_documents) -> head = RAG_HEAD_POOLER_CLS
+ * Tokenisation (WordPiece) stays on the host (ragmi.encoders, `tokenizers` + a local vocab).
+ *
+ * Inputs are PACKED sequences: token ids / token-type ids of all B sequences back to back
+ * (int32 [T]) and cu_seqlens (int32 [B+1], cu[0] = 0, cu[B] = T). Right padding in the
+ * reference never changes a valid token's output, so packing is exact.
+ * Outputs: RAG_HEAD_CLS_L2 -> fp32 [B][hidden] (L2-normalised CLS vector);
+ *          RAG_HEAD_POOLER_CLS -> fp32 [B] (raw logit, identity activation).
+ * Built shapes: hidden 384, heads 12 (head_dim 32), intermediate 1536, max_pos <= 512.
+ * Numerics: fp16 GEMM operands, fp32 accumulation / residual stream / LayerNorm / softmax.
+ */
+#ifndef RAGMI_BERT_H
+#define RAGMI_BERT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { RAG_HEAD_CLS_L2 = 0, RAG_HEAD_POOLER_CLS = 1 };
+
+typedef struct {
+  int vocab, hidden, layers, heads, intermediate, max_position, type_vocab;
+  float layer_norm_eps;
+  int head; /* RAG_HEAD_* */
+} rag_bert_config;
+
+typedef struct rag_encoder rag_encoder_t;
+
+/* Number of weight tensors rag_encoder_create expects for `cfg`:
+ * 5 + 16 * layers (+ 4 for RAG_HEAD_POOLER_CLS). */
+int rag_encoder_num_weights(const rag_bert_config* cfg);
+
+/* weights: host fp32 tensors in HF state-dict layout (Linear weight = [out][in]), order:
+ *   embeddings.word_embeddings [vocab][H], .position_embeddings [max_pos][H],
+ *   .token_type_embeddings [type_vocab][H], .LayerNorm.weight [H], .LayerNorm.bias [H];
+ *   per layer l: attention.self.query.{weight [H][H], bias}, .key.{w,b}, .value.{w,b},
+ *     attention.output.dense.{w,b}, attention.output.LayerNorm.{weight,bias},
+ *     intermediate.dense.{weight [I][H], bias [I]}, output.dense.{weight [H][I], bias [H]},
+ *     output.LayerNorm.{weight,bias};
+ *   RAG_HEAD_POOLER_CLS: pooler.dense.{weight [H][H], bias}, classifier.{weight [1][H], bias [1]}. */
+int rag_encoder_create(const rag_bert_config* cfg, const float* const* weights, int n_weights,
+                       int device, rag_encoder_t** out);
+int rag_encoder_destroy(rag_encoder_t* enc);
+
+/* Device pointers, asynchronous on `stream` (hipStream_t). max_len = longest sequence. */
+int rag_encoder_forward(rag_encoder_t* enc, const int32_t* ids_dev, const int32_t* types_dev,
+                        const int32_t* cu_seqlens_dev, int B, int T, int max_len,
+                        float* out_dev, void* stream);
+/* Host pointers, synchronous. */
+int rag_encoder_forward_host(rag_encoder_t* enc, const int32_t* ids, const int32_t* types,
+                             const int32_t* cu_seqlens, int B, int T, float* out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RAGMI_BERT_H */

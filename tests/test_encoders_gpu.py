@@ -1,0 +1,148 @@
+"""GPU tests of the HIP encoders against the encoder oracle (oracle/bert_ref.py, itself pinned
+to transformers by tests/test_oracle_bert.py) and the transformers fixtures.
+
+Tolerances (fp16 GEMM operands, fp32 accumulation/residual/LayerNorm/softmax):
+  bge embeddings (unit vectors): max |diff| <= 2e-3, cosine >= 0.99995
+  cross-encoder logits (|logit| up to ~12 here): max |diff| <= 2e-2 absolute and the
+  reference's rerank order (np.argsort(scores)[::-1][:top_k], main.py:246) preserved on the
+  15-candidate case unless two oracle scores are closer than the tolerance.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import bert_ref as R
+
+pytestmark = pytest.mark.gpu
+
+BGE_ATOL, BGE_COS, CE_ATOL = 2e-3, 0.99995, 2e-2
+
+
+@pytest.fixture(scope="module")
+def golden():
+    from conftest import GOLDEN
+    return dict(np.load(os.path.join(GOLDEN, "bert_golden.npz")))
+
+
+@pytest.fixture(scope="module")
+def bge(gpu, golden):
+    from ragmi.encoders import HEAD_CLS_L2, BertEncoder
+    w = R.make_weights(R.BGE_SMALL, int(golden["bge_seed"]))
+    return BertEncoder(R.BGE_SMALL, w, HEAD_CLS_L2, gpu), w
+
+
+@pytest.fixture(scope="module")
+def ce(gpu, golden):
+    from ragmi.encoders import HEAD_POOLER_CLS, BertEncoder
+    w = R.make_weights(R.MINILM_CE, int(golden["ce_seed"]))
+    return BertEncoder(R.MINILM_CE, w, HEAD_POOLER_CLS, gpu), w
+
+
+def _report(name, a, b):
+    d = np.abs(a - b)
+    print(f"{name}: max|d|={d.max():.3e} mean|d|={d.mean():.3e}")
+    return d.max()
+
+
+def test_bge_golden(bge, golden):
+    enc, w = bge
+    g = golden
+    out = enc.forward_padded(g["ids_q"], g["tt_q"], g["m_q"]).cpu().numpy()
+    assert _report("bge vs transformers", out, g["bge_emb"]) <= BGE_ATOL
+    cos = (out * g["bge_emb"]).sum(1) / np.linalg.norm(out, axis=1)
+    assert cos.min() >= BGE_COS
+    np.testing.assert_allclose(np.linalg.norm(out, axis=1), 1.0, atol=1e-5)
+
+
+def test_ce_golden(ce, golden):
+    enc, w = ce
+    g = golden
+    out = enc.forward_padded(g["ids_p"], g["tt_p"], g["m_p"]).cpu().numpy()
+    assert _report("ce vs transformers", out, g["ce_logits"]) <= CE_ATOL
+
+
+def test_bge_query_batch_32(bge):
+    """main2.py batch_processor shape: 32 queries of 8-32 tokens in one call."""
+    enc, w = bge
+    rng = np.random.default_rng(3)
+    ids, tt, m = R.random_batch(rng, 32, 32)
+    out = enc.forward_padded(ids, tt, m).cpu().numpy()
+    ref = R.bge_embed(w, R.BGE_SMALL, ids, tt, m)
+    assert _report("bge32", out, ref) <= BGE_ATOL
+
+
+def test_ce_rerank_15_pairs(ce):
+    """rerank_documents shape: 15 (query, chunk) pairs of ~100-290 tokens (main.py:241-247)."""
+    enc, w = ce
+    rng = np.random.default_rng(4)
+    ids, tt, m = R.random_batch(rng, 15, 288, pair=True)
+    out = enc.forward_padded(ids, tt, m).cpu().numpy()
+    ref = R.ce_logits(w, R.MINILM_CE, ids, tt, m)
+    assert _report("ce15", out, ref) <= CE_ATOL
+    order, ref_order = R.rerank_order(out, 5), R.rerank_order(ref, 5)
+    srt = np.sort(ref)[::-1]
+    if np.min(np.abs(np.diff(srt[:6]))) > 2 * CE_ATOL:
+        np.testing.assert_array_equal(order, ref_order)
+
+
+def test_batch_independence_bitwise(bge):
+    """A sequence's output does not depend on what else is in the packed batch."""
+    enc, w = bge
+    rng = np.random.default_rng(5)
+    ids, tt, m = R.random_batch(rng, 7, 40)
+    full = enc.forward_padded(ids, tt, m).cpu().numpy()
+    for b in (0, 3, 6):
+        one = enc.forward_padded(ids[b:b + 1], tt[b:b + 1], m[b:b + 1]).cpu().numpy()
+        np.testing.assert_array_equal(one[0], full[b])
+
+
+def test_max_length_512(ce):
+    enc, w = ce
+    rng = np.random.default_rng(6)
+    ids, tt, m = R.random_batch(rng, 2, 512, pair=True)
+    out = enc.forward_padded(ids, tt, m).cpu().numpy()
+    ref = R.ce_logits(w, R.MINILM_CE, ids, tt, m)
+    assert _report("ce512", out, ref) <= CE_ATOL
+    with pytest.raises(ValueError):
+        enc.forward_packed(np.ones(513, np.int32), np.zeros(513, np.int32),
+                           np.array([0, 513], np.int32))
+
+
+def test_text_api_with_local_vocab(gpu, tmp_path):
+    """SentenceTransformer.encode / CrossEncoder.predict end to end from text, with a local
+    vocab.txt (synthetic: the real one is not on disk) and a safetensors checkpoint."""
+    from safetensors.numpy import save_file
+
+    from ragmi.encoders import CrossEncoder, SentenceTransformer
+    words = ["[PAD]"] + [f"[unused{i}]" for i in range(99)] + ["[UNK]", "[CLS]", "[SEP]",
+                                                               "[MASK]"]
+    words += sorted({w.lower().strip("?,.") for w in (
+        "what was apple total revenue in fiscal 2023 how much did the company spend on "
+        "research and development risk factors net income iphone services margin").split()})
+    words += [chr(c) for c in range(ord("a"), ord("z") + 1)] + [str(d) for d in range(10)]
+    voc = tmp_path / "vocab.txt"
+    voc.write_text("\n".join(words) + "\n")
+    cfg = dict(R.BGE_SMALL, vocab=len(words), layers=2)
+    w = R.make_weights(cfg, 7)
+    d = tmp_path / "bge"
+    d.mkdir()
+    save_file(w, str(d / "model.safetensors"))
+    (d / "config.json").write_text(
+        '{"vocab_size": %d, "hidden_size": 384, "num_hidden_layers": 2, '
+        '"num_attention_heads": 12, "intermediate_size": 1536, '
+        '"max_position_embeddings": 512, "type_vocab_size": 2, "layer_norm_eps": 1e-12}'
+        % len(words))
+    (d / "vocab.txt").write_text(voc.read_text())
+    st = SentenceTransformer(str(d), device=gpu)
+    one = st.encode("What was Apple total revenue in fiscal 2023?")
+    many = st.encode(["What was Apple total revenue in fiscal 2023?", "risk factors"])
+    assert one.shape == (384,) and many.shape == (2, 384) and one.dtype == np.float32
+    np.testing.assert_array_equal(one, many[0])
+    assert st.encode([]).shape == (0, 384)
+    cw = R.make_weights(dict(R.MINILM_CE, vocab=len(words), layers=2), 8)
+    ce = CrossEncoder(device=gpu, cfg=dict(R.MINILM_CE, vocab=len(words), layers=2),
+                      weights=cw, vocab_file=str(voc))
+    s = ce.predict([["net income", "apple net income 2023"], ["net income", "iphone margin"]])
+    assert s.shape == (2,) and s.dtype == np.float32
