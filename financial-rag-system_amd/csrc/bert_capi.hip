@@ -16,14 +16,19 @@ using namespace ragmi::bert;
 
 struct Layer {
   _Float16 *wqkv = nullptr, *wo = nullptr, *w1 = nullptr, *w2 = nullptr;
+  _Float16 *wqkv_l = nullptr, *wo_l = nullptr, *w1_l = nullptr, *w2_l = nullptr;  // fp16x3
   float *bqkv = nullptr, *bo = nullptr, *g1 = nullptr, *be1 = nullptr, *bi1 = nullptr,
         *bi2 = nullptr, *g2 = nullptr, *be2 = nullptr;
 };
 
 __global__ void f32_to_f16_kernel(const float* __restrict__ in, _Float16* __restrict__ out,
-                                  int64_t n) {
+                                  _Float16* __restrict__ out_lo, int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = (_Float16)in[i];
+  if (i < n) {
+    const _Float16 h = (_Float16)in[i];
+    out[i] = h;
+    if (out_lo) out_lo[i] = lo_part(in[i], h);
+  }
 }
 
 }  // namespace
@@ -40,6 +45,7 @@ struct rag_encoder {
   int64_t cap_t = 0;
   float *x = nullptr, *y = nullptr;
   _Float16 *xh = nullptr, *qkv = nullptr, *ctx = nullptr, *ff = nullptr;
+  _Float16 *xl = nullptr, *qkv_l = nullptr, *ctx_l = nullptr, *ff_l = nullptr;  // fp16x3
   // host-entry staging
   void* stage = nullptr;
   size_t stage_bytes = 0;
@@ -61,12 +67,18 @@ int up_f32(rag_encoder* e, float** dst, const float* src, size_t n) {
   return RAG_OK;
 }
 
-// fp16 copy of one or more host fp32 blocks laid end to end ([rows][K] each)
-int up_f16(rag_encoder* e, _Float16** dst, std::initializer_list<std::pair<const float*, size_t>> parts) {
+// fp16 copy (and, for fp16x3, the fp16 residual lo = fp16(w - hi)) of one or more host fp32
+// blocks laid end to end ([rows][K] each)
+int up_f16(rag_encoder* e, _Float16** dst, _Float16** dst_lo,
+           std::initializer_list<std::pair<const float*, size_t>> parts) {
   size_t n = 0;
   for (auto& p : parts) n += p.second;
   int rc = dalloc(e, dst, n);
   if (rc) return rc;
+  if (dst_lo) {
+    rc = dalloc(e, dst_lo, n);
+    if (rc) return rc;
+  }
   float* tmp = nullptr;
   RAG_HIP(hipMalloc(reinterpret_cast<void**>(&tmp), n * 4));
   size_t off = 0;
@@ -77,7 +89,8 @@ int up_f16(rag_encoder* e, _Float16** dst, std::initializer_list<std::pair<const
     }
     off += p.second;
   }
-  f32_to_f16_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256)>>>(tmp, *dst, (int64_t)n);
+  f32_to_f16_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256)>>>(
+      tmp, *dst, dst_lo ? *dst_lo : nullptr, (int64_t)n);
   RAG_HIP(hipDeviceSynchronize());
   (void)hipFree(tmp);
   return RAG_OK;
@@ -87,11 +100,18 @@ int ensure_ws(rag_encoder* e, int64_t T) {
   if (T <= e->cap_t) return RAG_OK;
   const int64_t cap = std::max<int64_t>(T, std::max<int64_t>(2 * e->cap_t, 1024));
   for (void* p : {(void*)e->x, (void*)e->y, (void*)e->xh, (void*)e->qkv, (void*)e->ctx,
-                  (void*)e->ff})
+                  (void*)e->ff, (void*)e->xl, (void*)e->qkv_l, (void*)e->ctx_l, (void*)e->ff_l})
     if (p) (void)hipFree(p);
   e->x = e->y = nullptr;
   e->xh = e->qkv = e->ctx = e->ff = nullptr;
+  e->xl = e->qkv_l = e->ctx_l = e->ff_l = nullptr;
   e->cap_t = 0;
+  if (e->cfg.precision == RAG_PREC_FP16X3) {
+    RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->xl), cap * H * 2));
+    RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->qkv_l), cap * 3 * H * 2));
+    RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->ctx_l), cap * H * 2));
+    RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->ff_l), cap * FF * 2));
+  }
   RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->x), cap * H * 4));
   RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->y), cap * H * 4));
   RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->xh), cap * H * 2));
@@ -103,10 +123,14 @@ int ensure_ws(rag_encoder* e, int64_t T) {
 }
 
 template <int EPI>
-void gemm(const _Float16* A, const _Float16* W, const float* bias, int M, int N, int K, void* C,
-          hipStream_t st) {
-  gemm_kernel<EPI><<<dim3(N / BN, (M + BM - 1) / BM), dim3(256), 0, st>>>(A, W, bias, M, N, K,
-                                                                          C);
+void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float16* Wl,
+          const float* bias, int M, int N, int K, void* C, _Float16* Clo, hipStream_t st) {
+  const dim3 grid(N / BN, (M + BM - 1) / BM);
+  if (Al)
+    gemm_kernel<EPI, true><<<grid, dim3(256), 0, st>>>(A, Al, W, Wl, bias, M, N, K, C, Clo);
+  else
+    gemm_kernel<EPI, false><<<grid, dim3(256), 0, st>>>(A, nullptr, W, nullptr, bias, M, N, K,
+                                                        C, nullptr);
 }
 
 int forward_locked(rag_encoder* e, const int32_t* ids, const int32_t* types, const int32_t* cu,
@@ -116,20 +140,25 @@ int forward_locked(rag_encoder* e, const int32_t* ids, const int32_t* types, con
   if (rc) return rc;
   embed_ln_kernel<<<dim3((max_len + 3) / 4, B), dim3(256), 0, st>>>(
       ids, types, cu, e->wemb, e->pemb, e->temb, e->eg, e->eb, c.layer_norm_eps, c.vocab,
-      c.type_vocab, c.max_position, e->x, e->xh);
+      c.type_vocab, c.max_position, e->x, e->xh, e->xl);
   const float scale = 1.0f / sqrtf((float)HD);
   const unsigned ln_grid = (unsigned)((T + 3) / 4);
+  const dim3 agrid((max_len + 63) / 64, NH, B);
   for (const Layer& L : e->layers) {
-    gemm<kEpiF16>(e->xh, L.wqkv, L.bqkv, T, 3 * H, H, e->qkv, st);
-    attn_kernel<<<dim3((max_len + 63) / 64, NH, B), dim3(256), 0, st>>>(e->qkv, cu, scale,
-                                                                        e->ctx);
-    gemm<kEpiF32>(e->ctx, L.wo, L.bo, T, H, H, e->y, st);
+    gemm<kEpiF16>(e->xh, e->xl, L.wqkv, L.wqkv_l, L.bqkv, T, 3 * H, H, e->qkv, e->qkv_l, st);
+    if (e->xl)
+      attn_kernel<true><<<agrid, dim3(256), 0, st>>>(e->qkv, e->qkv_l, cu, scale, e->ctx,
+                                                     e->ctx_l);
+    else
+      attn_kernel<false><<<agrid, dim3(256), 0, st>>>(e->qkv, nullptr, cu, scale, e->ctx,
+                                                      nullptr);
+    gemm<kEpiF32>(e->ctx, e->ctx_l, L.wo, L.wo_l, L.bo, T, H, H, e->y, nullptr, st);
     add_ln_kernel<<<dim3(ln_grid), dim3(256), 0, st>>>(e->x, e->y, L.g1, L.be1,
-                                                       c.layer_norm_eps, e->xh, T);
-    gemm<kEpiGeluF16>(e->xh, L.w1, L.bi1, T, FF, H, e->ff, st);
-    gemm<kEpiF32>(e->ff, L.w2, L.bi2, T, H, FF, e->y, st);
+                                                       c.layer_norm_eps, e->xh, e->xl, T);
+    gemm<kEpiGeluF16>(e->xh, e->xl, L.w1, L.w1_l, L.bi1, T, FF, H, e->ff, e->ff_l, st);
+    gemm<kEpiF32>(e->ff, e->ff_l, L.w2, L.w2_l, L.bi2, T, H, FF, e->y, nullptr, st);
     add_ln_kernel<<<dim3(ln_grid), dim3(256), 0, st>>>(e->x, e->y, L.g2, L.be2,
-                                                       c.layer_norm_eps, e->xh, T);
+                                                       c.layer_norm_eps, e->xh, e->xl, T);
   }
   if (c.head == RAG_HEAD_CLS_L2)
     cls_normalize_kernel<<<dim3(B), dim3(64), 0, st>>>(e->x, cu, out);
@@ -160,6 +189,8 @@ int rag_encoder_create(const rag_bert_config* cfg, const float* const* w, int n_
     return ragmi::fail(RAG_EINVAL, "bad config");
   if (cfg->head != RAG_HEAD_CLS_L2 && cfg->head != RAG_HEAD_POOLER_CLS)
     return ragmi::fail(RAG_EINVAL, "unknown head");
+  if (cfg->precision != RAG_PREC_FP16 && cfg->precision != RAG_PREC_FP16X3)
+    return ragmi::fail(RAG_EINVAL, "unknown precision");
   if (n_weights != rag_encoder_num_weights(cfg))
     return ragmi::fail(RAG_EINVAL, "wrong number of weight tensors");
   for (int i = 0; i < n_weights; ++i)
@@ -182,7 +213,9 @@ int rag_encoder_create(const rag_bert_config* cfg, const float* const* w, int n_
   for (int l = 0; l < cfg->layers && !rc; ++l) {
     const float* const* p = w + 5 + 16 * l;
     Layer& L = e->layers[l];
-    chk(up_f16(e, &L.wqkv, {{p[0], Hs * H}, {p[2], Hs * H}, {p[4], Hs * H}}));
+    const bool sp = cfg->precision == RAG_PREC_FP16X3;
+    chk(up_f16(e, &L.wqkv, sp ? &L.wqkv_l : nullptr,
+               {{p[0], Hs * H}, {p[2], Hs * H}, {p[4], Hs * H}}));
     {
       std::vector<float> b(3 * H);
       std::copy(p[1], p[1] + H, b.begin());
@@ -190,13 +223,13 @@ int rag_encoder_create(const rag_bert_config* cfg, const float* const* w, int n_
       std::copy(p[5], p[5] + H, b.begin() + 2 * H);
       chk(up_f32(e, &L.bqkv, b.data(), 3 * Hs));
     }
-    chk(up_f16(e, &L.wo, {{p[6], Hs * H}}));
+    chk(up_f16(e, &L.wo, sp ? &L.wo_l : nullptr, {{p[6], Hs * H}}));
     chk(up_f32(e, &L.bo, p[7], Hs));
     chk(up_f32(e, &L.g1, p[8], Hs));
     chk(up_f32(e, &L.be1, p[9], Hs));
-    chk(up_f16(e, &L.w1, {{p[10], (size_t)FF * H}}));
+    chk(up_f16(e, &L.w1, sp ? &L.w1_l : nullptr, {{p[10], (size_t)FF * H}}));
     chk(up_f32(e, &L.bi1, p[11], FF));
-    chk(up_f16(e, &L.w2, {{p[12], Hs * FF}}));
+    chk(up_f16(e, &L.w2, sp ? &L.w2_l : nullptr, {{p[12], Hs * FF}}));
     chk(up_f32(e, &L.bi2, p[13], Hs));
     chk(up_f32(e, &L.g2, p[14], Hs));
     chk(up_f32(e, &L.be2, p[15], Hs));
@@ -223,7 +256,8 @@ int rag_encoder_destroy(rag_encoder_t* e) {
   (void)hipDeviceSynchronize();
   for (void* p : e->allocs) (void)hipFree(p);
   for (void* p : {(void*)e->x, (void*)e->y, (void*)e->xh, (void*)e->qkv, (void*)e->ctx,
-                  (void*)e->ff, e->stage})
+                  (void*)e->ff, (void*)e->xl, (void*)e->qkv_l, (void*)e->ctx_l, (void*)e->ff_l,
+                  e->stage})
     if (p) (void)hipFree(p);
   delete e;
   return RAG_OK;

@@ -23,6 +23,10 @@ constexpr int FF = 1536;    // intermediate
 
 typedef _Float16 half4 __attribute__((ext_vector_type(4)));
 
+// fp16x3 split: v = hi + lo with hi = fp16(v), lo = fp16(v - hi); a*b ~ ah*bh + ah*bl + al*bh
+// (relative error ~2^-22) on the fp16 MFMA pipe.
+__device__ __forceinline__ _Float16 lo_part(float v, _Float16 hi) { return (_Float16)(v - (float)hi); }
+
 __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
 }
@@ -34,7 +38,8 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(
     const int* __restrict__ ids, const int* __restrict__ types, const int* __restrict__ cu,
     const float* __restrict__ wemb, const float* __restrict__ pemb, const float* __restrict__ temb,
     const float* __restrict__ g, const float* __restrict__ bt, float eps, int vocab,
-    int type_vocab, int max_pos, float* __restrict__ x, _Float16* __restrict__ xh) {
+    int type_vocab, int max_pos, float* __restrict__ x, _Float16* __restrict__ xh,
+    _Float16* __restrict__ xl) {
   const int b = blockIdx.y;
   const int pos = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -67,7 +72,9 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(
     const int c = lane + 64 * j;
     const float y = (v[j] - mu) * rs * g[c] + bt[c];
     x[t * H + c] = y;
-    xh[t * H + c] = (_Float16)y;
+    const _Float16 yh = (_Float16)y;
+    xh[t * H + c] = yh;
+    if (xl) xl[t * H + c] = lo_part(y, yh);
   }
 }
 
@@ -78,7 +85,8 @@ __global__ __launch_bounds__(256) void add_ln_kernel(float* __restrict__ x,
                                                      const float* __restrict__ y,
                                                      const float* __restrict__ g,
                                                      const float* __restrict__ bt, float eps,
-                                                     _Float16* __restrict__ xh, int T) {
+                                                     _Float16* __restrict__ xh,
+                                                     _Float16* __restrict__ xl, int T) {
   const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (t >= T) return;
@@ -104,7 +112,9 @@ __global__ __launch_bounds__(256) void add_ln_kernel(float* __restrict__ x,
     const int c = lane + 64 * j;
     const float o = (v[j] - mu) * rs * g[c] + bt[c];
     x[t * H + c] = o;
-    xh[t * H + c] = (_Float16)o;
+    const _Float16 oh = (_Float16)o;
+    xh[t * H + c] = oh;
+    if (xl) xl[t * H + c] = lo_part(o, oh);
   }
 }
 
@@ -119,37 +129,44 @@ constexpr int BM = 128, BN = 128, BK = 64;
 
 __device__ __forceinline__ int swz(int row, int chunk) { return row * 8 + (chunk ^ (row & 7)); }
 
-template <int EPI>
+template <int EPI, bool SPLIT>
 __global__ __launch_bounds__(256) void gemm_kernel(const _Float16* __restrict__ A,
+                                                   const _Float16* __restrict__ Al,
                                                    const _Float16* __restrict__ W,
+                                                   const _Float16* __restrict__ Wl,
                                                    const float* __restrict__ bias, int M, int N,
-                                                   int K, void* __restrict__ Cout) {
-  __shared__ half8 lds[2 * 2 * BM * (BK / 8)];   // [buf][A|B][row][8 chunks]
+                                                   int K, void* __restrict__ Cout,
+                                                   _Float16* __restrict__ Clo) {
+  // SPLIT (fp16x3): tiles of A_hi, A_lo, W_hi, W_lo; 3 MFMAs per product.
+  constexpr int NP = SPLIT ? 4 : 2;                     // staged planes
+  __shared__ half8 lds[2 * NP * BM * (BK / 8)];         // [buf][plane][row][8 chunks]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
   const int nk = K / BK;
+  const _Float16* src[4] = {A, W, Al, Wl};
 
-  half8 ra[4], rb[4];
+  half8 rg[NP][4];
   auto gload = [&](int kt) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = tid + 256 * i;
-      const int row = c >> 3, ch = c & 7;
-      const int am = min(m0 + row, M - 1);
-      ra[i] = *reinterpret_cast<const half8*>(A + (int64_t)am * K + kt * BK + ch * 8);
-      rb[i] = *reinterpret_cast<const half8*>(W + (int64_t)(n0 + row) * K + kt * BK + ch * 8);
-    }
+    for (int p = 0; p < NP; ++p)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = tid + 256 * i;
+        const int row = c >> 3, ch = c & 7;
+        const int r = (p & 1) ? (n0 + row) : min(m0 + row, M - 1);   // planes 0,2: A; 1,3: W
+        rg[p][i] = *reinterpret_cast<const half8*>(src[p] + (int64_t)r * K + kt * BK + ch * 8);
+      }
   };
   auto lstore = [&](int buf) {
-    half8* la = lds + buf * (2 * BM * 8);
-    half8* lb = la + BM * 8;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = tid + 256 * i;
-      const int row = c >> 3, ch = c & 7;
-      la[swz(row, ch)] = ra[i];
-      lb[swz(row, ch)] = rb[i];
+    for (int p = 0; p < NP; ++p) {
+      half8* lp = lds + (buf * NP + p) * (BM * 8);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = tid + 256 * i;
+        lp[swz(c >> 3, c & 7)] = rg[p][i];
+      }
     }
   };
 
@@ -165,8 +182,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(const _Float16* __restrict__ 
   for (int kt = 0; kt < nk; ++kt) {
     const int buf = kt & 1;
     if (kt + 1 < nk) gload(kt + 1);
-    const half8* la = lds + buf * (2 * BM * 8);
-    const half8* lb = la + BM * 8;
+    const half8* la = lds + (buf * NP + 0) * (BM * 8);
+    const half8* lb = lds + (buf * NP + 1) * (BM * 8);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       half8 af[4], bf[4];
@@ -175,6 +192,22 @@ __global__ __launch_bounds__(256) void gemm_kernel(const _Float16* __restrict__ 
       for (int i = 0; i < 4; ++i) af[i] = la[swz(wr * 64 + i * 16 + (lane & 15), ch)];
 #pragma unroll
       for (int j = 0; j < 4; ++j) bf[j] = lb[swz(wc * 64 + j * 16 + (lane & 15), ch)];
+      if constexpr (SPLIT) {
+        const half8* lal = lds + (buf * NP + 2) * (BM * 8);
+        const half8* lbl = lds + (buf * NP + 3) * (BM * 8);
+        half8 afl[4], bfl[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) afl[i] = lal[swz(wr * 64 + i * 16 + (lane & 15), ch)];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bfl[j] = lbl[swz(wc * 64 + j * 16 + (lane & 15), ch)];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(afl[i], bf[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bfl[j], acc[i][j], 0, 0, 0);
+          }
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -201,7 +234,9 @@ __global__ __launch_bounds__(256) void gemm_kernel(const _Float16* __restrict__ 
             static_cast<float*>(Cout)[(int64_t)m * N + n] = v;
           } else {
             if constexpr (EPI == kEpiGeluF16) v = gelu_erf(v);
-            static_cast<_Float16*>(Cout)[(int64_t)m * N + n] = (_Float16)v;
+            const _Float16 vh = (_Float16)v;
+            static_cast<_Float16*>(Cout)[(int64_t)m * N + n] = vh;
+            if constexpr (SPLIT) Clo[(int64_t)m * N + n] = lo_part(v, vh);
           }
         }
       }
@@ -216,24 +251,31 @@ __global__ __launch_bounds__(256) void gemm_kernel(const _Float16* __restrict__ 
 // v_mfma_f32_16x16x32_f16 (head_dim 32 = one K step); online softmax in fp32.
 // qkv: fp16 [T][3H] (Q | K | V, head h = columns h*32 .. +31 of each); ctx: fp16 [T][H].
 // ----------------------------------------------------------------------------------------
+template <bool SPLIT>
 __global__ __launch_bounds__(256) void attn_kernel(const _Float16* __restrict__ qkv,
+                                                   const _Float16* __restrict__ qkv_lo,
                                                    const int* __restrict__ cu, float scale,
-                                                   _Float16* __restrict__ ctx) {
-  __shared__ _Float16 kl[32][HD + 8];     // [key][dim] (+8 pad: 80-B rows)
-  __shared__ _Float16 vt[HD][32 + 8];     // [dim][key]
-  __shared__ _Float16 pl[4][16][32 + 8];  // per wave P tile [row][key]
+                                                   _Float16* __restrict__ ctx,
+                                                   _Float16* __restrict__ ctx_lo) {
+  constexpr int NP = SPLIT ? 2 : 1;
+  __shared__ _Float16 kl[NP][32][HD + 8];     // [plane][key][dim] (+8 pad: 80-B rows)
+  __shared__ _Float16 vt[NP][HD][32 + 8];     // [plane][dim][key]
+  __shared__ _Float16 pl[NP][4][16][32 + 8];  // [plane][wave] P tile [row][key]
   const int b = blockIdx.z, h = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int base = cu[b], len = cu[b + 1] - cu[b];
   const int q0 = blockIdx.x * 64 + wid * 16;
   if (blockIdx.x * 64 >= len) return;
   const int qrow = q0 + (lane & 15);
+  const _Float16* planes[2] = {qkv, qkv_lo};
 
-  half8 qf;
+  half8 qf[NP];
   {
     const int r = min(qrow, len - 1);
-    qf = *reinterpret_cast<const half8*>(qkv + (int64_t)(base + r) * (3 * H) + h * HD +
-                                         8 * (lane >> 4));
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+      qf[p] = *reinterpret_cast<const half8*>(planes[p] + (int64_t)(base + r) * (3 * H) +
+                                              h * HD + 8 * (lane >> 4));
   }
   floatx4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = {0.f, 0.f, 0.f, 0.f};
   float mrow[4], lrow[4];
@@ -247,23 +289,32 @@ __global__ __launch_bounds__(256) void attn_kernel(const _Float16* __restrict__ 
     // stage K and V^T of keys kb .. kb+31 (zeros past the end)
     {
       const int key = tid >> 3, dc = (tid & 7) * 4;
-      half4 kv = {0, 0, 0, 0}, vv = {0, 0, 0, 0};
-      if (kb + key < len) {
-        const _Float16* src = qkv + (int64_t)(base + kb + key) * (3 * H) + h * HD + dc;
-        kv = *reinterpret_cast<const half4*>(src + H);
-        vv = *reinterpret_cast<const half4*>(src + 2 * H);
-      }
-      *reinterpret_cast<half4*>(&kl[key][dc]) = kv;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) vt[dc + e][key] = vv[e];
+      for (int p = 0; p < NP; ++p) {
+        half4 kv = {0, 0, 0, 0}, vv = {0, 0, 0, 0};
+        if (kb + key < len) {
+          const _Float16* src = planes[p] + (int64_t)(base + kb + key) * (3 * H) + h * HD + dc;
+          kv = *reinterpret_cast<const half4*>(src + H);
+          vv = *reinterpret_cast<const half4*>(src + 2 * H);
+        }
+        *reinterpret_cast<half4*>(&kl[p][key][dc]) = kv;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) vt[p][dc + e][key] = vv[e];
+      }
     }
     __syncthreads();
     // S = Q K^T for two 16-key tiles
     floatx4 s[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const half8 kf = *reinterpret_cast<const half8*>(&kl[16 * j + (lane & 15)][8 * (lane >> 4)]);
-      s[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(qf, kf, floatx4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      const half8 kf = *reinterpret_cast<const half8*>(&kl[0][16 * j + (lane & 15)][8 * (lane >> 4)]);
+      s[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(qf[0], kf, floatx4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      if constexpr (SPLIT) {
+        const half8 kfl =
+            *reinterpret_cast<const half8*>(&kl[1][16 * j + (lane & 15)][8 * (lane >> 4)]);
+        s[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(qf[1], kf, s[j], 0, 0, 0);
+        s[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(qf[0], kfl, s[j], 0, 0, 0);
+      }
     }
     // lane: rows 4(l>>4)+i, keys kb + 16j + (l&15)
     float p[2][4];
@@ -285,7 +336,8 @@ __global__ __launch_bounds__(256) void attn_kernel(const _Float16* __restrict__ 
       float rsum = 0.f;
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const float e = (float)(_Float16)__expf(s[j][i] - mnew);   // P as MFMA sees it
+        float e = __expf(s[j][i] - mnew);
+        if constexpr (!SPLIT) e = (float)(_Float16)e;   // P exactly as the MFMA sees it
         p[j][i] = e;
         rsum += e;
       }
@@ -302,11 +354,24 @@ __global__ __launch_bounds__(256) void attn_kernel(const _Float16* __restrict__ 
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) pl[wid][4 * (lane >> 4) + i][16 * j + (lane & 15)] = (_Float16)p[j][i];
+      for (int i = 0; i < 4; ++i) {
+        const _Float16 ph = (_Float16)p[j][i];
+        pl[0][wid][4 * (lane >> 4) + i][16 * j + (lane & 15)] = ph;
+        if constexpr (SPLIT) pl[1][wid][4 * (lane >> 4) + i][16 * j + (lane & 15)] = lo_part(p[j][i], ph);
+      }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    const half8 pf = *reinterpret_cast<const half8*>(&pl[wid][lane & 15][8 * (lane >> 4)]);
-    const half8 v0 = *reinterpret_cast<const half8*>(&vt[lane & 15][8 * (lane >> 4)]);
-    const half8 v1 = *reinterpret_cast<const half8*>(&vt[16 + (lane & 15)][8 * (lane >> 4)]);
+    const half8 pf = *reinterpret_cast<const half8*>(&pl[0][wid][lane & 15][8 * (lane >> 4)]);
+    const half8 v0 = *reinterpret_cast<const half8*>(&vt[0][lane & 15][8 * (lane >> 4)]);
+    const half8 v1 = *reinterpret_cast<const half8*>(&vt[0][16 + (lane & 15)][8 * (lane >> 4)]);
+    if constexpr (SPLIT) {
+      const half8 pfl = *reinterpret_cast<const half8*>(&pl[1][wid][lane & 15][8 * (lane >> 4)]);
+      const half8 v0l = *reinterpret_cast<const half8*>(&vt[1][lane & 15][8 * (lane >> 4)]);
+      const half8 v1l = *reinterpret_cast<const half8*>(&vt[1][16 + (lane & 15)][8 * (lane >> 4)]);
+      o0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(pfl, v0, o0, 0, 0, 0);
+      o1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(pfl, v1, o1, 0, 0, 0);
+      o0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(pf, v0l, o0, 0, 0, 0);
+      o1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(pf, v1l, o1, 0, 0, 0);
+    }
     o0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(pf, v0, o0, 0, 0, 0);
     o1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(pf, v1, o1, 0, 0, 0);
     __syncthreads();
@@ -317,9 +382,15 @@ __global__ __launch_bounds__(256) void attn_kernel(const _Float16* __restrict__ 
     const int r = q0 + 4 * (lane >> 4) + i;
     if (r < len) {
       const float inv = 1.0f / lrow[i];
-      _Float16* dst = ctx + (int64_t)(base + r) * H + h * HD;
-      dst[lane & 15] = (_Float16)(o0[i] * inv);
-      dst[16 + (lane & 15)] = (_Float16)(o1[i] * inv);
+      const int64_t off = (int64_t)(base + r) * H + h * HD;
+      const float a = o0[i] * inv, c = o1[i] * inv;
+      const _Float16 ah = (_Float16)a, ch = (_Float16)c;
+      ctx[off + (lane & 15)] = ah;
+      ctx[off + 16 + (lane & 15)] = ch;
+      if constexpr (SPLIT) {
+        ctx_lo[off + (lane & 15)] = lo_part(a, ah);
+        ctx_lo[off + 16 + (lane & 15)] = lo_part(c, ch);
+      }
     }
   }
 }

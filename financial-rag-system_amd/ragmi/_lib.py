@@ -72,7 +72,8 @@ class RagBertConfig(ctypes.Structure):
     _fields_ = [("vocab", ctypes.c_int), ("hidden", ctypes.c_int), ("layers", ctypes.c_int),
                 ("heads", ctypes.c_int), ("intermediate", ctypes.c_int),
                 ("max_position", ctypes.c_int), ("type_vocab", ctypes.c_int),
-                ("layer_norm_eps", ctypes.c_float), ("head", ctypes.c_int)]
+                ("layer_norm_eps", ctypes.c_float), ("head", ctypes.c_int),
+                ("precision", ctypes.c_int)]
 
 
 c_i32p_ = ctypes.POINTER(ctypes.c_int32)

@@ -25,6 +25,9 @@ from ._lib import check
 
 HEAD_CLS_L2 = 0        # sentence-transformers: Pooling(cls) + Normalize  (bge)
 HEAD_POOLER_CLS = 1    # BertForSequenceClassification, num_labels = 1   (cross-encoder)
+PREC_FP16 = 0          # fp16 GEMM / attention operands, fp32 accumulation
+PREC_FP16X3 = 1        # split fp16 products (a_hi b_hi + a_hi b_lo + a_lo b_hi): ~fp32 accuracy
+PRECISIONS = {"fp16": PREC_FP16, "fp16x3": PREC_FP16X3}
 
 
 # ------------------------------------------------------------------ weights
@@ -72,7 +75,8 @@ def config_from_hf(cfg: dict) -> dict:
 class BertEncoder:
     """One encoder instance in HBM (fp16 GEMM weights, fp32 norms/embeddings)."""
 
-    def __init__(self, cfg: dict, weights: dict, head: int, device=None):
+    def __init__(self, cfg: dict, weights: dict, head: int, device=None,
+                 precision: str = "fp16x3"):
         _lib.require_gpu()
         self._L = _lib.load()
         self.device = torch.device(device if device is not None else
@@ -80,8 +84,10 @@ class BertEncoder:
         if self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
         self.cfg, self.head = dict(cfg), head
+        self.precision = precision
         c = _lib.RagBertConfig(cfg["vocab"], cfg["hidden"], cfg["layers"], cfg["heads"],
-                               cfg["inter"], cfg["max_pos"], cfg["type_vocab"], cfg["eps"], head)
+                               cfg["inter"], cfg["max_pos"], cfg["type_vocab"], cfg["eps"], head,
+                               PRECISIONS[precision])
         names = weight_order(cfg["layers"], head)
         if self._L.rag_encoder_num_weights(ctypes.byref(c)) != len(names):
             raise RuntimeError("weight order / ABI mismatch")
@@ -176,12 +182,12 @@ class SentenceTransformer:
     """`SentenceTransformer(model_dir).encode(...)` for bge-small-en-v1.5 (CLS + L2 norm)."""
 
     def __init__(self, model_dir: str | None = None, device=None, *, cfg=None, weights=None,
-                 vocab_file=None, max_seq_length: int = 512):
+                 vocab_file=None, max_seq_length: int = 512, precision: str = "fp16x3"):
         if model_dir is not None:
             cfg, weights, vocab_file = _load_dir(model_dir)
         if cfg is None or weights is None:
             raise ValueError("need a local model_dir or cfg + weights (no hub access)")
-        self.encoder = BertEncoder(cfg, weights, HEAD_CLS_L2, device)
+        self.encoder = BertEncoder(cfg, weights, HEAD_CLS_L2, device, precision)
         self.tokenizer = WordPiece(vocab_file, max_seq_length) if vocab_file else None
         self.max_seq_length = max_seq_length
 
@@ -212,12 +218,12 @@ class CrossEncoder:
     (identity activation, num_labels = 1)."""
 
     def __init__(self, model_dir: str | None = None, device=None, *, cfg=None, weights=None,
-                 vocab_file=None, max_length: int = 512):
+                 vocab_file=None, max_length: int = 512, precision: str = "fp16x3"):
         if model_dir is not None:
             cfg, weights, vocab_file = _load_dir(model_dir)
         if cfg is None or weights is None:
             raise ValueError("need a local model_dir or cfg + weights (no hub access)")
-        self.encoder = BertEncoder(cfg, weights, HEAD_POOLER_CLS, device)
+        self.encoder = BertEncoder(cfg, weights, HEAD_POOLER_CLS, device, precision)
         self.tokenizer = WordPiece(vocab_file, max_length) if vocab_file else None
 
     def predict(self, sentences, batch_size: int = 32, convert_to_numpy: bool = True, **kwargs):

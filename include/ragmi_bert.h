@@ -16,7 +16,8 @@
  * Outputs: RAG_HEAD_CLS_L2 -> fp32 [B][hidden] (L2-normalised CLS vector);
  *          RAG_HEAD_POOLER_CLS -> fp32 [B] (raw logit, identity activation).
  * Built shapes: hidden 384, heads 12 (head_dim 32), intermediate 1536, max_pos <= 512.
- * Numerics: fp16 GEMM operands, fp32 accumulation / residual stream / LayerNorm / softmax.
+ * Numerics: fp16 (or split fp16x3) GEMM/attention operands, fp32 accumulation / residual
+ * stream / LayerNorm / softmax statistics.
  */
 #ifndef RAGMI_BERT_H
 #define RAGMI_BERT_H
@@ -29,10 +30,15 @@ extern "C" {
 
 enum { RAG_HEAD_CLS_L2 = 0, RAG_HEAD_POOLER_CLS = 1 };
 
+enum { RAG_PREC_FP16 = 0, RAG_PREC_FP16X3 = 1 };
+
 typedef struct {
   int vocab, hidden, layers, heads, intermediate, max_position, type_vocab;
   float layer_norm_eps;
-  int head; /* RAG_HEAD_* */
+  int head;      /* RAG_HEAD_* */
+  int precision; /* RAG_PREC_FP16: fp16 GEMM/attention operands (fastest);
+                    RAG_PREC_FP16X3: every product as a_hi*b_hi + a_hi*b_lo + a_lo*b_hi on the
+                    fp16 MFMA pipe (~fp32 accuracy, 3x the MFMA work) */
 } rag_bert_config;
 
 typedef struct rag_encoder rag_encoder_t;

@@ -1,10 +1,12 @@
 """GPU tests of the HIP encoders against the encoder oracle (oracle/bert_ref.py, itself pinned
 to transformers by tests/test_oracle_bert.py) and the transformers fixtures.
 
-Tolerances (fp16 GEMM operands, fp32 accumulation/residual/LayerNorm/softmax):
-  bge embeddings (unit vectors): max |diff| <= 2e-3, cosine >= 0.99995
-  cross-encoder logits (|logit| up to ~12 here): max |diff| <= 2e-2 absolute and the
-  reference's rerank order (np.argsort(scores)[::-1][:top_k], main.py:246) preserved on the
+Tolerances (fp32 accumulation / residual stream / LayerNorm / softmax in both modes):
+  precision "fp16x3" (default; split fp16 products, ~fp32):
+      cross-encoder logits max |diff| <= 1e-3 absolute (north_star: "rerank scores within
+      1e-3"), bge embeddings max |diff| <= 5e-5
+  precision "fp16" (fast mode): logits <= 2e-2, embeddings <= 2e-3
+  and the reference's rerank order (np.argsort(scores)[::-1][:top_k], main.py:246) on the
   15-candidate case unless two oracle scores are closer than the tolerance.
 """
 import os
@@ -17,7 +19,8 @@ import bert_ref as R
 
 pytestmark = pytest.mark.gpu
 
-BGE_ATOL, BGE_COS, CE_ATOL = 2e-3, 0.99995, 2e-2
+TOL = {"fp16x3": dict(bge=5e-5, cos=0.9999999, ce=1e-3),
+       "fp16": dict(bge=2e-3, cos=0.99995, ce=2e-2)}
 
 
 @pytest.fixture(scope="module")
@@ -26,18 +29,23 @@ def golden():
     return dict(np.load(os.path.join(GOLDEN, "bert_golden.npz")))
 
 
+@pytest.fixture(scope="module", params=["fp16x3", "fp16"])
+def prec(request):
+    return request.param
+
+
 @pytest.fixture(scope="module")
-def bge(gpu, golden):
+def bge(gpu, golden, prec):
     from ragmi.encoders import HEAD_CLS_L2, BertEncoder
     w = R.make_weights(R.BGE_SMALL, int(golden["bge_seed"]))
-    return BertEncoder(R.BGE_SMALL, w, HEAD_CLS_L2, gpu), w
+    return BertEncoder(R.BGE_SMALL, w, HEAD_CLS_L2, gpu, prec), w
 
 
 @pytest.fixture(scope="module")
-def ce(gpu, golden):
+def ce(gpu, golden, prec):
     from ragmi.encoders import HEAD_POOLER_CLS, BertEncoder
     w = R.make_weights(R.MINILM_CE, int(golden["ce_seed"]))
-    return BertEncoder(R.MINILM_CE, w, HEAD_POOLER_CLS, gpu), w
+    return BertEncoder(R.MINILM_CE, w, HEAD_POOLER_CLS, gpu, prec), w
 
 
 def _report(name, a, b):
@@ -46,44 +54,44 @@ def _report(name, a, b):
     return d.max()
 
 
-def test_bge_golden(bge, golden):
+def test_bge_golden(bge, golden, prec):
     enc, w = bge
     g = golden
     out = enc.forward_padded(g["ids_q"], g["tt_q"], g["m_q"]).cpu().numpy()
-    assert _report("bge vs transformers", out, g["bge_emb"]) <= BGE_ATOL
+    assert _report(f"[{prec}] bge vs transformers", out, g["bge_emb"]) <= TOL[prec]["bge"]
     cos = (out * g["bge_emb"]).sum(1) / np.linalg.norm(out, axis=1)
-    assert cos.min() >= BGE_COS
+    assert cos.min() >= TOL[prec]["cos"]
     np.testing.assert_allclose(np.linalg.norm(out, axis=1), 1.0, atol=1e-5)
 
 
-def test_ce_golden(ce, golden):
+def test_ce_golden(ce, golden, prec):
     enc, w = ce
     g = golden
     out = enc.forward_padded(g["ids_p"], g["tt_p"], g["m_p"]).cpu().numpy()
-    assert _report("ce vs transformers", out, g["ce_logits"]) <= CE_ATOL
+    assert _report(f"[{prec}] ce vs transformers", out, g["ce_logits"]) <= TOL[prec]["ce"]
 
 
-def test_bge_query_batch_32(bge):
+def test_bge_query_batch_32(bge, prec):
     """main2.py batch_processor shape: 32 queries of 8-32 tokens in one call."""
     enc, w = bge
     rng = np.random.default_rng(3)
     ids, tt, m = R.random_batch(rng, 32, 32)
     out = enc.forward_padded(ids, tt, m).cpu().numpy()
     ref = R.bge_embed(w, R.BGE_SMALL, ids, tt, m)
-    assert _report("bge32", out, ref) <= BGE_ATOL
+    assert _report(f"[{prec}] bge32", out, ref) <= TOL[prec]["bge"]
 
 
-def test_ce_rerank_15_pairs(ce):
+def test_ce_rerank_15_pairs(ce, prec):
     """rerank_documents shape: 15 (query, chunk) pairs of ~100-290 tokens (main.py:241-247)."""
     enc, w = ce
     rng = np.random.default_rng(4)
     ids, tt, m = R.random_batch(rng, 15, 288, pair=True)
     out = enc.forward_padded(ids, tt, m).cpu().numpy()
     ref = R.ce_logits(w, R.MINILM_CE, ids, tt, m)
-    assert _report("ce15", out, ref) <= CE_ATOL
+    assert _report(f"[{prec}] ce15", out, ref) <= TOL[prec]["ce"]
     order, ref_order = R.rerank_order(out, 5), R.rerank_order(ref, 5)
     srt = np.sort(ref)[::-1]
-    if np.min(np.abs(np.diff(srt[:6]))) > 2 * CE_ATOL:
+    if np.min(np.abs(np.diff(srt[:6]))) > 2 * TOL[prec]["ce"]:
         np.testing.assert_array_equal(order, ref_order)
 
 
@@ -98,13 +106,13 @@ def test_batch_independence_bitwise(bge):
         np.testing.assert_array_equal(one[0], full[b])
 
 
-def test_max_length_512(ce):
+def test_max_length_512(ce, prec):
     enc, w = ce
     rng = np.random.default_rng(6)
     ids, tt, m = R.random_batch(rng, 2, 512, pair=True)
     out = enc.forward_padded(ids, tt, m).cpu().numpy()
     ref = R.ce_logits(w, R.MINILM_CE, ids, tt, m)
-    assert _report("ce512", out, ref) <= CE_ATOL
+    assert _report(f"[{prec}] ce512", out, ref) <= TOL[prec]["ce"]
     with pytest.raises(ValueError):
         enc.forward_packed(np.ones(513, np.int32), np.zeros(513, np.int32),
                            np.array([0, 513], np.int32))
