@@ -51,51 +51,43 @@ class UnsupportedFilter(NotImplementedError):
     pass
 
 
-class Collection:
-    """One COSINE collection: FlatIndex in HBM + host-side id/payload maps."""
+class PayloadTags:
+    """Dictionary-codes up to two keyword payload fields into a per-row uint32 tag
+    (16 bits per field, code 0 = field absent) and compiles Qdrant `must` filters on those
+    fields into (mask, value) so the GPU scan filters with (tag & mask) == value.
+    Host-only logic (no device code)."""
 
-    def __init__(self, name: str, dim: int, device, tag_fields=DEFAULT_TAG_FIELDS,
-                 capacity: int = 1024):
-        if len(tag_fields) > 2:
+    def __init__(self, fields=DEFAULT_TAG_FIELDS):
+        if len(fields) > 2:
             raise ValueError("at most two indexed keyword payload fields (16 bits each)")
-        self.name = name
-        self.dim = dim
-        self.index = FlatIndex(dim=dim, capacity=capacity, device=device)
-        self.tag_fields = tuple(tag_fields)
-        self.codes: list[dict[Any, int]] = [dict() for _ in self.tag_fields]
-        self.id_to_row: dict[Any, int] = {}
-        self.row_ids: list[Any] = []
-        self.payloads: list[dict | None] = []
-        self.versions: list[int] = []
-        self.op = 0
-        self.lock = threading.RLock()
+        self.fields = tuple(fields)
+        self.codes: list[dict[Any, int]] = [dict() for _ in self.fields]
 
-    # ---------------------------------------------------------------- tags / filters
-    def _code(self, f: int, value, create: bool) -> int | None:
+    def code(self, f: int, value, create: bool) -> int | None:
         if isinstance(value, (list, dict)) or value is None:
             return None
         table = self.codes[f]
         c = table.get(value)
         if c is None and create:
             if len(table) >= 0xFFFF:
-                raise OverflowError(f"more than 65535 distinct values for {self.tag_fields[f]}")
+                raise OverflowError(f"more than 65535 distinct values for {self.fields[f]}")
             c = len(table) + 1          # 0 = field absent
             table[value] = c
         return c
 
-    def _tag(self, payload: dict | None) -> int:
+    def tag(self, payload: dict | None) -> int:
         tag = 0
         if payload:
-            for f, key in enumerate(self.tag_fields):
+            for f, key in enumerate(self.fields):
                 if key in payload:
-                    c = self._code(f, payload[key], create=True)
+                    c = self.code(f, payload[key], create=True)
                     if c:
                         tag |= c << (16 * f)
         return tag
 
-    def compile_filter(self, flt: models.Filter | None):
-        """Filter(must=[FieldCondition(key, MatchValue(v))...]) -> (mask, value), or None for
-        "matches nothing" (a value never ingested), or (0, 0) for no filter."""
+    def compile(self, flt: models.Filter | None):
+        """Filter(must=[FieldCondition(key, MatchValue(v))...]) -> (mask, value); None when
+        nothing can match (a value never ingested); (0, 0) for no filter."""
         if flt is None:
             return (0, 0)
         if flt.should or flt.must_not:
@@ -104,14 +96,14 @@ class Collection:
         for cond in flt.must or []:
             if not isinstance(cond, models.FieldCondition) or cond.range is not None:
                 raise UnsupportedFilter("only FieldCondition(key, match=MatchValue) is supported")
-            if cond.key not in self.tag_fields:
+            if cond.key not in self.fields:
                 raise UnsupportedFilter(
                     f"payload key {cond.key!r} is not an indexed keyword field "
-                    f"{self.tag_fields}; create the collection with payload_tag_fields")
+                    f"{self.fields}; create the collection with payload_tag_fields")
             if not isinstance(cond.match, models.MatchValue):
                 raise UnsupportedFilter("only MatchValue matches are supported")
-            f = self.tag_fields.index(cond.key)
-            c = self._code(f, cond.match.value, create=False)
+            f = self.fields.index(cond.key)
+            c = self.code(f, cond.match.value, create=False)
             if c is None:
                 return None
             m = 0xFFFF << (16 * f)
@@ -120,6 +112,26 @@ class Collection:
             mask |= m
             value |= c << (16 * f)
         return (mask, value)
+
+
+class Collection:
+    """One COSINE collection: FlatIndex in HBM + host-side id/payload maps."""
+
+    def __init__(self, name: str, dim: int, device, tag_fields=DEFAULT_TAG_FIELDS,
+                 capacity: int = 1024):
+        self.name = name
+        self.dim = dim
+        self.tags = PayloadTags(tag_fields)
+        self.index = FlatIndex(dim=dim, capacity=capacity, device=device)
+        self.id_to_row: dict[Any, int] = {}
+        self.row_ids: list[Any] = []
+        self.payloads: list[dict | None] = []
+        self.versions: list[int] = []
+        self.op = 0
+        self.lock = threading.RLock()
+
+    def compile_filter(self, flt):
+        return self.tags.compile(flt)
 
     # ---------------------------------------------------------------- writes
     def upsert(self, ids: list, vectors, payloads: list) -> int:
@@ -149,7 +161,7 @@ class Collection:
                 self.versions[r] = self.op
                 rows.append(r)
                 sel.append(i)
-                tags.append(self._tag(p))
+                tags.append(self.tags.tag(p))
             if new_count > self.index.capacity:
                 self.index.reserve(max(new_count, 2 * self.index.capacity))
             if rows:
