@@ -125,7 +125,8 @@ int ensure_ws(rag_encoder* e, int64_t T) {
 template <int EPI>
 void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float16* Wl,
           const float* bias, int M, int N, int K, void* C, _Float16* Clo, hipStream_t st) {
-  const dim3 grid(N / BN, (M + BM - 1) / BM);
+  const unsigned tiles = (unsigned)((N / BN) * ((M + BM - 1) / BM));
+  const dim3 grid((tiles + 7) / 8 * 8);          // multiple of 8: XCD-aware tile order
   if (Al)
     gemm_kernel<EPI, true><<<grid, dim3(256), 0, st>>>(A, Al, W, Wl, bias, M, N, K, C, Clo);
   else

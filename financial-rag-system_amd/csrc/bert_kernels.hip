@@ -142,7 +142,15 @@ __global__ __launch_bounds__(256) void gemm_kernel(const _Float16* __restrict__ 
   __shared__ half8 lds[2 * NP * BM * (BK / 8)];         // [buf][plane][row][8 chunks]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  // XCD-aware tile order: blocks are dealt round-robin over the 8 XCDs, so XCD x runs
+  // blocks x, x+8, ...; give it the contiguous tile range [x*cpx, (x+1)*cpx) with the N
+  // tiles of one M tile adjacent, so the A panel is fetched into that XCD's L2 once and
+  // reused by all N/BN column tiles (instead of once per XCD).
+  const int nN = N / BN, nM = (M + BM - 1) / BM;
+  const int cpx = gridDim.x >> 3;
+  const int tile = (blockIdx.x & 7) * cpx + (blockIdx.x >> 3);
+  if (tile >= nM * nN) return;
+  const int m0 = (tile / nN) * BM, n0 = (tile % nN) * BN;
   const int nk = K / BK;
   const _Float16* src[4] = {A, W, Al, Wl};
 
@@ -218,29 +226,59 @@ __global__ __launch_bounds__(256) void gemm_kernel(const _Float16* __restrict__ 
     __syncthreads();
   }
 
-  // epilogue: lane holds C[rows 4(l>>4)+r][col l&15] of each 16x16 tile
+  // epilogue: lane holds C[rows 16i + 4(l>>4) + r][col 16j + (l&15)] of the wave's 64x64
+  // tile. Stage 32-row halves through the (now idle) LDS as fp32 [32][68] per wave (stride
+  // 68 dwords: the four 16-lane row groups land on disjoint banks), then each lane takes
+  // 8 consecutive columns of a row: bias + activation + conversion there, and 16-B stores
+  // (full 128-B row segments per 8 lanes) instead of 2-B scattered ones.
+  constexpr int ES = 68;
+  float* ep = reinterpret_cast<float*>(lds) + wid * (32 * ES);
+  const int rr = lane >> 3, cc = (lane & 7) * 8;       // read: row rr + 8s, cols cc..cc+7
+  const int gn = n0 + wc * 64 + cc;
+  float bn[8];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int n = n0 + wc * 64 + j * 16 + (lane & 15);
-    const float bn = bias[n];
+  for (int e = 0; e < 8; ++e) bn[e] = bias[gn + e];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+  for (int hf = 0; hf < 2; ++hf) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wr * 64 + i * 16 + 4 * (lane >> 4) + r;
-        if (m < M) {
-          float v = acc[i][j][r] + bn;
-          if constexpr (EPI == kEpiF32) {
-            static_cast<float*>(Cout)[(int64_t)m * N + n] = v;
-          } else {
-            if constexpr (EPI == kEpiGeluF16) v = gelu_erf(v);
-            const _Float16 vh = (_Float16)v;
-            static_cast<_Float16*>(Cout)[(int64_t)m * N + n] = vh;
-            if constexpr (SPLIT) Clo[(int64_t)m * N + n] = lo_part(v, vh);
+    for (int i2 = 0; i2 < 2; ++i2)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          ep[(i2 * 16 + 4 * (lane >> 4) + r) * ES + j * 16 + (lane & 15)] = acc[hf * 2 + i2][j][r];
+    __builtin_amdgcn_s_waitcnt(0xc07f);                 // lgkmcnt(0): own LDS writes landed
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int s8 = 0; s8 < 4; ++s8) {
+      const int lr = rr + 8 * s8;
+      const int m = m0 + wr * 64 + hf * 32 + lr;
+      const floatx4 lo4 = *reinterpret_cast<const floatx4*>(ep + lr * ES + cc);
+      const floatx4 hi4 = *reinterpret_cast<const floatx4*>(ep + lr * ES + cc + 4);
+      float v[8] = {lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        v[e] += bn[e];
+        if constexpr (EPI == kEpiGeluF16) v[e] = gelu_erf(v[e]);
+      }
+      if (m < M) {
+        if constexpr (EPI == kEpiF32) {
+          float* o = static_cast<float*>(Cout) + (int64_t)m * N + gn;
+          *reinterpret_cast<floatx4*>(o) = floatx4{v[0], v[1], v[2], v[3]};
+          *reinterpret_cast<floatx4*>(o + 4) = floatx4{v[4], v[5], v[6], v[7]};
+        } else {
+          half8 h, l;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            h[e] = (_Float16)v[e];
+            if constexpr (SPLIT) l[e] = lo_part(v[e], h[e]);
           }
+          *reinterpret_cast<half8*>(static_cast<_Float16*>(Cout) + (int64_t)m * N + gn) = h;
+          if constexpr (SPLIT) *reinterpret_cast<half8*>(Clo + (int64_t)m * N + gn) = l;
         }
       }
     }
+    __builtin_amdgcn_wave_barrier();
   }
 }
 

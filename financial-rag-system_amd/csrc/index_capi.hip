@@ -148,6 +148,13 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
 }
 
 template <int D>
+void launch_import(rag_index* h, const half8* in, int64_t row0, int64_t n, hipStream_t st) {
+  const int64_t total = n * (D / 8);
+  ragmi::import_kernel<D><<<dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st>>>(
+      in, row0, n, h->corpus);
+}
+
+template <int D>
 void launch_export(rag_index* h, int64_t row0, int64_t n, half8* out, hipStream_t st) {
   const int64_t total = n * (D / 8);
   const int blocks = (int)((total + 255) / 256);
@@ -465,6 +472,32 @@ int rag_index_export_rows(rag_index_t* h, int64_t row0, int64_t n, uint16_t* out
   RAG_HIP(hipGetLastError());
   RAG_HIP(hipDeviceSynchronize());
   RAG_HIP(hipMemcpy(out, h->stage, bytes, hipMemcpyDeviceToHost));
+  return RAG_OK;
+}
+
+int rag_index_import_rows(rag_index_t* h, int64_t row0, int64_t n, const uint16_t* rows,
+                          const uint32_t* tags, int64_t new_count) {
+  ragmi::clear_error();
+  if (!h || (n > 0 && !rows) || row0 < 0 || n < 0 || row0 + n > h->cap_rows)
+    return ragmi::fail(RAG_EINVAL, "bad import range (reserve capacity first)");
+  if (new_count < 0 || new_count > h->cap_rows)
+    return ragmi::fail(RAG_ERANGE, "new_count exceeds capacity");
+  std::lock_guard<std::mutex> lk(h->mu);
+  RAG_HIP(hipSetDevice(h->device));
+  if (n > 0) {
+    const size_t bytes = (size_t)n * h->dim * 2;
+    int rc = ensure_stage(h, bytes);
+    if (rc) return rc;
+    RAG_HIP(hipDeviceSynchronize());
+    RAG_HIP(hipMemcpy(h->stage, rows, bytes, hipMemcpyHostToDevice));
+    RAG_DISPATCH_DIM(h->dim, launch_import, h, static_cast<const half8*>(h->stage), row0, n,
+                     nullptr);
+    RAG_HIP(hipGetLastError());
+    if (tags)
+      RAG_HIP(hipMemcpy(h->tags + row0, tags, (size_t)n * 4, hipMemcpyHostToDevice));
+    RAG_HIP(hipDeviceSynchronize());
+  }
+  h->count = new_count;
   return RAG_OK;
 }
 

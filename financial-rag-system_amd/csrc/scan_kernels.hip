@@ -888,4 +888,19 @@ __global__ void export_kernel(const half8* __restrict__ corpus, int64_t row0, in
   out[idx] = corpus[t * (steps<D>() * 64) + (c >> 2) * 64 + (c & 3) * 16 + r];
 }
 
+// ----------------------------------------------------------------------------------------
+// import: row-major fp16 -> tile16, stored bits unchanged (persistence: loading a saved shard
+// must not renormalise already-normalised rows)
+// ----------------------------------------------------------------------------------------
+template <int D>
+__global__ void import_kernel(const half8* __restrict__ in, int64_t row0, int64_t n,
+                              half8* __restrict__ corpus) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n * (D / 8)) return;
+  const int64_t i = idx / (D / 8);
+  const int c = (int)(idx % (D / 8));
+  const int64_t row = row0 + i;
+  corpus[(row >> 4) * (steps<D>() * 64) + (c >> 2) * 64 + (c & 3) * 16 + (row & 15)] = in[idx];
+}
+
 }  // namespace ragmi

@@ -59,6 +59,8 @@ INDEX_API = {
                                              ctypes.c_int64, c_f32p, c_i64p]),
     "rag_index_export_rows": (ctypes.c_int, [c_vp, ctypes.c_int64, ctypes.c_int64, c_u16p]),
     "rag_index_export_tags": (ctypes.c_int, [c_vp, ctypes.c_int64, ctypes.c_int64, c_u32p]),
+    "rag_index_import_rows": (ctypes.c_int, [c_vp, ctypes.c_int64, ctypes.c_int64, c_u16p,
+                                             c_u32p, ctypes.c_int64]),
     "rag_merge_topk": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                       c_vp, c_vp, c_vp]),
     "rag_bench_scan": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,

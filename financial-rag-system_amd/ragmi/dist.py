@@ -106,3 +106,13 @@ class ShardedIndex:
             return s, i
         gs, gi = all_gather_lists(s, i, self.group)
         return self.merge(gs, gi, k)
+
+    def save(self, path: str) -> None:
+        """Collective: write the whole collection to one shard directory (ragmi.store)."""
+        from .store import save_sharded
+        save_sharded(self, path)
+
+    def load(self, path: str) -> int:
+        """Load this rank's rows from a shard directory saved at any world size."""
+        from .store import load_sharded
+        return load_sharded(self, path)

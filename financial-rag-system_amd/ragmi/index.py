@@ -153,6 +153,28 @@ class FlatIndex:
                                             out.ctypes.data_as(_lib.c_u16p)))
         return out
 
+    def import_rows(self, rows_f16, row0: int = 0, tags=None,
+                    new_count: int | None = None) -> None:
+        """Write already-stored fp16 rows [n, dim] (float16 or uint16 bits, host) back into
+        rows [row0, row0+n) unchanged — the load side of persistence (no renormalisation)."""
+        a = np.ascontiguousarray(rows_f16)
+        if a.dtype == np.float16:
+            a = a.view(np.uint16)
+        if a.dtype != np.uint16 or a.ndim != 2 or a.shape[1] != self.dim:
+            raise ValueError(f"rows must be float16/uint16 [n, {self.dim}]")
+        n = a.shape[0]
+        t = None
+        if tags is not None:
+            t = np.ascontiguousarray(tags, dtype=np.uint32)
+            if t.shape != (n,):
+                raise ValueError("tags must be [n]")
+        if new_count is None:
+            new_count = max(self.count, row0 + n)
+        torch.cuda.current_stream(self.device).synchronize()
+        check(self._L.rag_index_import_rows(
+            self._h, int(row0), int(n), a.ctypes.data_as(_lib.c_u16p),
+            t.ctypes.data_as(_lib.c_u32p) if t is not None else None, int(new_count)))
+
     def export_tags(self, row0: int = 0, n: int | None = None) -> np.ndarray:
         if n is None:
             n = self.count - row0

@@ -11,13 +11,17 @@ plus query_batch_points (one GPU scan for a whole micro-batch; main2.py:281-295 
 count, retrieve and delete_collection.
 
 `url` is accepted and ignored: the collection lives in this process's GPU memory (the
-Qdrant service of docker-compose.yml:22 is replaced, not contacted). Payloads stay host-side
+Qdrant service of docker-compose.yml:22 is replaced, not contacted). `path=` plays the role
+of Qdrant's local mode / storage volume: existing collections under it are loaded at
+construction and `save()` / `close()` write them back (ragmi.store shard format). Payloads stay host-side
 keyed by row; the keyword payload fields used by the reference's `must` filter (`ticker`,
 `document_type`, main.py:218-230) are dictionary-coded into a per-row uint32 tag in HBM
 (16 bits per field) so filtering runs inside the scan kernel.
 """
 from __future__ import annotations
 
+import os
+import shutil
 import threading
 import uuid
 from typing import Any, Iterable
@@ -207,11 +211,37 @@ class Collection:
 class QdrantClient:
     """In-process, GPU-resident replacement for qdrant_client.QdrantClient."""
 
-    def __init__(self, url: str | None = None, *args, device=None, **kwargs):
+    def __init__(self, url: str | None = None, *args, device=None, path: str | None = None,
+                 **kwargs):
         self.url = url
         self.device = device
+        self.path = path
         self._collections: dict[str, Collection] = {}
         self._lock = threading.Lock()
+        if path is not None and os.path.isdir(path):
+            from .store import load_collection
+            for name in sorted(os.listdir(path)):
+                d = os.path.join(path, name)
+                if os.path.isfile(os.path.join(d, "collection.json")):
+                    col = load_collection(d, device)
+                    self._collections[col.name] = col
+
+    def save(self, path: str | None = None) -> None:
+        """Persist every collection under `path` (default: the client's path); collection
+        directories of deleted collections are removed."""
+        from .store import save_collection
+        path = path or self.path
+        if path is None:
+            raise ValueError("no storage path: pass path= here or to QdrantClient(...)")
+        os.makedirs(path, exist_ok=True)
+        with self._lock:
+            cols = dict(self._collections)
+        for name, col in cols.items():
+            save_collection(col, os.path.join(path, name))
+        for name in os.listdir(path):
+            d = os.path.join(path, name)
+            if name not in cols and os.path.isfile(os.path.join(d, "collection.json")):
+                shutil.rmtree(d)
 
     # ---------------------------------------------------------------- collections
     def get_collections(self) -> models.CollectionsResponse:
@@ -316,6 +346,8 @@ class QdrantClient:
                                  with_payload).points
 
     def close(self) -> None:
+        if self.path is not None and self._collections:
+            self.save()
         with self._lock:
             cols = list(self._collections.values())
             self._collections.clear()

@@ -104,6 +104,11 @@ int rag_index_search_host(rag_index_t* index, const float* queries_host, int B, 
 
 /* Copy stored rows [row0, row0+n) out as row-major fp16 bits ([n][dim] uint16, host). */
 int rag_index_export_rows(rag_index_t* index, int64_t row0, int64_t n, uint16_t* out_host);
+/* Load already-stored rows back (persistence): row-major fp16 bits [n][dim] (host) are
+ * written to rows [row0, row0+n) unchanged (no renormalisation), tags (host, may be NULL)
+ * likewise; `new_count` = valid rows afterwards. Synchronous. */
+int rag_index_import_rows(rag_index_t* index, int64_t row0, int64_t n, const uint16_t* rows_host,
+                          const uint32_t* tags_host, int64_t new_count);
 /* Copy stored tags of rows [row0, row0+n) to host. */
 int rag_index_export_tags(rag_index_t* index, int64_t row0, int64_t n, uint32_t* out_host);
 

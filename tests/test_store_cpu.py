@@ -1,0 +1,162 @@
+"""CPU tests of the persistence layer (ragmi.store): shard directory
+format, chunked save/load, row-range loads, the collective sharded save at world size 2 and
+reload at world size 3 (gloo on 127.0.0.1). The index here is a numpy stand-in with the
+FlatIndex row I/O surface (export_rows/export_tags/import_rows/reserve); the GPU round trip
+through libragmi is tests/test_store_gpu.py."""
+import json
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+
+def _paths():
+    for p in (ROOT, os.path.join(ROOT, "financial-rag-system_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+
+
+class HostIndex:
+    """numpy stand-in for FlatIndex's row I/O (stored rows as uint16 fp16 bits)."""
+
+    def __init__(self, dim, capacity=16):
+        self.dim = dim
+        self.rows = np.zeros((capacity, dim), np.uint16)
+        self.tags = np.zeros(capacity, np.uint32)
+        self.count = 0
+
+    @property
+    def capacity(self):
+        return self.rows.shape[0]
+
+    def reserve(self, cap):
+        if cap > self.capacity:
+            r = np.zeros((cap, self.dim), np.uint16)
+            t = np.zeros(cap, np.uint32)
+            r[:self.capacity], t[:self.capacity] = self.rows, self.tags
+            self.rows, self.tags = r, t
+
+    def export_rows(self, row0=0, n=None):
+        n = self.count - row0 if n is None else n
+        return self.rows[row0:row0 + n].copy()
+
+    def export_tags(self, row0=0, n=None):
+        n = self.count - row0 if n is None else n
+        return self.tags[row0:row0 + n].copy()
+
+    def import_rows(self, a, row0=0, tags=None, new_count=None):
+        a = np.asarray(a)
+        a = a.view(np.uint16) if a.dtype == np.float16 else a
+        assert row0 + len(a) <= self.capacity
+        self.rows[row0:row0 + len(a)] = a
+        if tags is not None:
+            self.tags[row0:row0 + len(a)] = tags
+        self.count = new_count if new_count is not None else max(self.count, row0 + len(a))
+
+
+def _filled(n, dim, seed):
+    rng = np.random.default_rng(seed)
+    h = HostIndex(dim, n)
+    h.import_rows(rng.standard_normal((n, dim)).astype(np.float16), 0,
+                  rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32), n)
+    return h
+
+
+def test_save_load_roundtrip_chunked(tmp_path):
+    _paths()
+    from ragmi import store
+    src = _filled(1000, 384, 0)
+    store.save_index(src, str(tmp_path / "s"), chunk_rows=97)
+    meta = json.loads((tmp_path / "s" / "meta.json").read_text())
+    assert meta == {"format": "ragmi-shard", "version": 1, "dim": 384, "count": 1000}
+    v = np.load(tmp_path / "s" / "vectors.f16.npy")
+    assert v.dtype == np.float16 and v.shape == (1000, 384)
+    dst = HostIndex(384)
+    assert store.load_into(dst, str(tmp_path / "s"), chunk_rows=128) == 1000
+    assert dst.count == 1000
+    np.testing.assert_array_equal(dst.export_rows(), src.export_rows())
+    np.testing.assert_array_equal(dst.export_tags(), src.export_tags())
+    part = HostIndex(384)
+    store.load_into(part, str(tmp_path / "s"), rows=(300, 650), chunk_rows=64)
+    np.testing.assert_array_equal(part.export_rows(), src.export_rows(300, 350))
+
+
+def test_incomplete_or_foreign_directories_refused(tmp_path):
+    _paths()
+    from ragmi import store
+    src = _filled(10, 32, 1)
+    store.save_index(src, str(tmp_path / "s"))
+    os.remove(tmp_path / "s" / "meta.json")             # incomplete save
+    with pytest.raises(FileNotFoundError):
+        store.load_into(HostIndex(32), str(tmp_path / "s"))
+    store.save_index(src, str(tmp_path / "s"))
+    with pytest.raises(ValueError):
+        store.load_into(HostIndex(64), str(tmp_path / "s"))      # dim mismatch
+    (tmp_path / "s" / "meta.json").write_text(json.dumps({"format": "x", "version": 1}))
+    with pytest.raises(ValueError):
+        store.load_into(HostIndex(32), str(tmp_path / "s"))
+    with pytest.raises(ValueError):
+        store.save_index(src, str(tmp_path / "t"))
+        store.load_into(HostIndex(32), str(tmp_path / "t"), rows=(5, 11))
+
+
+def test_empty_index(tmp_path):
+    _paths()
+    from ragmi import store
+    store.save_index(HostIndex(384), str(tmp_path / "e"))
+    dst = HostIndex(384)
+    assert store.load_into(dst, str(tmp_path / "e")) == 0 and dst.count == 0
+
+
+def _worker(rank, world, port, n, path, mode, q):
+    _paths()
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ragmi.dist import ShardedIndex
+        full = _filled(n, 64, 7)
+        if mode == "save":
+            sh = ShardedIndex(n, local=HostIndex(64))
+            sh.local.reserve(sh.rows)
+            sh.local.import_rows(full.rows[sh.lo:sh.hi], 0, full.tags[sh.lo:sh.hi], sh.rows)
+            sh.save(path)
+        else:
+            sh = ShardedIndex(n, local=HostIndex(64))
+            got = sh.load(path)
+            ok = (got == sh.rows and sh.local.count == sh.rows and
+                  np.array_equal(sh.local.export_rows(), full.rows[sh.lo:sh.hi]) and
+                  np.array_equal(sh.local.export_tags(), full.tags[sh.lo:sh.hi]))
+            q.put((rank, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_sharded_save_world2_load_world3(tmp_path):
+    n, path = 1001, str(tmp_path / "g")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    mp.start_processes(_worker, args=(2, _free_port(), n, path, "save", q), nprocs=2,
+                       start_method="spawn")
+    meta = json.loads(open(os.path.join(path, "meta.json")).read())
+    assert meta["count"] == n
+    full = _filled(n, 64, 7)
+    np.testing.assert_array_equal(np.load(os.path.join(path, "vectors.f16.npy")).view(np.uint16),
+                                  full.rows)
+    mp.start_processes(_worker, args=(3, _free_port(), n, path, "load", q), nprocs=3,
+                       start_method="spawn")
+    res = sorted(q.get(timeout=60) for _ in range(3))
+    assert res == [(0, True), (1, True), (2, True)]
