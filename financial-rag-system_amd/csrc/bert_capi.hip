@@ -144,15 +144,17 @@ int forward_locked(rag_encoder* e, const int32_t* ids, const int32_t* types, con
       c.type_vocab, c.max_position, e->x, e->xh, e->xl);
   const float scale = 1.0f / sqrtf((float)HD);
   const unsigned ln_grid = (unsigned)((T + 3) / 4);
-  const dim3 agrid((max_len + 63) / 64, NH, B);
+  const dim3 agrid(NH, B);
+  const int sp = (max_len + 31) & ~31;
+  const size_t alds = (size_t)attn_lds_bytes(sp, e->xl ? 2 : 1);
   for (const Layer& L : e->layers) {
     gemm<kEpiF16>(e->xh, e->xl, L.wqkv, L.wqkv_l, L.bqkv, T, 3 * H, H, e->qkv, e->qkv_l, st);
     if (e->xl)
-      attn_kernel<true><<<agrid, dim3(256), 0, st>>>(e->qkv, e->qkv_l, cu, scale, e->ctx,
-                                                     e->ctx_l);
+      attn_kernel<true><<<agrid, dim3(kAttnThreads<true>), alds, st>>>(e->qkv, e->qkv_l, cu, max_len,
+                                                                 scale, e->ctx, e->ctx_l);
     else
-      attn_kernel<false><<<agrid, dim3(256), 0, st>>>(e->qkv, nullptr, cu, scale, e->ctx,
-                                                      nullptr);
+      attn_kernel<false><<<agrid, dim3(kAttnThreads<false>), alds, st>>>(e->qkv, nullptr, cu, max_len,
+                                                                  scale, e->ctx, nullptr);
     gemm<kEpiF32>(e->ctx, e->ctx_l, L.wo, L.wo_l, L.bo, T, H, H, e->y, nullptr, st);
     add_ln_kernel<<<dim3(ln_grid), dim3(256), 0, st>>>(e->x, e->y, L.g1, L.be1,
                                                        c.layer_norm_eps, e->xh, e->xl, T);
@@ -197,6 +199,11 @@ int rag_encoder_create(const rag_bert_config* cfg, const float* const* w, int n_
   for (int i = 0; i < n_weights; ++i)
     if (!w[i]) return ragmi::fail(RAG_EINVAL, "NULL weight tensor");
   RAG_HIP(hipSetDevice(device));
+  // attention stages K/V of a whole sequence in dynamic LDS (up to 148 KB at 512 tokens, split)
+  RAG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_kernel<true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  RAG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_kernel<false>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   auto* e = new rag_encoder();
   e->cfg = *cfg;
   e->device = device;

@@ -22,13 +22,25 @@ constexpr int HD = 32;      // head dim
 constexpr int FF = 1536;    // intermediate
 
 typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+typedef _Float16 half2 __attribute__((ext_vector_type(2)));
 
 // fp16x3 split: v = hi + lo with hi = fp16(v), lo = fp16(v - hi); a*b ~ ah*bh + ah*bl + al*bh
 // (relative error ~2^-22) on the fp16 MFMA pipe.
 __device__ __forceinline__ _Float16 lo_part(float v, _Float16 hi) { return (_Float16)(v - (float)hi); }
 
+// erf-GELU, 0.5 x (1 + erf(x / sqrt 2)), with erfc(|z|) from Abramowitz & Stegun 7.1.26
+// (|error of erf| <= 1.5e-7 absolute, i.e. at fp32 rounding level for the GELU output):
+// 1 + erf(z) = 2 - erfc(z) for z >= 0 and erfc(-z) for z < 0 (no cancellation for z << 0).
+// Two transcendentals (rcp, exp2) and 7 FMAs instead of the libm erff's branchy polynomial.
 __device__ __forceinline__ float gelu_erf(float x) {
-  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
+  const float z = fabsf(x) * 0.70710678118654752440f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  float q = fmaf(1.061405429f, t, -1.453152027f);
+  q = fmaf(q, t, 1.421413741f);
+  q = fmaf(q, t, -0.284496736f);
+  q = fmaf(q, t, 0.254829592f);
+  q *= t * __builtin_amdgcn_exp2f(-z * z * 1.44269504088896341f);   // erfc(z)
+  return 0.5f * x * (x >= 0.f ? 2.0f - q : q);
 }
 
 // ----------------------------------------------------------------------------------------
@@ -120,14 +132,25 @@ __global__ __launch_bounds__(256) void add_ln_kernel(float* __restrict__ x,
 
 // ----------------------------------------------------------------------------------------
 // GEMM: C[M,N] = A[M,K] . W[N,K]^T + bias[N]   (A fp16 row-major, W fp16 [N][K] = HF Linear)
-// 128x128 tile, BK = 64, 256 threads = 2x2 waves of 64x64, v_mfma_f32_16x16x32_f16.
+// 128x128 tile, BK = 64 (fp16) / 32 (fp16x3), 256 threads = 2x2 waves of 64x64,
+// v_mfma_f32_16x16x32_f16.
 // Register-staged double-buffered LDS (one barrier per K step), XOR-swizzled 16-B chunks.
 // ----------------------------------------------------------------------------------------
 enum Epi { kEpiF16 = 0, kEpiGeluF16 = 1, kEpiF32 = 2 };
 
-constexpr int BM = 128, BN = 128, BK = 64;
+constexpr int BM = 128, BN = 128;
 
-__device__ __forceinline__ int swz(int row, int chunk) { return row * 8 + (chunk ^ (row & 7)); }
+// K step: 64 for fp16 (2 planes: 64 KB double-buffered LDS), 32 for fp16x3 (4 planes, also
+// 64 KB) so both modes fit two workgroups per CU.
+template <bool SPLIT> constexpr int kBK = SPLIT ? 32 : 64;
+
+// 16-B chunk swizzle: the 16 rows an MFMA fragment read touches (same logical chunk) land
+// on 16 distinct 4-bank groups for ds_read_b128.
+template <int CPR>
+__device__ __forceinline__ int swz(int row, int chunk) {
+  if constexpr (CPR == 8) return row * 8 + (chunk ^ (row & 7));
+  else return row * 4 + (chunk ^ ((row >> 2) & 3));
+}
 
 template <int EPI, bool SPLIT>
 __global__ __launch_bounds__(256) void gemm_kernel(const _Float16* __restrict__ A,
@@ -139,7 +162,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(const _Float16* __restrict__ 
                                                    _Float16* __restrict__ Clo) {
   // SPLIT (fp16x3): tiles of A_hi, A_lo, W_hi, W_lo; 3 MFMAs per product.
   constexpr int NP = SPLIT ? 4 : 2;                     // staged planes
-  __shared__ half8 lds[2 * NP * BM * (BK / 8)];         // [buf][plane][row][8 chunks]
+  constexpr int BK = kBK<SPLIT>, CPR = BK / 8, LPT = BM * CPR / 256;   // loads/thread/plane
+  __shared__ half8 lds[2 * NP * BM * CPR];              // [buf][plane][row][CPR chunks]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
   // XCD-aware tile order: blocks are dealt round-robin over the 8 XCDs, so XCD x runs
@@ -154,14 +178,14 @@ __global__ __launch_bounds__(256) void gemm_kernel(const _Float16* __restrict__ 
   const int nk = K / BK;
   const _Float16* src[4] = {A, W, Al, Wl};
 
-  half8 rg[NP][4];
+  half8 rg[NP][LPT];
   auto gload = [&](int kt) {
 #pragma unroll
     for (int p = 0; p < NP; ++p)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < LPT; ++i) {
         const int c = tid + 256 * i;
-        const int row = c >> 3, ch = c & 7;
+        const int row = c / CPR, ch = c % CPR;
         const int r = (p & 1) ? (n0 + row) : min(m0 + row, M - 1);   // planes 0,2: A; 1,3: W
         rg[p][i] = *reinterpret_cast<const half8*>(src[p] + (int64_t)r * K + kt * BK + ch * 8);
       }
@@ -169,11 +193,11 @@ __global__ __launch_bounds__(256) void gemm_kernel(const _Float16* __restrict__ 
   auto lstore = [&](int buf) {
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
-      half8* lp = lds + (buf * NP + p) * (BM * 8);
+      half8* lp = lds + (buf * NP + p) * (BM * CPR);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < LPT; ++i) {
         const int c = tid + 256 * i;
-        lp[swz(c >> 3, c & 7)] = rg[p][i];
+        lp[swz<CPR>(c / CPR, c % CPR)] = rg[p][i];
       }
     }
   };
@@ -190,24 +214,24 @@ __global__ __launch_bounds__(256) void gemm_kernel(const _Float16* __restrict__ 
   for (int kt = 0; kt < nk; ++kt) {
     const int buf = kt & 1;
     if (kt + 1 < nk) gload(kt + 1);
-    const half8* la = lds + (buf * NP + 0) * (BM * 8);
-    const half8* lb = lds + (buf * NP + 1) * (BM * 8);
+    const half8* la = lds + (buf * NP + 0) * (BM * CPR);
+    const half8* lb = lds + (buf * NP + 1) * (BM * CPR);
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < BK / 32; ++ks) {
       half8 af[4], bf[4];
       const int ch = ks * 4 + (lane >> 4);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = la[swz(wr * 64 + i * 16 + (lane & 15), ch)];
+      for (int i = 0; i < 4; ++i) af[i] = la[swz<CPR>(wr * 64 + i * 16 + (lane & 15), ch)];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bf[j] = lb[swz(wc * 64 + j * 16 + (lane & 15), ch)];
+      for (int j = 0; j < 4; ++j) bf[j] = lb[swz<CPR>(wc * 64 + j * 16 + (lane & 15), ch)];
       if constexpr (SPLIT) {
-        const half8* lal = lds + (buf * NP + 2) * (BM * 8);
-        const half8* lbl = lds + (buf * NP + 3) * (BM * 8);
+        const half8* lal = lds + (buf * NP + 2) * (BM * CPR);
+        const half8* lbl = lds + (buf * NP + 3) * (BM * CPR);
         half8 afl[4], bfl[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) afl[i] = lal[swz(wr * 64 + i * 16 + (lane & 15), ch)];
+        for (int i = 0; i < 4; ++i) afl[i] = lal[swz<CPR>(wr * 64 + i * 16 + (lane & 15), ch)];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) bfl[j] = lbl[swz(wc * 64 + j * 16 + (lane & 15), ch)];
+        for (int j = 0; j < 4; ++j) bfl[j] = lbl[swz<CPR>(wc * 64 + j * 16 + (lane & 15), ch)];
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -283,151 +307,183 @@ __global__ __launch_bounds__(256) void gemm_kernel(const _Float16* __restrict__ 
 }
 
 // ----------------------------------------------------------------------------------------
-// attention (flash style, varlen): grid (ceil(maxlen/64), NH, B), 256 threads; wave w owns
-// query rows qb*64 + 16w .. +15 of sequence b, head h. Key blocks of 32 staged in LDS
-// (K as [key][dim], V transposed as [dim][key]); S = Q K^T and O += P V on
-// v_mfma_f32_16x16x32_f16 (head_dim 32 = one K step); online softmax in fp32.
-// qkv: fp16 [T][3H] (Q | K | V, head h = columns h*32 .. +31 of each); ctx: fp16 [T][H].
+// attention (varlen, one workgroup per (head, sequence), 8 waves (fp16) / 16 (fp16x3)).
+// K and V of the whole (sequence, head) are staged into LDS ONCE (S <= 512 keys, 64 B per key
+// per plane), then every wave walks its own 16-query blocks over all
+// key blocks of 32 with no further barriers (qb = wave, wave + waves, ...).
+// Transposed formulation keeps P in registers:
+//   S^T[key][q] = K . Q^T   (A = K rows from LDS, B = Q^T fragment held for the block)
+//   O^T[d][q]  += V^T . P^T (A = V^T rows from LDS, B = P^T = the lane's own S^T values)
+// The MFMA C layout puts query q = lane&15 in every lane's column, so the softmax running
+// max / sum and the O rescale are per-lane scalars; the P^T fragment slot 8g+j (g = lane>>4)
+// holds key 4g+j (j<4) or 16+4g+(j-4) (j>=4) of the block, i.e. exactly the lane's two S^T
+// accumulators — V^T is stored in LDS with its keys permuted the same way.
+// qkv: fp16 [T][3H] (Q | K | V; head h = columns h*32 .. +31 of each); ctx: fp16 [T][H].
+// LDS (dynamic): per plane K [Sp][40] + V^T [32][Sp+8] halves, Sp = roundup(len, 32).
 // ----------------------------------------------------------------------------------------
+template <bool SPLIT> constexpr int kAttnThreads = SPLIT ? 1024 : 512;   // 4 / 2 waves per SIMD
+constexpr int kKRow = HD + 8;                         // 80-B K rows: conflict-free b128 reads
+
+__host__ __device__ constexpr int attn_lds_bytes(int sp, int planes) {
+  return planes * (sp * kKRow + HD * (sp + 8)) * 2;
+}
+
+__device__ __forceinline__ int vperm(int k) {       // key k of a 32-block -> P^T slot
+  return 8 * ((k & 15) >> 2) + (k & 3) + ((k >> 4) << 2);
+}
+
 template <bool SPLIT>
-__global__ __launch_bounds__(256) void attn_kernel(const _Float16* __restrict__ qkv,
-                                                   const _Float16* __restrict__ qkv_lo,
-                                                   const int* __restrict__ cu, float scale,
-                                                   _Float16* __restrict__ ctx,
-                                                   _Float16* __restrict__ ctx_lo) {
+__global__ __launch_bounds__(kAttnThreads<SPLIT>) void attn_kernel(const _Float16* __restrict__ qkv,
+                                                            const _Float16* __restrict__ qkv_lo,
+                                                            const int* __restrict__ cu,
+                                                            int max_len, float scale,
+                                                            _Float16* __restrict__ ctx,
+                                                            _Float16* __restrict__ ctx_lo) {
   constexpr int NP = SPLIT ? 2 : 1;
-  __shared__ _Float16 kl[NP][32][HD + 8];     // [plane][key][dim] (+8 pad: 80-B rows)
-  __shared__ _Float16 vt[NP][HD][32 + 8];     // [plane][dim][key]
-  __shared__ _Float16 pl[NP][4][16][32 + 8];  // [plane][wave] P tile [row][key]
-  const int b = blockIdx.z, h = blockIdx.y;
+  extern __shared__ _Float16 alds[];
+  const int h = blockIdx.x, b = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int base = cu[b], len = cu[b + 1] - cu[b];
-  const int q0 = blockIdx.x * 64 + wid * 16;
-  if (blockIdx.x * 64 >= len) return;
-  const int qrow = q0 + (lane & 15);
+  // LDS was sized for max_len on the host: a longer sequence (a caller breaking the
+  // max_len contract of rag_encoder_forward) is truncated rather than overrunning LDS
+  const int base = cu[b], len = min(cu[b + 1] - cu[b], max_len);
+  if (len <= 0) return;
+  const int sp = (len + 31) & ~31;
+  const int vrow = sp + 8;
+  _Float16* kls[2] = {alds, alds + sp * kKRow + HD * vrow};
+  _Float16* vts[2] = {alds + sp * kKRow, alds + 2 * sp * kKRow + HD * vrow};
   const _Float16* planes[2] = {qkv, qkv_lo};
 
-  half8 qf[NP];
-  {
-    const int r = min(qrow, len - 1);
+  // ---- stage K (row-major, padded) and V^T (key-permuted) of this (sequence, head)
+  for (int c = tid; c < sp * 4; c += kAttnThreads<SPLIT>) {
+    const int key = c >> 2, dc = (c & 3) * 8;
 #pragma unroll
-    for (int p = 0; p < NP; ++p)
-      qf[p] = *reinterpret_cast<const half8*>(planes[p] + (int64_t)(base + r) * (3 * H) +
-                                              h * HD + 8 * (lane >> 4));
-  }
-  floatx4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = {0.f, 0.f, 0.f, 0.f};
-  float mrow[4], lrow[4];
+    for (int p = 0; p < NP; ++p) {
+      half8 kv = {}, vv = {};
+      if (key < len) {
+        const _Float16* src = planes[p] + (int64_t)(base + key) * (3 * H) + h * HD + dc;
+        kv = *reinterpret_cast<const half8*>(src + H);
+        vv = *reinterpret_cast<const half8*>(src + 2 * H);
+      }
+      *reinterpret_cast<half8*>(kls[p] + key * kKRow + dc) = kv;
+      const int pos = (key & ~31) + vperm(key & 31);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    mrow[i] = kNegInf;
-    lrow[i] = 0.f;
+      for (int e = 0; e < 8; ++e) vts[p][(dc + e) * vrow + pos] = vv[e];
+    }
   }
+  __syncthreads();
 
-  for (int kb = 0; kb < len; kb += 32) {
-    // stage K and V^T of keys kb .. kb+31 (zeros past the end)
+  const int g = lane >> 4, ql = lane & 15;
+  const int nqb = (len + 15) >> 4;
+  for (int qb = wid; qb < nqb; qb += kAttnThreads<SPLIT> / 64) {
+    const int q = qb * 16 + ql;
+    half8 qf[NP];
     {
-      const int key = tid >> 3, dc = (tid & 7) * 4;
+      const int r = min(q, len - 1);
 #pragma unroll
-      for (int p = 0; p < NP; ++p) {
-        half4 kv = {0, 0, 0, 0}, vv = {0, 0, 0, 0};
-        if (kb + key < len) {
-          const _Float16* src = planes[p] + (int64_t)(base + kb + key) * (3 * H) + h * HD + dc;
-          kv = *reinterpret_cast<const half4*>(src + H);
-          vv = *reinterpret_cast<const half4*>(src + 2 * H);
+      for (int p = 0; p < NP; ++p)
+        qf[p] = *reinterpret_cast<const half8*>(planes[p] + (int64_t)(base + r) * (3 * H) +
+                                                h * HD + 8 * g);
+    }
+    floatx4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = {0.f, 0.f, 0.f, 0.f};
+    float m = kNegInf, lsum = 0.f;
+    const float c2 = scale * 1.44269504088896341f;
+    for (int kb = 0; kb < sp; kb += 32) {
+      floatx4 st[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int kr = (kb + 16 * j + ql) * kKRow + 8 * g;
+        const half8 kf = *reinterpret_cast<const half8*>(kls[0] + kr);
+        st[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qf[0], floatx4{0.f, 0.f, 0.f, 0.f},
+                                                       0, 0, 0);
+        if constexpr (SPLIT) {
+          const half8 kfl = *reinterpret_cast<const half8*>(kls[1] + kr);
+          st[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kfl, qf[0], st[j], 0, 0, 0);
+          st[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qf[1], st[j], 0, 0, 0);
         }
-        *reinterpret_cast<half4*>(&kl[p][key][dc]) = kv;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) vt[p][dc + e][key] = vv[e];
       }
-    }
-    __syncthreads();
-    // S = Q K^T for two 16-key tiles
-    floatx4 s[2];
+      // lane: S^T[key kb + 16j + 4g + r][q]. Softmax in base 2 with the 1/sqrt(d) scale
+      // folded into one FMA: p = 2^(s*c - m*c), c = scale*log2(e) > 0 (max commutes).
+      float mx;
+      if (kb + 32 <= len) {
+        mx = fmaxf(fmaxf(fmaxf(st[0][0], st[0][1]), fmaxf(st[0][2], st[0][3])),
+                   fmaxf(fmaxf(st[1][0], st[1][1]), fmaxf(st[1][2], st[1][3])));
+      } else {
+        mx = kNegInf;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const half8 kf = *reinterpret_cast<const half8*>(&kl[0][16 * j + (lane & 15)][8 * (lane >> 4)]);
-      s[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(qf[0], kf, floatx4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            if (kb + 16 * j + 4 * g + r >= len) st[j][r] = kNegInf;
+            mx = fmaxf(mx, st[j][r]);
+          }
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mnew = fmaxf(m, mx);
+      const float corr = __builtin_amdgcn_exp2f((m - mnew) * c2);
+      const float nm = -mnew * c2;
+      half8 ph, pl;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = __builtin_amdgcn_exp2f(fmaf(st[j][r], c2, nm));
+          const _Float16 eh = (_Float16)e;
+          ph[4 * j + r] = eh;
+          if constexpr (SPLIT) pl[4 * j + r] = lo_part(e, eh);
+        }
+      // lane-partial row sum of P exactly as the MFMA sees it (hi [+ lo]), fp32 dot2
+      float rs = 0.f;
+      const half2 one2 = {(_Float16)1.0f, (_Float16)1.0f};
+#pragma unroll
+      for (int e2 = 0; e2 < 4; ++e2) {
+        rs = __builtin_amdgcn_fdot2(half2{ph[2 * e2], ph[2 * e2 + 1]}, one2, rs, false);
+        if constexpr (SPLIT)
+          rs = __builtin_amdgcn_fdot2(half2{pl[2 * e2], pl[2 * e2 + 1]}, one2, rs, false);
+      }
+      lsum = lsum * corr + rs;                          // reduced across g at the end
+      m = mnew;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        o0[r] *= corr;
+        o1[r] *= corr;
+      }
+      const int vr0 = ql * vrow + kb + 8 * g, vr1 = (16 + ql) * vrow + kb + 8 * g;
+      const half8 v0 = *reinterpret_cast<const half8*>(vts[0] + vr0);
+      const half8 v1 = *reinterpret_cast<const half8*>(vts[0] + vr1);
       if constexpr (SPLIT) {
-        const half8 kfl =
-            *reinterpret_cast<const half8*>(&kl[1][16 * j + (lane & 15)][8 * (lane >> 4)]);
-        s[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(qf[1], kf, s[j], 0, 0, 0);
-        s[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(qf[0], kfl, s[j], 0, 0, 0);
+        const half8 v0l = *reinterpret_cast<const half8*>(vts[1] + vr0);
+        const half8 v1l = *reinterpret_cast<const half8*>(vts[1] + vr1);
+        o0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(v0l, ph, o0, 0, 0, 0);
+        o1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(v1l, ph, o1, 0, 0, 0);
+        o0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(v0, pl, o0, 0, 0, 0);
+        o1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(v1, pl, o1, 0, 0, 0);
       }
+      o0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(v0, ph, o0, 0, 0, 0);
+      o1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(v1, ph, o1, 0, 0, 0);
     }
-    // lane: rows 4(l>>4)+i, keys kb + 16j + (l&15)
-    float p[2][4];
+    lsum += __shfl_xor(lsum, 16, 64);
+    lsum += __shfl_xor(lsum, 32, 64);
+    if (q < len) {
+      // lane: O^T[d = 4g + r][q] (o0) and d = 16 + 4g + r (o1)
+      const float inv = 1.0f / lsum;
+      const int64_t off = (int64_t)(base + q) * H + h * HD + 4 * g;
+      half4 a, c, al, cl;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      float mx = kNegInf;
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const bool ok = kb + 16 * j + (lane & 15) < len;
-        s[j][i] = ok ? s[j][i] * scale : kNegInf;
-        mx = fmaxf(mx, s[j][i]);
+      for (int r = 0; r < 4; ++r) {
+        const float x0 = o0[r] * inv, x1 = o1[r] * inv;
+        a[r] = (_Float16)x0;
+        c[r] = (_Float16)x1;
+        if constexpr (SPLIT) {
+          al[r] = lo_part(x0, a[r]);
+          cl[r] = lo_part(x1, c[r]);
+        }
       }
-      mx = fmaxf(mx, xor_lane_f<1>(mx));
-      mx = fmaxf(mx, xor_lane_f<2>(mx));
-      mx = fmaxf(mx, xor_lane_f<4>(mx));
-      mx = fmaxf(mx, xor_lane_f<8>(mx));
-      const float mnew = fmaxf(mrow[i], mx);
-      const float corr = __expf(mrow[i] - mnew);
-      float rsum = 0.f;
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        float e = __expf(s[j][i] - mnew);
-        if constexpr (!SPLIT) e = (float)(_Float16)e;   // P exactly as the MFMA sees it
-        p[j][i] = e;
-        rsum += e;
-      }
-      rsum += xor_lane_f<1>(rsum);
-      rsum += xor_lane_f<2>(rsum);
-      rsum += xor_lane_f<4>(rsum);
-      rsum += xor_lane_f<8>(rsum);
-      lrow[i] = lrow[i] * corr + rsum;
-      mrow[i] = mnew;
-      o0[i] *= corr;
-      o1[i] *= corr;
-    }
-    // P -> LDS (this wave's tile) -> A fragment
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const _Float16 ph = (_Float16)p[j][i];
-        pl[0][wid][4 * (lane >> 4) + i][16 * j + (lane & 15)] = ph;
-        if constexpr (SPLIT) pl[1][wid][4 * (lane >> 4) + i][16 * j + (lane & 15)] = lo_part(p[j][i], ph);
-      }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    const half8 pf = *reinterpret_cast<const half8*>(&pl[0][wid][lane & 15][8 * (lane >> 4)]);
-    const half8 v0 = *reinterpret_cast<const half8*>(&vt[0][lane & 15][8 * (lane >> 4)]);
-    const half8 v1 = *reinterpret_cast<const half8*>(&vt[0][16 + (lane & 15)][8 * (lane >> 4)]);
-    if constexpr (SPLIT) {
-      const half8 pfl = *reinterpret_cast<const half8*>(&pl[1][wid][lane & 15][8 * (lane >> 4)]);
-      const half8 v0l = *reinterpret_cast<const half8*>(&vt[1][lane & 15][8 * (lane >> 4)]);
-      const half8 v1l = *reinterpret_cast<const half8*>(&vt[1][16 + (lane & 15)][8 * (lane >> 4)]);
-      o0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(pfl, v0, o0, 0, 0, 0);
-      o1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(pfl, v1, o1, 0, 0, 0);
-      o0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(pf, v0l, o0, 0, 0, 0);
-      o1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(pf, v1l, o1, 0, 0, 0);
-    }
-    o0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(pf, v0, o0, 0, 0, 0);
-    o1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(pf, v1, o1, 0, 0, 0);
-    __syncthreads();
-  }
-  // O: lane rows 4(l>>4)+i, dims (l&15) and 16 + (l&15)
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = q0 + 4 * (lane >> 4) + i;
-    if (r < len) {
-      const float inv = 1.0f / lrow[i];
-      const int64_t off = (int64_t)(base + r) * H + h * HD;
-      const float a = o0[i] * inv, c = o1[i] * inv;
-      const _Float16 ah = (_Float16)a, ch = (_Float16)c;
-      ctx[off + (lane & 15)] = ah;
-      ctx[off + 16 + (lane & 15)] = ch;
+      *reinterpret_cast<half4*>(ctx + off) = a;
+      *reinterpret_cast<half4*>(ctx + off + 16) = c;
       if constexpr (SPLIT) {
-        ctx_lo[off + (lane & 15)] = lo_part(a, ah);
-        ctx_lo[off + 16 + (lane & 15)] = lo_part(c, ch);
+        *reinterpret_cast<half4*>(ctx_lo + off) = al;
+        *reinterpret_cast<half4*>(ctx_lo + off + 16) = cl;
       }
     }
   }
