@@ -59,7 +59,9 @@ int rag_encoder_create(const rag_bert_config* cfg, const float* const* weights, 
                        int device, rag_encoder_t** out);
 int rag_encoder_destroy(rag_encoder_t* enc);
 
-/* Device pointers, asynchronous on `stream` (hipStream_t). max_len = longest sequence. */
+/* Device pointers, asynchronous on `stream` (hipStream_t). max_len must be >= the longest
+ * sequence (it sizes the attention kernel's LDS; a longer sequence is truncated to max_len
+ * instead of overrunning it). */
 int rag_encoder_forward(rag_encoder_t* enc, const int32_t* ids_dev, const int32_t* types_dev,
                         const int32_t* cu_seqlens_dev, int B, int T, int max_len,
                         float* out_dev, void* stream);
