@@ -30,6 +30,9 @@ K_TOP = 15          # limit=15, main.py:215
 B = 32              # MAX_BATCH_SIZE, main2.py:51
 CHUNK = 1_000_000
 HBM_PEAK = 8.0e12   # B/s, MI355X_MICROARCH.md chip table (spec)
+# scan-kernel HIP events on every PROF_EVERY-th step of the timed region (an event record
+# idles the queue for a few us; sampling keeps the timed steps unperturbed)
+PROF_EVERY = 4
 
 
 def gen_chunk(c: int, dev, rows: int = CHUNK) -> torch.Tensor:
@@ -177,7 +180,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    idx.profile(True)
+    idx.profile(PROF_EVERY)
     first = None
     t0 = time.perf_counter()
     for k in range(args.steps):

@@ -20,7 +20,12 @@ using ragmi::half8;
 
 namespace {
 
-constexpr int kRing = 4;            // workspace slots (concurrent searches in flight)
+// Per-pass workspace slots. A slot is bound to the stream of its last pass: passes on the
+// same stream are ordered by the stream itself, so the hot path records no events at all (an
+// event record idles the queue for ~5 us between kernels). Up to kRing streams search
+// concurrently without interference; a further stream drains the device once and rebinds
+// the least recently used slot.
+constexpr int kRing = 4;
 
 struct Workspace {
   float* qn = nullptr;
@@ -33,7 +38,9 @@ struct Workspace {
   float* heads_s = nullptr;   // [32][n_lists]
   int* heads_i = nullptr;
   int* heads_n = nullptr;
-  hipEvent_t done = nullptr;
+  hipStream_t owner = nullptr;  // stream of the last pass that used this slot
+  bool used = false;
+  uint64_t tick = 0;            // last use (LRU rebinding)
 };
 
 struct ProfPair {
@@ -52,12 +59,13 @@ struct rag_index {
   int max_wgs = 0;        // scan workgroups at full occupancy
   std::mutex mu;
   Workspace ws[kRing];
-  int ws_next = 0;
+  uint64_t ws_tick = 0;
   // host staging for *_host entry points
   void* stage = nullptr;
   size_t stage_bytes = 0;
   // profiling
-  bool prof = false;
+  int prof = 0;                // 0 off; n > 0: time every n-th scan launch
+  int64_t prof_seq = 0;
   std::vector<ProfPair> prof_pairs;
 };
 
@@ -122,7 +130,8 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
   int grid = (int)std::min<int64_t>(h->max_wgs, std::max<int64_t>(1, (n_tiles + 3) / 4));
   grid = std::min(grid, kMaxLists / kWavesPerWG);
   ProfPair pp{};
-  if (h->prof) {
+  const bool timed = h->prof > 0 && (h->prof_seq++ % h->prof) == 0;
+  if (timed) {
     RAG_HIP(hipEventCreate(&pp.a));
     RAG_HIP(hipEventCreate(&pp.b));
     RAG_HIP(hipEventRecord(pp.a, st));
@@ -135,7 +144,7 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
     scan_kernel<D, false><<<dim3(grid), dim3(256), 0, st>>>(
         h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, (int)n_tiles, w.seed, w.part_s,
         w.part_i, w.heads_s, w.heads_i, w.heads_n);
-  if (h->prof) {
+  if (timed) {
     RAG_HIP(hipEventRecord(pp.b, st));
     h->prof_pairs.push_back(pp);
   }
@@ -193,9 +202,23 @@ int search_locked(rag_index* h, const float* q, int B, int k, const uint32_t* fi
   RAG_HIP(hipSetDevice(h->device));
   for (int b0 = 0; b0 < B; b0 += ragmi::kQ) {
     const int Bq = std::min(ragmi::kQ, B - b0);
-    Workspace& w = h->ws[h->ws_next];
-    h->ws_next = (h->ws_next + 1) % kRing;
-    RAG_HIP(hipStreamWaitEvent(st, w.done, 0));
+    Workspace* wp = nullptr;
+    for (auto& s : h->ws)
+      if (s.used && s.owner == st) { wp = &s; break; }
+    if (!wp)
+      for (auto& s : h->ws)
+        if (!s.used) { wp = &s; break; }
+    if (!wp) {
+      // every slot is bound to another stream whose last pass may still be running
+      RAG_HIP(hipDeviceSynchronize());
+      wp = &h->ws[0];
+      for (auto& s : h->ws)
+        if (s.tick < wp->tick) wp = &s;
+    }
+    Workspace& w = *wp;
+    w.used = true;
+    w.owner = st;
+    w.tick = ++h->ws_tick;
     int rc;
     if (h->dim == 384)
       rc = launch_search_pass<384>(h, w, q + (int64_t)b0 * h->dim, Bq, k,
@@ -206,7 +229,6 @@ int search_locked(rag_index* h, const float* q, int B, int k, const uint32_t* fi
                                     filt ? filt + 2 * b0 : nullptr, id_offset,
                                     out_s + (int64_t)b0 * k, out_i + (int64_t)b0 * k, st);
     if (rc) return rc;
-    RAG_HIP(hipEventRecord(w.done, st));
   }
   return RAG_OK;
 }
@@ -315,8 +337,7 @@ int rag_index_create(int dim, int64_t capacity_rows, int device, rag_index_t** o
               hipMalloc(reinterpret_cast<void**>(&w.part_s),
                         (size_t)max_lists * ragmi::kQ * ragmi::kKS * 4) == hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&w.part_i),
-                        (size_t)max_lists * ragmi::kQ * ragmi::kKS * 4) == hipSuccess &&
-              hipEventCreateWithFlags(&w.done, hipEventDisableTiming) == hipSuccess;
+                        (size_t)max_lists * ragmi::kQ * ragmi::kKS * 4) == hipSuccess;
     if (!ok) {
       rag_index_destroy(h);
       return ragmi::fail(RAG_ENOMEM, "workspace allocation failed");
@@ -342,7 +363,6 @@ int rag_index_destroy(rag_index_t* h) {
     if (w.seed) (void)hipFree(w.seed);
     if (w.part_s) (void)hipFree(w.part_s);
     if (w.part_i) (void)hipFree(w.part_i);
-    if (w.done) (void)hipEventDestroy(w.done);
   }
   for (auto& p : h->prof_pairs) {
     (void)hipEventDestroy(p.a);
@@ -540,7 +560,8 @@ int rag_profile_enable(rag_index_t* h, int enable) {
   ragmi::clear_error();
   if (!h) return ragmi::fail(RAG_EINVAL, "index is NULL");
   std::lock_guard<std::mutex> lk(h->mu);
-  h->prof = enable != 0;
+  h->prof = enable < 0 ? 0 : enable;
+  h->prof_seq = 0;
   return RAG_OK;
 }
 

@@ -185,8 +185,9 @@ class FlatIndex:
         return out
 
     # ---------------------------------------------------------------- profiling
-    def profile(self, enable: bool) -> None:
-        check(self._L.rag_profile_enable(self._h, int(bool(enable))))
+    def profile(self, every: int | bool) -> None:
+        """Time every `every`-th scan launch with HIP events (0/False: off, True: every one)."""
+        check(self._L.rag_profile_enable(self._h, int(every)))
 
     def bench_scan(self, queries: torch.Tensor, variant: int, reps: int = 10) -> float:
         """Diagnostic: avg device ms per launch of scan variant `variant` (rag_bench_scan)."""

@@ -118,9 +118,10 @@ int rag_index_export_tags(rag_index_t* index, int64_t row0, int64_t n, uint32_t*
 int rag_merge_topk(const float* in_scores_dev, const int64_t* in_ids_dev, int n_lists, int B,
                    int k, float* out_scores_dev, int64_t* out_ids_dev, void* stream);
 
-/* Kernel timing hook for bench.py: average device time (ms) of the last `rag_index_search`
- * scan-kernel launches measured with HIP events on the launch stream. enable != 0 turns on
- * event recording around the scan kernel (adds two event records per pass). */
+/* Kernel timing hook for bench.py: average device time (ms) of `rag_index_search` scan-kernel
+ * launches measured with HIP events on the launch stream. enable = 0 off; enable = n > 0 records
+ * an event pair around every n-th scan launch (each record costs a few us of device idle
+ * time, so bench.py samples instead of timing every pass). */
 int rag_profile_enable(rag_index_t* index, int enable);
 int rag_profile_scan_ms(rag_index_t* index, double* total_ms, int64_t* launches);
 
