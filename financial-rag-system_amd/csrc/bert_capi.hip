@@ -106,6 +106,7 @@ int ensure_ws(rag_encoder* e, int64_t T) {
   e->xh = e->qkv = e->ctx = e->ff = nullptr;
   e->xl = e->qkv_l = e->ctx_l = e->ff_l = nullptr;
   e->cap_t = 0;
+  const int64_t H = e->cfg.hidden, FF = e->cfg.intermediate;
   if (e->cfg.precision == RAG_PREC_FP16X3) {
     RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->xl), cap * H * 2));
     RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->qkv_l), cap * 3 * H * 2));
@@ -134,41 +135,69 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
                                                         C, nullptr);
 }
 
-int forward_locked(rag_encoder* e, const int32_t* ids, const int32_t* types, const int32_t* cu,
-                   int B, int T, int max_len, float* out, hipStream_t st) {
+template <int H, int HD>
+int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const int32_t* cu,
+              int B, int T, int max_len, float* out, hipStream_t st) {
   const rag_bert_config& c = e->cfg;
+  const int NH = H / HD, FF = c.intermediate;
   int rc = ensure_ws(e, T);
   if (rc) return rc;
-  embed_ln_kernel<<<dim3((max_len + 3) / 4, B), dim3(256), 0, st>>>(
+  embed_ln_kernel<H><<<dim3((max_len + 3) / 4, B), dim3(256), 0, st>>>(
       ids, types, cu, e->wemb, e->pemb, e->temb, e->eg, e->eb, c.layer_norm_eps, c.vocab,
       c.type_vocab, c.max_position, e->x, e->xh, e->xl);
   const float scale = 1.0f / sqrtf((float)HD);
   const unsigned ln_grid = (unsigned)((T + 3) / 4);
   const dim3 agrid(NH, B);
-  const int sp = (max_len + 31) & ~31;
-  const size_t alds = (size_t)attn_lds_bytes(sp, e->xl ? 2 : 1);
+  const int planes = e->xl ? 2 : 1;
+  const int kc = attn_chunk_keys<HD>(max_len, planes);
+  const size_t alds = (size_t)attn_lds_bytes<HD>(kc, planes);
   for (const Layer& L : e->layers) {
     gemm<kEpiF16>(e->xh, e->xl, L.wqkv, L.wqkv_l, L.bqkv, T, 3 * H, H, e->qkv, e->qkv_l, st);
     if (e->xl)
-      attn_kernel<true><<<agrid, dim3(kAttnThreads<true>), alds, st>>>(e->qkv, e->qkv_l, cu, max_len,
-                                                                 scale, e->ctx, e->ctx_l);
+      attn_kernel<H, HD, true><<<agrid, dim3(kAttnThreads<true>), alds, st>>>(
+          e->qkv, e->qkv_l, cu, max_len, kc, scale, e->ctx, e->ctx_l);
     else
-      attn_kernel<false><<<agrid, dim3(kAttnThreads<false>), alds, st>>>(e->qkv, nullptr, cu, max_len,
-                                                                  scale, e->ctx, nullptr);
+      attn_kernel<H, HD, false><<<agrid, dim3(kAttnThreads<false>), alds, st>>>(
+          e->qkv, nullptr, cu, max_len, kc, scale, e->ctx, nullptr);
     gemm<kEpiF32>(e->ctx, e->ctx_l, L.wo, L.wo_l, L.bo, T, H, H, e->y, nullptr, st);
-    add_ln_kernel<<<dim3(ln_grid), dim3(256), 0, st>>>(e->x, e->y, L.g1, L.be1,
+    add_ln_kernel<H><<<dim3(ln_grid), dim3(256), 0, st>>>(e->x, e->y, L.g1, L.be1,
                                                        c.layer_norm_eps, e->xh, e->xl, T);
     gemm<kEpiGeluF16>(e->xh, e->xl, L.w1, L.w1_l, L.bi1, T, FF, H, e->ff, e->ff_l, st);
     gemm<kEpiF32>(e->ff, e->ff_l, L.w2, L.w2_l, L.bi2, T, H, FF, e->y, nullptr, st);
-    add_ln_kernel<<<dim3(ln_grid), dim3(256), 0, st>>>(e->x, e->y, L.g2, L.be2,
+    add_ln_kernel<H><<<dim3(ln_grid), dim3(256), 0, st>>>(e->x, e->y, L.g2, L.be2,
                                                        c.layer_norm_eps, e->xh, e->xl, T);
   }
   if (c.head == RAG_HEAD_CLS_L2)
-    cls_normalize_kernel<<<dim3(B), dim3(64), 0, st>>>(e->x, cu, out);
+    cls_normalize_kernel<H><<<dim3(B), dim3(64), 0, st>>>(e->x, cu, out);
   else
-    ce_head_kernel<<<dim3(B), dim3(256), 0, st>>>(e->x, cu, e->wp, e->bp, e->wc, e->bc, out);
+    ce_head_kernel<H><<<dim3(B), dim3(256), 0, st>>>(e->x, cu, e->wp, e->bp, e->wc, e->bc, out);
   RAG_HIP(hipGetLastError());
   return RAG_OK;
+}
+
+// Built (hidden, head_dim) shapes: 384/32 (bge-small, MiniLM-L6), 768/64 (bge-base),
+// 1024/64 (bge-large, SURVEY config 5).
+bool shape_supported(int hidden, int heads) {
+  return (hidden == 384 && heads == 12) || (hidden == 768 && heads == 12) ||
+         (hidden == 1024 && heads == 16);
+}
+
+template <int H, int HD>
+int set_attn_lds_attr() {
+  RAG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_kernel<H, HD, true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kAttnLdsMax));
+  RAG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_kernel<H, HD, false>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kAttnLdsMax));
+  return RAG_OK;
+}
+
+int forward_locked(rag_encoder* e, const int32_t* ids, const int32_t* types, const int32_t* cu,
+                   int B, int T, int max_len, float* out, hipStream_t st) {
+  switch (e->cfg.hidden) {
+    case 384: return forward_t<384, 32>(e, ids, types, cu, B, T, max_len, out, st);
+    case 768: return forward_t<768, 64>(e, ids, types, cu, B, T, max_len, out, st);
+    default: return forward_t<1024, 64>(e, ids, types, cu, B, T, max_len, out, st);
+  }
 }
 
 }  // namespace
@@ -185,8 +214,11 @@ int rag_encoder_create(const rag_bert_config* cfg, const float* const* w, int n_
   ragmi::clear_error();
   if (!cfg || !w || !out) return ragmi::fail(RAG_EINVAL, "NULL argument");
   *out = nullptr;
-  if (cfg->hidden != H || cfg->heads != NH || cfg->intermediate != FF)
-    return ragmi::fail(RAG_EINVAL, "built for hidden 384, 12 heads, intermediate 1536");
+  if (!shape_supported(cfg->hidden, cfg->heads) || cfg->intermediate < 128 ||
+      cfg->intermediate % 128 != 0)
+    return ragmi::fail(RAG_EINVAL,
+                       "built for hidden/heads 384/12, 768/12, 1024/16 and intermediate a "
+                       "multiple of 128");
   if (cfg->layers < 1 || cfg->layers > 64 || cfg->vocab < 1 || cfg->type_vocab < 1 ||
       cfg->max_position < 1 || cfg->max_position > 4096)
     return ragmi::fail(RAG_EINVAL, "bad config");
@@ -199,11 +231,13 @@ int rag_encoder_create(const rag_bert_config* cfg, const float* const* w, int n_
   for (int i = 0; i < n_weights; ++i)
     if (!w[i]) return ragmi::fail(RAG_EINVAL, "NULL weight tensor");
   RAG_HIP(hipSetDevice(device));
-  // attention stages K/V of a whole sequence in dynamic LDS (up to 148 KB at 512 tokens, split)
-  RAG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_kernel<true>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-  RAG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_kernel<false>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  // attention stages K/V in dynamic LDS (up to 160 KB)
+  {
+    const int arc = cfg->hidden == 384    ? set_attn_lds_attr<384, 32>()
+                    : cfg->hidden == 768 ? set_attn_lds_attr<768, 64>()
+                                         : set_attn_lds_attr<1024, 64>();
+    if (arc) return arc;
+  }
   auto* e = new rag_encoder();
   e->cfg = *cfg;
   e->device = device;
@@ -211,7 +245,7 @@ int rag_encoder_create(const rag_bert_config* cfg, const float* const* w, int n_
   auto chk = [&](int r) {
     if (r && !rc) rc = r;
   };
-  const size_t Hs = H;
+  const size_t Hs = cfg->hidden, H = cfg->hidden, FF = cfg->intermediate;
   chk(up_f32(e, &e->wemb, w[0], (size_t)cfg->vocab * Hs));
   chk(up_f32(e, &e->pemb, w[1], (size_t)cfg->max_position * Hs));
   chk(up_f32(e, &e->temb, w[2], (size_t)cfg->type_vocab * Hs));
@@ -297,7 +331,7 @@ int rag_encoder_forward_host(rag_encoder_t* e, const int32_t* ids, const int32_t
   for (int t = 0; t < T; ++t)
     if (ids[t] < 0 || ids[t] >= e->cfg.vocab || types[t] < 0 || types[t] >= e->cfg.type_vocab)
       return ragmi::fail(RAG_EINVAL, "token id / type out of range");
-  const size_t ob = (size_t)B * (e->cfg.head == RAG_HEAD_CLS_L2 ? H : 1) * 4;
+  const size_t ob = (size_t)B * (e->cfg.head == RAG_HEAD_CLS_L2 ? e->cfg.hidden : 1) * 4;
   const size_t need = (size_t)T * 8 + (size_t)(B + 1) * 4 + ob + 64;
   std::lock_guard<std::mutex> lk(e->mu);
   RAG_HIP(hipSetDevice(e->device));

@@ -16,10 +16,9 @@
 namespace ragmi {
 namespace bert {
 
-constexpr int H = 384;      // hidden
-constexpr int NH = 12;      // heads
-constexpr int HD = 32;      // head dim
-constexpr int FF = 1536;    // intermediate
+// Built shapes (template parameters below): hidden H in {384, 768, 1024} with head_dim HD in
+// {32, 64} (bge-small / MiniLM: 384/32; bge-base: 768/64; bge-large: 1024/64); intermediate
+// size is a runtime GEMM dimension.
 
 typedef _Float16 half4 __attribute__((ext_vector_type(4)));
 typedef _Float16 half2 __attribute__((ext_vector_type(2)));
@@ -46,6 +45,7 @@ __device__ __forceinline__ float gelu_erf(float x) {
 // ----------------------------------------------------------------------------------------
 // embeddings: x = LN(word[id] + type[tt] + pos[p]); one wave per token, grid (ceil(L/4), B)
 // ----------------------------------------------------------------------------------------
+template <int H>
 __global__ __launch_bounds__(256) void embed_ln_kernel(
     const int* __restrict__ ids, const int* __restrict__ types, const int* __restrict__ cu,
     const float* __restrict__ wemb, const float* __restrict__ pemb, const float* __restrict__ temb,
@@ -93,6 +93,7 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(
 // ----------------------------------------------------------------------------------------
 // residual + LayerNorm: x = LN(x + y) (fp32, in place), xh = fp16(x); one wave per row
 // ----------------------------------------------------------------------------------------
+template <int H>
 __global__ __launch_bounds__(256) void add_ln_kernel(float* __restrict__ x,
                                                      const float* __restrict__ y,
                                                      const float* __restrict__ g,
@@ -308,38 +309,56 @@ __global__ __launch_bounds__(256) void gemm_kernel(const _Float16* __restrict__ 
 
 // ----------------------------------------------------------------------------------------
 // attention (varlen, one workgroup per (head, sequence), 8 waves (fp16) / 16 (fp16x3)).
-// K and V of the whole (sequence, head) are staged into LDS ONCE (S <= 512 keys, 64 B per key
-// per plane), then every wave walks its own 16-query blocks over all
-// key blocks of 32 with no further barriers (qb = wave, wave + waves, ...).
+// K and V of the sequence's keys are staged into LDS (all of them when they fit — always for
+// head_dim 32, and for head_dim 64 up to ~288 keys in fp16x3 — else in chunks of kc keys),
+// then every wave walks its own 16-query blocks over all key blocks of 32 with no further
+// barriers.
 // Transposed formulation keeps P in registers:
-//   S^T[key][q] = K . Q^T   (A = K rows from LDS, B = Q^T fragment held for the block)
+//   S^T[key][q] = K . Q^T   (A = K rows from LDS, B = Q^T fragments held for the block)
 //   O^T[d][q]  += V^T . P^T (A = V^T rows from LDS, B = P^T = the lane's own S^T values)
 // The MFMA C layout puts query q = lane&15 in every lane's column, so the softmax running
 // max / sum and the O rescale are per-lane scalars; the P^T fragment slot 8g+j (g = lane>>4)
 // holds key 4g+j (j<4) or 16+4g+(j-4) (j>=4) of the block, i.e. exactly the lane's two S^T
 // accumulators — V^T is stored in LDS with its keys permuted the same way.
-// qkv: fp16 [T][3H] (Q | K | V; head h = columns h*32 .. +31 of each); ctx: fp16 [T][H].
-// LDS (dynamic): per plane K [Sp][40] + V^T [32][Sp+8] halves, Sp = roundup(len, 32).
+// qkv: fp16 [T][3H] (Q | K | V; head h = columns h*HD .. +HD-1 of each); ctx: fp16 [T][H].
+// LDS (dynamic) per plane: K [cap][HD+8] + V^T [HD][cap+8] halves, cap = keys staged at once.
 // ----------------------------------------------------------------------------------------
 template <bool SPLIT> constexpr int kAttnThreads = SPLIT ? 1024 : 512;   // 4 / 2 waves per SIMD
-constexpr int kKRow = HD + 8;                         // 80-B K rows: conflict-free b128 reads
+constexpr int kAttnLdsMax = 160 * 1024;
 
-__host__ __device__ constexpr int attn_lds_bytes(int sp, int planes) {
-  return planes * (sp * kKRow + HD * (sp + 8)) * 2;
+template <int HD>
+__host__ __device__ constexpr int attn_lds_bytes(int cap, int planes) {
+  return planes * (cap * (HD + 8) + HD * (cap + 8)) * 2;
+}
+// keys staged per chunk (multiple of 32): all of them if they fit, else the most that fit
+template <int HD>
+__host__ __device__ constexpr int attn_chunk_keys(int max_len, int planes) {
+  const int sp = (max_len + 31) & ~31;
+  int kc = sp;
+  while (kc > 32 && attn_lds_bytes<HD>(kc, planes) > kAttnLdsMax) kc -= 32;
+  return kc;
 }
 
 __device__ __forceinline__ int vperm(int k) {       // key k of a 32-block -> P^T slot
   return 8 * ((k & 15) >> 2) + (k & 3) + ((k >> 4) << 2);
 }
 
-template <bool SPLIT>
-__global__ __launch_bounds__(kAttnThreads<SPLIT>) void attn_kernel(const _Float16* __restrict__ qkv,
-                                                            const _Float16* __restrict__ qkv_lo,
-                                                            const int* __restrict__ cu,
-                                                            int max_len, float scale,
-                                                            _Float16* __restrict__ ctx,
-                                                            _Float16* __restrict__ ctx_lo) {
-  constexpr int NP = SPLIT ? 2 : 1;
+template <int HD, bool SPLIT>
+struct AttnState {
+  static constexpr int DT = HD / 16, KS = HD / 32, NP = SPLIT ? 2 : 1;
+  half8 qf[KS][NP];
+  floatx4 o[DT];
+  float m, lsum;
+};
+
+template <int H, int HD, bool SPLIT>
+__global__ __launch_bounds__(kAttnThreads<SPLIT>) void attn_kernel(
+    const _Float16* __restrict__ qkv, const _Float16* __restrict__ qkv_lo,
+    const int* __restrict__ cu, int max_len, int kc, float scale, _Float16* __restrict__ ctx,
+    _Float16* __restrict__ ctx_lo) {
+  using St = AttnState<HD, SPLIT>;
+  constexpr int NP = St::NP, KS = St::KS, DT = St::DT, KROW = HD + 8;
+  constexpr int NW = kAttnThreads<SPLIT> / 64;
   extern __shared__ _Float16 alds[];
   const int h = blockIdx.x, b = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -348,86 +367,93 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>) void attn_kernel(const _Float1
   const int base = cu[b], len = min(cu[b + 1] - cu[b], max_len);
   if (len <= 0) return;
   const int sp = (len + 31) & ~31;
-  const int vrow = sp + 8;
-  _Float16* kls[2] = {alds, alds + sp * kKRow + HD * vrow};
-  _Float16* vts[2] = {alds + sp * kKRow, alds + 2 * sp * kKRow + HD * vrow};
+  const int cap = min(sp, kc);                      // keys per staged chunk
+  const int nch = (sp + cap - 1) / cap;
+  const int vrow = cap + 8;
+  _Float16* kls[2] = {alds, alds + cap * KROW + HD * vrow};
+  _Float16* vts[2] = {alds + cap * KROW, alds + 2 * cap * KROW + HD * vrow};
   const _Float16* planes[2] = {qkv, qkv_lo};
-
-  // ---- stage K (row-major, padded) and V^T (key-permuted) of this (sequence, head)
-  for (int c = tid; c < sp * 4; c += kAttnThreads<SPLIT>) {
-    const int key = c >> 2, dc = (c & 3) * 8;
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-      half8 kv = {}, vv = {};
-      if (key < len) {
-        const _Float16* src = planes[p] + (int64_t)(base + key) * (3 * H) + h * HD + dc;
-        kv = *reinterpret_cast<const half8*>(src + H);
-        vv = *reinterpret_cast<const half8*>(src + 2 * H);
-      }
-      *reinterpret_cast<half8*>(kls[p] + key * kKRow + dc) = kv;
-      const int pos = (key & ~31) + vperm(key & 31);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) vts[p][(dc + e) * vrow + pos] = vv[e];
-    }
-  }
-  __syncthreads();
-
   const int g = lane >> 4, ql = lane & 15;
-  const int nqb = (len + 15) >> 4;
-  for (int qb = wid; qb < nqb; qb += kAttnThreads<SPLIT> / 64) {
-    const int q = qb * 16 + ql;
-    half8 qf[NP];
-    {
-      const int r = min(q, len - 1);
+  const float c2 = scale * 1.44269504088896341f;
+
+  // ---- stage keys [k0, k0 + n) (n multiple of 32; zeros past len): K row-major, V^T permuted
+  auto stage = [&](int k0, int n) {
+    for (int c = tid; c < n * (HD / 8); c += kAttnThreads<SPLIT>) {
+      const int kl = c / (HD / 8), dc = (c % (HD / 8)) * 8, key = k0 + kl;
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        half8 kv = {}, vv = {};
+        if (key < len) {
+          const _Float16* src = planes[p] + (int64_t)(base + key) * (3 * H) + h * HD + dc;
+          kv = *reinterpret_cast<const half8*>(src + H);
+          vv = *reinterpret_cast<const half8*>(src + 2 * H);
+        }
+        *reinterpret_cast<half8*>(kls[p] + kl * KROW + dc) = kv;
+        const int pos = (kl & ~31) + vperm(kl & 31);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) vts[p][(dc + e) * vrow + pos] = vv[e];
+      }
+    }
+  };
+  auto init = [&](St& st, int qb) {
+    const int r = min(qb * 16 + ql, len - 1);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
       for (int p = 0; p < NP; ++p)
-        qf[p] = *reinterpret_cast<const half8*>(planes[p] + (int64_t)(base + r) * (3 * H) +
-                                                h * HD + 8 * g);
-    }
-    floatx4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = {0.f, 0.f, 0.f, 0.f};
-    float m = kNegInf, lsum = 0.f;
-    const float c2 = scale * 1.44269504088896341f;
-    for (int kb = 0; kb < sp; kb += 32) {
-      floatx4 st[2];
+        st.qf[ks][p] = *reinterpret_cast<const half8*>(
+            planes[p] + (int64_t)(base + r) * (3 * H) + h * HD + 32 * ks + 8 * g);
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) st.o[dt] = floatx4{0.f, 0.f, 0.f, 0.f};
+    st.m = kNegInf;
+    st.lsum = 0.f;
+  };
+  // keys [k0, k0 + n) of the staged chunk (LDS positions 0 .. n-1)
+  auto attend = [&](St& st, int k0, int n) {
+    for (int kb = 0; kb < n; kb += 32) {
+      floatx4 sc[2];
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const int kr = (kb + 16 * j + ql) * kKRow + 8 * g;
-        const half8 kf = *reinterpret_cast<const half8*>(kls[0] + kr);
-        st[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qf[0], floatx4{0.f, 0.f, 0.f, 0.f},
-                                                       0, 0, 0);
-        if constexpr (SPLIT) {
-          const half8 kfl = *reinterpret_cast<const half8*>(kls[1] + kr);
-          st[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kfl, qf[0], st[j], 0, 0, 0);
-          st[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qf[1], st[j], 0, 0, 0);
+        sc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          const int kr = (kb + 16 * j + ql) * KROW + 32 * ks + 8 * g;
+          const half8 kf = *reinterpret_cast<const half8*>(kls[0] + kr);
+          sc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, st.qf[ks][0], sc[j], 0, 0, 0);
+          if constexpr (SPLIT) {
+            const half8 kfl = *reinterpret_cast<const half8*>(kls[1] + kr);
+            sc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kfl, st.qf[ks][0], sc[j], 0, 0, 0);
+            sc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, st.qf[ks][1], sc[j], 0, 0, 0);
+          }
         }
       }
-      // lane: S^T[key kb + 16j + 4g + r][q]. Softmax in base 2 with the 1/sqrt(d) scale
+      // lane: S^T[key k0 + kb + 16j + 4g + r][q]. Softmax in base 2 with the 1/sqrt(d) scale
       // folded into one FMA: p = 2^(s*c - m*c), c = scale*log2(e) > 0 (max commutes).
       float mx;
-      if (kb + 32 <= len) {
-        mx = fmaxf(fmaxf(fmaxf(st[0][0], st[0][1]), fmaxf(st[0][2], st[0][3])),
-                   fmaxf(fmaxf(st[1][0], st[1][1]), fmaxf(st[1][2], st[1][3])));
+      if (k0 + kb + 32 <= len) {
+        mx = fmaxf(fmaxf(fmaxf(sc[0][0], sc[0][1]), fmaxf(sc[0][2], sc[0][3])),
+                   fmaxf(fmaxf(sc[1][0], sc[1][1]), fmaxf(sc[1][2], sc[1][3])));
       } else {
         mx = kNegInf;
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            if (kb + 16 * j + 4 * g + r >= len) st[j][r] = kNegInf;
-            mx = fmaxf(mx, st[j][r]);
+            if (k0 + kb + 16 * j + 4 * g + r >= len) sc[j][r] = kNegInf;
+            mx = fmaxf(mx, sc[j][r]);
           }
       }
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mnew = fmaxf(m, mx);
-      const float corr = __builtin_amdgcn_exp2f((m - mnew) * c2);
+      const float mnew = fmaxf(st.m, mx);
+      const float corr = __builtin_amdgcn_exp2f((st.m - mnew) * c2);
       const float nm = -mnew * c2;
       half8 ph, pl;
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float e = __builtin_amdgcn_exp2f(fmaf(st[j][r], c2, nm));
+          const float e = __builtin_amdgcn_exp2f(fmaf(sc[j][r], c2, nm));
           const _Float16 eh = (_Float16)e;
           ph[4 * j + r] = eh;
           if constexpr (SPLIT) pl[4 * j + r] = lo_part(e, eh);
@@ -441,50 +467,72 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>) void attn_kernel(const _Float1
         if constexpr (SPLIT)
           rs = __builtin_amdgcn_fdot2(half2{pl[2 * e2], pl[2 * e2 + 1]}, one2, rs, false);
       }
-      lsum = lsum * corr + rs;                          // reduced across g at the end
-      m = mnew;
+      st.lsum = st.lsum * corr + rs;                  // reduced across g at the end
+      st.m = mnew;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        o0[r] *= corr;
-        o1[r] *= corr;
-      }
-      const int vr0 = ql * vrow + kb + 8 * g, vr1 = (16 + ql) * vrow + kb + 8 * g;
-      const half8 v0 = *reinterpret_cast<const half8*>(vts[0] + vr0);
-      const half8 v1 = *reinterpret_cast<const half8*>(vts[0] + vr1);
-      if constexpr (SPLIT) {
-        const half8 v0l = *reinterpret_cast<const half8*>(vts[1] + vr0);
-        const half8 v1l = *reinterpret_cast<const half8*>(vts[1] + vr1);
-        o0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(v0l, ph, o0, 0, 0, 0);
-        o1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(v1l, ph, o1, 0, 0, 0);
-        o0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(v0, pl, o0, 0, 0, 0);
-        o1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(v1, pl, o1, 0, 0, 0);
-      }
-      o0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(v0, ph, o0, 0, 0, 0);
-      o1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(v1, ph, o1, 0, 0, 0);
-    }
-    lsum += __shfl_xor(lsum, 16, 64);
-    lsum += __shfl_xor(lsum, 32, 64);
-    if (q < len) {
-      // lane: O^T[d = 4g + r][q] (o0) and d = 16 + 4g + r (o1)
-      const float inv = 1.0f / lsum;
-      const int64_t off = (int64_t)(base + q) * H + h * HD + 4 * g;
-      half4 a, c, al, cl;
+      for (int dt = 0; dt < DT; ++dt) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float x0 = o0[r] * inv, x1 = o1[r] * inv;
-        a[r] = (_Float16)x0;
-        c[r] = (_Float16)x1;
+        for (int r = 0; r < 4; ++r) st.o[dt][r] *= corr;
+        const int vr = (16 * dt + ql) * vrow + kb + 8 * g;
+        const half8 v = *reinterpret_cast<const half8*>(vts[0] + vr);
         if constexpr (SPLIT) {
-          al[r] = lo_part(x0, a[r]);
-          cl[r] = lo_part(x1, c[r]);
+          const half8 vl = *reinterpret_cast<const half8*>(vts[1] + vr);
+          st.o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vl, ph, st.o[dt], 0, 0, 0);
+          st.o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(v, pl, st.o[dt], 0, 0, 0);
         }
+        st.o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(v, ph, st.o[dt], 0, 0, 0);
       }
-      *reinterpret_cast<half4*>(ctx + off) = a;
-      *reinterpret_cast<half4*>(ctx + off + 16) = c;
-      if constexpr (SPLIT) {
-        *reinterpret_cast<half4*>(ctx_lo + off) = al;
-        *reinterpret_cast<half4*>(ctx_lo + off + 16) = cl;
+    }
+  };
+  auto finish = [&](St& st, int qb) {
+    float l = st.lsum;
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const int q = qb * 16 + ql;
+    if (q < len) {
+      // lane: O^T[d = 16dt + 4g + r][q]
+      const float inv = 1.0f / l;
+      const int64_t off = (int64_t)(base + q) * H + h * HD + 4 * g;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        half4 a, al;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float x = st.o[dt][r] * inv;
+          a[r] = (_Float16)x;
+          if constexpr (SPLIT) al[r] = lo_part(x, a[r]);
+        }
+        *reinterpret_cast<half4*>(ctx + off + 16 * dt) = a;
+        if constexpr (SPLIT) *reinterpret_cast<half4*>(ctx_lo + off + 16 * dt) = al;
       }
+    }
+  };
+
+  const int nqb = (len + 15) >> 4;
+  if (nch == 1) {
+    stage(0, sp);
+    __syncthreads();
+    for (int qb = wid; qb < nqb; qb += NW) {
+      St st;
+      init(st, qb);
+      attend(st, 0, sp);
+      finish(st, qb);
+    }
+  } else {
+    // keys do not fit at once: for each round of query blocks, stream the key chunks
+    // (every wave joins every barrier; waves without a block this round only stage)
+    for (int q0 = 0; q0 < nqb; q0 += NW) {
+      const int qb = q0 + wid;
+      St st;
+      if (qb < nqb) init(st, qb);
+      for (int ch = 0; ch < nch; ++ch) {
+        const int k0 = ch * cap, n = min(cap, sp - k0);
+        __syncthreads();
+        stage(k0, n);
+        __syncthreads();
+        if (qb < nqb) attend(st, k0, n);
+      }
+      if (qb < nqb) finish(st, qb);
     }
   }
 }
@@ -493,6 +541,7 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>) void attn_kernel(const _Float1
 // heads
 // ----------------------------------------------------------------------------------------
 // bge (sentence-transformers Pooling(cls) + Normalize): out[b] = x[cls] / max(||x[cls]||, 1e-12)
+template <int H>
 __global__ __launch_bounds__(64) void cls_normalize_kernel(const float* __restrict__ x,
                                                            const int* __restrict__ cu,
                                                            float* __restrict__ out) {
@@ -513,6 +562,7 @@ __global__ __launch_bounds__(64) void cls_normalize_kernel(const float* __restri
 }
 
 // cross-encoder: pooled = tanh(Wp x[cls] + bp); logit = Wc pooled + bc (num_labels = 1)
+template <int H>
 __global__ __launch_bounds__(256) void ce_head_kernel(const float* __restrict__ x,
                                                       const int* __restrict__ cu,
                                                       const float* __restrict__ wp,

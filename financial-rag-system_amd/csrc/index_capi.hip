@@ -127,7 +127,10 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
   else
     launch_seed<D, false>(h, w, st);
   const int64_t n_tiles = (h->count + 15) / 16;
-  int grid = (int)std::min<int64_t>(h->max_wgs, std::max<int64_t>(1, (n_tiles + 3) / 4));
+  // D <= 384: queries in VGPRs, 2 workgroups per CU; wider rows: queries in LDS, 1 per CU
+  constexpr bool kLdsQ = D > 384;
+  const int max_wgs = kLdsQ ? h->max_wgs / 2 : h->max_wgs;
+  int grid = (int)std::min<int64_t>(max_wgs, std::max<int64_t>(1, (n_tiles + 3) / 4));
   grid = std::min(grid, kMaxLists / kWavesPerWG);
   ProfPair pp{};
   const bool timed = h->prof > 0 && (h->prof_seq++ % h->prof) == 0;
@@ -136,14 +139,21 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
     RAG_HIP(hipEventCreate(&pp.b));
     RAG_HIP(hipEventRecord(pp.a, st));
   }
-  if (filt)
-    scan_kernel<D, true><<<dim3(grid), dim3(256), 0, st>>>(
-        h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, (int)n_tiles, w.seed, w.part_s,
-        w.part_i, w.heads_s, w.heads_i, w.heads_n);
-  else
-    scan_kernel<D, false><<<dim3(grid), dim3(256), 0, st>>>(
-        h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, (int)n_tiles, w.seed, w.part_s,
-        w.part_i, w.heads_s, w.heads_i, w.heads_n);
+#define RAG_SCAN_ARGS                                                                    \
+  h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, (int)n_tiles, w.seed, w.part_s, w.part_i, \
+      w.heads_s, w.heads_i, w.heads_n
+  if constexpr (kLdsQ) {
+    if (filt)
+      scan_lds_kernel<D, true><<<dim3(grid), dim3(256), 0, st>>>(RAG_SCAN_ARGS);
+    else
+      scan_lds_kernel<D, false><<<dim3(grid), dim3(256), 0, st>>>(RAG_SCAN_ARGS);
+  } else {
+    if (filt)
+      scan_kernel<D, true><<<dim3(grid), dim3(256), 0, st>>>(RAG_SCAN_ARGS);
+    else
+      scan_kernel<D, false><<<dim3(grid), dim3(256), 0, st>>>(RAG_SCAN_ARGS);
+  }
+#undef RAG_SCAN_ARGS
   if (timed) {
     RAG_HIP(hipEventRecord(pp.b, st));
     h->prof_pairs.push_back(pp);

@@ -168,6 +168,181 @@ __device__ __forceinline__ void flush_mask(const WaveTopK& w, uint64_t b, int qt
   }
 }
 
+// Per-wave top-k state of a scan (shared by the VGPR-query and LDS-query scan kernels).
+struct ScanTopK {
+  WaveTopK w;
+  float thr0, thr1;
+  int cnt0, cnt1;
+  uint32_t fm0, fv0, fm1, fv1;
+};
+
+template <bool FILTER>
+__device__ __forceinline__ void topk_init(ScanTopK& st, int* lds, int wid, int lane,
+                                          const float* __restrict__ seed_thr,
+                                          const uint32_t* __restrict__ filt) {
+  st.w.keep_s = reinterpret_cast<float*>(lds + wid * kLdsPerWave);
+  st.w.keep_i = lds + wid * kLdsPerWave + 1024;
+  st.w.pend_s = reinterpret_cast<float*>(lds + wid * kLdsPerWave + 2048);
+  st.w.pend_i = lds + wid * kLdsPerWave + 3072;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    st.w.keep_s[lane + 64 * j] = kNegInf;
+    st.w.keep_i[lane + 64 * j] = kIdNone32;
+    st.w.pend_s[lane + 64 * j] = kNegInf;
+    st.w.pend_i[lane + 64 * j] = kIdNone32;
+  }
+  lds_fence();
+  // Seed thresholds: seed_thr[q] is a lower bound of the global 32nd-best score (32 rows
+  // scoring >= it exist, sample_kernel), so rows scoring below it can never be in the top-32.
+  // `> pred(T)` == `>= T`; thresholds only ever rise.
+  st.thr0 = kNegInf;
+  st.thr1 = kNegInf;
+  if (seed_thr) {
+    const float T0 = seed_thr[lane & 15], T1 = seed_thr[16 + (lane & 15)];
+    st.thr0 = T0 == kNegInf ? kNegInf : nextafterf(T0, kNegInf);
+    st.thr1 = T1 == kNegInf ? kNegInf : nextafterf(T1, kNegInf);
+  }
+  st.cnt0 = 0;
+  st.cnt1 = 0;
+  st.fm0 = st.fv0 = st.fm1 = st.fv1 = 0;
+  if constexpr (FILTER) {
+    st.fm0 = filt[2 * (lane & 15)];
+    st.fv0 = filt[2 * (lane & 15) + 1];
+    st.fm1 = filt[2 * (16 + (lane & 15))];
+    st.fv1 = filt[2 * (16 + (lane & 15)) + 1];
+  }
+}
+
+// Scores of tile t (acc0: queries 0-15, acc1: 16-31; lane rows 16t + 4(l>>4) + r) -> pending
+// entries above the thresholds, flushing queries whose lanes run out of pending slots.
+template <bool FILTER>
+__device__ __forceinline__ void topk_tile(ScanTopK& st, const floatx4& acc0, const floatx4& acc1,
+                                          int t, int n_rows, const uint32_t* __restrict__ tags,
+                                          int lane) {
+  const int rbase = t * kTileRows + 4 * (lane >> 4);
+  uint4 tg = {0u, 0u, 0u, 0u};
+  if constexpr (FILTER) tg = *reinterpret_cast<const uint4*>(tags + rbase);
+  float v0[4], v1[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const bool ok = (rbase + r) < n_rows;
+    bool ok0 = ok, ok1 = ok;
+    if constexpr (FILTER) {
+      const uint32_t tr = r == 0 ? tg.x : r == 1 ? tg.y : r == 2 ? tg.z : tg.w;
+      ok0 = ok0 && ((tr & st.fm0) == st.fv0);
+      ok1 = ok1 && ((tr & st.fm1) == st.fv1);
+    }
+    v0[r] = ok0 ? acc0[r] : kNegInf;
+    v1[r] = ok1 ? acc1[r] : kNegInf;
+  }
+  const float m0 = fmaxf(fmaxf(v0[0], v0[1]), fmaxf(v0[2], v0[3]));
+  const float m1 = fmaxf(fmaxf(v1[0], v1[1]), fmaxf(v1[2], v1[3]));
+  if (__ballot((m0 > st.thr0) || (m1 > st.thr1))) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (v0[r] > st.thr0) {
+        st.w.pend_s[st.cnt0 * 64 + lane] = v0[r];
+        st.w.pend_i[st.cnt0 * 64 + lane] = rbase + r;
+        ++st.cnt0;
+      }
+      if (v1[r] > st.thr1) {
+        st.w.pend_s[(kP + st.cnt1) * 64 + lane] = v1[r];
+        st.w.pend_i[(kP + st.cnt1) * 64 + lane] = rbase + r;
+        ++st.cnt1;
+      }
+    }
+    lds_fence();
+    const uint64_t b0 = __ballot(st.cnt0 > kP - 4);
+    const uint64_t b1 = __ballot(st.cnt1 > kP - 4);
+    if (b0) flush_mask(st.w, b0, 0, lane, st.thr0, st.cnt0, st.thr1, st.cnt1);
+    if (b1) flush_mask(st.w, b1, 1, lane, st.thr0, st.cnt0, st.thr1, st.cnt1);
+  }
+}
+
+// End of scan: flush what is pending and write this wave's sorted list (finite entries), its
+// head and its length per query.
+__device__ __forceinline__ void topk_finish(ScanTopK& st, int lane, int gw, int nw,
+                                            float* __restrict__ part_s, int* __restrict__ part_i,
+                                            float* __restrict__ heads_s,
+                                            int* __restrict__ heads_i, int* __restrict__ heads_n) {
+  WaveTopK& w = st.w;
+  // With seeded thresholds most queries never flushed during the scan: their keep list is
+  // empty and their <= 32 pending entries (4 lanes x 8 slots) only need a 32-wide sort, two
+  // queries per pass. Queries with a non-empty keep list take flush_query.
+  {
+    const uint64_t b0 = __ballot(st.cnt0 > 0);
+    const uint64_t b1 = __ballot(st.cnt1 > 0);
+    const uint32_t p0 = (uint32_t)((b0 | (b0 >> 16) | (b0 >> 32) | (b0 >> 48)) & 0xffffu);
+    const uint32_t p1 = (uint32_t)((b1 | (b1 >> 16) | (b1 >> 32) | (b1 >> 48)) & 0xffffu);
+    const uint32_t pend = p0 | (p1 << 16);
+    const uint32_t kept =
+        (uint32_t)__ballot(lane < kQ && w.keep_s[(lane & 31) * kKS] != kNegInf);
+    uint32_t full = pend & kept;
+    uint32_t only = pend & ~kept;
+    while (full) {
+      const int q = __builtin_ctz(full);
+      full &= full - 1;
+      flush_query(w, q, lane, st.thr0, st.cnt0, st.thr1, st.cnt1);
+    }
+    while (only) {
+      const int qa = __builtin_ctz(only);
+      only &= only - 1;
+      const int qb = only ? __builtin_ctz(only) : -1;
+      if (only) only &= only - 1;
+      const int q = lane < 32 ? qa : qb;
+      const int j = lane & 31;
+      float s = kNegInf;
+      int id = kIdNone32;
+      if (q >= 0) {
+        const int pidx = (((q >> 4) * kP + (j & 7)) * 64) + (q & 15) + 16 * (j >> 3);
+        s = w.pend_s[pidx];
+        id = w.pend_i[pidx];
+      }
+      lds_fence();
+      bitonic_sort32x2(s, id, lane);
+      if (q >= 0) {
+        w.keep_s[q * kKS + j] = s;
+        w.keep_i[q * kKS + j] = id;
+      }
+      lds_fence();
+    }
+  }
+  float* ps = part_s + (int64_t)gw * (kQ * kKS);
+  int* pi = part_i + (int64_t)gw * (kQ * kKS);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const float v = w.keep_s[lane + 64 * j];
+    if (v != kNegInf) {
+      ps[lane + 64 * j] = v;
+      pi[lane + 64 * j] = w.keep_i[lane + 64 * j];
+    }
+  }
+  if (lane < kQ) {
+    int n = 0;
+    for (int j = 0; j < kKS; ++j) n += w.keep_s[lane * kKS + j] != kNegInf;
+    heads_s[lane * nw + gw] = w.keep_s[lane * kKS];
+    heads_i[lane * nw + gw] = n > 0 ? w.keep_i[lane * kKS] : kIdNone32;
+    heads_n[lane * nw + gw] = n;
+  }
+}
+
+// Tile sequence of wave gw of nw: t_j = t_first + j * t_step, j < n_mine (always increasing,
+// which the strict `> thr` tie rule relies on). STRIDED: t = gw, gw + nw, ... (the chip sweeps
+// one window of the corpus at a time); else contiguous ranges.
+template <bool STRIDED>
+__device__ __forceinline__ void tile_sequence(int gw, int nw, int n_tiles, int& t_first,
+                                              int& t_step, int& n_mine) {
+  if constexpr (STRIDED) {
+    t_first = gw;
+    t_step = nw;
+    n_mine = gw < n_tiles ? (n_tiles - 1 - gw) / nw + 1 : 0;
+  } else {
+    t_first = (int)((int64_t)n_tiles * gw / nw);
+    t_step = 1;
+    n_mine = (int)((int64_t)n_tiles * (gw + 1) / nw) - t_first;
+  }
+}
+
 // Variant knobs (A/B'd by rag_bench_scan; the production instance is scan_kernel<D, F>):
 //   MODE 0 full scan + top-k; 1 MFMA only (running max, no top-k); 2 loads only
 //   STRIDED tile order gw, gw+nw, ... (the chip sweeps one window) vs contiguous ranges
@@ -175,6 +350,7 @@ __device__ __forceinline__ void flush_mask(const WaveTopK& w, uint64_t b, int qt
 //      'nt-weights': once-read streams)
 //   SB sched_barrier after each tile's load batch, so the scheduler cannot sink the next
 //      tile's loads below the current tile's wait (which leaves one tile in flight)
+// Query B-operands live in VGPRs (2 x D/32 half8 per lane): the D = 384 production kernel.
 template <int D, bool FILTER, int MODE = 0, bool STRIDED = true, bool NT = true, bool SB = true>
 __global__ __launch_bounds__(256, 2) void scan_kernel(
     const half8* __restrict__ corpus, const uint32_t* __restrict__ tags,
@@ -185,34 +361,13 @@ __global__ __launch_bounds__(256, 2) void scan_kernel(
   __shared__ int lds[kWavesPerWG * kLdsPerWave];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
-  WaveTopK w;
-  w.keep_s = reinterpret_cast<float*>(lds + wid * kLdsPerWave);
-  w.keep_i = lds + wid * kLdsPerWave + 1024;
-  w.pend_s = reinterpret_cast<float*>(lds + wid * kLdsPerWave + 2048);
-  w.pend_i = lds + wid * kLdsPerWave + 3072;
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    w.keep_s[lane + 64 * j] = kNegInf;
-    w.keep_i[lane + 64 * j] = kIdNone32;
-    w.pend_s[lane + 64 * j] = kNegInf;
-    w.pend_i[lane + 64 * j] = kIdNone32;
-  }
-  lds_fence();
+  ScanTopK st;
+  topk_init<FILTER>(st, lds, wid, lane, seed_thr, filt);
 
   const int gw = blockIdx.x * kWavesPerWG + __builtin_amdgcn_readfirstlane(wid);
   const int nw = gridDim.x * kWavesPerWG;
-  // tile sequence of this wave: t_j = t_first + j * t_step, j < n_mine (always increasing,
-  // which the strict `> thr` tie rule relies on)
   int t_first, t_step, n_mine;
-  if constexpr (STRIDED) {
-    t_first = gw;
-    t_step = nw;
-    n_mine = gw < n_tiles ? (n_tiles - 1 - gw) / nw + 1 : 0;
-  } else {
-    t_first = (int)((int64_t)n_tiles * gw / nw);
-    t_step = 1;
-    n_mine = (int)((int64_t)n_tiles * (gw + 1) / nw) - t_first;
-  }
+  tile_sequence<STRIDED>(gw, nw, n_tiles, t_first, t_step, n_mine);
 
   half8 q0[S], q1[S];
 #pragma unroll
@@ -221,78 +376,14 @@ __global__ __launch_bounds__(256, 2) void scan_kernel(
     q1[s] = qfrag[(S + s) * 64 + lane];
   }
 
-  // Seed thresholds: seed_thr[q] is a lower bound of the global 32nd-best score (32 rows
-  // scoring >= it exist, sample_kernel), so rows scoring below it can never be in the top-32.
-  // `> pred(T)` == `>= T`; thresholds only ever rise.
-  float thr0 = kNegInf, thr1 = kNegInf;
-  if (seed_thr) {
-    const float T0 = seed_thr[lane & 15], T1 = seed_thr[16 + (lane & 15)];
-    thr0 = T0 == kNegInf ? kNegInf : nextafterf(T0, kNegInf);
-    thr1 = T1 == kNegInf ? kNegInf : nextafterf(T1, kNegInf);
-  }
-  int cnt0 = 0, cnt1 = 0;
-  const int rsub = 4 * (lane >> 4);
-  uint32_t fm0 = 0, fv0 = 0, fm1 = 0, fv1 = 0;
-  if constexpr (FILTER) {
-    fm0 = filt[2 * (lane & 15)];
-    fv0 = filt[2 * (lane & 15) + 1];
-    fm1 = filt[2 * (16 + (lane & 15))];
-    fv1 = filt[2 * (16 + (lane & 15)) + 1];
-  }
-
-  auto process = [&](const half8(&a)[S], int t) {
-    floatx4 acc0 = {0.f, 0.f, 0.f, 0.f};
-    floatx4 acc1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < S; ++s) {
-      acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[s], q0[s], acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[s], q1[s], acc1, 0, 0, 0);
-    }
-    const int rbase = t * kTileRows + rsub;
-    uint4 tg = {0u, 0u, 0u, 0u};
-    if constexpr (FILTER) tg = *reinterpret_cast<const uint4*>(tags + rbase);
-    float v0[4], v1[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const bool ok = (rbase + r) < n_rows;
-      bool ok0 = ok, ok1 = ok;
-      if constexpr (FILTER) {
-        const uint32_t tr = r == 0 ? tg.x : r == 1 ? tg.y : r == 2 ? tg.z : tg.w;
-        ok0 = ok0 && ((tr & fm0) == fv0);
-        ok1 = ok1 && ((tr & fm1) == fv1);
-      }
-      v0[r] = ok0 ? acc0[r] : kNegInf;
-      v1[r] = ok1 ? acc1[r] : kNegInf;
-    }
-    const float m0 = fmaxf(fmaxf(v0[0], v0[1]), fmaxf(v0[2], v0[3]));
-    const float m1 = fmaxf(fmaxf(v1[0], v1[1]), fmaxf(v1[2], v1[3]));
-    if (__ballot((m0 > thr0) || (m1 > thr1))) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (v0[r] > thr0) {
-          w.pend_s[cnt0 * 64 + lane] = v0[r];
-          w.pend_i[cnt0 * 64 + lane] = rbase + r;
-          ++cnt0;
-        }
-        if (v1[r] > thr1) {
-          w.pend_s[(kP + cnt1) * 64 + lane] = v1[r];
-          w.pend_i[(kP + cnt1) * 64 + lane] = rbase + r;
-          ++cnt1;
-        }
-      }
-      lds_fence();
-      const uint64_t b0 = __ballot(cnt0 > kP - 4);
-      const uint64_t b1 = __ballot(cnt1 > kP - 4);
-      if (b0) flush_mask(w, b0, 0, lane, thr0, cnt0, thr1, cnt1);
-      if (b1) flush_mask(w, b1, 1, lane, thr0, cnt0, thr1, cnt1);
-    }
-  };
-
   float vmax = kNegInf;   // MODE 1/2: keeps the work alive
   auto process_v = [&](const half8(&a)[S], int t) {
-    if constexpr (MODE == 0) {
-      process(a, t);
-    } else if constexpr (MODE == 1) {
+    if constexpr (MODE == 2) {
+      half8 x = a[0];
+#pragma unroll
+      for (int s = 1; s < S; ++s) x += a[s];
+      vmax = fmaxf(vmax, (float)(x[0] + x[1] + x[2] + x[3] + x[4] + x[5] + x[6] + x[7]));
+    } else {
       floatx4 acc0 = {0.f, 0.f, 0.f, 0.f};
       floatx4 acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -300,13 +391,11 @@ __global__ __launch_bounds__(256, 2) void scan_kernel(
         acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[s], q0[s], acc0, 0, 0, 0);
         acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[s], q1[s], acc1, 0, 0, 0);
       }
-      vmax = fmaxf(vmax, fmaxf(fmaxf(fmaxf(acc0[0], acc0[1]), fmaxf(acc0[2], acc0[3])),
-                               fmaxf(fmaxf(acc1[0], acc1[1]), fmaxf(acc1[2], acc1[3]))));
-    } else {
-      half8 x = a[0];
-#pragma unroll
-      for (int s = 1; s < S; ++s) x += a[s];
-      vmax = fmaxf(vmax, (float)(x[0] + x[1] + x[2] + x[3] + x[4] + x[5] + x[6] + x[7]));
+      if constexpr (MODE == 0)
+        topk_tile<FILTER>(st, acc0, acc1, t, n_rows, tags, lane);
+      else
+        vmax = fmaxf(vmax, fmaxf(fmaxf(fmaxf(acc0[0], acc0[1]), fmaxf(acc0[2], acc0[3])),
+                                 fmaxf(fmaxf(acc1[0], acc1[1]), fmaxf(acc1[2], acc1[3]))));
     }
   };
 
@@ -344,66 +433,75 @@ __global__ __launch_bounds__(256, 2) void scan_kernel(
     if (vmax == 12345.0f) part_s[gw] = vmax;   // never true in practice; defeats DCE
     return;
   }
+  topk_finish(st, lane, gw, nw, part_s, part_i, heads_s, heads_i, heads_n);
+}
 
-  // ---- final flush. With seeded thresholds most queries never flushed during the scan:
-  // their keep list is empty and their <= 32 pending entries (4 lanes x 8 slots) only need a
-  // 32-wide sort, two queries per pass. Queries with a non-empty keep list take flush_query.
-  {
-    const uint64_t b0 = __ballot(cnt0 > 0);
-    const uint64_t b1 = __ballot(cnt1 > 0);
-    const uint32_t p0 = (uint32_t)((b0 | (b0 >> 16) | (b0 >> 32) | (b0 >> 48)) & 0xffffu);
-    const uint32_t p1 = (uint32_t)((b1 | (b1 >> 16) | (b1 >> 32) | (b1 >> 48)) & 0xffffu);
-    const uint32_t pend = p0 | (p1 << 16);
-    const uint32_t kept =
-        (uint32_t)__ballot(lane < kQ && w.keep_s[(lane & 31) * kKS] != kNegInf);
-    uint32_t full = pend & kept;
-    uint32_t only = pend & ~kept;
-    while (full) {
-      const int q = __builtin_ctz(full);
-      full &= full - 1;
-      flush_query(w, q, lane, thr0, cnt0, thr1, cnt1);
-    }
-    while (only) {
-      const int qa = __builtin_ctz(only);
-      only &= only - 1;
-      const int qb = only ? __builtin_ctz(only) : -1;
-      if (only) only &= only - 1;
-      const int q = lane < 32 ? qa : qb;
-      const int j = lane & 31;
-      float s = kNegInf;
-      int id = kIdNone32;
-      if (q >= 0) {
-        const int pidx = (((q >> 4) * kP + (j & 7)) * 64) + (q & 15) + 16 * (j >> 3);
-        s = w.pend_s[pidx];
-        id = w.pend_i[pidx];
-      }
-      lds_fence();
-      bitonic_sort32x2(s, id, lane);
-      if (q >= 0) {
-        w.keep_s[q * kKS + j] = s;
-        w.keep_i[q * kKS + j] = id;
-      }
-      lds_fence();
-    }
-  }
-  // ---- outputs: finite entries of each sorted keep list, list heads and lengths
-  float* ps = part_s + (int64_t)gw * (kQ * kKS);
-  int* pi = part_i + (int64_t)gw * (kQ * kKS);
+// LDS-query scan for wide rows (D = 1024: the B-operands of 32 queries are 64 KB, too many
+// VGPRs). The fragments are staged into LDS once per workgroup (one workgroup per CU: 64 KB
+// queries + 64 KB top-k state); each wave streams its tiles in chunks of 8 k-steps (8 KB) through
+// a ring of D/256 chunk registers, so while one chunk is multiplied the remaining chunks of the
+// tile (and the next tile's first chunks) are in flight — 3 x 8 KB per wave, enough to cover
+// HBM latency at one wave per SIMD. Per chunk: 8 A-fragments (buffer loads off a wave-uniform
+// descriptor, non-temporal), 16 B-fragments from LDS (conflict-free: lane-linear), 16 MFMAs.
+template <int D, bool FILTER>
+__global__ __launch_bounds__(256, 1) void scan_lds_kernel(
+    const half8* __restrict__ corpus, const uint32_t* __restrict__ tags,
+    const uint32_t* __restrict__ filt, const half8* __restrict__ qfrag, int n_rows, int n_tiles,
+    const float* __restrict__ seed_thr, float* __restrict__ part_s, int* __restrict__ part_i,
+    float* __restrict__ heads_s, int* __restrict__ heads_i, int* __restrict__ heads_n) {
+  constexpr int S = steps<D>(), CH = 8, NCH = S / CH;
+  static_assert(S % CH == 0 && NCH >= 2, "LDS-query scan: D must be a multiple of 256 (>= 512)");
+  __shared__ int lds[kWavesPerWG * kLdsPerWave];
+  __shared__ half8 qb[2 * S * 64];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < 2 * S * 64; i += 256) qb[i] = qfrag[i];
+  ScanTopK st;
+  topk_init<FILTER>(st, lds, wid, lane, seed_thr, filt);
+  __syncthreads();
+
+  const int gw = blockIdx.x * kWavesPerWG + __builtin_amdgcn_readfirstlane(wid);
+  const int nw = gridDim.x * kWavesPerWG;
+  int t_first, t_step, n_mine;
+  tile_sequence<true>(gw, nw, n_tiles, t_first, t_step, n_mine);
+
+  if (n_mine > 0) {
+    half8 buf[NCH][CH];
+    const char* cbase = reinterpret_cast<const char*>(corpus);
+    const int voff = lane * 16;
+    auto load_chunk = [&](half8(&a)[CH], int j, int c) {
+      const int t = __builtin_amdgcn_readfirstlane(t_first + j * t_step);
+      const char* tp = cbase + (int64_t)t * (S * 1024) + c * (CH * 1024);
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(tp), 0, CH * 1024, 0x00020000);
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const float v = w.keep_s[lane + 64 * j];
-    if (v != kNegInf) {
-      ps[lane + 64 * j] = v;
-      pi[lane + 64 * j] = w.keep_i[lane + 64 * j];
+      for (int s = 0; s < CH; ++s) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, s * 1024, 2);
+        a[s] = __builtin_bit_cast(half8, v);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    };
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) load_chunk(buf[c], 0, c);
+    for (int j = 0; j < n_mine; ++j) {
+      const int jn = min(j + 1, n_mine - 1);
+      floatx4 acc0 = {0.f, 0.f, 0.f, 0.f};
+      floatx4 acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+#pragma unroll
+        for (int s = 0; s < CH; ++s) {
+          const half8 b0 = qb[(c * CH + s) * 64 + lane];
+          const half8 b1 = qb[(S + c * CH + s) * 64 + lane];
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(buf[c][s], b0, acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(buf[c][s], b1, acc1, 0, 0, 0);
+        }
+        load_chunk(buf[c], jn, c);
+      }
+      topk_tile<FILTER>(st, acc0, acc1, t_first + j * t_step, n_rows, tags, lane);
     }
   }
-  if (lane < kQ) {
-    int n = 0;
-    for (int j = 0; j < kKS; ++j) n += w.keep_s[lane * kKS + j] != kNegInf;
-    heads_s[lane * nw + gw] = w.keep_s[lane * kKS];
-    heads_i[lane * nw + gw] = n > 0 ? w.keep_i[lane * kKS] : kIdNone32;
-    heads_n[lane * nw + gw] = n;
-  }
+  topk_finish(st, lane, gw, nw, part_s, part_i, heads_s, heads_i, heads_n);
 }
 
 // ----------------------------------------------------------------------------------------
@@ -431,13 +529,56 @@ __global__ __launch_bounds__(256) void sample_kernel(const half8* __restrict__ c
   const int t1 = two ? (int)(((int64_t)(j0 + 1) * n_tiles) / n_sample) : t0;
   const half8* p0 = corpus + (int64_t)t0 * (S * 64) + lane;
   const half8* p1 = corpus + (int64_t)t1 * (S * 64) + lane;
-  half8 a0[S], a1[S], b0[S], b1[S];
+  // scores of the two sample tiles: all loads in flight at once (D <= 384), or in chunks of 8
+  // k-steps with the query fragments re-read from L2 (wide rows: 4 x D/32 half8 would spill)
+  floatx4 sc[2][2];
+  if constexpr (S <= 12) {
+    half8 a0[S], a1[S], b0[S], b1[S];
 #pragma unroll
-  for (int s = 0; s < S; ++s) {
-    a0[s] = __builtin_nontemporal_load(p0 + s * 64);
-    a1[s] = __builtin_nontemporal_load(p1 + s * 64);
-    b0[s] = qfrag[s * 64 + lane];
-    b1[s] = qfrag[(S + s) * 64 + lane];
+    for (int s = 0; s < S; ++s) {
+      a0[s] = __builtin_nontemporal_load(p0 + s * 64);
+      a1[s] = __builtin_nontemporal_load(p1 + s * 64);
+      b0[s] = qfrag[s * 64 + lane];
+      b1[s] = qfrag[(S + s) * 64 + lane];
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const half8(&a)[S] = u == 0 ? a0 : a1;
+      floatx4 acc0 = {0.f, 0.f, 0.f, 0.f};
+      floatx4 acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[s], b0[s], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[s], b1[s], acc1, 0, 0, 0);
+      }
+      sc[u][0] = acc0;
+      sc[u][1] = acc1;
+    }
+  } else {
+    constexpr int CH = 8;
+    static_assert(S % CH == 0, "sample: wide D must be a multiple of 256");
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const half8* p = u == 0 ? p0 : p1;
+      floatx4 acc0 = {0.f, 0.f, 0.f, 0.f};
+      floatx4 acc1 = {0.f, 0.f, 0.f, 0.f};
+      for (int c = 0; c < S / CH; ++c) {
+        half8 a[CH], b0[CH], b1[CH];
+#pragma unroll
+        for (int s = 0; s < CH; ++s) {
+          a[s] = __builtin_nontemporal_load(p + (c * CH + s) * 64);
+          b0[s] = qfrag[(c * CH + s) * 64 + lane];
+          b1[s] = qfrag[(S + c * CH + s) * 64 + lane];
+        }
+#pragma unroll
+        for (int s = 0; s < CH; ++s) {
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[s], b0[s], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[s], b1[s], acc1, 0, 0, 0);
+        }
+      }
+      sc[u][0] = acc0;
+      sc[u][1] = acc1;
+    }
   }
   uint32_t fm0 = 0, fv0 = 0, fm1 = 0, fv1 = 0;
   if constexpr (FILTER) {
@@ -449,15 +590,8 @@ __global__ __launch_bounds__(256) void sample_kernel(const half8* __restrict__ c
   float mx[2][2];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
-    const half8(&a)[S] = u == 0 ? a0 : a1;
     const int t = u == 0 ? t0 : t1;
-    floatx4 acc0 = {0.f, 0.f, 0.f, 0.f};
-    floatx4 acc1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < S; ++s) {
-      acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[s], b0[s], acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[s], b1[s], acc1, 0, 0, 0);
-    }
+    const floatx4 acc0 = sc[u][0], acc1 = sc[u][1];
     const int rbase = t * kTileRows + 4 * (lane >> 4);
     uint4 tg = {0u, 0u, 0u, 0u};
     if constexpr (FILTER) tg = *reinterpret_cast<const uint4*>(tags + rbase);

@@ -27,6 +27,9 @@ from scipy.special import erf
 
 BGE_SMALL = dict(vocab=30522, hidden=384, layers=12, heads=12, inter=1536, max_pos=512,
                  type_vocab=2, eps=1e-12, pooler=False)
+# bge-large-en-v1.5 shape (1024-d vectors)
+BGE_LARGE = dict(vocab=30522, hidden=1024, layers=24, heads=16, inter=4096, max_pos=512,
+                 type_vocab=2, eps=1e-12, pooler=False)
 MINILM_CE = dict(vocab=30522, hidden=384, layers=6, heads=12, inter=1536, max_pos=512,
                  type_vocab=2, eps=1e-12, pooler=True, num_labels=1)
 

@@ -22,7 +22,7 @@ def find(d, pat):
 def main():
     tag, trace_dir, pmc_dir = sys.argv[1], sys.argv[2], sys.argv[3]
     bench_log = sys.argv[4] if len(sys.argv) > 4 else None
-    out = os.path.join(ROOT, "profiles")
+    out = os.environ.get("PROFILES_DIR", os.path.join(ROOT, "profiles"))
     os.makedirs(out, exist_ok=True)
     stats = find(trace_dir, "*kernel_stats.csv")
     summary = {}

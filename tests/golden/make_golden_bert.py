@@ -17,6 +17,8 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 import bert_ref as R  # noqa: E402
 
+BGE_LARGE_2L = dict(R.BGE_LARGE, layers=2)
+
 
 def hf_model(cfg, w, seq_cls):
     from transformers import BertConfig, BertForSequenceClassification, BertModel
@@ -63,10 +65,16 @@ def main():
     wc = R.make_weights(R.MINILM_CE, seed=12)
     emb = hf_bge(R.BGE_SMALL, wb, ids_q, tt_q, m_q)
     logit = hf_ce(R.MINILM_CE, wc, ids_p, tt_p, m_p)
+    # bge-large shape (hidden 1024, 16 heads of 64, FFN 4096), 2 of its 24 layers: the layer
+    # arithmetic is the same per layer, the fixture stays small
+    ids_l, tt_l, m_l = R.random_batch(rng, 5, 30)
+    wl = R.make_weights(BGE_LARGE_2L, seed=13)
+    emb_l = hf_bge(BGE_LARGE_2L, wl, ids_l, tt_l, m_l)
     np.savez_compressed(os.path.join(HERE, "bert_golden.npz"), ids_q=ids_q, tt_q=tt_q, m_q=m_q,
                         ids_p=ids_p, tt_p=tt_p, m_p=m_p, bge_emb=emb, ce_logits=logit,
-                        bge_seed=11, ce_seed=12)
-    print("bge", emb.shape, "ce", logit)
+                        bge_seed=11, ce_seed=12, ids_l=ids_l, tt_l=tt_l, m_l=m_l,
+                        bgel_emb=emb_l, bgel_seed=13)
+    print("bge", emb.shape, "ce", logit, "bge-large-2L", emb_l.shape)
 
 
 if __name__ == "__main__":

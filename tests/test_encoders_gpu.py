@@ -95,6 +95,33 @@ def test_ce_rerank_15_pairs(ce, prec):
         np.testing.assert_array_equal(order, ref_order)
 
 
+@pytest.fixture(scope="module")
+def bgel(gpu, golden, prec):
+    from ragmi.encoders import HEAD_CLS_L2, BertEncoder
+    cfg = dict(R.BGE_LARGE, layers=2)
+    w = R.make_weights(cfg, int(golden["bgel_seed"]))
+    return BertEncoder(cfg, w, HEAD_CLS_L2, gpu, prec), w, cfg
+
+
+def test_bge_large_shape_golden(bgel, golden, prec):
+    """bge-large-en-v1.5 shape (config 5: hidden 1024, 16 heads of 64, FFN 4096)."""
+    enc, w, cfg = bgel
+    g = golden
+    out = enc.forward_padded(g["ids_l"], g["tt_l"], g["m_l"]).cpu().numpy()
+    assert _report(f"[{prec}] bge-large vs transformers", out, g["bgel_emb"]) <= TOL[prec]["bge"]
+
+
+def test_bge_large_shape_long_sequences(bgel, prec):
+    """512-token sequences at head_dim 64: in fp16x3 the keys no longer fit LDS at once, so
+    this exercises the chunked-key attention path (kc < len)."""
+    enc, w, cfg = bgel
+    rng = np.random.default_rng(9)
+    ids, tt, m = R.random_batch(rng, 3, 512)
+    out = enc.forward_padded(ids, tt, m).cpu().numpy()
+    ref = R.bge_embed(w, cfg, ids, tt, m)
+    assert _report(f"[{prec}] bge-large 512", out, ref) <= TOL[prec]["bge"]
+
+
 def test_batch_independence_bitwise(bge):
     """A sequence's output does not depend on what else is in the packed batch."""
     enc, w = bge

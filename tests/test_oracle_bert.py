@@ -29,6 +29,15 @@ def test_ce_oracle_matches_transformers_fixture(golden):
     np.testing.assert_allclose(lg, g["ce_logits"], rtol=0, atol=2e-5)
 
 
+def test_bge_large_shape_oracle_matches_transformers_fixture(golden):
+    """bge-large shape (hidden 1024, 16 heads x 64, FFN 4096; 2 of 24 layers), config 5."""
+    g = golden
+    cfg = dict(R.BGE_LARGE, layers=2)
+    w = R.make_weights(cfg, int(g["bgel_seed"]))
+    emb = R.bge_embed(w, cfg, g["ids_l"], g["tt_l"], g["m_l"])
+    np.testing.assert_allclose(emb, g["bgel_emb"], rtol=0, atol=2e-6)
+
+
 def test_padding_does_not_change_valid_outputs(golden):
     """Right padding to a longer batch length leaves every sequence's output unchanged
     (what lets the HIP path pack sequences without padding)."""

@@ -201,3 +201,54 @@ def test_one_million_rows_planted_and_exact(gpu):
     [t.join() for t in th]
     for t in range(6):
         np.testing.assert_array_equal(res[t][1], i)
+
+
+# ---- D = 1024 (config 5: bge-large vectors; queries in LDS, scan_lds_kernel)
+@pytest.mark.parametrize("n,b,k", [(5003, 32, 15), (4096, 128, 15), (777, 45, 16), (33, 3, 5)])
+def test_search_d1024_vs_oracle(gpu, n, b, k):
+    rng = np.random.default_rng(n * 7 + b)
+    x = rng.standard_normal((n, 1024)).astype(np.float32)
+    q = rng.standard_normal((b, 1024)).astype(np.float32)
+    idx = make_index(gpu, x)
+    enc = O.encode_rows(x)
+    np.testing.assert_array_equal(idx.export_rows(), enc)
+    s, i = search(idx, q, k)
+    s2, i2 = O.search(enc, q, k)
+    np.testing.assert_array_equal(i, i2)
+    np.testing.assert_array_equal(s, s2)
+
+
+def test_search_d1024_filtered_per_query(gpu):
+    rng = np.random.default_rng(11)
+    n, b = 6000, 40
+    x = rng.standard_normal((n, 1024)).astype(np.float32)
+    tags = rng.integers(0, 6, n).astype(np.uint32) | (rng.integers(1, 3, n).astype(np.uint32) << 16)
+    q = rng.standard_normal((b, 1024)).astype(np.float32)
+    filt = np.zeros((b, 2), np.uint32)
+    filt[:, 0] = np.where(np.arange(b) % 3 == 0, 0xFFFF, 0xFFFFFFFF)
+    filt[:, 1] = rng.integers(0, 6, b).astype(np.uint32) | np.where(
+        np.arange(b) % 3 == 0, 0, 1 << 16).astype(np.uint32)
+    idx = make_index(gpu, x, tags)
+    s, i = search(idx, q, 15, filters=filt)
+    enc = O.encode_rows(x)
+    for j in range(b):
+        s2, i2 = O.search(enc, q[j:j + 1], 15, tags=tags, mask=int(filt[j, 0]),
+                          value=int(filt[j, 1]), use_filter=True)
+        np.testing.assert_array_equal(i[j], i2[0])
+        np.testing.assert_array_equal(s[j], s2[0])
+
+
+def test_d1024_planted_200k_batch128(gpu):
+    """Config-5 shape at a size the oracle shortlist finishes quickly: planted queries find
+    their source row first; full top-15 equals the exact oracle."""
+    rng = np.random.default_rng(12)
+    n, b = 200_000, 128
+    x = rng.standard_normal((n, 1024)).astype(np.float32)
+    src = rng.choice(n, b, replace=False)
+    q = x[src] + 0.05 * rng.standard_normal((b, 1024)).astype(np.float32)
+    idx = make_index(gpu, x)
+    s, i = search(idx, q, 15)
+    assert (i[:, 0] == src).all()
+    s2, i2 = O.search_fast(idx.export_rows(), q, 15)
+    np.testing.assert_array_equal(i, i2)
+    np.testing.assert_array_equal(s, s2)
