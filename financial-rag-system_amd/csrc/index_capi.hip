@@ -26,6 +26,7 @@ namespace {
 // concurrently without interference; a further stream drains the device once and rebinds
 // the least recently used slot.
 constexpr int kRing = 4;
+constexpr int kMaxGroups = 4;   // query groups of 32 per pass (wide rows)
 
 struct Workspace {
   float* qn = nullptr;
@@ -38,6 +39,7 @@ struct Workspace {
   float* heads_s = nullptr;   // [32][n_lists]
   int* heads_i = nullptr;
   int* heads_n = nullptr;
+  int* progress = nullptr;      // [lists][groups] shared-group scan throttle words
   hipStream_t owner = nullptr;  // stream of the last pass that used this slot
   bool used = false;
   uint64_t tick = 0;            // last use (LRU rebinding)
@@ -57,6 +59,7 @@ struct rag_index {
   half8* corpus = nullptr;
   uint32_t* tags = nullptr;
   int max_wgs = 0;        // scan workgroups at full occupancy
+  int groups = 1;         // query groups of 32 per search pass
   std::mutex mu;
   Workspace ws[kRing];
   uint64_t ws_tick = 0;
@@ -106,14 +109,14 @@ void launch_upsert(rag_index* h, const float* v, const int64_t* rows, const uint
 // sample + thresh: seed thresholds for the scan (see sample_kernel). ~0.8% of the shard's
 // tiles, spread evenly, at least 256 tiles (all of them for small shards).
 template <int D, bool FILTER>
-void launch_seed(rag_index* h, Workspace& w, hipStream_t st) {
+void launch_seed(rag_index* h, Workspace& w, int groups, hipStream_t st) {
   using namespace ragmi;
   const int n_tiles = (int)((h->count + 15) / 16);
   if (n_tiles == 0) return;   // the scan visits no tile; seeds are never read
   const int n_sample = std::min({n_tiles, std::max(256, n_tiles / 128), kMaxSample});
-  sample_kernel<D, FILTER><<<dim3((n_sample + 7) / 8), dim3(256), 0, st>>>(
+  sample_kernel<D, FILTER><<<dim3((n_sample + 7) / 8, groups), dim3(256), 0, st>>>(
       h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, n_tiles, n_sample, w.smax);
-  thresh_kernel<<<dim3(kQ), dim3(256), 0, st>>>(w.smax, n_sample, w.seed);
+  thresh_kernel<<<dim3(kQ, groups), dim3(256), 0, st>>>(w.smax, n_sample, w.seed);
 }
 
 template <int D>
@@ -121,17 +124,27 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
                        const uint32_t* filt, int64_t id_offset, float* out_s, int64_t* out_i,
                        hipStream_t st) {
   using namespace ragmi;
-  qprep_kernel<D><<<dim3(kQ), dim3(64), 0, st>>>(q, Bq, filt, w.qn, w.qfrag, w.filt);
+  // Bq <= 32 * h->groups queries: `groups` query groups of 32 (one for D <= 384)
+  const int groups = (Bq + kQ - 1) / kQ;
+  qprep_kernel<D><<<dim3(groups * kQ), dim3(64), 0, st>>>(q, Bq, filt, w.qn, w.qfrag, w.filt);
   if (filt)
-    launch_seed<D, true>(h, w, st);
+    launch_seed<D, true>(h, w, groups, st);
   else
-    launch_seed<D, false>(h, w, st);
+    launch_seed<D, false>(h, w, groups, st);
   const int64_t n_tiles = (h->count + 15) / 16;
-  // D <= 384: queries in VGPRs, 2 workgroups per CU; wider rows: queries in LDS, 1 per CU
+  // D <= 384: queries in VGPRs, 2 workgroups per CU; wider rows: queries in LDS, 1 per CU,
+  // R workgroups per query group (R % 8 == 0: XCD pairing of the groups, scan_lds_kernel)
   constexpr bool kLdsQ = D > 384;
-  const int max_wgs = kLdsQ ? h->max_wgs / 2 : h->max_wgs;
-  int grid = (int)std::min<int64_t>(max_wgs, std::max<int64_t>(1, (n_tiles + 3) / 4));
-  grid = std::min(grid, kMaxLists / kWavesPerWG);
+  int grid;
+  if constexpr (kLdsQ) {
+    const int per_group = std::max(8, (h->max_wgs / 2 / groups) & ~7);
+    const int need = (int)std::min<int64_t>(
+        per_group, ((n_tiles + kLdsWaves - 1) / kLdsWaves + 7) & ~int64_t(7));
+    grid = std::max(8, std::min(need, kMaxLists / kLdsWaves));
+  } else {
+    grid = (int)std::min<int64_t>(h->max_wgs, std::max<int64_t>(1, (n_tiles + 3) / 4));
+    grid = std::min(grid, kMaxLists / kWavesPerWG);
+  }
   ProfPair pp{};
   const bool timed = h->prof > 0 && (h->prof_seq++ % h->prof) == 0;
   if (timed) {
@@ -143,10 +156,19 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
   h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, (int)n_tiles, w.seed, w.part_s, w.part_i, \
       w.heads_s, w.heads_i, w.heads_n
   if constexpr (kLdsQ) {
-    if (filt)
-      scan_lds_kernel<D, true><<<dim3(grid), dim3(256), 0, st>>>(RAG_SCAN_ARGS);
-    else
-      scan_lds_kernel<D, false><<<dim3(grid), dim3(256), 0, st>>>(RAG_SCAN_ARGS);
+    const dim3 g3(grid * groups), b3(64 * kLdsWaves);
+    if (groups == 1) {
+      if (filt)
+        scan_lds_kernel<D, true, true><<<g3, b3, 0, st>>>(RAG_SCAN_ARGS, groups, w.progress);
+      else
+        scan_lds_kernel<D, false, true><<<g3, b3, 0, st>>>(RAG_SCAN_ARGS, groups, w.progress);
+    } else {
+      RAG_HIP(hipMemsetAsync(w.progress, 0, (size_t)grid * kLdsWaves * groups * 4, st));
+      if (filt)
+        scan_lds_kernel<D, true, false><<<g3, b3, 0, st>>>(RAG_SCAN_ARGS, groups, w.progress);
+      else
+        scan_lds_kernel<D, false, false><<<g3, b3, 0, st>>>(RAG_SCAN_ARGS, groups, w.progress);
+    }
   } else {
     if (filt)
       scan_kernel<D, true><<<dim3(grid), dim3(256), 0, st>>>(RAG_SCAN_ARGS);
@@ -158,7 +180,7 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
     RAG_HIP(hipEventRecord(pp.b, st));
     h->prof_pairs.push_back(pp);
   }
-  const int n_lists = grid * kWavesPerWG;
+  const int n_lists = grid * (kLdsQ ? kLdsWaves : kWavesPerWG);   // lists per query group
   select_kernel<D><<<dim3(Bq), dim3(256), 0, st>>>(w.part_s, w.part_i, w.heads_s, w.heads_i,
                                                    w.heads_n, n_lists, h->corpus, w.qn, k, id_offset,
                                                    out_s, out_i);
@@ -210,8 +232,9 @@ int search_locked(rag_index* h, const float* q, int B, int k, const uint32_t* fi
   if (B < 0 || (B > 0 && (!q || !out_s || !out_i))) return ragmi::fail(RAG_EINVAL, "bad search args");
   if (k < 1 || k > RAG_MAX_K) return ragmi::fail(RAG_ERANGE, "k must be in [1, RAG_MAX_K=32]");
   RAG_HIP(hipSetDevice(h->device));
-  for (int b0 = 0; b0 < B; b0 += ragmi::kQ) {
-    const int Bq = std::min(ragmi::kQ, B - b0);
+  const int per_pass = ragmi::kQ * h->groups;
+  for (int b0 = 0; b0 < B; b0 += per_pass) {
+    const int Bq = std::min(per_pass, B - b0);
     Workspace* wp = nullptr;
     for (auto& s : h->ws)
       if (s.used && s.owner == st) { wp = &s; break; }
@@ -267,7 +290,7 @@ int bench_scan(rag_index* h, const float* q, int B, int variant, int reps, doubl
   RAG_HIP(hipDeviceSynchronize());
   qprep_kernel<D><<<dim3(kQ), dim3(64), 0, nullptr>>>(q, std::min(B, kQ), nullptr, w.qn,
                                                       w.qfrag, w.filt);
-  launch_seed<D, false>(h, w, nullptr);
+  launch_seed<D, false>(h, w, 1, nullptr);
   const int64_t n_tiles = (h->count + 15) / 16;
   int grid = (int)std::min<int64_t>(h->max_wgs, std::max<int64_t>(1, (n_tiles + 3) / 4));
   grid = std::min(grid, kMaxLists / kWavesPerWG);
@@ -329,25 +352,30 @@ int rag_index_create(int dim, int64_t capacity_rows, int device, rag_index_t** o
       n_cu <= 0)
     n_cu = 256;
   h->max_wgs = n_cu * 2;  // 2 x 256-thread workgroups per CU (__launch_bounds__(256, 2))
+  // wide rows (LDS-query scan) take up to 4 query groups (128 queries) per pass
+  h->groups = dim > 384 ? kMaxGroups : 1;
+  const size_t G = (size_t)h->groups, Q = ragmi::kQ;
   const int max_lists = std::min(h->max_wgs * ragmi::kWavesPerWG, ragmi::kMaxLists);
   for (auto& w : h->ws) {
-    bool ok = hipMalloc(reinterpret_cast<void**>(&w.qn), ragmi::kQ * dim * 4) == hipSuccess &&
-              hipMalloc(reinterpret_cast<void**>(&w.qfrag), 2 * (dim / 32) * 64 * 16) ==
+    bool ok = hipMalloc(reinterpret_cast<void**>(&w.qn), G * Q * dim * 4) == hipSuccess &&
+              hipMalloc(reinterpret_cast<void**>(&w.qfrag), G * 2 * (dim / 32) * 64 * 16) ==
                   hipSuccess &&
-              hipMalloc(reinterpret_cast<void**>(&w.filt), ragmi::kQ * 2 * 4) == hipSuccess &&
+              hipMalloc(reinterpret_cast<void**>(&w.filt), G * Q * 2 * 4) == hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&w.smax),
-                        (size_t)ragmi::kMaxSample * ragmi::kQ * 4) == hipSuccess &&
+                        G * ragmi::kMaxSample * Q * 4) == hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&w.heads_s),
-                        (size_t)ragmi::kMaxLists * ragmi::kQ * 4) == hipSuccess &&
+                        G * ragmi::kMaxLists * Q * 4) == hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&w.heads_i),
-                        (size_t)ragmi::kMaxLists * ragmi::kQ * 4) == hipSuccess &&
+                        G * ragmi::kMaxLists * Q * 4) == hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&w.heads_n),
-                        (size_t)ragmi::kMaxLists * ragmi::kQ * 4) == hipSuccess &&
-              hipMalloc(reinterpret_cast<void**>(&w.seed), ragmi::kQ * 4) == hipSuccess &&
+                        G * ragmi::kMaxLists * Q * 4) == hipSuccess &&
+              hipMalloc(reinterpret_cast<void**>(&w.seed), G * Q * 4) == hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&w.part_s),
-                        (size_t)max_lists * ragmi::kQ * ragmi::kKS * 4) == hipSuccess &&
+                        G * max_lists * Q * ragmi::kKS * 4) == hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&w.part_i),
-                        (size_t)max_lists * ragmi::kQ * ragmi::kKS * 4) == hipSuccess;
+                        G * max_lists * Q * ragmi::kKS * 4) == hipSuccess &&
+              hipMalloc(reinterpret_cast<void**>(&w.progress),
+                        G * ragmi::kMaxLists * 4) == hipSuccess;
     if (!ok) {
       rag_index_destroy(h);
       return ragmi::fail(RAG_ENOMEM, "workspace allocation failed");
@@ -373,6 +401,7 @@ int rag_index_destroy(rag_index_t* h) {
     if (w.seed) (void)hipFree(w.seed);
     if (w.part_s) (void)hipFree(w.part_s);
     if (w.part_i) (void)hipFree(w.part_i);
+    if (w.progress) (void)hipFree(w.progress);
   }
   for (auto& p : h->prof_pairs) {
     (void)hipEventDestroy(p.a);

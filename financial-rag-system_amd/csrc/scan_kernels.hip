@@ -436,32 +436,289 @@ __global__ __launch_bounds__(256, 2) void scan_kernel(
   topk_finish(st, lane, gw, nw, part_s, part_i, heads_s, heads_i, heads_n);
 }
 
+// ---- register-pending top-k (LDS-query scan): the pending candidates of a lane live in
+// VGPRs (8 slots per query tile, pushed by shifting: static register indices), so a wave's
+// LDS is only its keep lists (8 KB) plus a 512-B gather scratch — which lets 8 waves share one
+// workgroup's 64 KB of query fragments (2 waves per SIMD).
+constexpr int kRP = 8;          // pending slots per (lane, query tile); flush at > kRP - 4
+constexpr int kLdsWaves = 8;    // waves per scan_lds_kernel workgroup
+
+struct RegTopK {
+  float* keep_s;   // LDS [32 queries][32] best-first
+  int* keep_i;
+  float* xs;       // LDS [64] gather scratch
+  int* xi;
+  float thr0, thr1;
+  int cnt0, cnt1;
+  float p0s[kRP], p1s[kRP];
+  int p0i[kRP], p1i[kRP];
+  uint32_t fm0, fv0, fm1, fv1;
+};
+
+template <bool FILTER>
+__device__ __forceinline__ void rtopk_init(RegTopK& st, int* lds, int wid, int lane,
+                                           const float* __restrict__ seed_thr,
+                                           const uint32_t* __restrict__ filt) {
+  int* base = lds + wid * (2 * kQ * kKS + 128);
+  st.keep_s = reinterpret_cast<float*>(base);
+  st.keep_i = base + kQ * kKS;
+  st.xs = reinterpret_cast<float*>(base + 2 * kQ * kKS);
+  st.xi = base + 2 * kQ * kKS + 64;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    st.keep_s[lane + 64 * j] = kNegInf;
+    st.keep_i[lane + 64 * j] = kIdNone32;
+  }
+#pragma unroll
+  for (int sl = 0; sl < kRP; ++sl) {
+    st.p0s[sl] = st.p1s[sl] = kNegInf;
+    st.p0i[sl] = st.p1i[sl] = kIdNone32;
+  }
+  lds_fence();
+  st.thr0 = st.thr1 = kNegInf;
+  if (seed_thr) {
+    const float T0 = seed_thr[lane & 15], T1 = seed_thr[16 + (lane & 15)];
+    st.thr0 = T0 == kNegInf ? kNegInf : nextafterf(T0, kNegInf);
+    st.thr1 = T1 == kNegInf ? kNegInf : nextafterf(T1, kNegInf);
+  }
+  st.cnt0 = st.cnt1 = 0;
+  st.fm0 = st.fv0 = st.fm1 = st.fv1 = 0;
+  if constexpr (FILTER) {
+    st.fm0 = filt[2 * (lane & 15)];
+    st.fv0 = filt[2 * (lane & 15) + 1];
+    st.fm1 = filt[2 * (16 + (lane & 15))];
+    st.fv1 = filt[2 * (16 + (lane & 15)) + 1];
+  }
+}
+
+// this lane's pending entries of query tile qt -> scratch slots (lane >> 4) * 8 + sl (+ off)
+__device__ __forceinline__ void rtopk_spill(const RegTopK& st, int qt, int lane, int off) {
+#pragma unroll
+  for (int sl = 0; sl < kRP; ++sl) {
+    st.xs[off + (lane >> 4) * kRP + sl] = qt == 0 ? st.p0s[sl] : st.p1s[sl];
+    st.xi[off + (lane >> 4) * kRP + sl] = qt == 0 ? st.p0i[sl] : st.p1i[sl];
+  }
+}
+
+__device__ __forceinline__ void rtopk_clear(RegTopK& st, int qt) {
+#pragma unroll
+  for (int sl = 0; sl < kRP; ++sl) {
+    if (qt == 0) {
+      st.p0s[sl] = kNegInf;
+      st.p0i[sl] = kIdNone32;
+    } else {
+      st.p1s[sl] = kNegInf;
+      st.p1i[sl] = kIdNone32;
+    }
+  }
+  if (qt == 0) st.cnt0 = 0; else st.cnt1 = 0;
+}
+
+// merge query q's keep list (32) with its pending entries (4 lanes x 8 slots), keep 32
+__device__ __forceinline__ void rtopk_flush(RegTopK& st, int q, int lane) {
+  const int qt = q >> 4, c = q & 15;
+  const bool owner = (lane & 15) == c;
+  if (owner) rtopk_spill(st, qt, lane, 0);
+  lds_fence();
+  float s;
+  int id;
+  if (lane < 32) {
+    s = st.keep_s[q * kKS + lane];
+    id = st.keep_i[q * kKS + lane];
+  } else {
+    s = st.xs[lane - 32];
+    id = st.xi[lane - 32];
+  }
+  lds_fence();
+  bitonic_sort64(s, id, lane);
+  if (lane < 32) {
+    st.keep_s[q * kKS + lane] = s;
+    st.keep_i[q * kKS + lane] = id;
+  }
+  lds_fence();
+  const float nt = __shfl(s, 31, 64);
+  if (owner) {
+    rtopk_clear(st, qt);
+    if (qt == 0) st.thr0 = fmaxf(st.thr0, nt); else st.thr1 = fmaxf(st.thr1, nt);
+  }
+}
+
+__device__ __forceinline__ void rtopk_flush_mask(RegTopK& st, uint64_t b, int qt, int lane) {
+  uint32_t m = (uint32_t)((b | (b >> 16) | (b >> 32) | (b >> 48)) & 0xffffu);
+  while (m) {
+    const int c = __builtin_ctz(m);
+    m &= m - 1;
+    rtopk_flush(st, qt * 16 + c, lane);
+  }
+}
+
+template <bool FILTER>
+__device__ __forceinline__ void rtopk_tile(RegTopK& st, const floatx4& acc0, const floatx4& acc1,
+                                           int t, int n_rows, const uint32_t* __restrict__ tags,
+                                           int lane) {
+  const int rbase = t * kTileRows + 4 * (lane >> 4);
+  uint4 tg = {0u, 0u, 0u, 0u};
+  if constexpr (FILTER) tg = *reinterpret_cast<const uint4*>(tags + rbase);
+  float v0[4], v1[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const bool ok = (rbase + r) < n_rows;
+    bool ok0 = ok, ok1 = ok;
+    if constexpr (FILTER) {
+      const uint32_t tr = r == 0 ? tg.x : r == 1 ? tg.y : r == 2 ? tg.z : tg.w;
+      ok0 = ok0 && ((tr & st.fm0) == st.fv0);
+      ok1 = ok1 && ((tr & st.fm1) == st.fv1);
+    }
+    v0[r] = ok0 ? acc0[r] : kNegInf;
+    v1[r] = ok1 ? acc1[r] : kNegInf;
+  }
+  const float m0 = fmaxf(fmaxf(v0[0], v0[1]), fmaxf(v0[2], v0[3]));
+  const float m1 = fmaxf(fmaxf(v1[0], v1[1]), fmaxf(v1[2], v1[3]));
+  if (__ballot((m0 > st.thr0) || (m1 > st.thr1))) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (v0[r] > st.thr0) {
+#pragma unroll
+        for (int sl = kRP - 1; sl > 0; --sl) {
+          st.p0s[sl] = st.p0s[sl - 1];
+          st.p0i[sl] = st.p0i[sl - 1];
+        }
+        st.p0s[0] = v0[r];
+        st.p0i[0] = rbase + r;
+        ++st.cnt0;
+      }
+      if (v1[r] > st.thr1) {
+#pragma unroll
+        for (int sl = kRP - 1; sl > 0; --sl) {
+          st.p1s[sl] = st.p1s[sl - 1];
+          st.p1i[sl] = st.p1i[sl - 1];
+        }
+        st.p1s[0] = v1[r];
+        st.p1i[0] = rbase + r;
+        ++st.cnt1;
+      }
+    }
+    const uint64_t b0 = __ballot(st.cnt0 > kRP - 4);
+    const uint64_t b1 = __ballot(st.cnt1 > kRP - 4);
+    if (b0) rtopk_flush_mask(st, b0, 0, lane);
+    if (b1) rtopk_flush_mask(st, b1, 1, lane);
+  }
+}
+
+__device__ __forceinline__ void rtopk_finish(RegTopK& st, int lane, int gw, int nw,
+                                             float* __restrict__ part_s, int* __restrict__ part_i,
+                                             float* __restrict__ heads_s,
+                                             int* __restrict__ heads_i,
+                                             int* __restrict__ heads_n) {
+  const uint64_t b0 = __ballot(st.cnt0 > 0);
+  const uint64_t b1 = __ballot(st.cnt1 > 0);
+  const uint32_t p0 = (uint32_t)((b0 | (b0 >> 16) | (b0 >> 32) | (b0 >> 48)) & 0xffffu);
+  const uint32_t p1 = (uint32_t)((b1 | (b1 >> 16) | (b1 >> 32) | (b1 >> 48)) & 0xffffu);
+  const uint32_t pend = p0 | (p1 << 16);
+  const uint32_t kept = (uint32_t)__ballot(lane < kQ && st.keep_s[(lane & 31) * kKS] != kNegInf);
+  uint32_t full = pend & kept;
+  uint32_t only = pend & ~kept;
+  while (full) {
+    const int q = __builtin_ctz(full);
+    full &= full - 1;
+    rtopk_flush(st, q, lane);
+  }
+  // queries that never flushed: their <= 32 pending entries only need a 32-wide sort, two
+  // queries per pass (scratch halves 0..31 and 32..63)
+  while (only) {
+    const int qa = __builtin_ctz(only);
+    only &= only - 1;
+    const int qb = only ? __builtin_ctz(only) : -1;
+    if (only) only &= only - 1;
+    if ((lane & 15) == (qa & 15)) rtopk_spill(st, qa >> 4, lane, 0);
+    if (qb >= 0 && (lane & 15) == (qb & 15)) rtopk_spill(st, qb >> 4, lane, 32);
+    lds_fence();
+    const int q = lane < 32 ? qa : qb;
+    const int j = lane & 31;
+    float s = kNegInf;
+    int id = kIdNone32;
+    if (q >= 0) {
+      s = st.xs[lane];
+      id = st.xi[lane];
+    }
+    lds_fence();
+    bitonic_sort32x2(s, id, lane);
+    if (q >= 0) {
+      st.keep_s[q * kKS + j] = s;
+      st.keep_i[q * kKS + j] = id;
+    }
+    lds_fence();
+  }
+  float* ps = part_s + (int64_t)gw * (kQ * kKS);
+  int* pi = part_i + (int64_t)gw * (kQ * kKS);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const float v = st.keep_s[lane + 64 * j];
+    if (v != kNegInf) {
+      ps[lane + 64 * j] = v;
+      pi[lane + 64 * j] = st.keep_i[lane + 64 * j];
+    }
+  }
+  if (lane < kQ) {
+    int n = 0;
+    for (int j = 0; j < kKS; ++j) n += st.keep_s[lane * kKS + j] != kNegInf;
+    heads_s[lane * nw + gw] = st.keep_s[lane * kKS];
+    heads_i[lane * nw + gw] = n > 0 ? st.keep_i[lane * kKS] : kIdNone32;
+    heads_n[lane * nw + gw] = n;
+  }
+}
+
 // LDS-query scan for wide rows (D = 1024: the B-operands of 32 queries are 64 KB, too many
-// VGPRs). The fragments are staged into LDS once per workgroup (one workgroup per CU: 64 KB
-// queries + 64 KB top-k state); each wave streams its tiles in chunks of 8 k-steps (8 KB) through
-// a ring of D/256 chunk registers, so while one chunk is multiplied the remaining chunks of the
-// tile (and the next tile's first chunks) are in flight — 3 x 8 KB per wave, enough to cover
-// HBM latency at one wave per SIMD. Per chunk: 8 A-fragments (buffer loads off a wave-uniform
-// descriptor, non-temporal), 16 B-fragments from LDS (conflict-free: lane-linear), 16 MFMAs.
-template <int D, bool FILTER>
-__global__ __launch_bounds__(256, 1) void scan_lds_kernel(
+// VGPRs). The fragments are staged into LDS once per workgroup (one 8-wave workgroup per CU:
+// 64 KB queries + 8 x 8.5 KB keep lists / scratch; pending candidates in VGPRs); each wave
+// streams its tiles in chunks of 8 k-steps (8 KB) through a ring of D/256 chunk registers,
+// so while one chunk is multiplied the rest of the tile (and the next tile's first chunks)
+// are in flight. Per chunk: 8 A-fragments (buffer loads off a wave-uniform descriptor),
+// 16 B-fragments from LDS (lane-linear: conflict-free), 16 MFMAs.
+//
+// Batches of more than 32 queries run as G query groups in ONE launch: grid = G x R
+// workgroups; the G workgroups of tile range r (one per group) are dealt to the same XCD
+// back to back (blocks go round-robin over the 8 XCDs) and walk identical tile sequences, so
+// a tile comes from HBM once and from that XCD's L2 for the other G-1 groups (instead of G
+// full passes over the corpus).
+// NT: non-temporal loads (single group: the corpus is read once); shared groups need the
+// default policy so the tile stays in L2 for the partner groups.
+constexpr int kShareEvery = 2;    // progress exchange every 2 tiles
+constexpr int kShareLead = 2;     // max tiles a wave may run ahead of its partners
+constexpr int kShareSpin = 256;   // bounded wait (x s_sleep 4 = 256 clocks each)
+
+template <int D, bool FILTER, bool NT>
+__global__ __launch_bounds__(64 * kLdsWaves, 1) void scan_lds_kernel(
     const half8* __restrict__ corpus, const uint32_t* __restrict__ tags,
     const uint32_t* __restrict__ filt, const half8* __restrict__ qfrag, int n_rows, int n_tiles,
     const float* __restrict__ seed_thr, float* __restrict__ part_s, int* __restrict__ part_i,
-    float* __restrict__ heads_s, int* __restrict__ heads_i, int* __restrict__ heads_n) {
+    float* __restrict__ heads_s, int* __restrict__ heads_i, int* __restrict__ heads_n,
+    int groups, int* __restrict__ progress) {
   constexpr int S = steps<D>(), CH = 8, NCH = S / CH;
   static_assert(S % CH == 0 && NCH >= 2, "LDS-query scan: D must be a multiple of 256 (>= 512)");
-  __shared__ int lds[kWavesPerWG * kLdsPerWave];
+  __shared__ int lds[kLdsWaves * (2 * kQ * kKS + 128)];
   __shared__ half8 qb[2 * S * 64];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
-  for (int i = threadIdx.x; i < 2 * S * 64; i += 256) qb[i] = qfrag[i];
-  ScanTopK st;
-  topk_init<FILTER>(st, lds, wid, lane, seed_thr, filt);
+  // block -> (tile range r, query group g); gridDim.x = groups * R with R % 8 == 0
+  const int R = gridDim.x / groups;
+  const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
+  const int r = (loc / groups) * 8 + xcd, g = loc % groups;
+  qfrag += g * (2 * S * 64);
+  filt += g * (2 * kQ);
+  seed_thr += g * kQ;
+  const int nw = R * kLdsWaves;                      // lists per group
+  part_s += (int64_t)g * nw * (kQ * kKS);
+  part_i += (int64_t)g * nw * (kQ * kKS);
+  heads_s += (int64_t)g * kQ * nw;
+  heads_i += (int64_t)g * kQ * nw;
+  heads_n += (int64_t)g * kQ * nw;
+  for (int i = threadIdx.x; i < 2 * S * 64; i += 64 * kLdsWaves) qb[i] = qfrag[i];
+  RegTopK st;
+  rtopk_init<FILTER>(st, lds, wid, lane, seed_thr, filt);
   __syncthreads();
 
-  const int gw = blockIdx.x * kWavesPerWG + __builtin_amdgcn_readfirstlane(wid);
-  const int nw = gridDim.x * kWavesPerWG;
+  const int gw = r * kLdsWaves + __builtin_amdgcn_readfirstlane(wid);
   int t_first, t_step, n_mine;
   tile_sequence<true>(gw, nw, n_tiles, t_first, t_step, n_mine);
 
@@ -476,7 +733,7 @@ __global__ __launch_bounds__(256, 1) void scan_lds_kernel(
           __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(tp), 0, CH * 1024, 0x00020000);
 #pragma unroll
       for (int s = 0; s < CH; ++s) {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, s * 1024, 2);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, s * 1024, NT ? 2 : 0);
         a[s] = __builtin_bit_cast(half8, v);
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -484,6 +741,28 @@ __global__ __launch_bounds__(256, 1) void scan_lds_kernel(
 #pragma unroll
     for (int c = 0; c < NCH; ++c) load_chunk(buf[c], 0, c);
     for (int j = 0; j < n_mine; ++j) {
+      if constexpr (!NT) {
+        // Shared groups: keep this wave within kShareLead tiles of its partner waves (same
+        // tile sequence, other query groups), so the partners' reads of a tile hit the L2
+        // line this wave's read brought in. Progress words are agent-scope atomics; the wait
+        // is bounded (a throttle, never a dependency: if a partner is not running, the wave
+        // proceeds after kShareSpin polls).
+        if ((j & (kShareEvery - 1)) == 0) {
+          int* mine = progress + (int64_t)gw * groups;
+          if (lane == 0)
+            __hip_atomic_store(mine + g, j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          for (int it = 0; it < kShareSpin; ++it) {
+            int lag = 0;
+            for (int gg = 0; gg < groups; ++gg) {
+              const int v = __hip_atomic_load(mine + gg, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+              lag = max(lag, (j + 1) - v);
+            }
+            if (__builtin_amdgcn_readfirstlane(lag) <= kShareLead) break;
+            __builtin_amdgcn_s_sleep(4);
+          }
+        }
+      }
       const int jn = min(j + 1, n_mine - 1);
       floatx4 acc0 = {0.f, 0.f, 0.f, 0.f};
       floatx4 acc1 = {0.f, 0.f, 0.f, 0.f};
@@ -498,10 +777,16 @@ __global__ __launch_bounds__(256, 1) void scan_lds_kernel(
         }
         load_chunk(buf[c], jn, c);
       }
-      topk_tile<FILTER>(st, acc0, acc1, t_first + j * t_step, n_rows, tags, lane);
+      rtopk_tile<FILTER>(st, acc0, acc1, t_first + j * t_step, n_rows, tags, lane);
     }
   }
-  topk_finish(st, lane, gw, nw, part_s, part_i, heads_s, heads_i, heads_n);
+  if constexpr (!NT) {
+    // finished (or no tiles): never hold partners back
+    if (lane == 0)
+      __hip_atomic_store(progress + (int64_t)gw * groups + g, 0x3fffffff, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+  }
+  rtopk_finish(st, lane, gw, nw, part_s, part_i, heads_s, heads_i, heads_n);
 }
 
 // ----------------------------------------------------------------------------------------
@@ -519,6 +804,10 @@ __global__ __launch_bounds__(256) void sample_kernel(const half8* __restrict__ c
                                                      int n_rows, int n_tiles, int n_sample,
                                                      float* __restrict__ smax) {
   constexpr int S = steps<D>();
+  // query group (32 queries) blockIdx.y: its fragments, filters and maxima
+  qfrag += blockIdx.y * (2 * S * 64);
+  filt += blockIdx.y * (2 * kQ);
+  smax += (int64_t)blockIdx.y * kQ * n_sample;
   const int lane = threadIdx.x & 63;
   const int w = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // two sample tiles per wave (j = 2w, 2w+1), all loads in flight at once
@@ -642,6 +931,8 @@ __global__ __launch_bounds__(256) void thresh_kernel(const float* __restrict__ s
   // maxima is attained by 32 distinct rows, so it is a valid lower bound.
   __shared__ float w_s[4][32];
   const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  smax += (int64_t)blockIdx.y * kQ * n_sample;   // query group
+  seed_thr += blockIdx.y * kQ;
   const float* v = smax + (int64_t)q * n_sample;
   float m = kNegInf;
   float x[kMaxSample / 256];
@@ -754,7 +1045,14 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
   __shared__ int c_i[4][32];
   __shared__ float e_s[32];
   __shared__ int e_i[32];
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // query bq of the batch = slot b of query group grp (the scan's per-group lists)
+  const int bq = blockIdx.x, grp = bq / kQ, b = bq % kQ;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  part_s += (int64_t)grp * n_lists * (kQ * kKS);
+  part_i += (int64_t)grp * n_lists * (kQ * kKS);
+  heads_s += (int64_t)grp * kQ * n_lists;
+  heads_i += (int64_t)grp * kQ * n_lists;
+  heads_n += (int64_t)grp * kQ * n_lists;
   auto at = [&](int l, int pos) { return ((int64_t)l * kQ + b) * kKS + pos; };
 
   // ---- 1. the 32 best list heads (a list = one scan wave; under the interleaved tile order
@@ -934,7 +1232,7 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
 
   // ---- 3. exact rescoring, 8 candidates per wave (one round trip)
   {
-    const float* qq = qn + b * D;
+    const float* qq = qn + (int64_t)bq * D;
     int rows[8];
     float es[8];
 #pragma unroll
@@ -960,8 +1258,8 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
     bitonic_sort64(s, id, lane);
     if (lane < k) {
       const bool ok = s != kNegInf;
-      out_s[(int64_t)b * k + lane] = s;
-      out_i[(int64_t)b * k + lane] = ok ? (int64_t)id + id_offset : (int64_t)-1;
+      out_s[(int64_t)bq * k + lane] = s;
+      out_i[(int64_t)bq * k + lane] = ok ? (int64_t)id + id_offset : (int64_t)-1;
     }
   }
 }
