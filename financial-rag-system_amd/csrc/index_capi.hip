@@ -155,9 +155,16 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
 #define RAG_SCAN_ARGS                                                                    \
   h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, (int)n_tiles, w.seed, w.part_s, w.part_i, \
       w.heads_s, w.heads_i, w.heads_n
+  const bool wide = kLdsQ && groups > 1 && !filt;
+  if (wide) grid = (int)std::min<int64_t>(h->max_wgs / 2, std::max<int64_t>(1, n_tiles));
   if constexpr (kLdsQ) {
     const dim3 g3(grid * groups), b3(64 * kLdsWaves);
-    if (groups == 1) {
+    if (wide) {
+      // all groups in every workgroup, one pass over the corpus (scan_wide_kernel)
+      scan_wide_kernel<D><<<dim3(grid), dim3(64 * kWideWaves), 0, st>>>(
+          h->corpus, w.qfrag, (int)h->count, (int)n_tiles, w.seed, w.part_s, w.part_i,
+          w.heads_s, w.heads_i, w.heads_n, groups);
+    } else if (groups == 1) {
       if (filt)
         scan_lds_kernel<D, true, true><<<g3, b3, 0, st>>>(RAG_SCAN_ARGS, groups, w.progress);
       else
@@ -180,7 +187,7 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
     RAG_HIP(hipEventRecord(pp.b, st));
     h->prof_pairs.push_back(pp);
   }
-  const int n_lists = grid * (kLdsQ ? kLdsWaves : kWavesPerWG);   // lists per query group
+  const int n_lists = wide ? grid : grid * (kLdsQ ? kLdsWaves : kWavesPerWG);   // per group
   select_kernel<D><<<dim3(Bq), dim3(256), 0, st>>>(w.part_s, w.part_i, w.heads_s, w.heads_i,
                                                    w.heads_n, n_lists, h->corpus, w.qn, k, id_offset,
                                                    out_s, out_i);

@@ -789,6 +789,262 @@ __global__ __launch_bounds__(64 * kLdsWaves, 1) void scan_lds_kernel(
   rtopk_finish(st, lane, gw, nw, part_s, part_i, heads_s, heads_i, heads_n);
 }
 
+// ---- one-query-tile register top-k (scan_wide_kernel): 16 queries per wave, pending in
+// VGPRs, keep lists in LDS (4 KB/wave), and the flush gathers the pending entries with lane
+// shuffles instead of an LDS scratch.
+struct WideTopK {
+  float* keep_s;   // LDS [16][32]
+  int* keep_i;
+  float thr;
+  int cnt;
+  float ps[kRP];
+  int pi[kRP];
+};
+
+__device__ __forceinline__ void wtopk_init(WideTopK& st, int* keep, int lane,
+                                           const float* __restrict__ seed_thr) {
+  st.keep_s = reinterpret_cast<float*>(keep);
+  st.keep_i = keep + 16 * kKS;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    st.keep_s[lane + 64 * j] = kNegInf;
+    st.keep_i[lane + 64 * j] = kIdNone32;
+  }
+#pragma unroll
+  for (int sl = 0; sl < kRP; ++sl) {
+    st.ps[sl] = kNegInf;
+    st.pi[sl] = kIdNone32;
+  }
+  lds_fence();
+  st.thr = kNegInf;
+  if (seed_thr) {
+    const float T = seed_thr[lane & 15];
+    st.thr = T == kNegInf ? kNegInf : nextafterf(T, kNegInf);
+  }
+  st.cnt = 0;
+}
+
+// pending entry (lane's slot `sl` of lane `src`), for 32 consumer lanes: consumer j takes
+// slot j & 7 of lane (c + 16 * (j >> 3)) — the 4 lanes x 8 slots of query column c
+__device__ __forceinline__ void wtopk_gather(const WideTopK& st, int c, int j, float& s, int& id) {
+  const int src = c + 16 * ((j >> 3) & 3), want = j & 7;
+  s = kNegInf;
+  id = kIdNone32;
+#pragma unroll
+  for (int sl = 0; sl < kRP; ++sl) {
+    const float vs = __shfl(st.ps[sl], src, 64);
+    const int vi = __shfl(st.pi[sl], src, 64);
+    if (want == sl) {
+      s = vs;
+      id = vi;
+    }
+  }
+}
+
+__device__ __forceinline__ void wtopk_flush(WideTopK& st, int c, int lane) {
+  // the shuffles run on all 64 lanes (a source lane must be active); lanes 0..31 then take
+  // the keep list instead
+  float s;
+  int id;
+  wtopk_gather(st, c, lane & 31, s, id);
+  if (lane < 32) {
+    s = st.keep_s[c * kKS + lane];
+    id = st.keep_i[c * kKS + lane];
+  }
+  lds_fence();
+  bitonic_sort64(s, id, lane);
+  if (lane < 32) {
+    st.keep_s[c * kKS + lane] = s;
+    st.keep_i[c * kKS + lane] = id;
+  }
+  lds_fence();
+  const float nt = __shfl(s, 31, 64);
+  if ((lane & 15) == c) {
+#pragma unroll
+    for (int sl = 0; sl < kRP; ++sl) {
+      st.ps[sl] = kNegInf;
+      st.pi[sl] = kIdNone32;
+    }
+    st.cnt = 0;
+    st.thr = fmaxf(st.thr, nt);
+  }
+}
+
+__device__ __forceinline__ void wtopk_tile(WideTopK& st, const floatx4& acc, int t, int n_rows,
+                                           int lane) {
+  const int rbase = t * kTileRows + 4 * (lane >> 4);
+  float v[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) v[r] = (rbase + r) < n_rows ? acc[r] : kNegInf;
+  const float m = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+  if (__ballot(m > st.thr)) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (v[r] > st.thr) {
+#pragma unroll
+        for (int sl = kRP - 1; sl > 0; --sl) {
+          st.ps[sl] = st.ps[sl - 1];
+          st.pi[sl] = st.pi[sl - 1];
+        }
+        st.ps[0] = v[r];
+        st.pi[0] = rbase + r;
+        ++st.cnt;
+      }
+    }
+    const uint64_t bm = __ballot(st.cnt > kRP - 4);
+    if (bm) {
+      uint32_t mm = (uint32_t)((bm | (bm >> 16) | (bm >> 32) | (bm >> 48)) & 0xffffu);
+      while (mm) {
+        const int c = __builtin_ctz(mm);
+        mm &= mm - 1;
+        wtopk_flush(st, c, lane);
+      }
+    }
+  }
+}
+
+// end of scan: flush, then write this wave's 16 query rows of its group's list b
+__device__ __forceinline__ void wtopk_finish(WideTopK& st, int lane, int qt, int b, int nw,
+                                             float* __restrict__ part_s, int* __restrict__ part_i,
+                                             float* __restrict__ heads_s,
+                                             int* __restrict__ heads_i,
+                                             int* __restrict__ heads_n) {
+  const uint64_t bp = __ballot(st.cnt > 0);
+  const uint32_t pend = (uint32_t)((bp | (bp >> 16) | (bp >> 32) | (bp >> 48)) & 0xffffu);
+  const uint32_t kept = (uint32_t)__ballot(lane < 16 && st.keep_s[(lane & 15) * kKS] != kNegInf);
+  uint32_t full = pend & kept;
+  uint32_t only = pend & ~kept;
+  while (full) {
+    const int c = __builtin_ctz(full);
+    full &= full - 1;
+    wtopk_flush(st, c, lane);
+  }
+  while (only) {   // never-flushed columns: 32-wide sorts, two columns per pass
+    const int ca = __builtin_ctz(only);
+    only &= only - 1;
+    const int cb = only ? __builtin_ctz(only) : -1;
+    if (only) only &= only - 1;
+    const int c = lane < 32 ? ca : cb;
+    float s;
+    int id;
+    wtopk_gather(st, c < 0 ? 0 : c, lane & 31, s, id);
+    if (c < 0) {
+      s = kNegInf;
+      id = kIdNone32;
+    }
+    bitonic_sort32x2(s, id, lane);
+    if (c >= 0) {
+      st.keep_s[c * kKS + (lane & 31)] = s;
+      st.keep_i[c * kKS + (lane & 31)] = id;
+    }
+    lds_fence();
+  }
+  float* ps = part_s + (int64_t)b * (kQ * kKS) + qt * 16 * kKS;
+  int* pi = part_i + (int64_t)b * (kQ * kKS) + qt * 16 * kKS;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float v = st.keep_s[lane + 64 * j];
+    if (v != kNegInf) {
+      ps[lane + 64 * j] = v;
+      pi[lane + 64 * j] = st.keep_i[lane + 64 * j];
+    }
+  }
+  if (lane < 16) {
+    int n = 0;
+    for (int j = 0; j < kKS; ++j) n += st.keep_s[lane * kKS + j] != kNegInf;
+    const int q = qt * 16 + lane;
+    heads_s[q * nw + b] = st.keep_s[lane * kKS];
+    heads_i[q * nw + b] = n > 0 ? st.keep_i[lane * kKS] : kIdNone32;
+    heads_n[q * nw + b] = n;
+  }
+}
+
+// Wide rows, several query groups, ONE pass over the corpus (D = 1024, 2..4 groups of 32,
+// unfiltered): each workgroup (8 waves, one per CU) streams its tiles t = b, b + nb, ... into
+// a 4-tile LDS ring by direct global->LDS loads (global_load_lds_dwordx4; the tile16 layout
+// is already lane-linear, so the LDS image is the HBM image), three tiles in flight, and ALL
+// 8 waves consume every tile: wave w = (group w/2, query tile w%2) holds its 16 queries'
+// fragments over all 1024 dims in VGPRs (32 half8) and runs their top-k (16 columns,
+// register pending). A tile is read from HBM once for all groups. Sync: counted vmcnt + one
+// raw s_barrier per tile (tile j landed AND every wave is done with tile j-1, whose slot the
+// next load reuses). The loop issues no VMEM besides the ring loads, so the counts are exact.
+constexpr int kWideBufs = 4;
+constexpr int kWideWaves = 8;
+
+template <int D>
+__global__ __launch_bounds__(64 * kWideWaves, 1) void scan_wide_kernel(
+    const half8* __restrict__ corpus, const half8* __restrict__ qfrag, int n_rows, int n_tiles,
+    const float* __restrict__ seed_thr, float* __restrict__ part_s, int* __restrict__ part_i,
+    float* __restrict__ heads_s, int* __restrict__ heads_i, int* __restrict__ heads_n,
+    int groups) {
+  constexpr int S = steps<D>();
+  constexpr int TILE = S * 64;                                   // half8 per tile
+  constexpr int TK = 2 * 16 * kKS;                               // ints of keep state per wave
+  static_assert(S * 1024 == kWideWaves * 4096, "wide scan: 8 waves x 4 KB = one tile");
+  // one LDS object (ring | keep lists): a second __shared__ object next to a
+  // global_load_lds target can make hipcc drain vmcnt before every ds_read
+  __shared__ half8 lds[kWideBufs * TILE + kWideWaves * TK / 4];
+  half8* ring = lds;
+  int* keep = reinterpret_cast<int*>(lds + kWideBufs * TILE);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int g = wid >> 1, qt = wid & 1;
+  const bool active = g < groups;
+  const int nb = gridDim.x, b = blockIdx.x;
+
+  half8 qf[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const half8 z = {};
+    qf[s] = active ? qfrag[g * (2 * S * 64) + (qt * S + s) * 64 + lane] : z;
+  }
+  WideTopK st;
+  wtopk_init(st, keep + wid * TK, lane, active ? seed_thr + g * kQ + qt * 16 : nullptr);
+  const int nw = nb;                                             // lists per group
+  part_s += (int64_t)g * nw * (kQ * kKS);
+  part_i += (int64_t)g * nw * (kQ * kKS);
+  heads_s += (int64_t)g * kQ * nw;
+  heads_i += (int64_t)g * kQ * nw;
+  heads_n += (int64_t)g * kQ * nw;
+
+  const int n_mine = b < n_tiles ? (n_tiles - 1 - b) / nb + 1 : 0;
+  const char* cbase = reinterpret_cast<const char*>(corpus);
+  auto issue = [&](int j) {   // this wave's 4 KB of tile j -> ring slot j % 4
+    if (j < n_mine) {
+      const int t = b + j * nb;
+      const char* src = cbase + (int64_t)t * (S * 1024) + wid * 4096 + lane * 16;
+      char* dst = reinterpret_cast<char*>(ring + (j % kWideBufs) * TILE) + wid * 4096;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)(src + i * 1024),
+            (__attribute__((address_space(3))) void*)(dst + i * 1024), 16, 0, 0);
+    }
+  };
+  issue(0);
+  issue(1);
+  issue(2);
+  for (int j = 0; j < n_mine; ++j) {
+    const int later = min(2, n_mine - 1 - j);                  // tiles issued after j
+    if (later == 2)
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (later == 1)
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();   // tile j landed for all; everyone is past tile j-1
+    issue(j + 3);                   // slot (j+3)%4 == (j-1)%4
+    if (active) {                   // waves of absent groups (B <= 96) only stage and sync
+      const half8* tb = ring + (j % kWideBufs) * TILE + lane;
+      floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < S; ++s)
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(tb[s * 64], qf[s], acc, 0, 0, 0);
+      wtopk_tile(st, acc, b + j * nb, n_rows, lane);
+    }
+  }
+  if (active) wtopk_finish(st, lane, qt, b, nw, part_s, part_i, heads_s, heads_i, heads_n);
+}
+
 // ----------------------------------------------------------------------------------------
 // sample: seed thresholds for the scan. Sample wave w scores the corpus tiles
 //   t = (j * n_tiles) / n_sample, j = w, w + n_waves, ...   (spread over the shard)
