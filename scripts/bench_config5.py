@@ -172,7 +172,7 @@ def main():
             "recall_at_5_vs_fp32": recall5,
             "roofline": {"bound": "hbm", "achieved": round(ach / 1e9, 1),
                          "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": round(ach / HBM_PEAK, 4),
-                         "kernel": "scan_lds_kernel<1024,false>", "avg_ms": round(scan_avg, 4),
+                         "kernel": "scan_wide_kernel<1024>" if args.batch > 32 else "scan_lds_kernel<1024,false,true>", "avg_ms": round(scan_avg, 4),
                          "algorithmic_bytes_per_launch": algo},
             "build_s": round(t_build, 2),
         }), flush=True)

@@ -1,6 +1,7 @@
 """Stage benchmark of the encoders (BASELINE configs 2-3):
 
   encode_q   bge-small, 32 queries x 16-32 tokens        (main2.py batch_processor stage 1)
+  encode_q_large  bge-large shape (1024/16 heads/4096, 24 layers), 128 queries (config 5)
   encode_c   bge-small, 64 chunks x 200-260 tokens       (ingest.py embed_chunks, EMBED_BATCH=64)
   rerank     MiniLM-L6 CE, 32 queries x 15 pairs x ~288 tokens (config 3 stage 2)
 
@@ -27,10 +28,11 @@ from ragmi.encoders import HEAD_CLS_L2, HEAD_POOLER_CLS, BertEncoder  # noqa: E4
 PEAK_F16 = 2.5e15   # dense fp16 MFMA, MI355X_MICROARCH.md
 
 
-def flops_per_token(layers, S):
-    gemm = 2 * (4 * 384 * 384 + 2 * 384 * 1536)
-    attn = 4 * S * 384
-    return layers * (gemm + attn)
+def flops_per_token(cfg, S):
+    H, FF = cfg["hidden"], cfg["inter"]
+    gemm = 2 * (4 * H * H + 2 * H * FF)
+    attn = 4 * S * H
+    return cfg["layers"] * (gemm + attn)
 
 
 def batch(rng, B, lo, hi, pair=False):
@@ -99,7 +101,9 @@ def main():
     do_cpu = os.environ.get("CPU", "1") == "1"
     stages = [("encode_q", R.BGE_SMALL, HEAD_CLS_L2, (32, 16, 32, False)),
               ("encode_c", R.BGE_SMALL, HEAD_CLS_L2, (64, 200, 260, False)),
-              ("rerank", R.MINILM_CE, HEAD_POOLER_CLS, (480, 200, 288, True))]
+              ("rerank", R.MINILM_CE, HEAD_POOLER_CLS, (480, 200, 288, True)),
+              # config 5 query encoder: bge-large-en-v1.5 shape, 128 queries
+              ("encode_q_large", R.BGE_LARGE, HEAD_CLS_L2, (128, 16, 32, False))]
     for prec in ("fp16", "fp16x3"):
         for name, cfg, head, (B, lo, hi, pair) in stages:
             w = R.make_weights(cfg, 1)
@@ -108,7 +112,7 @@ def main():
             ms = run(enc, ids, tt, cu, reps)
             T = int(cu[-1])
             S = float(np.mean(np.diff(cu)))
-            fl = T * flops_per_token(cfg["layers"], S)
+            fl = T * flops_per_token(cfg, S)
             mult = 3 if prec == "fp16x3" else 1
             line = {"stage": name, "precision": prec, "sequences": B, "tokens": T,
                     "ms": round(ms, 4), "tokens_per_s": round(T / ms * 1e3, 1),
