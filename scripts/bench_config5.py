@@ -1,9 +1,9 @@
 """Config 5 (BASELINE.json / SURVEY §8d, §8f row 4): queries/sec + recall@5 of cosine top-15
 over a 50M x 1024 fp16 corpus (bge-large-en-v1.5 vector width) at batch 128.
 
-One step = one batch of 128 queries: query prep -> seed sampling -> ONE scan launch with the
-four 32-query groups co-scheduled per XCD (scan_lds_kernel: each tile comes from HBM once and
-from L2 for the other groups) -> exact select. N > 1: same contiguous-shard + RCCL all-gather
+One step = one batch of 128 queries: query prep -> seed sampling -> ONE scan launch that
+serves all four 32-query groups (scan_wide_kernel: every tile is staged into LDS once and
+consumed by all groups' waves) -> exact select. N > 1: same contiguous-shard + RCCL all-gather
 merge as bench.py (python -m torch.distributed.run --nproc-per-node N scripts/bench_config5.py).
 50M x 1024 fp16 = 102.4 GB: fits one MI355X (288 GB).
 
@@ -172,7 +172,9 @@ def main():
             "recall_at_5_vs_fp32": recall5,
             "roofline": {"bound": "hbm", "achieved": round(ach / 1e9, 1),
                          "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": round(ach / HBM_PEAK, 4),
-                         "kernel": "scan_wide_kernel<1024>" if args.batch > 32 else "scan_lds_kernel<1024,false,true>", "avg_ms": round(scan_avg, 4),
+                         "kernel": ("scan_wide_kernel<1024>" if args.batch > 32
+                                    else "scan_lds_kernel<1024,false,true>"),
+                         "avg_ms": round(scan_avg, 4),
                          "algorithmic_bytes_per_launch": algo},
             "build_s": round(t_build, 2),
         }), flush=True)
