@@ -122,7 +122,7 @@ void launch_seed(rag_index* h, Workspace& w, int groups, hipStream_t st) {
 template <int D>
 int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k,
                        const uint32_t* filt, int64_t id_offset, float* out_s, int64_t* out_i,
-                       hipStream_t st) {
+                       int32_t* out_packed, hipStream_t st) {
   using namespace ragmi;
   // Bq <= 32 * h->groups queries: `groups` query groups of 32 (one for D <= 384)
   const int groups = (Bq + kQ - 1) / kQ;
@@ -190,7 +190,7 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
   const int n_lists = wide ? grid : grid * (kLdsQ ? kLdsWaves : kWavesPerWG);   // per group
   select_kernel<D><<<dim3(Bq), dim3(256), 0, st>>>(w.part_s, w.part_i, w.heads_s, w.heads_i,
                                                    w.heads_n, n_lists, h->corpus, w.qn, k, id_offset,
-                                                   out_s, out_i);
+                                                   out_s, out_i, out_packed);
   RAG_HIP(hipGetLastError());
   return RAG_OK;
 }
@@ -235,8 +235,10 @@ int upsert_locked(rag_index* h, const float* vecs, const int64_t* rows, const ui
 }
 
 int search_locked(rag_index* h, const float* q, int B, int k, const uint32_t* filt,
-                  int64_t id_offset, float* out_s, int64_t* out_i, hipStream_t st) {
-  if (B < 0 || (B > 0 && (!q || !out_s || !out_i))) return ragmi::fail(RAG_EINVAL, "bad search args");
+                  int64_t id_offset, float* out_s, int64_t* out_i, int32_t* out_packed,
+                  hipStream_t st) {
+  if (B < 0 || (B > 0 && (!q || (!out_packed && (!out_s || !out_i)))))
+    return ragmi::fail(RAG_EINVAL, "bad search args");
   if (k < 1 || k > RAG_MAX_K) return ragmi::fail(RAG_ERANGE, "k must be in [1, RAG_MAX_K=32]");
   RAG_HIP(hipSetDevice(h->device));
   const int per_pass = ragmi::kQ * h->groups;
@@ -261,13 +263,17 @@ int search_locked(rag_index* h, const float* q, int B, int k, const uint32_t* fi
     w.tick = ++h->ws_tick;
     int rc;
     if (h->dim == 384)
-      rc = launch_search_pass<384>(h, w, q + (int64_t)b0 * h->dim, Bq, k,
-                                   filt ? filt + 2 * b0 : nullptr, id_offset,
-                                   out_s + (int64_t)b0 * k, out_i + (int64_t)b0 * k, st);
+      rc = launch_search_pass<384>(
+          h, w, q + (int64_t)b0 * h->dim, Bq, k, filt ? filt + 2 * b0 : nullptr, id_offset,
+          out_packed ? nullptr : out_s + (int64_t)b0 * k,
+          out_packed ? nullptr : out_i + (int64_t)b0 * k,
+          out_packed ? out_packed + (int64_t)b0 * k * 2 : nullptr, st);
     else
-      rc = launch_search_pass<1024>(h, w, q + (int64_t)b0 * h->dim, Bq, k,
-                                    filt ? filt + 2 * b0 : nullptr, id_offset,
-                                    out_s + (int64_t)b0 * k, out_i + (int64_t)b0 * k, st);
+      rc = launch_search_pass<1024>(
+          h, w, q + (int64_t)b0 * h->dim, Bq, k, filt ? filt + 2 * b0 : nullptr, id_offset,
+          out_packed ? nullptr : out_s + (int64_t)b0 * k,
+          out_packed ? nullptr : out_i + (int64_t)b0 * k,
+          out_packed ? out_packed + (int64_t)b0 * k * 2 : nullptr, st);
     if (rc) return rc;
   }
   return RAG_OK;
@@ -490,7 +496,19 @@ int rag_index_search(rag_index_t* h, const float* q, int B, int k, const uint32_
   ragmi::clear_error();
   if (!h) return ragmi::fail(RAG_EINVAL, "index is NULL");
   std::lock_guard<std::mutex> lk(h->mu);
-  return search_locked(h, q, B, k, filters, id_offset, out_s, out_i,
+  return search_locked(h, q, B, k, filters, id_offset, out_s, out_i, nullptr,
+                       static_cast<hipStream_t>(stream));
+}
+
+int rag_index_search_packed(rag_index_t* h, const float* q, int B, int k,
+                            const uint32_t* filters, int64_t id_offset, int32_t* out_packed,
+                            void* stream) {
+  ragmi::clear_error();
+  if (!h || (B > 0 && !out_packed)) return ragmi::fail(RAG_EINVAL, "bad packed search args");
+  if (id_offset < 0 || id_offset + h->count > INT32_MAX)
+    return ragmi::fail(RAG_ERANGE, "packed ids are int32: global rows must stay below 2^31");
+  std::lock_guard<std::mutex> lk(h->mu);
+  return search_locked(h, q, B, k, filters, id_offset, nullptr, nullptr, out_packed,
                        static_cast<hipStream_t>(stream));
 }
 
@@ -504,22 +522,24 @@ int rag_index_search_host(rag_index_t* h, const float* q, int B, int k,
   if (B == 0) return RAG_OK;
   std::lock_guard<std::mutex> lk(h->mu);
   RAG_HIP(hipSetDevice(h->device));
-  const size_t qb = (size_t)B * h->dim * 4, sb = (size_t)B * k * 4, ib = (size_t)B * k * 8;
-  const size_t fb = (size_t)B * 8;
+  // staging offsets rounded to 16 B (the int64 ids must be 8-B aligned for any B * k)
+  auto up16 = [](size_t x) { return (x + 15) & ~size_t(15); };
+  const size_t qb = up16((size_t)B * h->dim * 4), sb = up16((size_t)B * k * 4);
+  const size_t ib = up16((size_t)B * k * 8), fb = (size_t)B * 8;
   int rc = ensure_stage(h, qb + sb + ib + fb + 64);
   if (rc) return rc;
   char* base = static_cast<char*>(h->stage);
   RAG_HIP(hipDeviceSynchronize());
-  RAG_HIP(hipMemcpy(base, q, qb, hipMemcpyHostToDevice));
+  RAG_HIP(hipMemcpy(base, q, (size_t)B * h->dim * 4, hipMemcpyHostToDevice));
   if (filters) RAG_HIP(hipMemcpy(base + qb + sb + ib, filters, fb, hipMemcpyHostToDevice));
   rc = search_locked(h, reinterpret_cast<float*>(base), B, k,
                      filters ? reinterpret_cast<uint32_t*>(base + qb + sb + ib) : nullptr,
                      id_offset, reinterpret_cast<float*>(base + qb),
-                     reinterpret_cast<int64_t*>(base + qb + sb), nullptr);
+                     reinterpret_cast<int64_t*>(base + qb + sb), nullptr, nullptr);
   if (rc) return rc;
   RAG_HIP(hipDeviceSynchronize());
-  RAG_HIP(hipMemcpy(out_s, base + qb, sb, hipMemcpyDeviceToHost));
-  RAG_HIP(hipMemcpy(out_i, base + qb + sb, ib, hipMemcpyDeviceToHost));
+  RAG_HIP(hipMemcpy(out_s, base + qb, (size_t)B * k * 4, hipMemcpyDeviceToHost));
+  RAG_HIP(hipMemcpy(out_i, base + qb + sb, (size_t)B * k * 8, hipMemcpyDeviceToHost));
   return RAG_OK;
 }
 
@@ -585,8 +605,20 @@ int rag_merge_topk(const float* in_s, const int64_t* in_i, int n_lists, int B, i
   if (n_lists < 1 || B < 0 || k < 1 || k > RAG_MAX_K)
     return ragmi::fail(RAG_EINVAL, "bad merge args");
   if (B == 0) return RAG_OK;
-  ragmi::merge_exact_kernel<<<dim3(B), dim3(64), 0, static_cast<hipStream_t>(stream)>>>(
+  ragmi::merge_exact_kernel<false><<<dim3(B), dim3(64), 0, static_cast<hipStream_t>(stream)>>>(
       in_s, in_i, n_lists, B, k, out_s, out_i);
+  RAG_HIP(hipGetLastError());
+  return RAG_OK;
+}
+
+int rag_merge_topk_packed(const int32_t* in_packed, int n_lists, int B, int k, float* out_s,
+                          int64_t* out_i, void* stream) {
+  ragmi::clear_error();
+  if (n_lists < 1 || B < 0 || k < 1 || k > RAG_MAX_K || (B > 0 && !in_packed))
+    return ragmi::fail(RAG_EINVAL, "bad merge args");
+  if (B == 0) return RAG_OK;
+  ragmi::merge_exact_kernel<true><<<dim3(B), dim3(64), 0, static_cast<hipStream_t>(stream)>>>(
+      reinterpret_cast<const float*>(in_packed), nullptr, n_lists, B, k, out_s, out_i);
   RAG_HIP(hipGetLastError());
   return RAG_OK;
 }

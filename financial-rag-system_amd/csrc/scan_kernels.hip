@@ -1288,7 +1288,8 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
                                                      const float* __restrict__ qn, int k,
                                                      int64_t id_offset,
                                                      float* __restrict__ out_s,
-                                                     int64_t* __restrict__ out_i) {
+                                                     int64_t* __restrict__ out_i,
+                                                     int32_t* __restrict__ out_packed) {
   __shared__ float w_s[4][32];
   __shared__ int w_i[4][32];
   __shared__ int sel[32];
@@ -1514,8 +1515,14 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
     bitonic_sort64(s, id, lane);
     if (lane < k) {
       const bool ok = s != kNegInf;
-      out_s[(int64_t)bq * k + lane] = s;
-      out_i[(int64_t)bq * k + lane] = ok ? (int64_t)id + id_offset : (int64_t)-1;
+      if (out_packed) {
+        // multi-GPU exchange format: [B][k][2] int32 = (score bits, global row; -1 = none)
+        out_packed[((int64_t)bq * k + lane) * 2] = __float_as_int(s);
+        out_packed[((int64_t)bq * k + lane) * 2 + 1] = ok ? (int32_t)(id + id_offset) : -1;
+      } else {
+        out_s[(int64_t)bq * k + lane] = s;
+        out_i[(int64_t)bq * k + lane] = ok ? (int64_t)id + id_offset : (int64_t)-1;
+      }
     }
   }
 }
@@ -1523,6 +1530,9 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
 // ----------------------------------------------------------------------------------------
 // merge of exact per-shard lists (after the RCCL all-gather): [n_lists][B][k] -> [B][k]
 // ----------------------------------------------------------------------------------------
+// PACKED: input is the [n_lists][B][k][2] int32 (score bits, row) exchange format of
+// rag_index_search_packed (one all-gather instead of two); in_s then points at it.
+template <bool PACKED>
 __global__ __launch_bounds__(64) void merge_exact_kernel(const float* __restrict__ in_s,
                                                          const int64_t* __restrict__ in_i,
                                                          int n_lists, int B, int k,
@@ -1534,10 +1544,18 @@ __global__ __launch_bounds__(64) void merge_exact_kernel(const float* __restrict
     id = INT64_MAX;
     if (l < n_lists && pos < k) {
       const int64_t off = ((int64_t)l * B + b) * k + pos;
-      const int64_t v = in_i[off];
-      if (v >= 0) {
-        s = in_s[off];
-        id = v;
+      if constexpr (PACKED) {
+        const int2 pv = reinterpret_cast<const int2*>(in_s)[off];
+        if (pv.y >= 0) {
+          s = __int_as_float(pv.x);
+          id = pv.y;
+        }
+      } else {
+        const int64_t v = in_i[off];
+        if (v >= 0) {
+          s = in_s[off];
+          id = v;
+        }
       }
     }
   };

@@ -55,6 +55,8 @@ INDEX_API = {
                                              ctypes.c_int64]),
     "rag_index_search": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, ctypes.c_int, c_vp,
                                         ctypes.c_int64, c_vp, c_vp, c_vp]),
+    "rag_index_search_packed": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, ctypes.c_int, c_vp,
+                                               ctypes.c_int64, c_vp, c_vp]),
     "rag_index_search_host": (ctypes.c_int, [c_vp, c_f32p, ctypes.c_int, ctypes.c_int, c_u32p,
                                              ctypes.c_int64, c_f32p, c_i64p]),
     "rag_index_export_rows": (ctypes.c_int, [c_vp, ctypes.c_int64, ctypes.c_int64, c_u16p]),
@@ -63,6 +65,8 @@ INDEX_API = {
                                              c_u32p, ctypes.c_int64]),
     "rag_merge_topk": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                       c_vp, c_vp, c_vp]),
+    "rag_merge_topk_packed": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                             c_vp, c_vp, c_vp]),
     "rag_bench_scan": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                       ctypes.POINTER(ctypes.c_double)]),
     "rag_profile_enable": (ctypes.c_int, [c_vp, ctypes.c_int]),

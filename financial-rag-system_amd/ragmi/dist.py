@@ -3,8 +3,8 @@
 One process per GPU. Rank r holds the contiguous global rows [lo_r, hi_r) of the collection
 in its own in-HBM FlatIndex. A search is:
   local scan + per-wave top-k + exact-rescoring select   (libragmi.so, this rank's stream)
-  -> all-gather of the per-shard exact top-k (score f32, global id i64: B*k*12 bytes/rank)
-     over RCCL/xGMI (torch.distributed backend "nccl" = RCCL on ROCm)
+  -> ONE all-gather of the per-shard exact top-k, packed as int32 pairs (score bits, global
+     row: B*k*8 bytes/rank) over RCCL/xGMI (torch.distributed backend "nccl" = RCCL on ROCm)
   -> GPU merge of world lists by (score desc, id asc)  (rag_merge_topk)
 Because every shard reports canonical exact scores, the merged result equals the unsharded
 one id-for-id (tests/test_scan_gpu.py::test_sharded_merge_equals_unsharded).
@@ -83,6 +83,11 @@ class ShardedIndex:
             local = FlatIndex(dim=dim, capacity=max(self.hi - self.lo, 16), device=device)
         self.local = local
         self.merge = merge or _gpu_merge
+        # packed exchange (one collective): device-resident FlatIndex shards over RCCL with
+        # the default GPU merge and global rows < 2^31
+        self.packed = (merge is None and hasattr(local, "search_packed") and
+                       self.n_total < 2 ** 31 and dist.is_initialized() and
+                       dist.get_backend(group) == "nccl")
 
     @property
     def rows(self) -> int:
@@ -101,6 +106,13 @@ class ShardedIndex:
             self.local.upsert(vectors[m], rows, t, new_count=cnt)
 
     def search(self, queries, k: int, filters=None):
+        if self.world > 1 and self.packed:
+            # one RCCL all-gather of the packed (score bits, int32 row) lists instead of two
+            p = self.local.search_packed(queries, k, filters=filters, id_offset=self.lo)
+            out = torch.empty((self.world,) + tuple(p.shape), dtype=p.dtype, device=p.device)
+            dist.all_gather_into_tensor(out, p, group=self.group)
+            from .index import merge_topk_packed
+            return merge_topk_packed(out, k)
         s, i = self.local.search(queries, k, filters=filters, id_offset=self.lo)
         if self.world == 1:
             return s, i

@@ -106,11 +106,7 @@ class FlatIndex:
                                        _stream_ptr(self.device)))
 
     # ---------------------------------------------------------------- search
-    def search(self, queries, k: int, filters=None, id_offset: int = 0,
-               out: tuple[torch.Tensor, torch.Tensor] | None = None):
-        """Top-k of each query row. Returns (scores fp32 [B,k], ids int64 [B,k]) as cuda
-        tensors, enqueued on the current stream (ids -1 where fewer than k rows match).
-        `filters`: None, or per-query (tag_mask, tag_value) pairs [B, 2] (uint32)."""
+    def _search_args(self, queries, k, filters):
         if not 1 <= k <= MAX_K:
             raise ValueError(f"k must be in [1, {MAX_K}]")
         q = _as_dev(queries, torch.float32, self.device)
@@ -119,11 +115,6 @@ class FlatIndex:
         if q.shape[-1] != self.dim:
             raise ValueError(f"query dim {q.shape[-1]} != index dim {self.dim}")
         B = q.shape[0]
-        if out is None:
-            out_s = torch.empty((B, k), dtype=torch.float32, device=self.device)
-            out_i = torch.empty((B, k), dtype=torch.int64, device=self.device)
-        else:
-            out_s, out_i = out
         f = None
         if filters is not None:
             if isinstance(filters, torch.Tensor):
@@ -134,6 +125,30 @@ class FlatIndex:
                 f = f.to(self.device)
             if f.shape != (B, 2):
                 raise ValueError("filters must be [B, 2] (tag_mask, tag_value)")
+        return q, B, f
+
+    def search_packed(self, queries, k: int, filters=None, id_offset: int = 0) -> torch.Tensor:
+        """Top-k in the multi-GPU exchange form: int32 [B, k, 2] = (fp32 score bits, global
+        row; -1 = none), enqueued on the current stream (rag_index_search_packed)."""
+        q, B, f = self._search_args(queries, k, filters)
+        out = torch.empty((B, k, 2), dtype=torch.int32, device=self.device)
+        check(self._L.rag_index_search_packed(self._h, q.data_ptr(), B, int(k),
+                                              f.data_ptr() if f is not None else None,
+                                              int(id_offset), out.data_ptr(),
+                                              _stream_ptr(self.device)))
+        return out
+
+    def search(self, queries, k: int, filters=None, id_offset: int = 0,
+               out: tuple[torch.Tensor, torch.Tensor] | None = None):
+        """Top-k of each query row. Returns (scores fp32 [B,k], ids int64 [B,k]) as cuda
+        tensors, enqueued on the current stream (ids -1 where fewer than k rows match).
+        `filters`: None, or per-query (tag_mask, tag_value) pairs [B, 2] (uint32)."""
+        q, B, f = self._search_args(queries, k, filters)
+        if out is None:
+            out_s = torch.empty((B, k), dtype=torch.float32, device=self.device)
+            out_i = torch.empty((B, k), dtype=torch.int64, device=self.device)
+        else:
+            out_s, out_i = out
         check(self._L.rag_index_search(self._h, q.data_ptr(), B, int(k),
                                        f.data_ptr() if f is not None else None,
                                        int(id_offset), out_s.data_ptr(), out_i.data_ptr(),
@@ -217,4 +232,18 @@ def merge_topk(scores: torch.Tensor, ids: torch.Tensor, k: int):
     out_i = torch.empty((B, k), dtype=torch.int64, device=scores.device)
     check(L.rag_merge_topk(scores.data_ptr(), ids.data_ptr(), n_lists, B, k, out_s.data_ptr(),
                            out_i.data_ptr(), _stream_ptr(scores.device)))
+    return out_s, out_i
+
+
+def merge_topk_packed(packed: torch.Tensor, k: int):
+    """Merge all-gathered packed lists int32 [n_lists, B, k, 2] -> (scores [B,k], ids [B,k])."""
+    L = _lib.load()
+    n_lists, B, kk, two = packed.shape
+    if kk != k or two != 2 or packed.dtype != torch.int32:
+        raise ValueError("packed lists must be int32 [n_lists, B, k, 2]")
+    packed = packed.contiguous()
+    out_s = torch.empty((B, k), dtype=torch.float32, device=packed.device)
+    out_i = torch.empty((B, k), dtype=torch.int64, device=packed.device)
+    check(L.rag_merge_topk_packed(packed.data_ptr(), n_lists, B, k, out_s.data_ptr(),
+                                  out_i.data_ptr(), _stream_ptr(packed.device)))
     return out_s, out_i

@@ -106,6 +106,14 @@ int rag_index_search_host(rag_index_t* index, const float* queries_host, int B, 
                           const uint32_t* filters_host, int64_t id_offset,
                           float* out_scores_host, int64_t* out_ids_host);
 
+/* Multi-GPU exchange form of rag_index_search: the result is written as ONE array
+ * out_packed [B][k][2] int32 = (fp32 score bits, global row id = local row + id_offset; -1
+ * where fewer than k rows match), so the per-shard lists travel in a single all-gather.
+ * Global row ids must stay below 2^31. */
+int rag_index_search_packed(rag_index_t* index, const float* queries_dev, int B, int k,
+                            const uint32_t* filters_dev, int64_t id_offset, int32_t* out_packed_dev,
+                            void* stream);
+
 /* Copy stored rows [row0, row0+n) out as row-major fp16 bits ([n][dim] uint16, host). */
 int rag_index_export_rows(rag_index_t* index, int64_t row0, int64_t n, uint16_t* out_host);
 /* Load already-stored rows back (persistence): row-major fp16 bits [n][dim] (host) are
@@ -121,6 +129,10 @@ int rag_index_export_tags(rag_index_t* index, int64_t row0, int64_t n, uint32_t*
  * all-gather of per-shard results. */
 int rag_merge_topk(const float* in_scores_dev, const int64_t* in_ids_dev, int n_lists, int B,
                    int k, float* out_scores_dev, int64_t* out_ids_dev, void* stream);
+/* Same merge over the packed exchange form ([n_lists][B][k][2] int32, see
+ * rag_index_search_packed) gathered from all shards. */
+int rag_merge_topk_packed(const int32_t* in_packed_dev, int n_lists, int B, int k,
+                          float* out_scores_dev, int64_t* out_ids_dev, void* stream);
 
 /* Kernel timing hook for bench.py: average device time (ms) of `rag_index_search` scan-kernel
  * launches measured with HIP events on the launch stream. enable = 0 off; enable = n > 0 records

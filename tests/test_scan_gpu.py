@@ -169,6 +169,33 @@ def test_sharded_merge_equals_unsharded(gpu):
         np.testing.assert_array_equal(ms.cpu().numpy(), s_ref)
 
 
+@pytest.mark.parametrize("dim", [384, 1024])
+def test_sharded_packed_exchange_equals_unsharded(gpu, dim):
+    """The one-collective exchange form (rag_index_search_packed -> all-gather ->
+    rag_merge_topk_packed) over G logical shards equals the unsharded search; a shard with
+    fewer than k rows contributes -1 entries that the merge skips."""
+    from ragmi.index import merge_topk_packed
+    rng = np.random.default_rng(14)
+    n, b, k = 5000, 40, 15
+    x = rng.standard_normal((n, dim)).astype(np.float32)
+    q = rng.standard_normal((b, dim)).astype(np.float32)
+    full = make_index(gpu, x)
+    s_ref, i_ref = search(full, q, k)
+    for bounds in ([0, 2500, 5000], [0, 7, 1200, 3000, 5000]):
+        packs = []
+        for lo, hi in zip(bounds[:-1], bounds[1:]):
+            sh = make_index(gpu, x[lo:hi])
+            p = sh.search_packed(q, k, id_offset=lo)
+            assert p.shape == (b, k, 2) and p.dtype == torch.int32
+            packs.append(p)
+        ms, mi = merge_topk_packed(torch.stack(packs), k)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(mi.cpu().numpy(), i_ref)
+        np.testing.assert_array_equal(ms.cpu().numpy(), s_ref)
+    with pytest.raises(Exception):
+        full.search_packed(q, k, id_offset=2 ** 31 - 10)
+
+
 def test_one_million_rows_planted_and_exact(gpu):
     """Full-size property test at the config-2 corpus (1M x 384): every planted query finds
     its source row first, and the top-15 equals the exact oracle (BLAS shortlist + canonical
