@@ -135,6 +135,8 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
                                                         C, nullptr);
 }
 
+
+
 template <int H, int HD>
 int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const int32_t* cu,
               int B, int T, int max_len, float* out, hipStream_t st) {

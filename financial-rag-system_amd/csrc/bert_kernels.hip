@@ -164,7 +164,9 @@ __global__ __launch_bounds__(256) void gemm_kernel(const _Float16* __restrict__ 
   // SPLIT (fp16x3): tiles of A_hi, A_lo, W_hi, W_lo; 3 MFMAs per product.
   constexpr int NP = SPLIT ? 4 : 2;                     // staged planes
   constexpr int BK = kBK<SPLIT>, CPR = BK / 8, LPT = BM * CPR / 256;   // loads/thread/plane
-  __shared__ half8 lds[2 * NP * BM * CPR];              // [buf][plane][row][CPR chunks]
+  // [buf][plane][row][CPR chunks]; also the epilogue's 4 x 32 x 68 fp32 staging (34 KB)
+  constexpr int kLdsH8 = 2 * NP * BM * CPR > 4 * 32 * 68 / 4 ? 2 * NP * BM * CPR : 4 * 32 * 68 / 4;
+  __shared__ half8 lds[kLdsH8];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
   // XCD-aware tile order: blocks are dealt round-robin over the 8 XCDs, so XCD x runs
