@@ -140,6 +140,26 @@ class BertEncoder:
                                           torch.cuda.current_stream(dev).cuda_stream))
         return out
 
+    def forward_device(self, ids: torch.Tensor, types: torch.Tensor, cu: torch.Tensor,
+                       max_len: int, out: torch.Tensor | None = None) -> torch.Tensor:
+        """Packed batch already in HBM (int32 ids/types [T], cu [B+1]; e.g. assembled on the
+        GPU from cached chunk tokens): no host round trip. `max_len` must bound every
+        sequence (<= max_position); out-of-range ids are clamped by the embedding kernel."""
+        B = cu.numel() - 1
+        T = ids.numel()
+        if B < 1 or types.numel() != T or not 1 <= max_len <= self.cfg["max_pos"]:
+            raise ValueError("bad device batch")
+        for t in (ids, types, cu):
+            if t.dtype != torch.int32 or not t.is_cuda or not t.is_contiguous():
+                raise ValueError("ids/types/cu must be contiguous int32 cuda tensors")
+        if out is None:
+            shape = (B, self.out_dim) if self.head == HEAD_CLS_L2 else (B,)
+            out = torch.empty(shape, dtype=torch.float32, device=self.device)
+        check(self._L.rag_encoder_forward(self._h, ids.data_ptr(), types.data_ptr(),
+                                          cu.data_ptr(), B, T, int(max_len), out.data_ptr(),
+                                          torch.cuda.current_stream(self.device).cuda_stream))
+        return out
+
     def forward_padded(self, ids: np.ndarray, types: np.ndarray, mask: np.ndarray):
         """HF-style right-padded [B, S] batch -> same outputs as the padded reference."""
         lens = mask.sum(1).astype(np.int32)

@@ -1,0 +1,52 @@
+"""GPU-side assembly of cross-encoder batches from cached token ids (SURVEY §8f rows 1-2:
+the batched rerank stage without a host round trip).
+
+At ingest every chunk is tokenised once; its WordPiece ids can stay in HBM next to its vector
+(a row-indexed [rows, Lmax] table + lengths). After the search returns the top-k rows of each
+query, the packed cross-encoder input for all (query, chunk) pairs is built on the device:
+
+    [CLS] q [SEP] c [SEP]      token types 0 ... 0 1 ... 1     (BertTokenizer pair encoding)
+
+with the chunk truncated so a pair fits max_len (`longest_first` truncation removes tokens from
+the longer side — the chunk, for the reference's short queries; main.py:241-247 via
+CrossEncoder.predict). Output: packed ids / types (int32 [T]), cu_seqlens (int32 [P+1]) and the
+longest pair, ready for BertEncoder.forward_device. Pure torch ops (works on CPU tensors too,
+which is how tests/test_pairs_cpu.py checks it against a per-pair loop).
+"""
+from __future__ import annotations
+
+import torch
+
+CLS, SEP = 101, 102
+
+
+def build_pairs(q_ids, q_cu, rows, c_toks, c_lens, max_len: int = 512):
+    """q_ids int32 [Tq] / q_cu [B+1]: the packed query tokens (each [CLS] ... [SEP]);
+    rows int64 [B, K]: search result rows (-1 = none: treated as row 0, caller masks);
+    c_toks [rows, Lmax] (int16/int32 ids, < 32768 for int16), c_lens [rows].
+    Returns (ids int32 [T], types int32 [T], cu int32 [B*K+1], longest pair)."""
+    dev = rows.device
+    Bq, Kq = rows.shape
+    # query tokens without their own [CLS]/[SEP]: the pair adds them back
+    q_len = (q_cu[1:] - q_cu[:-1]).long() - 2                      # [B]
+    ql = q_len.repeat_interleave(Kq)                                # [P]
+    r = rows.reshape(-1).clamp_min(0)
+    cl = torch.minimum(c_lens[r].long(), max_len - 3 - ql)
+    plen = ql + cl + 3
+    cu = torch.zeros(plen.numel() + 1, dtype=torch.int64, device=dev)
+    cu[1:] = torch.cumsum(plen, 0)
+    T = int(cu[-1])                                                 # one host sync per batch
+    t = torch.arange(T, device=dev)
+    p = torch.searchsorted(cu[1:], t, right=True)
+    off = t - cu[p]
+    qlp, clp = ql[p], cl[p]
+    qstart = q_cu[:-1].long().repeat_interleave(Kq)[p] + 1       # skip the query's [CLS]
+    qi = q_ids[(qstart + (off - 1).clamp(0, None)).clamp(max=q_ids.numel() - 1)]
+    ci = c_toks[r[p], (off - qlp - 2).clamp(0, c_toks.shape[1] - 1)].to(torch.int32) & 0xFFFF
+    ids = torch.where(off == 0, CLS,
+                      torch.where(off <= qlp, qi,
+                                  torch.where(off == qlp + 1, SEP,
+                                              torch.where(off < qlp + clp + 2, ci, SEP))))
+    types = (off > qlp + 1).to(torch.int32)
+    return ids.to(torch.int32).contiguous(), types.contiguous(), cu.to(torch.int32), \
+        int(plen.max())
