@@ -149,7 +149,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--streams", type=int, default=0,
                     help="batches in flight (0 = by shard size: 1 at >= 4M rows per GPU, "
-                         "else 3)")
+                         "else 2)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -182,9 +182,10 @@ def main():
     # Default depth by shard size: the fixed per-batch work (query prep, seed sampling,
     # select, exchange: ~35 us) is 3% of a 10M-row scan but ~20% of a 1.25M-row one
     # (8-GPU shard), so only small shards pipeline (measured on one MI355X: 1.25M rows
-    # 149K -> 191K qps with 3 streams; 10M rows +4.5% with 2). One stream keeps the N=1
-    # scan-kernel timing free of overlap with the other batch's kernels.
-    n_streams = args.streams or (1 if (hi - lo) >= 4_000_000 else 3)
+    # 149K -> 180K qps with 2 streams, 191K with 3; 10M rows +4.5% with 2). One stream keeps
+    # the N=1 scan-kernel timing free of overlap with the other batch's kernels; with 2 the
+    # per-launch time includes some overlap (0.180 -> 0.188 ms at 1.25M rows).
+    n_streams = args.streams or (1 if (hi - lo) >= 4_000_000 else 2)
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev)
                                                   for _ in range(n_streams - 1)]
     n_step = [0]
@@ -275,7 +276,9 @@ def main():
                          "frac": round(achieved / HBM_PEAK, 4),
                          "traffic": traffic,
                          "kernel": "scan_kernel<384,false>", "avg_ms": round(scan_avg_ms, 4),
-                         "algorithmic_bytes_per_launch": algo_bytes},
+                         "algorithmic_bytes_per_launch": algo_bytes,
+                         # whole-step view: the shard's bytes per batch over the step time
+                         "step_frac": round(algo_bytes / (elapsed / args.steps) / HBM_PEAK, 4)},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
