@@ -16,7 +16,9 @@ plus the batched forms a rewritten main2.batch_processor uses (SURVEY §8f rows 
   rerank_batch    -> one cross-encoder forward for all (query, chunk) pairs of a micro-batch
 
 Models come from local directories (env RAGMI_BGE_DIR, RAGMI_CE_DIR: config.json +
-model.safetensors + vocab.txt) — the reference's hub names cannot be fetched here.
+model.safetensors + vocab.txt) — the reference's hub names cannot be fetched here. Env
+RAGMI_STORAGE (optional) points the in-HBM collection at an on-disk shard directory
+(ragmi.store), the role of the reference's Qdrant storage volume.
 """
 from __future__ import annotations
 
@@ -72,7 +74,9 @@ def get_qdrant():
     if _testing():
         return None
     from .qdrant import QdrantClient
-    return QdrantClient(url=QDRANT_URL)
+    # RAGMI_STORAGE: directory of saved collections (the Qdrant volume's role); loaded here,
+    # written back by QdrantClient.save()/close()
+    return QdrantClient(url=QDRANT_URL, path=os.environ.get("RAGMI_STORAGE") or None)
 
 
 # ------------------------------------------------------------------ stage 1: embed
