@@ -149,7 +149,9 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
       c.type_vocab, c.max_position, e->x, e->xh, e->xl);
   const float scale = 1.0f / sqrtf((float)HD);
   const unsigned ln_grid = (unsigned)((T + 3) / 4);
-  const dim3 agrid(NH, B);
+  // 1-D grid of (sequence, head) pairs, padded to a multiple of 8 (XCD-aware order in the
+  // kernel; gridDim.x / NH = B after the padding is removed there)
+  const dim3 agrid((unsigned)((NH * B + 7) / 8 * 8));
   const int planes = e->xl ? 2 : 1;
   const int kc = attn_chunk_keys<HD>(max_len, planes);
   const size_t alds = (size_t)attn_lds_bytes<HD>(kc, planes);

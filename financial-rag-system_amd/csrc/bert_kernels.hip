@@ -362,7 +362,16 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>) void attn_kernel(
   constexpr int NP = St::NP, KS = St::KS, DT = St::DT, KROW = HD + 8;
   constexpr int NW = kAttnThreads<SPLIT> / 64;
   extern __shared__ _Float16 alds[];
-  const int h = blockIdx.x, b = blockIdx.y;
+  // XCD-aware (sequence, head) order: blocks are dealt round-robin over the 8 XCDs, so give
+  // XCD x a contiguous range of (sequence, head) pairs: the heads of one sequence run on one
+  // XCD back to back and share the 128-B lines of the Q|K|V rows (64 B per head) in its L2
+  // instead of each line being fetched once per head by different XCDs.
+  constexpr int NH = H / HD;
+  const int n_pairs = NH * (gridDim.x / NH);            // gridDim.x = NH * B rounded up to 8
+  const int per_xcd = gridDim.x >> 3;
+  const int pair = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+  if (pair >= n_pairs) return;
+  const int b = pair / NH, h = pair % NH;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   // LDS was sized for max_len on the host: a longer sequence (a caller breaking the
   // max_len contract of rag_encoder_forward) is truncated rather than overrunning LDS
