@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 #include <mutex>
 #include <vector>
 
@@ -123,9 +125,65 @@ int ensure_ws(rag_encoder* e, int64_t T) {
   return RAG_OK;
 }
 
+// GEMM variants: RAG_GEMM_TILE (gemm_kernel: one 128x128 tile per workgroup, 2 per CU) and
+// RAG_GEMM_PIPE (gemm_pipe_kernel: persistent, one 8-wave workgroup per CU, LDS-DMA ring
+// across tiles). AUTO takes PIPE once its 256x128 tiles cover every CU (large token counts:
+// rerank batches, chunk encode) and TILE below that (query batches: more, smaller tiles).
+int cu_count() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      v = 256;
+    return std::max(8, v / 8 * 8);
+  }();
+  return n;
+}
+
+int gemm_variant_default() {
+  static int v = [] {
+    const char* s = std::getenv("RAGMI_GEMM");
+    if (s && std::strcmp(s, "tile") == 0) return (int)RAG_GEMM_TILE;
+    if (s && std::strcmp(s, "pipe") == 0) return (int)RAG_GEMM_PIPE;
+    return (int)RAG_GEMM_AUTO;
+  }();
+  return v;
+}
+
+// PIPE addresses each operand and the output through 32-bit buffer extents
+bool pipe_ok(int M, int N, int K) {
+  return N % PBN == 0 && K % 64 == 0 && N <= kPipeBiasMax &&
+         (int64_t)M * K * 2 < (int64_t(1) << 31) && (int64_t)M * N * 4 < (int64_t(1) << 31);
+}
+
 template <int EPI>
 void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float16* Wl,
-          const float* bias, int M, int N, int K, void* C, _Float16* Clo, hipStream_t st) {
+          const float* bias, int M, int N, int K, void* C, _Float16* Clo, hipStream_t st,
+          int variant = RAG_GEMM_AUTO) {
+  if (variant == RAG_GEMM_AUTO) variant = gemm_variant_default();
+  const int pipe_tiles = (N / PBN) * ((M + PBM - 1) / PBM);
+  if (variant == RAG_GEMM_AUTO)
+    variant = (pipe_ok(M, N, K) && pipe_tiles >= cu_count()) ? RAG_GEMM_PIPE : RAG_GEMM_TILE;
+  if (variant >= 3 && pipe_ok(M, N, K)) {    // diagnostic probes of the PIPE kernel
+    const dim3 grid((unsigned)std::min(cu_count(), (pipe_tiles + 7) / 8 * 8));
+    if (variant == 3)
+      gemm_pipe_kernel<EPI, false, 1><<<grid, dim3(kPipeThreads), 0, st>>>(
+          A, nullptr, W, nullptr, bias, M, N, K, C, nullptr);
+    else
+      gemm_pipe_kernel<EPI, false, 2><<<grid, dim3(kPipeThreads), 0, st>>>(
+          A, nullptr, W, nullptr, bias, M, N, K, C, nullptr);
+    return;
+  }
+  if (variant == RAG_GEMM_PIPE && pipe_ok(M, N, K)) {
+    const dim3 grid((unsigned)std::min(cu_count(), (pipe_tiles + 7) / 8 * 8));
+    if (Al)
+      gemm_pipe_kernel<EPI, true><<<grid, dim3(kPipeThreads), 0, st>>>(A, Al, W, Wl, bias, M,
+                                                                       N, K, C, Clo);
+    else
+      gemm_pipe_kernel<EPI, false><<<grid, dim3(kPipeThreads), 0, st>>>(
+          A, nullptr, W, nullptr, bias, M, N, K, C, nullptr);
+    return;
+  }
   const unsigned tiles = (unsigned)((N / BN) * ((M + BM - 1) / BM));
   const dim3 grid((tiles + 7) / 8 * 8);          // multiple of 8: XCD-aware tile order
   if (Al)
@@ -318,6 +376,37 @@ int rag_encoder_forward(rag_encoder_t* e, const int32_t* ids, const int32_t* typ
   std::lock_guard<std::mutex> lk(e->mu);
   RAG_HIP(hipSetDevice(e->device));
   return forward_locked(e, ids, types, cu, B, T, max_len, out, static_cast<hipStream_t>(stream));
+}
+
+int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, const void* W,
+                  const void* W_lo, const float* bias, int M, int N, int K, void* C,
+                  void* C_lo, void* stream) {
+  ragmi::clear_error();
+  if (!A || !W || !bias || !C) return ragmi::fail(RAG_EINVAL, "NULL argument");
+  if (M < 1 || N < BN || K < 64 || N % BN != 0 || K % 64 != 0)
+    return ragmi::fail(RAG_EINVAL, "M >= 1, N and K multiples of 128 / 64 required");
+  if ((A_lo == nullptr) != (W_lo == nullptr))
+    return ragmi::fail(RAG_EINVAL, "A_lo and W_lo: both (fp16x3) or neither (fp16)");
+  if (A_lo && epilogue != kEpiF32 && !C_lo)
+    return ragmi::fail(RAG_EINVAL, "fp16x3 fp16-output GEMM needs C_lo");
+  if (variant == RAG_GEMM_PIPE && !pipe_ok(M, N, K))
+    return ragmi::fail(RAG_EINVAL, "pipe variant needs N % 128 == 0, K % 64 == 0, N <= 4096, M*K*2 and M*N*4 < 2^31");
+  if (variant < RAG_GEMM_AUTO || variant > 4 || (variant >= 3 && (A_lo || !pipe_ok(M, N, K))))
+    return ragmi::fail(RAG_EINVAL, "unknown GEMM variant");
+  auto* a = static_cast<const _Float16*>(A);
+  auto* al = static_cast<const _Float16*>(A_lo);
+  auto* w = static_cast<const _Float16*>(W);
+  auto* wl = static_cast<const _Float16*>(W_lo);
+  auto* clo = static_cast<_Float16*>(C_lo);
+  auto st = static_cast<hipStream_t>(stream);
+  switch (epilogue) {
+    case kEpiF16: gemm<kEpiF16>(a, al, w, wl, bias, M, N, K, C, clo, st, variant); break;
+    case kEpiGeluF16: gemm<kEpiGeluF16>(a, al, w, wl, bias, M, N, K, C, clo, st, variant); break;
+    case kEpiF32: gemm<kEpiF32>(a, al, w, wl, bias, M, N, K, C, clo, st, variant); break;
+    default: return ragmi::fail(RAG_EINVAL, "unknown epilogue");
+  }
+  RAG_HIP(hipGetLastError());
+  return RAG_OK;
 }
 
 int rag_encoder_forward_host(rag_encoder_t* e, const int32_t* ids, const int32_t* types,

@@ -310,6 +310,294 @@ __global__ __launch_bounds__(256) void gemm_kernel(const _Float16* __restrict__ 
 }
 
 // ----------------------------------------------------------------------------------------
+// Persistent pipelined GEMM for large token counts (rerank batches, chunk encode):
+// C[M,N] = A[M,K] . W[N,K]^T + bias, same epilogues as gemm_kernel.
+//
+// One 8-wave workgroup per CU loops over 256x128 output tiles (XCD-aware: in every round of
+// gridDim.x tiles, the workgroups of one XCD take a contiguous tile range, so the N tiles of
+// an A panel run on the same L2). K is short here (384 / 1024 / 1536), so a tile is only
+// 6-24 K steps: a per-tile load prologue would expose one HBM latency per few hundred MFMA
+// cycles. Instead the loads run on a flat (tile, k-step) sequence through a 3-stage LDS ring
+// filled by direct buffer->LDS DMA (buffer_load_dwordx4 ... lds), two stages in flight,
+// straight across tile boundaries — the next tile's first stages land while this tile's
+// epilogue runs.
+// Addressing is hoisted out of the loop: a tile's A and W panels are two buffer resources
+// (wave-uniform SGPRs, rebuilt once per tile; A's extent ends at row M, so rows past M read
+// as zeros), every lane's byte offset inside a panel is a launch constant (the XOR swizzle of
+// the LDS image is applied to it), and a K step only moves the scalar soffset. A step costs
+// 6 DMAs + their M0 writes besides its 32 (fp16) / 48 (fp16x3) MFMAs and 16 ds_read_b128.
+// Sync per K step: counted `s_waitcnt vmcnt` + one raw s_barrier (step g landed for every
+// wave AND every wave is done reading step g-1, whose slot the next DMA reuses). Besides the
+// DMAs the loop issues only the epilogue's stores, a fixed number S per tile (buffer stores
+// bounded to the M x N output: rows past M are dropped by the range check, never by exec
+// masking), so every vmcnt is exact.
+// Operands are swapped in the MFMA (D = W . A^T): lane l holds C[m][n .. n+3] for
+// m = row (l & 15) of the fragment and 4 consecutive features n, so the epilogue adds bias
+// (staged in LDS once per launch), applies GELU and stores 8-B (fp16) / 16-B (fp32) vectors
+// straight from registers; the LDS stays the ring's.
+// ----------------------------------------------------------------------------------------
+constexpr int PBM = 256, PBN = 128, PNS = 3;
+constexpr int kPipeThreads = 512;
+constexpr int kPipeBiasMax = 4096;            // floats of bias staged in LDS (N <= 4096)
+
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// 16 B per lane buffer -> LDS DMA: lane l's bytes at panel + soff + voff land at LDS byte
+// address lds_addr + 16 l. Inline asm for the same reason as glds16 (device_common.hpp).
+__device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff,
+                                       uint32_t lds_addr) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(rs), "s"(lds_addr), "s"(soff)
+      : "memory");
+}
+
+// raw buffer resource over [base, base + bytes) from wave-uniform inputs (reads past the
+// end return zeros, stores past it are dropped); bytes < 2^31 (checked by the launcher)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t panel(const void* base, int64_t bytes) {
+  const int nb = bytes > 0 ? (int)bytes : 0;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0,
+                                           __builtin_amdgcn_readfirstlane(nb), 0x00020000);
+}
+
+// PROBE (diagnostic builds only, rag_bert_gemm variants 3/4): 1 = no MFMAs, 2 = no DMAs
+template <int EPI, bool SPLIT, int PROBE = 0>
+__global__ __launch_bounds__(kPipeThreads, 1) void gemm_pipe_kernel(
+    const _Float16* __restrict__ A, const _Float16* __restrict__ Al,
+    const _Float16* __restrict__ W, const _Float16* __restrict__ Wl,
+    const float* __restrict__ bias, int M, int N, int K, void* __restrict__ Cout,
+    _Float16* __restrict__ Clo) {
+  constexpr int BK = kBK<SPLIT>, CPR = BK / 8;
+  constexpr int NPL = SPLIT ? 2 : 1;                     // planes per operand (hi[, lo])
+  constexpr int A_H8 = PBM * CPR, W_H8 = PBN * CPR;      // half8 per plane per stage
+  constexpr int STAGE_H8 = NPL * (A_H8 + W_H8);          // 48 KB either mode
+  constexpr int LA = A_H8 / kPipeThreads, LW = W_H8 / kPipeThreads;   // DMAs/wave/plane
+  constexpr int L = NPL * (LA + LW);                      // DMAs per wave per stage (6)
+  // epilogue stores per wave: 16 B each; fp16 outputs pair two fragments per store
+  constexpr int S = EPI == kEpiF32 ? 16 : (SPLIT ? 16 : 8);
+  constexpr int OUT_B = EPI == kEpiF32 ? 4 : 2;           // output element bytes
+  static_assert(A_H8 % kPipeThreads == 0 && W_H8 % kPipeThreads == 0, "stage split");
+  // one LDS object (ring | bias): a second __shared__ object beside a DMA target can make
+  // hipcc drain vmcnt before every ds_read
+  __shared__ half8 lds[PNS * STAGE_H8 + kPipeBiasMax / 4];
+  float* bias_l = reinterpret_cast<float*>(lds + PNS * STAGE_H8);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 1, wc = wid & 1;                 // 4 (M) x 2 (N) waves of 64x64
+  const uint32_t lbase = lds_addr_of(lds);
+  const int nN = N / PBN, nM = (M + PBM - 1) / PBM, n_tiles = nM * nN;
+  const int nk = K / BK;
+  const int G = gridDim.x, per_xcd = G >> 3;
+  const int off = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+  const int n_mine = off < n_tiles ? (n_tiles - off + G - 1) / G : 0;
+  const int steps = n_mine * nk;
+
+  for (int i = tid * 4; i < N; i += kPipeThreads * 4)
+    *reinterpret_cast<floatx4*>(bias_l + i) = *reinterpret_cast<const floatx4*>(bias + i);
+  __syncthreads();
+
+  // per-lane byte offsets inside a panel (launch constants): LDS position q of the
+  // lane-linear image holds row q / CPR, 16-B chunk (q % CPR) ^ swizzle(row)
+  uint32_t voA[LA], voW[LW];
+#pragma unroll
+  for (int i = 0; i < LA; ++i) {
+    const int q = (wid * LA + i) * 64 + lane, r = q / CPR, cs = q % CPR;
+    const int c = (CPR == 8) ? (cs ^ (r & 7)) : (cs ^ ((r >> 2) & 3));
+    voA[i] = (uint32_t)(r * K + c * 8) * 2u;
+  }
+#pragma unroll
+  for (int i = 0; i < LW; ++i) {
+    const int q = (wid * LW + i) * 64 + lane, r = q / CPR, cs = q % CPR;
+    const int c = (CPR == 8) ? (cs ^ (r & 7)) : (cs ^ ((r >> 2) & 3));
+    voW[i] = (uint32_t)(r * K + c * 8) * 2u;
+  }
+
+  // issue side: next (tile iteration, k-step) to load, its panels and ring slot
+  // A tile's K steps run in a rotated order, starting at k-step (n-tile % nk): the nN tiles
+  // that share an A panel (same XCD, same time) then touch different K slices of it at any
+  // moment, so one of them takes each slice's L2 miss and the others hit, instead of all of
+  // them waiting on the same HBM fetch at every step.
+  int it_i = 0, kt_i = 0, kr_i = 0, slot_i = 0;
+  __amdgpu_buffer_rsrc_t rA0 = panel(A, 0), rA1 = rA0, rW0 = rA0, rW1 = rA0;
+  auto issue_next = [&]() {
+    if (it_i >= n_mine) return;
+    if constexpr (PROBE == 2) {
+      if (++kt_i == nk) { kt_i = 0; ++it_i; }
+      return;
+    }
+    if (kt_i == 0) {
+      const int tile = it_i * G + off;
+      const int m0 = (tile / nN) * PBM, n0 = (tile % nN) * PBN;
+      kr_i = (tile % nN) % nk;
+      const int64_t abytes = (int64_t)(M - m0) * K * 2, wbytes = (int64_t)PBN * K * 2;
+      rA0 = panel(A + (int64_t)m0 * K, abytes);
+      rW0 = panel(W + (int64_t)n0 * K, wbytes);
+      if constexpr (SPLIT) {
+        rA1 = panel(Al + (int64_t)m0 * K, abytes);
+        rW1 = panel(Wl + (int64_t)n0 * K, wbytes);
+      }
+    }
+    const uint32_t soff = (uint32_t)kr_i * (BK * 2);
+    if (++kr_i == nk) kr_i = 0;
+    const uint32_t slot = lbase + (uint32_t)slot_i * (STAGE_H8 * 16);
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const uint32_t d = slot + (uint32_t)((wid * LA + i) * 64 * 16);
+      blds16(rA0, voA[i], soff, d);
+      if constexpr (SPLIT) blds16(rA1, voA[i], soff, d + A_H8 * 16);
+    }
+#pragma unroll
+    for (int i = 0; i < LW; ++i) {
+      const uint32_t d = slot + (uint32_t)((NPL * A_H8 + (wid * LW + i) * 64) * 16);
+      blds16(rW0, voW[i], soff, d);
+      if constexpr (SPLIT) blds16(rW1, voW[i], soff, d + W_H8 * 16);
+    }
+    if (++kt_i == nk) { kt_i = 0; ++it_i; }
+    if (++slot_i == PNS) slot_i = 0;
+  };
+
+  floatx4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  issue_next();
+  issue_next();
+  int kt_c = 0, it_c = 0, slot_c = 0;
+  for (int g = 0; g < steps; ++g) {
+    const bool more = g + 1 < steps;                      // step g+1's DMAs are younger
+    const bool stored = g > 0 && kt_c == 0;               // so are the last epilogue's stores
+    if (more && stored)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L + S) : "memory");
+    else if (more)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L) : "memory");
+    else if (stored)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(S) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();     // step g landed for all waves; all are past step g-1
+    issue_next();                     // step g+2 -> slot (g+2) % 3 == (g-1) % 3
+
+    const half8* sa = lds + slot_c * STAGE_H8;
+    const half8* sw = sa + NPL * A_H8;
+#pragma unroll
+    for (int ks = 0; ks < (PROBE == 1 ? 0 : BK / 32); ++ks) {
+      const int ch = ks * 4 + (lane >> 4);
+      half8 af[4], wf[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = sa[swz<CPR>(wr * 64 + i * 16 + (lane & 15), ch)];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) wf[j] = sw[swz<CPR>(wc * 64 + j * 16 + (lane & 15), ch)];
+      if constexpr (SPLIT) {
+        half8 afl[4], wfl[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) afl[i] = sa[A_H8 + swz<CPR>(wr * 64 + i * 16 + (lane & 15), ch)];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) wfl[j] = sw[W_H8 + swz<CPR>(wc * 64 + j * 16 + (lane & 15), ch)];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wfl[j], af[i], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[j], afl[i], acc[i][j], 0, 0, 0);
+          }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[j], af[i], acc[i][j], 0, 0, 0);
+    }
+    if (++slot_c == PNS) slot_c = 0;
+
+    if (++kt_c == nk) {               // tile done: epilogue from registers
+      kt_c = 0;
+      const int tile = it_c * G + off;
+      ++it_c;
+      const int m0 = (tile / nN) * PBM, n0 = (tile % nN) * PBN;
+      const int64_t cbytes = (int64_t)(M - m0) * N * OUT_B;
+      const __amdgpu_buffer_rsrc_t rc =
+          panel(static_cast<char*>(Cout) + (int64_t)m0 * N * OUT_B, cbytes);
+      __amdgpu_buffer_rsrc_t rl = rc;
+      if constexpr (SPLIT && EPI != kEpiF32) rl = panel(Clo + (int64_t)m0 * N, cbytes);
+      if constexpr (EPI == kEpiF32) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int nl = wc * 64 + j * 16 + 4 * (lane >> 4);
+          const floatx4 bj = *reinterpret_cast<const floatx4*>(bias_l + n0 + nl);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int ml = wr * 64 + i * 16 + (lane & 15);
+            const floatx4 v = acc[i][j] + bj;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rc,
+                                                   (ml * N + n0 + nl) * 4, 0, 0);
+          }
+        }
+      } else {
+        // fp16 out: fragments j, j+1 of a row pair up through one v_permlane16_swap per
+        // dword (lanes 16-31 of the j value <-> lanes 0-15 of the j+1 value, same for
+        // 48-63 / 32-47), after which every lane holds 8 consecutive columns: 16-B stores,
+        // half the store instructions of 8-B ones (the epilogue is store-issue-bound).
+        // Lane group g = lane >> 4 then owns columns 16 j + {0, 16, 8, 24}[g] .. +7.
+        const int g = lane >> 4;
+        const int cofs = 8 * ((g & 1) * 2 + (g >> 1));
+#pragma unroll
+        for (int jp = 0; jp < 4; jp += 2) {
+          floatx4 b0 = *reinterpret_cast<const floatx4*>(bias_l + n0 + wc * 64 + jp * 16 + 4 * g);
+          floatx4 b1 = *reinterpret_cast<const floatx4*>(bias_l + n0 + wc * 64 + jp * 16 + 16 + 4 * g);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int ml = wr * 64 + i * 16 + (lane & 15);
+            const int vo = (ml * N + n0 + wc * 64 + jp * 16 + cofs) * 2;
+            floatx4 va = acc[i][jp] + b0, vb = acc[i][jp + 1] + b1;
+            if constexpr (EPI == kEpiGeluF16) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                va[r] = gelu_erf(va[r]);
+                vb[r] = gelu_erf(vb[r]);
+              }
+            }
+            half4 ha, hb;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              ha[r] = (_Float16)va[r];
+              hb[r] = (_Float16)vb[r];
+            }
+            auto store_pair = [&](half4 xa, half4 xb, __amdgpu_buffer_rsrc_t rsc) {
+              u32x2 a = __builtin_bit_cast(u32x2, xa), b = __builtin_bit_cast(u32x2, xb);
+              const auto r0 = __builtin_amdgcn_permlane16_swap(a[0], b[0], false, false);
+              const auto r1 = __builtin_amdgcn_permlane16_swap(a[1], b[1], false, false);
+              const u32x4 d = {r0[0], r1[0], r0[1], r1[1]};
+              __builtin_amdgcn_raw_buffer_store_b128(d, rsc, vo, 0, 0);
+            };
+            store_pair(ha, hb, rc);
+            if constexpr (SPLIT) {
+              half4 la, lb;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                la[r] = lo_part(va[r], ha[r]);
+                lb[r] = lo_part(vb[r], hb[r]);
+              }
+              store_pair(la, lb, rl);
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------------
 // attention (varlen, one workgroup per (head, sequence), 8 waves (fp16) / 16 (fp16x3)).
 // K and V of the sequence's keys are staged into LDS (all of them when they fit — always for
 // head_dim 32, and for head_dim 64 up to ~288 keys in fp16x3 — else in chunks of kc keys),

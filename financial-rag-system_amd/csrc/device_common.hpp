@@ -16,6 +16,31 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 constexpr float kNegInf = -__builtin_inff();
 constexpr int kIdNone32 = 0x7fffffff;
 
+// 16 B per lane global -> LDS DMA (global_load_lds_dwordx4): lane l's 16 bytes from `gsrc`
+// land at LDS byte address lds_addr + 16 l (lds_addr wave-uniform).
+// Issued through inline asm on purpose: hipcc (ROCm 7.2) tracks the builtin's LDS write and
+// puts `s_waitcnt vmcnt(0)` before the first ds_read after it (it cannot prove the read
+// misses the DMA target), which drains a multi-stage ring on every step. Hidden in asm, the
+// DMA is invisible to its waitcnt bookkeeping: the caller retires it with its own counted
+// `s_waitcnt vmcnt(N)` + barrier before reading the slot. M0 is compiler-reserved, so it is
+// saved and restored inside the statement.
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_addr) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_addr)
+      : "memory");
+}
+
+// LDS byte address of a __shared__ pointer (for glds16), made provably wave-uniform
+template <typename T>
+__device__ __forceinline__ uint32_t lds_addr_of(const T* p) {
+  return __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) T*)p);
+}
+
 // Total order used everywhere for ranking: score descending, then id ascending
 // ("sorted by (score desc, row id asc)"). Bitwise ops, no short-circuit: the
 // comparator must compile to v_cmp + mask logic, not exec-masked branches.

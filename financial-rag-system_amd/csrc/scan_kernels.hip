@@ -990,6 +990,8 @@ __global__ __launch_bounds__(64 * kWideWaves, 1) void scan_wide_kernel(
   const int g = wid >> 1, qt = wid & 1;
   const bool active = g < groups;
   const int nb = gridDim.x, b = blockIdx.x;
+  const int wid_u = __builtin_amdgcn_readfirstlane(wid);
+  const uint32_t ring_addr = lds_addr_of(ring);
 
   half8 qf[S];
 #pragma unroll
@@ -1006,18 +1008,20 @@ __global__ __launch_bounds__(64 * kWideWaves, 1) void scan_wide_kernel(
   heads_i += (int64_t)g * kQ * nw;
   heads_n += (int64_t)g * kQ * nw;
 
+  // settle the query-fragment loads here: left pending into the loop, hipcc would put a
+  // `vmcnt(0)` (draining the DMA ring) before their first MFMA use in every iteration
+#pragma unroll
+  for (int s = 0; s < S; ++s) asm volatile("" : "+v"(qf[s]));
+  asm volatile("" : "+v"(st.thr));
   const int n_mine = b < n_tiles ? (n_tiles - 1 - b) / nb + 1 : 0;
   const char* cbase = reinterpret_cast<const char*>(corpus);
   auto issue = [&](int j) {   // this wave's 4 KB of tile j -> ring slot j % 4
     if (j < n_mine) {
       const int t = b + j * nb;
-      const char* src = cbase + (int64_t)t * (S * 1024) + wid * 4096 + lane * 16;
-      char* dst = reinterpret_cast<char*>(ring + (j % kWideBufs) * TILE) + wid * 4096;
+      const char* src = cbase + (int64_t)t * (S * 1024) + wid_u * 4096 + lane * 16;
+      const uint32_t dst = ring_addr + (j % kWideBufs) * (TILE * 16) + wid_u * 4096;
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        __builtin_amdgcn_global_load_lds(
-            (const __attribute__((address_space(1))) void*)(src + i * 1024),
-            (__attribute__((address_space(3))) void*)(dst + i * 1024), 16, 0, 0);
+      for (int i = 0; i < 4; ++i) glds16(src + i * 1024, dst + i * 1024);
     }
   };
   issue(0);

@@ -71,6 +71,37 @@ def config_from_hf(cfg: dict) -> dict:
                 type_vocab=cfg.get("type_vocab_size", 2), eps=cfg.get("layer_norm_eps", 1e-12))
 
 
+# ------------------------------------------------------------------ one encoder GEMM
+GEMM_AUTO, GEMM_TILE, GEMM_PIPE = 0, 1, 2          # rag_bert_gemm variants (ragmi_bert.h)
+EPI_F16, EPI_GELU_F16, EPI_F32 = 0, 1, 2            # epilogues
+
+
+def linear(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, epilogue: int = EPI_F32,
+           a_lo: torch.Tensor | None = None, w_lo: torch.Tensor | None = None,
+           variant: int = GEMM_AUTO):
+    """nn.Linear of the encoder layers (modeling_bert.py BertSelfAttention / BertIntermediate /
+    BertOutput dense) through the forward's own GEMM kernels: a fp16 [M,K], w fp16 [N,K],
+    bias fp32 [N] -> fp32 [M,N] (EPI_F32) or fp16 [M,N] (+ lo plane when a_lo/w_lo are
+    given, the fp16x3 mode). Diagnostic entry for parity tests and the GEMM benchmark."""
+    M, K = a.shape
+    N = w.shape[0]
+    for t, dt in ((a, torch.float16), (w, torch.float16), (bias, torch.float32)):
+        if t.dtype != dt or not t.is_cuda or not t.is_contiguous():
+            raise ValueError("a, w: contiguous fp16 cuda; bias: contiguous fp32 cuda")
+    split = a_lo is not None
+    odt = torch.float32 if epilogue == EPI_F32 else torch.float16
+    c = torch.empty((M, N), dtype=odt, device=a.device)
+    c_lo = torch.empty((M, N), dtype=torch.float16, device=a.device) \
+        if split and epilogue != EPI_F32 else None
+    L = _lib.load()
+    check(L.rag_bert_gemm(variant, epilogue, a.data_ptr(), a_lo.data_ptr() if split else None,
+                          w.data_ptr(), w_lo.data_ptr() if w_lo is not None else None,
+                          bias.data_ptr(), M, N, K, c.data_ptr(),
+                          c_lo.data_ptr() if c_lo is not None else None,
+                          torch.cuda.current_stream(a.device).cuda_stream))
+    return (c, c_lo) if c_lo is not None else c
+
+
 # ------------------------------------------------------------------ device encoder
 class BertEncoder:
     """One encoder instance in HBM (fp16 GEMM weights, fp32 norms/embeddings)."""

@@ -69,6 +69,19 @@ int rag_encoder_forward(rag_encoder_t* enc, const int32_t* ids_dev, const int32_
 int rag_encoder_forward_host(rag_encoder_t* enc, const int32_t* ids, const int32_t* types,
                              const int32_t* cu_seqlens, int B, int T, float* out);
 
+/* Diagnostic entry (parity tests and the GEMM benchmark; not called by the reference path):
+ * one encoder GEMM C[M,N] = A[M,K] . W[N,K]^T + bias[N] (the nn.Linear of modeling_bert.py
+ * BertSelfAttention/BertIntermediate/BertOutput), device pointers, async on `stream`.
+ * A, W fp16 row-major; A_lo/W_lo the fp16x3 residual planes (both NULL = plain fp16).
+ * epilogue: RAG_EPI_F16 (C fp16 [+ C_lo]), RAG_EPI_GELU_F16 (erf-GELU, fp16 [+ C_lo]),
+ * RAG_EPI_F32 (C fp32). variant: RAG_GEMM_AUTO (what the forward uses), _TILE, _PIPE.
+ * N % 128 == 0, K % 64 == 0 (PIPE also N <= 4096). */
+enum { RAG_EPI_F16 = 0, RAG_EPI_GELU_F16 = 1, RAG_EPI_F32 = 2 };
+enum { RAG_GEMM_AUTO = 0, RAG_GEMM_TILE = 1, RAG_GEMM_PIPE = 2 };
+int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, const void* W,
+                  const void* W_lo, const float* bias, int M, int N, int K, void* C,
+                  void* C_lo, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
