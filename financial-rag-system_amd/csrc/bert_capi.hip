@@ -125,10 +125,10 @@ int ensure_ws(rag_encoder* e, int64_t T) {
   return RAG_OK;
 }
 
-// GEMM variants: RAG_GEMM_TILE (gemm_kernel: one 128x128 tile per workgroup, 2 per CU) and
-// RAG_GEMM_PIPE (gemm_pipe_kernel: persistent, one 8-wave workgroup per CU, LDS-DMA ring
-// across tiles). AUTO takes PIPE once its 256x128 tiles cover every CU (large token counts:
-// rerank batches, chunk encode) and TILE below that (query batches: more, smaller tiles).
+// GEMM variants: RAG_GEMM_TILE (gemm_kernel: one 128x128 tile per workgroup, 2 per CU),
+// RAG_GEMM_PIPE (gemm_pipe_kernel<PipeLarge>: persistent, one 8-wave workgroup per CU, LDS-DMA
+// ring across 256x128 tiles) and RAG_GEMM_SMALL (gemm_pipe_kernel<PipeSmall>: 64x64 tiles,
+// the K panel in flight at once); AUTO's choice is below.
 int cu_count() {
   static int n = [] {
     int dev = 0, v = 0;
@@ -145,15 +145,26 @@ int gemm_variant_default() {
     const char* s = std::getenv("RAGMI_GEMM");
     if (s && std::strcmp(s, "tile") == 0) return (int)RAG_GEMM_TILE;
     if (s && std::strcmp(s, "pipe") == 0) return (int)RAG_GEMM_PIPE;
+    if (s && std::strcmp(s, "small") == 0) return (int)RAG_GEMM_SMALL;
     return (int)RAG_GEMM_AUTO;
   }();
   return v;
 }
 
-// PIPE addresses each operand and the output through 32-bit buffer extents
+// the DMA kernels address each operand and the output through 32-bit buffer extents
 bool pipe_ok(int M, int N, int K) {
   return N % PBN == 0 && K % 64 == 0 && N <= kPipeBiasMax &&
          (int64_t)M * K * 2 < (int64_t(1) << 31) && (int64_t)M * N * 4 < (int64_t(1) << 31);
+}
+
+template <int EPI, bool SPLIT, typename CFG, int PROBE = 0>
+void launch_pipe(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float16* Wl,
+                 const float* bias, int M, int N, int K, void* C, _Float16* Clo, hipStream_t st,
+                 int max_wg) {
+  const int tiles = (N / CFG::BN) * ((M + CFG::BM - 1) / CFG::BM);
+  const dim3 grid((unsigned)std::min(max_wg, (tiles + 7) / 8 * 8));   // multiple of 8
+  gemm_pipe_kernel<EPI, SPLIT, CFG, PROBE><<<grid, dim3(CFG::THREADS), 0, st>>>(
+      A, Al, W, Wl, bias, M, N, K, C, Clo);
 }
 
 template <int EPI>
@@ -162,26 +173,41 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
           int variant = RAG_GEMM_AUTO) {
   if (variant == RAG_GEMM_AUTO) variant = gemm_variant_default();
   const int pipe_tiles = (N / PBN) * ((M + PBM - 1) / PBM);
+  // SMALL while its 64x64 tiles fit about two per CU (every query-batch GEMM; the N = 384
+  // ones up to ~5K tokens), PIPE once its 256x128 tiles cover the CUs, TILE in between
+  const int small_tiles = (N / 64) * ((M + 63) / 64);
   if (variant == RAG_GEMM_AUTO)
-    variant = (pipe_ok(M, N, K) && pipe_tiles >= cu_count()) ? RAG_GEMM_PIPE : RAG_GEMM_TILE;
-  if (variant >= 3 && pipe_ok(M, N, K)) {    // diagnostic probes of the PIPE kernel
-    const dim3 grid((unsigned)std::min(cu_count(), (pipe_tiles + 7) / 8 * 8));
-    if (variant == 3)
-      gemm_pipe_kernel<EPI, false, 1><<<grid, dim3(kPipeThreads), 0, st>>>(
-          A, nullptr, W, nullptr, bias, M, N, K, C, nullptr);
-    else
-      gemm_pipe_kernel<EPI, false, 2><<<grid, dim3(kPipeThreads), 0, st>>>(
-          A, nullptr, W, nullptr, bias, M, N, K, C, nullptr);
+    variant = !pipe_ok(M, N, K)                  ? RAG_GEMM_TILE
+              : small_tiles <= 2 * cu_count()    ? RAG_GEMM_SMALL
+              : pipe_tiles >= cu_count()         ? RAG_GEMM_PIPE
+                                                 : RAG_GEMM_TILE;
+  if (variant != RAG_GEMM_TILE && !pipe_ok(M, N, K)) variant = RAG_GEMM_TILE;
+  if (variant == RAG_GEMM_PROBE_NO_MFMA) {       // diagnostic probes of the PIPE kernel
+    launch_pipe<EPI, false, PipeLarge, 1>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st,
+                                          cu_count());
     return;
   }
-  if (variant == RAG_GEMM_PIPE && pipe_ok(M, N, K)) {
-    const dim3 grid((unsigned)std::min(cu_count(), (pipe_tiles + 7) / 8 * 8));
+  if (variant == RAG_GEMM_PROBE_NO_DMA) {
+    launch_pipe<EPI, false, PipeLarge, 2>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st,
+                                          cu_count());
+    return;
+  }
+  if (variant == RAG_GEMM_PIPE) {
     if (Al)
-      gemm_pipe_kernel<EPI, true><<<grid, dim3(kPipeThreads), 0, st>>>(A, Al, W, Wl, bias, M,
-                                                                       N, K, C, Clo);
+      launch_pipe<EPI, true, PipeLarge>(A, Al, W, Wl, bias, M, N, K, C, Clo, st, cu_count());
     else
-      gemm_pipe_kernel<EPI, false><<<grid, dim3(kPipeThreads), 0, st>>>(
-          A, nullptr, W, nullptr, bias, M, N, K, C, nullptr);
+      launch_pipe<EPI, false, PipeLarge>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st,
+                                         cu_count());
+    return;
+  }
+  if (variant == RAG_GEMM_SMALL) {
+    // fp16: 80 KB LDS -> 2 workgroups per CU; fp16x3: 112 KB -> 1
+    if (Al)
+      launch_pipe<EPI, true, PipeSmall<true>>(A, Al, W, Wl, bias, M, N, K, C, Clo, st,
+                                              cu_count());
+    else
+      launch_pipe<EPI, false, PipeSmall<false>>(A, nullptr, W, nullptr, bias, M, N, K, C,
+                                                nullptr, st, 2 * cu_count());
     return;
   }
   const unsigned tiles = (unsigned)((N / BN) * ((M + BM - 1) / BM));
@@ -192,8 +218,6 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
     gemm_kernel<EPI, false><<<grid, dim3(256), 0, st>>>(A, nullptr, W, nullptr, bias, M, N, K,
                                                         C, nullptr);
 }
-
-
 
 template <int H, int HD>
 int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const int32_t* cu,
@@ -389,10 +413,13 @@ int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, co
     return ragmi::fail(RAG_EINVAL, "A_lo and W_lo: both (fp16x3) or neither (fp16)");
   if (A_lo && epilogue != kEpiF32 && !C_lo)
     return ragmi::fail(RAG_EINVAL, "fp16x3 fp16-output GEMM needs C_lo");
-  if (variant == RAG_GEMM_PIPE && !pipe_ok(M, N, K))
-    return ragmi::fail(RAG_EINVAL, "pipe variant needs N % 128 == 0, K % 64 == 0, N <= 4096, M*K*2 and M*N*4 < 2^31");
-  if (variant < RAG_GEMM_AUTO || variant > 4 || (variant >= 3 && (A_lo || !pipe_ok(M, N, K))))
-    return ragmi::fail(RAG_EINVAL, "unknown GEMM variant");
+  if ((variant == RAG_GEMM_PIPE || variant == RAG_GEMM_SMALL) && !pipe_ok(M, N, K))
+    return ragmi::fail(RAG_EINVAL, "pipe/small variants need N % 128 == 0, K % 64 == 0, "
+                                   "N <= 4096, M*K*2 and M*N*4 < 2^31");
+  const bool probe = variant == RAG_GEMM_PROBE_NO_MFMA || variant == RAG_GEMM_PROBE_NO_DMA;
+  if (variant < RAG_GEMM_AUTO || variant > RAG_GEMM_SMALL ||
+      (probe && (A_lo || !pipe_ok(M, N, K))))
+    return ragmi::fail(RAG_EINVAL, "unknown GEMM variant (probes: fp16 only)");
   auto* a = static_cast<const _Float16*>(A);
   auto* al = static_cast<const _Float16*>(A_lo);
   auto* w = static_cast<const _Float16*>(W);

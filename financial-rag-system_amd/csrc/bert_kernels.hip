@@ -336,8 +336,21 @@ __global__ __launch_bounds__(256) void gemm_kernel(const _Float16* __restrict__ 
 // (staged in LDS once per launch), applies GELU and stores 8-B (fp16) / 16-B (fp32) vectors
 // straight from registers; the LDS stays the ring's.
 // ----------------------------------------------------------------------------------------
-constexpr int PBM = 256, PBN = 128, PNS = 3;
-constexpr int kPipeThreads = 512;
+// Two shapes of the same kernel (PipeCfg): LARGE — 256x128 tiles, 8 waves of 64x64, 3-stage
+// ring, one workgroup per CU, persistent (rerank / chunk-encode token counts); SMALL —
+// 64x64 tiles, 4 waves of 32x32, a 4-stage ring (fp16: the whole K = 384 of a tile in
+// flight after the prologue), for query batches of a few hundred to a few thousand tokens,
+// where a GEMM is a handful of tiles per CU and latency, not MFMA rate, sets its time.
+template <int BM_, int BN_, int WAVES_M_, int WAVES_N_, int NS_>
+struct PipeCfg {
+  static constexpr int BM = BM_, BN = BN_, WAVES_M = WAVES_M_, WAVES_N = WAVES_N_, NS = NS_;
+  static constexpr int THREADS = 64 * WAVES_M * WAVES_N;
+  static constexpr int FM = BM / WAVES_M / 16, FN = BN / WAVES_N / 16;   // 16x16 frags/wave
+};
+using PipeLarge = PipeCfg<256, 128, 4, 2, 3>;
+template <bool SPLIT> using PipeSmall = PipeCfg<64, 64, 2, 2, SPLIT ? 3 : 4>;
+constexpr int PBM = PipeLarge::BM, PBN = PipeLarge::BN;
+constexpr int kPipeThreads = PipeLarge::THREADS;
 constexpr int kPipeBiasMax = 4096;            // floats of bias staged in LDS (N <= 4096)
 
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
@@ -364,40 +377,57 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t panel(const void* base, int64_
                                            __builtin_amdgcn_readfirstlane(nb), 0x00020000);
 }
 
+// s_waitcnt vmcnt(Y*L + (stored ? S : 0)) for a runtime Y in [0, Y_MAX] (vmcnt takes an
+// immediate): Y = ring stages issued after the one being waited for
+template <int L, int S, int Y>
+__device__ __forceinline__ void wait_ring(int y, bool stored) {
+  if (y == Y) {
+    if (stored)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Y * L + S) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Y * L) : "memory");
+    return;
+  }
+  if constexpr (Y > 0) wait_ring<L, S, Y - 1>(y, stored);
+}
+
 // PROBE (diagnostic builds only, rag_bert_gemm variants 3/4): 1 = no MFMAs, 2 = no DMAs
-template <int EPI, bool SPLIT, int PROBE = 0>
-__global__ __launch_bounds__(kPipeThreads, 1) void gemm_pipe_kernel(
+template <int EPI, bool SPLIT, typename CFG, int PROBE = 0>
+__global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
     const _Float16* __restrict__ A, const _Float16* __restrict__ Al,
     const _Float16* __restrict__ W, const _Float16* __restrict__ Wl,
     const float* __restrict__ bias, int M, int N, int K, void* __restrict__ Cout,
     _Float16* __restrict__ Clo) {
+  constexpr int BM = CFG::BM, BN = CFG::BN, NS = CFG::NS, TH = CFG::THREADS;
+  constexpr int FM = CFG::FM, FN = CFG::FN, WTM = 16 * FM, WTN = 16 * FN;
   constexpr int BK = kBK<SPLIT>, CPR = BK / 8;
   constexpr int NPL = SPLIT ? 2 : 1;                     // planes per operand (hi[, lo])
-  constexpr int A_H8 = PBM * CPR, W_H8 = PBN * CPR;      // half8 per plane per stage
-  constexpr int STAGE_H8 = NPL * (A_H8 + W_H8);          // 48 KB either mode
-  constexpr int LA = A_H8 / kPipeThreads, LW = W_H8 / kPipeThreads;   // DMAs/wave/plane
-  constexpr int L = NPL * (LA + LW);                      // DMAs per wave per stage (6)
+  constexpr int A_H8 = BM * CPR, W_H8 = BN * CPR;        // half8 per plane per stage
+  constexpr int STAGE_H8 = NPL * (A_H8 + W_H8);
+  constexpr int LA = A_H8 / TH, LW = W_H8 / TH;          // DMAs per wave per plane
+  constexpr int L = NPL * (LA + LW);                      // DMAs per wave per stage
   // epilogue stores per wave: 16 B each; fp16 outputs pair two fragments per store
-  constexpr int S = EPI == kEpiF32 ? 16 : (SPLIT ? 16 : 8);
+  constexpr int S = EPI == kEpiF32 ? FM * FN : FM * FN / 2 * (SPLIT ? 2 : 1);
   constexpr int OUT_B = EPI == kEpiF32 ? 4 : 2;           // output element bytes
-  static_assert(A_H8 % kPipeThreads == 0 && W_H8 % kPipeThreads == 0, "stage split");
+  static_assert(A_H8 % TH == 0 && W_H8 % TH == 0 && FN % 2 == 0, "tile shape");
+  static_assert((NS - 2) * L + S <= 63, "vmcnt range");
   // one LDS object (ring | bias): a second __shared__ object beside a DMA target can make
   // hipcc drain vmcnt before every ds_read
-  __shared__ half8 lds[PNS * STAGE_H8 + kPipeBiasMax / 4];
-  float* bias_l = reinterpret_cast<float*>(lds + PNS * STAGE_H8);
+  __shared__ half8 lds[NS * STAGE_H8 + kPipeBiasMax / 4];
+  float* bias_l = reinterpret_cast<float*>(lds + NS * STAGE_H8);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wid >> 1, wc = wid & 1;                 // 4 (M) x 2 (N) waves of 64x64
+  const int wr = wid / CFG::WAVES_N, wc = wid % CFG::WAVES_N;
   const uint32_t lbase = lds_addr_of(lds);
-  const int nN = N / PBN, nM = (M + PBM - 1) / PBM, n_tiles = nM * nN;
+  const int nN = N / BN, nM = (M + BM - 1) / BM, n_tiles = nM * nN;
   const int nk = K / BK;
   const int G = gridDim.x, per_xcd = G >> 3;
   const int off = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
   const int n_mine = off < n_tiles ? (n_tiles - off + G - 1) / G : 0;
   const int steps = n_mine * nk;
 
-  for (int i = tid * 4; i < N; i += kPipeThreads * 4)
+  for (int i = tid * 4; i < N; i += TH * 4)
     *reinterpret_cast<floatx4*>(bias_l + i) = *reinterpret_cast<const floatx4*>(bias + i);
   __syncthreads();
 
@@ -417,7 +447,7 @@ __global__ __launch_bounds__(kPipeThreads, 1) void gemm_pipe_kernel(
     voW[i] = (uint32_t)(r * K + c * 8) * 2u;
   }
 
-  // issue side: next (tile iteration, k-step) to load, its panels and ring slot
+  // issue side: next (tile iteration, k-step) to load, its panels and ring slot.
   // A tile's K steps run in a rotated order, starting at k-step (n-tile % nk): the nN tiles
   // that share an A panel (same XCD, same time) then touch different K slices of it at any
   // moment, so one of them takes each slice's L2 miss and the others hit, instead of all of
@@ -432,9 +462,9 @@ __global__ __launch_bounds__(kPipeThreads, 1) void gemm_pipe_kernel(
     }
     if (kt_i == 0) {
       const int tile = it_i * G + off;
-      const int m0 = (tile / nN) * PBM, n0 = (tile % nN) * PBN;
+      const int m0 = (tile / nN) * BM, n0 = (tile % nN) * BN;
       kr_i = (tile % nN) % nk;
-      const int64_t abytes = (int64_t)(M - m0) * K * 2, wbytes = (int64_t)PBN * K * 2;
+      const int64_t abytes = (int64_t)(M - m0) * K * 2, wbytes = (int64_t)BN * K * 2;
       rA0 = panel(A + (int64_t)m0 * K, abytes);
       rW0 = panel(W + (int64_t)n0 * K, wbytes);
       if constexpr (SPLIT) {
@@ -458,69 +488,62 @@ __global__ __launch_bounds__(kPipeThreads, 1) void gemm_pipe_kernel(
       if constexpr (SPLIT) blds16(rW1, voW[i], soff, d + W_H8 * 16);
     }
     if (++kt_i == nk) { kt_i = 0; ++it_i; }
-    if (++slot_i == PNS) slot_i = 0;
+    if (++slot_i == NS) slot_i = 0;
   };
 
-  floatx4 acc[4][4];
+  floatx4 acc[FM][FN];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  issue_next();
-  issue_next();
+#pragma unroll
+  for (int p = 0; p < NS - 1; ++p) issue_next();
   int kt_c = 0, it_c = 0, slot_c = 0;
   for (int g = 0; g < steps; ++g) {
-    const bool more = g + 1 < steps;                      // step g+1's DMAs are younger
-    const bool stored = g > 0 && kt_c == 0;               // so are the last epilogue's stores
-    if (more && stored)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L + S) : "memory");
-    else if (more)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L) : "memory");
-    else if (stored)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(S) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // stages issued after step g: min(NS - 2, steps - 1 - g); plus the last epilogue's
+    // stores when it ran at the end of step g-1
+    wait_ring<L, S, NS - 2>(min(NS - 2, steps - 1 - g), g > 0 && kt_c == 0);
     __builtin_amdgcn_s_barrier();     // step g landed for all waves; all are past step g-1
-    issue_next();                     // step g+2 -> slot (g+2) % 3 == (g-1) % 3
+    issue_next();                     // step g+NS-1 -> slot (g-1) % NS
 
     const half8* sa = lds + slot_c * STAGE_H8;
     const half8* sw = sa + NPL * A_H8;
 #pragma unroll
     for (int ks = 0; ks < (PROBE == 1 ? 0 : BK / 32); ++ks) {
       const int ch = ks * 4 + (lane >> 4);
-      half8 af[4], wf[4];
+      half8 af[FM], wf[FN];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = sa[swz<CPR>(wr * 64 + i * 16 + (lane & 15), ch)];
+      for (int i = 0; i < FM; ++i) af[i] = sa[swz<CPR>(wr * WTM + i * 16 + (lane & 15), ch)];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) wf[j] = sw[swz<CPR>(wc * 64 + j * 16 + (lane & 15), ch)];
+      for (int j = 0; j < FN; ++j) wf[j] = sw[swz<CPR>(wc * WTN + j * 16 + (lane & 15), ch)];
       if constexpr (SPLIT) {
-        half8 afl[4], wfl[4];
+        half8 afl[FM], wfl[FN];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) afl[i] = sa[A_H8 + swz<CPR>(wr * 64 + i * 16 + (lane & 15), ch)];
+        for (int i = 0; i < FM; ++i) afl[i] = sa[A_H8 + swz<CPR>(wr * WTM + i * 16 + (lane & 15), ch)];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) wfl[j] = sw[W_H8 + swz<CPR>(wc * 64 + j * 16 + (lane & 15), ch)];
+        for (int j = 0; j < FN; ++j) wfl[j] = sw[W_H8 + swz<CPR>(wc * WTN + j * 16 + (lane & 15), ch)];
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < FM; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
+          for (int j = 0; j < FN; ++j) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wfl[j], af[i], acc[i][j], 0, 0, 0);
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[j], afl[i], acc[i][j], 0, 0, 0);
           }
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[j], af[i], acc[i][j], 0, 0, 0);
     }
-    if (++slot_c == PNS) slot_c = 0;
+    if (++slot_c == NS) slot_c = 0;
 
     if (++kt_c == nk) {               // tile done: epilogue from registers
       kt_c = 0;
       const int tile = it_c * G + off;
       ++it_c;
-      const int m0 = (tile / nN) * PBM, n0 = (tile % nN) * PBN;
+      const int m0 = (tile / nN) * BM, n0 = (tile % nN) * BN;
       const int64_t cbytes = (int64_t)(M - m0) * N * OUT_B;
       const __amdgpu_buffer_rsrc_t rc =
           panel(static_cast<char*>(Cout) + (int64_t)m0 * N * OUT_B, cbytes);
@@ -528,12 +551,12 @@ __global__ __launch_bounds__(kPipeThreads, 1) void gemm_pipe_kernel(
       if constexpr (SPLIT && EPI != kEpiF32) rl = panel(Clo + (int64_t)m0 * N, cbytes);
       if constexpr (EPI == kEpiF32) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int nl = wc * 64 + j * 16 + 4 * (lane >> 4);
+        for (int j = 0; j < FN; ++j) {
+          const int nl = wc * WTN + j * 16 + 4 * (lane >> 4);
           const floatx4 bj = *reinterpret_cast<const floatx4*>(bias_l + n0 + nl);
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int ml = wr * 64 + i * 16 + (lane & 15);
+          for (int i = 0; i < FM; ++i) {
+            const int ml = wr * WTM + i * 16 + (lane & 15);
             const floatx4 v = acc[i][j] + bj;
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rc,
                                                    (ml * N + n0 + nl) * 4, 0, 0);
@@ -548,13 +571,13 @@ __global__ __launch_bounds__(kPipeThreads, 1) void gemm_pipe_kernel(
         const int g = lane >> 4;
         const int cofs = 8 * ((g & 1) * 2 + (g >> 1));
 #pragma unroll
-        for (int jp = 0; jp < 4; jp += 2) {
-          floatx4 b0 = *reinterpret_cast<const floatx4*>(bias_l + n0 + wc * 64 + jp * 16 + 4 * g);
-          floatx4 b1 = *reinterpret_cast<const floatx4*>(bias_l + n0 + wc * 64 + jp * 16 + 16 + 4 * g);
+        for (int jp = 0; jp < FN; jp += 2) {
+          const floatx4 b0 = *reinterpret_cast<const floatx4*>(bias_l + n0 + wc * WTN + jp * 16 + 4 * g);
+          const floatx4 b1 = *reinterpret_cast<const floatx4*>(bias_l + n0 + wc * WTN + jp * 16 + 16 + 4 * g);
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int ml = wr * 64 + i * 16 + (lane & 15);
-            const int vo = (ml * N + n0 + wc * 64 + jp * 16 + cofs) * 2;
+          for (int i = 0; i < FM; ++i) {
+            const int ml = wr * WTM + i * 16 + (lane & 15);
+            const int vo = (ml * N + n0 + wc * WTN + jp * 16 + cofs) * 2;
             floatx4 va = acc[i][jp] + b0, vb = acc[i][jp + 1] + b1;
             if constexpr (EPI == kEpiGeluF16) {
 #pragma unroll
@@ -590,9 +613,9 @@ __global__ __launch_bounds__(kPipeThreads, 1) void gemm_pipe_kernel(
         }
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
     }
   }
 }

@@ -72,7 +72,7 @@ def config_from_hf(cfg: dict) -> dict:
 
 
 # ------------------------------------------------------------------ one encoder GEMM
-GEMM_AUTO, GEMM_TILE, GEMM_PIPE = 0, 1, 2          # rag_bert_gemm variants (ragmi_bert.h)
+GEMM_AUTO, GEMM_TILE, GEMM_PIPE, GEMM_SMALL = 0, 1, 2, 5   # rag_bert_gemm variants (ragmi_bert.h)
 EPI_F16, EPI_GELU_F16, EPI_F32 = 0, 1, 2            # epilogues
 
 

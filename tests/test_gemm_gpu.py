@@ -8,7 +8,8 @@ Tolerances (C ~ N(0, 1): A ~ N(0, 1), W ~ N(0, 1/K)):
   fp16 out:                  |C - fp64 ref| <= 2^-10 |ref| + 2e-5  (one fp16 rounding)
   fp16x3 (hi + lo planes):   |C - fp64 ref((Ah+Al)(Wh+Wl))| <= 2e-5 + 2e-6 |ref|
   erf-GELU epilogue: the same bounds against 0.5 x (1 + erf(x / sqrt 2)) in fp64.
-TILE and PIPE must agree to the same bounds (they differ only in accumulation association).
+TILE, PIPE and SMALL must agree to the same bounds (they differ only in accumulation
+association).
 """
 import math
 
@@ -61,7 +62,7 @@ def _check(c, ref, epi, split):
 @pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "x".join(map(str, s)))
 @pytest.mark.parametrize("epi", [0, 1, 2], ids=["f16", "gelu", "f32"])
 @pytest.mark.parametrize("split", [False, True], ids=["fp16", "fp16x3"])
-@pytest.mark.parametrize("variant", [1, 2], ids=["tile", "pipe"])
+@pytest.mark.parametrize("variant", [1, 2, 5], ids=["tile", "pipe", "small"])
 def test_gemm_matches_fp64(gpu, shape, epi, split, variant):
     from ragmi.encoders import linear
     M, N, K = shape
