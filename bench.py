@@ -149,7 +149,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--streams", type=int, default=0,
                     help="batches in flight (0 = by shard size: 1 at >= 4M rows per GPU, "
-                         "else 2)")
+                         "else 4)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -175,17 +175,17 @@ def main():
     qs, _ = make_queries(nb, n_total, dev)
 
     # Consecutive batches alternate over `--streams` HIP streams (a serving loop keeps more
-    # than one batch in flight): batch i+1's query prep / seed sampling can run beside batch
-    # i's scan tail and select. Each stream owns its own search workspace (rag_index_search),
-    # so no cross-stream synchronisation is needed; the timed region still ends with a
-    # device-wide synchronize.
-    # Default depth by shard size: the fixed per-batch work (query prep, seed sampling,
-    # select, exchange: ~35 us) is 3% of a 10M-row scan but ~20% of a 1.25M-row one
-    # (8-GPU shard), so only small shards pipeline (measured on one MI355X: 1.25M rows
-    # 149K -> 180K qps with 2 streams, 191K with 3; 10M rows +4.5% with 2). One stream keeps
-    # the N=1 scan-kernel timing free of overlap with the other batch's kernels; with 2 the
-    # per-launch time includes some overlap (0.180 -> 0.188 ms at 1.25M rows).
-    n_streams = args.streams or (1 if (hi - lo) >= 4_000_000 else 2)
+    # than one batch in flight): batch i+1's query prep / seed sampling / scan start run beside
+    # batch i's scan tail and select. Each stream owns its own search workspace
+    # (rag_index_search), so no cross-stream synchronisation is needed; the timed region still
+    # ends with a device-wide synchronize.
+    # Default depth by shard size: a scan launch has a fixed ramp/tail (~30 us) and a batch
+    # ~35 us of latency-bound work around it (query prep, seed sampling, select, exchange) —
+    # 3% of a 10M-row step but ~20% of a 1.25M-row one (8-GPU shard). Measured on one MI355X
+    # (profiles/r01c_streams.txt), qps by batches in flight 1/2/3/4: 1.25M rows 146K / 177K /
+    # 185K / 196K; 2.5M 89K / 99K / - / 103K; 10M 26.5K / 27.9K / - / 27.7K. Small shards keep
+    # 4 in flight; 10M rows (N = 1) keeps 1, so its scan-kernel timing has no overlap.
+    n_streams = args.streams or (1 if (hi - lo) >= 4_000_000 else 4)
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev)
                                                   for _ in range(n_streams - 1)]
     n_step = [0]
@@ -218,12 +218,24 @@ def main():
     elapsed = time.perf_counter() - t0
     idx.profile(False)
     scan_ms, launches = idx.profile_scan_ms()
+    scan_avg_ms = scan_ms / max(launches, 1)
+    # With several batches in flight a scan launch shares HBM with the other batches' scans,
+    # so its duration over the timed region is not the kernel's own rate: time the same
+    # workload once more on ONE stream (after the timed region, not part of `value`).
+    alone_ms = scan_avg_ms
+    if len(streams) > 1:
+        torch.cuda.synchronize()
+        idx.profile(True)
+        for k in range(min(args.steps, 20)):
+            sh.search(qs[args.warmup + k], K_TOP)
+        torch.cuda.synchronize()
+        idx.profile(False)
+        a_ms, a_n = idx.profile_scan_ms()
+        alone_ms = a_ms / max(a_n, 1)
     if world > 1:
-        t = torch.tensor([elapsed, scan_ms / max(launches, 1)], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed, scan_avg_ms, alone_ms], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, scan_avg_ms = float(t[0]), float(t[1])
-    else:
-        scan_avg_ms = scan_ms / max(launches, 1)
+        elapsed, scan_avg_ms, alone_ms = float(t[0]), float(t[1]), float(t[2])
 
     recall5, exact = None, None
     if not args.no_recall:
@@ -278,7 +290,11 @@ def main():
                          "kernel": "scan_kernel<384,false>", "avg_ms": round(scan_avg_ms, 4),
                          "algorithmic_bytes_per_launch": algo_bytes,
                          # whole-step view: the shard's bytes per batch over the step time
-                         "step_frac": round(algo_bytes / (elapsed / args.steps) / HBM_PEAK, 4)},
+                         "step_frac": round(algo_bytes / (elapsed / args.steps) / HBM_PEAK, 4),
+                         # the same launch timed alone (differs from avg_ms only when several
+                         # batches are in flight and their scans overlap)
+                         "standalone_avg_ms": round(alone_ms, 4),
+                         "standalone_frac": round(algo_bytes / (alone_ms * 1e-3) / HBM_PEAK, 4)},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -391,8 +391,10 @@ __device__ __forceinline__ void wait_ring(int y, bool stored) {
   if constexpr (Y > 0) wait_ring<L, S, Y - 1>(y, stored);
 }
 
-// PROBE (diagnostic builds only, rag_bert_gemm variants 3/4): 1 = no MFMAs, 2 = no DMAs
-template <int EPI, bool SPLIT, typename CFG, int PROBE = 0>
+// PROBE (diagnostic builds only, rag_bert_gemm variants 3/4): 1 = no MFMAs, 2 = no DMAs;
+// OPT (schedule experiments, variants 6/7): 1 = s_setprio(1) around each MFMA cluster,
+// 2 = static priority 1 for the younger half of the waves
+template <int EPI, bool SPLIT, typename CFG, int PROBE = 0, int OPT = 0>
 __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
     const _Float16* __restrict__ A, const _Float16* __restrict__ Al,
     const _Float16* __restrict__ W, const _Float16* __restrict__ Wl,
@@ -499,12 +501,16 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
 
 #pragma unroll
   for (int p = 0; p < NS - 1; ++p) issue_next();
+  if constexpr (OPT == 2) {
+    if (wid >= CFG::WAVES_M * CFG::WAVES_N / 2) __builtin_amdgcn_s_setprio(1);
+  }
   int kt_c = 0, it_c = 0, slot_c = 0;
   for (int g = 0; g < steps; ++g) {
     // stages issued after step g: min(NS - 2, steps - 1 - g); plus the last epilogue's
     // stores when it ran at the end of step g-1
     wait_ring<L, S, NS - 2>(min(NS - 2, steps - 1 - g), g > 0 && kt_c == 0);
     __builtin_amdgcn_s_barrier();     // step g landed for all waves; all are past step g-1
+    asm volatile("" ::: "memory");    // no LDS read of step g may be scheduled above it
     issue_next();                     // step g+NS-1 -> slot (g-1) % NS
 
     const half8* sa = lds + slot_c * STAGE_H8;
@@ -513,6 +519,7 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
     for (int ks = 0; ks < (PROBE == 1 ? 0 : BK / 32); ++ks) {
       const int ch = ks * 4 + (lane >> 4);
       half8 af[FM], wf[FN];
+      if constexpr (OPT == 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < FM; ++i) af[i] = sa[swz<CPR>(wr * WTM + i * 16 + (lane & 15), ch)];
 #pragma unroll
@@ -536,6 +543,7 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
 #pragma unroll
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[j], af[i], acc[i][j], 0, 0, 0);
+      if constexpr (OPT == 1) __builtin_amdgcn_s_setprio(0);
     }
     if (++slot_c == NS) slot_c = 0;
 

@@ -1036,6 +1036,7 @@ __global__ __launch_bounds__(64 * kWideWaves, 1) void scan_wide_kernel(
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();   // tile j landed for all; everyone is past tile j-1
+    asm volatile("" ::: "memory");  // no LDS read of tile j may be scheduled above it
     issue(j + 3);                   // slot (j+3)%4 == (j-1)%4
     if (active) {                   // waves of absent groups (B <= 96) only stage and sync
       const half8* tb = ring + (j % kWideBufs) * TILE + lane;

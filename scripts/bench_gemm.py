@@ -19,7 +19,8 @@ sys.path.insert(0, os.path.join(ROOT, "financial-rag-system_amd"))
 from ragmi.encoders import EPI_F16, EPI_F32, EPI_GELU_F16, linear  # noqa: E402
 
 PEAK = 2.5e15
-VNAME = {0: "auto", 1: "tile", 2: "pipe", 3: "probe_no_mfma", 4: "probe_no_dma", 5: "small"}
+VNAME = {0: "auto", 1: "tile", 2: "pipe", 3: "probe_no_mfma", 4: "probe_no_dma", 5: "small",
+         6: "pipe_prio", 7: "pipe_prio_static"}
 LAYER = [("qkv", 1152, 384, EPI_F16), ("o", 384, 384, EPI_F32), ("ffn1", 1536, 384, EPI_GELU_F16),
          ("ffn2", 384, 1536, EPI_F32)]
 
