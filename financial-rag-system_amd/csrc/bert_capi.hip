@@ -175,10 +175,14 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
   const int pipe_tiles = (N / PBN) * ((M + PBM - 1) / PBM);
   // SMALL while its 64x64 tiles fit about two per CU (every query-batch GEMM; the N = 384
   // ones up to ~5K tokens), PIPE once its 256x128 tiles cover the CUs, TILE in between
+  // (WIDE, 256x256, for N % 256 == 0 once it has two tiles per CU: rerank-size FFN1,
+  // measured 0.236 -> 0.217 ms at 117K x 1536 x 384 fp16; below that PIPE is faster)
   const int small_tiles = (N / 64) * ((M + 63) / 64);
+  const int wide_tiles = N % 256 == 0 ? (N / 256) * ((M + 255) / 256) : 0;
   if (variant == RAG_GEMM_AUTO)
     variant = !pipe_ok(M, N, K)                  ? RAG_GEMM_TILE
               : small_tiles <= 2 * cu_count()    ? RAG_GEMM_SMALL
+              : wide_tiles >= 2 * cu_count()     ? RAG_GEMM_WIDE
               : pipe_tiles >= cu_count()         ? RAG_GEMM_PIPE
                                                  : RAG_GEMM_TILE;
   if (variant != RAG_GEMM_TILE && !pipe_ok(M, N, K)) variant = RAG_GEMM_TILE;
@@ -203,7 +207,17 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
     }
     return;
   }
-  if (variant == RAG_GEMM_PIPE) {
+  // (256x192 fp16x3 would split a stage's W rows unevenly over the waves: fp16 only)
+  if (variant == RAG_GEMM_WIDE && (N % 256 == 0 || (N % 192 == 0 && !Al))) {
+    if (N % 256 == 0) {
+      if (Al) launch_pipe<EPI, true, PipeWide256>(A, Al, W, Wl, bias, M, N, K, C, Clo, st, cu_count());
+      else launch_pipe<EPI, false, PipeWide256>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st, cu_count());
+    } else {
+      launch_pipe<EPI, false, PipeWide192>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st, cu_count());
+    }
+    return;
+  }
+  if (variant == RAG_GEMM_PIPE || variant == RAG_GEMM_WIDE) {
     if (Al)
       launch_pipe<EPI, true, PipeLarge>(A, Al, W, Wl, bias, M, N, K, C, Clo, st, cu_count());
     else
@@ -428,7 +442,7 @@ int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, co
     return ragmi::fail(RAG_EINVAL, "pipe/small variants need N % 128 == 0, K % 64 == 0, "
                                    "N <= 4096, M*K*2 and M*N*4 < 2^31");
   const bool probe = variant == RAG_GEMM_PROBE_NO_MFMA || variant == RAG_GEMM_PROBE_NO_DMA;
-  if (variant < RAG_GEMM_AUTO || variant > RAG_GEMM_PIPE_PRIO_STATIC ||
+  if (variant < RAG_GEMM_AUTO || variant > RAG_GEMM_WIDE ||
       (probe && (A_lo || !pipe_ok(M, N, K))))
     return ragmi::fail(RAG_EINVAL, "unknown GEMM variant (probes: fp16 only)");
   auto* a = static_cast<const _Float16*>(A);

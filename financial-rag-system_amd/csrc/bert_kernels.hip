@@ -349,6 +349,10 @@ struct PipeCfg {
 };
 using PipeLarge = PipeCfg<256, 128, 4, 2, 3>;
 template <bool SPLIT> using PipeSmall = PipeCfg<64, 64, 2, 2, SPLIT ? 3 : 4>;
+// wider N tiles: fewer panel bytes per FLOP (256x256: 128 FLOP/B fp16 vs 85 at 256x128) at
+// the price of a 2-stage ring (one stage in flight)
+using PipeWide256 = PipeCfg<256, 256, 4, 2, 2>;
+using PipeWide192 = PipeCfg<256, 192, 4, 2, 2>;
 constexpr int PBM = PipeLarge::BM, PBN = PipeLarge::BN;
 constexpr int kPipeThreads = PipeLarge::THREADS;
 constexpr int kPipeBiasMax = 4096;            // floats of bias staged in LDS (N <= 4096)

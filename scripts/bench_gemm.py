@@ -20,9 +20,14 @@ from ragmi.encoders import EPI_F16, EPI_F32, EPI_GELU_F16, linear  # noqa: E402
 
 PEAK = 2.5e15
 VNAME = {0: "auto", 1: "tile", 2: "pipe", 3: "probe_no_mfma", 4: "probe_no_dma", 5: "small",
-         6: "pipe_prio", 7: "pipe_prio_static"}
-LAYER = [("qkv", 1152, 384, EPI_F16), ("o", 384, 384, EPI_F32), ("ffn1", 1536, 384, EPI_GELU_F16),
-         ("ffn2", 384, 1536, EPI_F32)]
+         6: "pipe_prio", 7: "pipe_prio_static", 8: "wide"}
+LAYERS = {
+    "small": [("qkv", 1152, 384, EPI_F16), ("o", 384, 384, EPI_F32),
+              ("ffn1", 1536, 384, EPI_GELU_F16), ("ffn2", 384, 1536, EPI_F32)],
+    # bge-large-en-v1.5 (config 5 query encoder): hidden 1024, FFN 4096
+    "large": [("qkv", 3072, 1024, EPI_F16), ("o", 1024, 1024, EPI_F32),
+              ("ffn1", 4096, 1024, EPI_GELU_F16), ("ffn2", 1024, 4096, EPI_F32)],
+}
 
 
 def timeit(fn, reps=20):
@@ -49,7 +54,7 @@ def main():
     for M in Ms:
         for prec in ("fp16", "fp16x3"):
             tot = {v: 0.0 for v in variants}
-            for name, N, K, epi in LAYER:
+            for name, N, K, epi in LAYERS[os.environ.get("GEMM_LAYER", "small")]:
                 g = torch.Generator(device="cuda")
                 g.manual_seed(0)
                 a = torch.randn((M, K), generator=g, device="cuda").half()
@@ -72,7 +77,8 @@ def main():
                                       "TFLOPs": round(fl / ms / 1e9, 1),
                                       "mfma_frac": round(pipe_fl / ms / 1e-3 / PEAK, 4)}),
                           flush=True)
-            print(json.dumps({"M": M, "precision": prec, "layer_ms":
+            print(json.dumps({"M": M, "precision": prec,
+                              "layer": os.environ.get("GEMM_LAYER", "small"), "layer_ms":
                               {(VNAME[v]): round(t, 4)
                                for v, t in tot.items()}}), flush=True)
 
