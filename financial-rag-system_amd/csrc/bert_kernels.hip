@@ -376,9 +376,15 @@ __device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t rs, uint32_t voff,
 // raw buffer resource over [base, base + bytes) from wave-uniform inputs (reads past the
 // end return zeros, stores past it are dropped); bytes < 2^31 (checked by the launcher)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t panel(const void* base, int64_t bytes) {
+  // every input made provably wave-uniform (T20): a descriptor the compiler cannot prove
+  // uniform lands in VGPRs (asm "s" operand error / waterfall loops around buffer ops)
+  const uint64_t a = (uint64_t)(uintptr_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
   const int nb = bytes > 0 ? (int)bytes : 0;
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0,
-                                           __builtin_amdgcn_readfirstlane(nb), 0x00020000);
+  void* p = reinterpret_cast<void*>((uintptr_t)(((uint64_t)hi << 32) | lo));
+  return __builtin_amdgcn_make_buffer_rsrc(p, 0, __builtin_amdgcn_readfirstlane(nb),
+                                           0x00020000);
 }
 
 // s_waitcnt vmcnt(Y*L + (stored ? S : 0)) for a runtime Y in [0, Y_MAX] (vmcnt takes an
