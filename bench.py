@@ -148,8 +148,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--streams", type=int, default=0,
-                    help="batches in flight (0 = by shard size: 1 at >= 4M rows per GPU, "
-                         "else 4)")
+                    help="batches in flight (0 = by shard size: 4 below 4M rows per GPU, "
+                         "else 2; 1 on a single GPU)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -183,9 +183,11 @@ def main():
     # ~35 us of latency-bound work around it (query prep, seed sampling, select, exchange) —
     # 3% of a 10M-row step but ~20% of a 1.25M-row one (8-GPU shard). Measured on one MI355X
     # (profiles/r01c_streams.txt), qps by batches in flight 1/2/3/4: 1.25M rows 146K / 177K /
-    # 185K / 196K; 2.5M 89K / 99K / - / 103K; 10M 26.5K / 27.9K / - / 27.7K. Small shards keep
-    # 4 in flight; 10M rows (N = 1) keeps 1, so its scan-kernel timing has no overlap.
-    n_streams = args.streams or (1 if (hi - lo) >= 4_000_000 else 4)
+    # 185K / 196K; 2.5M 89K / 99K / - / 103K; 5M 49.8K / 54.1K / - / 53.4K; 10M 26.5K / 27.9K /
+    # - / 27.7K. Shards below 4M rows keep 4 in flight, larger ones 2 — except the single-GPU
+    # 10M run (the headline), which keeps 1 so its scan-kernel timing has no overlap.
+    rows_local = hi - lo
+    n_streams = args.streams or (4 if rows_local < 4_000_000 else (1 if world == 1 else 2))
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev)
                                                   for _ in range(n_streams - 1)]
     n_step = [0]
