@@ -145,12 +145,23 @@ constexpr int BM = 128, BN = 128;
 // 64 KB) so both modes fit two workgroups per CU.
 template <bool SPLIT> constexpr int kBK = SPLIT ? 32 : 64;
 
-// 16-B chunk swizzle: the 16 rows an MFMA fragment read touches (same logical chunk) land
-// on 16 distinct 4-bank groups for ds_read_b128.
+// 16-B chunk swizzle of a row-major [rows][CPR chunks] LDS image for the MFMA fragment read
+// (lane l: row l & 15 of a 16-row block, chunk c0 + (l >> 4)), conflict-free under the
+// ds_read_b128 lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31}, {32-35,44-47,52-59},
+// {36-43,48-51,60-63} (MI355X_MICROARCH.md §LDS): each group's 16 lanes must cover all 64
+// banks. CPR 8 (128-B rows, bank = 32 (r % 2) + 4 c'): c' = c ^ (r & 7). CPR 4 (64-B rows,
+// bank = 16 (r % 4) + 4 c'): c' = c ^ 3 [r & 8] — a group pairs rows {0-3, 12-15} at chunk c
+// with rows {4-11} at chunk c + 1, so the flip has to separate rows 0-7 from 8-15 (the
+// round-1 flip by row quad, c ^ (r / 4 % 4), left rows 0-3 and 4-7 on the same banks:
+// 2-way conflicts in every fp16x3 fragment read).
+template <int CPR>
+__device__ __forceinline__ int swz_chunk(int row, int chunk) {
+  if constexpr (CPR == 8) return chunk ^ (row & 7);
+  else return chunk ^ (((row >> 3) & 1) * 3);
+}
 template <int CPR>
 __device__ __forceinline__ int swz(int row, int chunk) {
-  if constexpr (CPR == 8) return row * 8 + (chunk ^ (row & 7));
-  else return row * 4 + (chunk ^ ((row >> 2) & 3));
+  return row * CPR + swz_chunk<CPR>(row, chunk);
 }
 
 template <int EPI, bool SPLIT>
@@ -449,13 +460,13 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
 #pragma unroll
   for (int i = 0; i < LA; ++i) {
     const int q = (wid * LA + i) * 64 + lane, r = q / CPR, cs = q % CPR;
-    const int c = (CPR == 8) ? (cs ^ (r & 7)) : (cs ^ ((r >> 2) & 3));
+    const int c = swz_chunk<CPR>(r, cs);
     voA[i] = (uint32_t)(r * K + c * 8) * 2u;
   }
 #pragma unroll
   for (int i = 0; i < LW; ++i) {
     const int q = (wid * LW + i) * 64 + lane, r = q / CPR, cs = q % CPR;
-    const int c = (CPR == 8) ? (cs ^ (r & 7)) : (cs ^ ((r >> 2) & 3));
+    const int c = swz_chunk<CPR>(r, cs);
     voW[i] = (uint32_t)(r * K + c * 8) * 2u;
   }
 
@@ -652,14 +663,16 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
 // holds key 4g+j (j<4) or 16+4g+(j-4) (j>=4) of the block, i.e. exactly the lane's two S^T
 // accumulators — V^T is stored in LDS with its keys permuted the same way.
 // qkv: fp16 [T][3H] (Q | K | V; head h = columns h*HD .. +HD-1 of each); ctx: fp16 [T][H].
-// LDS (dynamic) per plane: K [cap][HD+8] + V^T [HD][cap+8] halves, cap = keys staged at once.
+// LDS (dynamic) per plane: K [cap][HD] (16-B chunks swizzled as the GEMM images, swz_chunk)
+// + V^T [HD][cap+8] halves, cap = keys staged at once. The unpadded K lets two fp16x3
+// workgroups share a CU up to ~300 keys.
 // ----------------------------------------------------------------------------------------
 template <bool SPLIT> constexpr int kAttnThreads = SPLIT ? 1024 : 512;   // 4 / 2 waves per SIMD
 constexpr int kAttnLdsMax = 160 * 1024;
 
 template <int HD>
 __host__ __device__ constexpr int attn_lds_bytes(int cap, int planes) {
-  return planes * (cap * (HD + 8) + HD * (cap + 8)) * 2;
+  return planes * (cap * HD + HD * (cap + 8)) * 2;
 }
 // keys staged per chunk (multiple of 32): all of them if they fit, else the most that fit
 template <int HD>
@@ -688,7 +701,7 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>) void attn_kernel(
     const int* __restrict__ cu, int max_len, int kc, float scale, _Float16* __restrict__ ctx,
     _Float16* __restrict__ ctx_lo) {
   using St = AttnState<HD, SPLIT>;
-  constexpr int NP = St::NP, KS = St::KS, DT = St::DT, KROW = HD + 8;
+  constexpr int NP = St::NP, KS = St::KS, DT = St::DT, KROW = HD, KCPR = HD / 8;
   constexpr int NW = kAttnThreads<SPLIT> / 64;
   extern __shared__ _Float16 alds[];
   // XCD-aware (sequence, head) order: blocks are dealt round-robin over the 8 XCDs, so give
@@ -728,7 +741,7 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>) void attn_kernel(
           kv = *reinterpret_cast<const half8*>(src + H);
           vv = *reinterpret_cast<const half8*>(src + 2 * H);
         }
-        *reinterpret_cast<half8*>(kls[p] + kl * KROW + dc) = kv;
+        *reinterpret_cast<half8*>(kls[p] + kl * KROW + 8 * swz_chunk<KCPR>(kl, dc / 8)) = kv;
         const int pos = (kl & ~31) + vperm(kl & 31);
 #pragma unroll
         for (int e = 0; e < 8; ++e) vts[p][(dc + e) * vrow + pos] = vv[e];
@@ -757,7 +770,8 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>) void attn_kernel(
         sc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
-          const int kr = (kb + 16 * j + ql) * KROW + 32 * ks + 8 * g;
+          const int krow = kb + 16 * j + ql;
+          const int kr = krow * KROW + 8 * swz_chunk<KCPR>(krow, 4 * ks + g);
           const half8 kf = *reinterpret_cast<const half8*>(kls[0] + kr);
           sc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, st.qf[ks][0], sc[j], 0, 0, 0);
           if constexpr (SPLIT) {
