@@ -669,6 +669,9 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
 // ----------------------------------------------------------------------------------------
 template <bool SPLIT> constexpr int kAttnThreads = SPLIT ? 1024 : 512;   // 4 / 2 waves per SIMD
 constexpr int kAttnLdsMax = 160 * 1024;
+// occupancy: head_dim 32 fp16 fits 64 VGPRs (8 waves per SIMD: four 8-wave workgroups per
+// CU, LDS permitting) without spilling; the other instances would spill there
+template <int HD, bool SPLIT> constexpr int kAttnWavesPerEU = (HD == 32 && !SPLIT) ? 8 : 1;
 
 template <int HD>
 __host__ __device__ constexpr int attn_lds_bytes(int cap, int planes) {
@@ -696,7 +699,7 @@ struct AttnState {
 };
 
 template <int H, int HD, bool SPLIT>
-__global__ __launch_bounds__(kAttnThreads<SPLIT>) void attn_kernel(
+__global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) void attn_kernel(
     const _Float16* __restrict__ qkv, const _Float16* __restrict__ qkv_lo,
     const int* __restrict__ cu, int max_len, int kc, float scale, _Float16* __restrict__ ctx,
     _Float16* __restrict__ ctx_lo) {
