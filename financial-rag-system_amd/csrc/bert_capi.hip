@@ -157,13 +157,13 @@ bool pipe_ok(int M, int N, int K) {
          (int64_t)M * K * 2 < (int64_t(1) << 31) && (int64_t)M * N * 4 < (int64_t(1) << 31);
 }
 
-template <int EPI, bool SPLIT, typename CFG, int PROBE = 0, int OPT = 0>
+template <int EPI, bool SPLIT, typename CFG, int PROBE = 0>
 void launch_pipe(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float16* Wl,
                  const float* bias, int M, int N, int K, void* C, _Float16* Clo, hipStream_t st,
                  int max_wg) {
   const int tiles = (N / CFG::BN) * ((M + CFG::BM - 1) / CFG::BM);
   const dim3 grid((unsigned)std::min(max_wg, (tiles + 7) / 8 * 8));   // multiple of 8
-  gemm_pipe_kernel<EPI, SPLIT, CFG, PROBE, OPT><<<grid, dim3(CFG::THREADS), 0, st>>>(
+  gemm_pipe_kernel<EPI, SPLIT, CFG, PROBE><<<grid, dim3(CFG::THREADS), 0, st>>>(
       A, Al, W, Wl, bias, M, N, K, C, Clo);
 }
 
@@ -191,20 +191,14 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
                                           cu_count());
     return;
   }
+  if (variant == RAG_GEMM_PROBE_NO_SYNC) {
+    launch_pipe<EPI, false, PipeLarge, 3>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr,
+                                          st, cu_count());
+    return;
+  }
   if (variant == RAG_GEMM_PROBE_NO_DMA) {
     launch_pipe<EPI, false, PipeLarge, 2>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st,
                                           cu_count());
-    return;
-  }
-  if (variant == RAG_GEMM_PIPE_PRIO || variant == RAG_GEMM_PIPE_PRIO_STATIC) {
-    // schedule experiments of the PIPE kernel (diagnostic variants)
-    if (variant == RAG_GEMM_PIPE_PRIO) {
-      if (Al) launch_pipe<EPI, true, PipeLarge, 0, 1>(A, Al, W, Wl, bias, M, N, K, C, Clo, st, cu_count());
-      else launch_pipe<EPI, false, PipeLarge, 0, 1>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st, cu_count());
-    } else {
-      if (Al) launch_pipe<EPI, true, PipeLarge, 0, 2>(A, Al, W, Wl, bias, M, N, K, C, Clo, st, cu_count());
-      else launch_pipe<EPI, false, PipeLarge, 0, 2>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st, cu_count());
-    }
     return;
   }
   // (256x192 fp16x3 would split a stage's W rows unevenly over the waves: fp16 only)
@@ -438,12 +432,16 @@ int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, co
     return ragmi::fail(RAG_EINVAL, "A_lo and W_lo: both (fp16x3) or neither (fp16)");
   if (A_lo && epilogue != kEpiF32 && !C_lo)
     return ragmi::fail(RAG_EINVAL, "fp16x3 fp16-output GEMM needs C_lo");
-  if ((variant == RAG_GEMM_PIPE || variant == RAG_GEMM_SMALL) && !pipe_ok(M, N, K))
-    return ragmi::fail(RAG_EINVAL, "pipe/small variants need N % 128 == 0, K % 64 == 0, "
+  if ((variant == RAG_GEMM_PIPE || variant == RAG_GEMM_SMALL || variant == RAG_GEMM_WIDE) &&
+      !pipe_ok(M, N, K))
+    return ragmi::fail(RAG_EINVAL, "pipe/small/wide variants need N % 128 == 0, K % 64 == 0, "
                                    "N <= 4096, M*K*2 and M*N*4 < 2^31");
-  const bool probe = variant == RAG_GEMM_PROBE_NO_MFMA || variant == RAG_GEMM_PROBE_NO_DMA;
-  if (variant < RAG_GEMM_AUTO || variant > RAG_GEMM_WIDE ||
-      (probe && (A_lo || !pipe_ok(M, N, K))))
+  const bool probe = variant == RAG_GEMM_PROBE_NO_MFMA || variant == RAG_GEMM_PROBE_NO_DMA ||
+                     variant == RAG_GEMM_PROBE_NO_SYNC;
+  const bool known = variant == RAG_GEMM_AUTO || variant == RAG_GEMM_TILE ||
+                     variant == RAG_GEMM_PIPE || variant == RAG_GEMM_SMALL ||
+                     variant == RAG_GEMM_WIDE || probe;
+  if (!known || (probe && (A_lo || !pipe_ok(M, N, K))))
     return ragmi::fail(RAG_EINVAL, "unknown GEMM variant (probes: fp16 only)");
   auto* a = static_cast<const _Float16*>(A);
   auto* al = static_cast<const _Float16*>(A_lo);

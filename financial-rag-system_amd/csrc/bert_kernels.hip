@@ -412,10 +412,10 @@ __device__ __forceinline__ void wait_ring(int y, bool stored) {
   if constexpr (Y > 0) wait_ring<L, S, Y - 1>(y, stored);
 }
 
-// PROBE (diagnostic builds only, rag_bert_gemm variants 3/4): 1 = no MFMAs, 2 = no DMAs;
-// OPT (schedule experiments, variants 6/7): 1 = s_setprio(1) around each MFMA cluster,
-// 2 = static priority 1 for the younger half of the waves
-template <int EPI, bool SPLIT, typename CFG, int PROBE = 0, int OPT = 0>
+// PROBE (diagnostic builds only, rag_bert_gemm variants 3/4/9): timing probes of the same
+// kernel with parts removed — 1 = no MFMAs, 2 = no DMAs, 3 = no DMAs and no barriers.
+// (s_setprio around the MFMA clusters / for the younger waves measured +1-2%: not kept.)
+template <int EPI, bool SPLIT, typename CFG, int PROBE = 0>
 __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
     const _Float16* __restrict__ A, const _Float16* __restrict__ Al,
     const _Float16* __restrict__ W, const _Float16* __restrict__ Wl,
@@ -479,7 +479,7 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
   __amdgpu_buffer_rsrc_t rA0 = panel(A, 0), rA1 = rA0, rW0 = rA0, rW1 = rA0;
   auto issue_next = [&]() {
     if (it_i >= n_mine) return;
-    if constexpr (PROBE == 2) {
+    if constexpr (PROBE >= 2) {
       if (++kt_i == nk) { kt_i = 0; ++it_i; }
       return;
     }
@@ -522,25 +522,56 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
 
 #pragma unroll
   for (int p = 0; p < NS - 1; ++p) issue_next();
-  if constexpr (OPT == 2) {
-    if (wid >= CFG::WAVES_M * CFG::WAVES_N / 2) __builtin_amdgcn_s_setprio(1);
-  }
   int kt_c = 0, it_c = 0, slot_c = 0;
   for (int g = 0; g < steps; ++g) {
     // stages issued after step g: min(NS - 2, steps - 1 - g); plus the last epilogue's
     // stores when it ran at the end of step g-1
-    wait_ring<L, S, NS - 2>(min(NS - 2, steps - 1 - g), g > 0 && kt_c == 0);
-    __builtin_amdgcn_s_barrier();     // step g landed for all waves; all are past step g-1
+    if constexpr (PROBE < 3) {
+      wait_ring<L, S, NS - 2>(min(NS - 2, steps - 1 - g), g > 0 && kt_c == 0);
+      __builtin_amdgcn_s_barrier();   // step g landed for all waves; all are past step g-1
+    }
     asm volatile("" ::: "memory");    // no LDS read of step g may be scheduled above it
     issue_next();                     // step g+NS-1 -> slot (g-1) % NS
 
     const half8* sa = lds + slot_c * STAGE_H8;
     const half8* sw = sa + NPL * A_H8;
+    if constexpr (PROBE != 1 && CFG::BM >= 256) {
+      // every fragment of the K step issued back to back, then the MFMAs (left alone, the
+      // compiler loads each fragment just before its first use and waits every few MFMAs;
+      // this order measured ~3% faster on the 256-row tiles)
+      constexpr int KSN = BK / 32;
+      half8 af[KSN][NPL][FM], wf[KSN][NPL][FN];
 #pragma unroll
-    for (int ks = 0; ks < (PROBE == 1 ? 0 : BK / 32); ++ks) {
+      for (int ks = 0; ks < KSN; ++ks) {
+        const int ch = ks * 4 + (lane >> 4);
+#pragma unroll
+        for (int p = 0; p < NPL; ++p) {
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+            af[ks][p][i] = sa[p * A_H8 + swz<CPR>(wr * WTM + i * 16 + (lane & 15), ch)];
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            wf[ks][p][j] = sw[p * W_H8 + swz<CPR>(wc * WTN + j * 16 + (lane & 15), ch)];
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ks = 0; ks < KSN; ++ks)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            if constexpr (SPLIT) {   // small terms first: W_lo A_hi + W_hi A_lo + W_hi A_hi
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[ks][1][j], af[ks][0][i], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[ks][0][j], af[ks][1][i], acc[i][j], 0, 0, 0);
+            }
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[ks][0][j], af[ks][0][i], acc[i][j], 0, 0, 0);
+          }
+    }
+#pragma unroll
+    for (int ks = 0; ks < (PROBE == 1 || CFG::BM >= 256 ? 0 : BK / 32); ++ks) {
       const int ch = ks * 4 + (lane >> 4);
       half8 af[FM], wf[FN];
-      if constexpr (OPT == 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < FM; ++i) af[i] = sa[swz<CPR>(wr * WTM + i * 16 + (lane & 15), ch)];
 #pragma unroll
@@ -564,7 +595,6 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
 #pragma unroll
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[j], af[i], acc[i][j], 0, 0, 0);
-      if constexpr (OPT == 1) __builtin_amdgcn_s_setprio(0);
     }
     if (++slot_c == NS) slot_c = 0;
 

@@ -74,15 +74,14 @@ int rag_encoder_forward_host(rag_encoder_t* enc, const int32_t* ids, const int32
  * BertSelfAttention/BertIntermediate/BertOutput), device pointers, async on `stream`.
  * A, W fp16 row-major; A_lo/W_lo the fp16x3 residual planes (both NULL = plain fp16).
  * epilogue: RAG_EPI_F16 (C fp16 [+ C_lo]), RAG_EPI_GELU_F16 (erf-GELU, fp16 [+ C_lo]),
- * RAG_EPI_F32 (C fp32). variant: RAG_GEMM_AUTO (what the forward uses), _TILE, _PIPE, _SMALL;
- * _PIPE_PRIO[_STATIC] are s_setprio schedule experiments of _PIPE; _WIDE is _PIPE at 256x256
- * (N % 256 == 0) or 256x192 (N % 192 == 0) tiles;
- * _PROBE_* are timing probes of the PIPE kernel with its MFMAs / its loads removed (fp16,
- * results meaningless). N % 128 == 0, K % 64 == 0 (PIPE/SMALL also N <= 4096). */
+ * RAG_EPI_F32 (C fp32). variant: RAG_GEMM_AUTO (what the forward uses), _TILE, _PIPE, _SMALL,
+ * _WIDE (_PIPE at 256x256 (N % 256 == 0) or 256x192 (N % 192 == 0, fp16) tiles);
+ * _PROBE_* are timing probes of the PIPE kernel with its MFMAs / its loads / its loads and
+ * barriers removed (fp16, results meaningless). N % 128 == 0, K % 64 == 0 (PIPE/SMALL also N <= 4096). */
 enum { RAG_EPI_F16 = 0, RAG_EPI_GELU_F16 = 1, RAG_EPI_F32 = 2 };
 enum { RAG_GEMM_AUTO = 0, RAG_GEMM_TILE = 1, RAG_GEMM_PIPE = 2, RAG_GEMM_PROBE_NO_MFMA = 3,
-       RAG_GEMM_PROBE_NO_DMA = 4, RAG_GEMM_SMALL = 5, RAG_GEMM_PIPE_PRIO = 6,
-       RAG_GEMM_PIPE_PRIO_STATIC = 7, RAG_GEMM_WIDE = 8 };
+       RAG_GEMM_PROBE_NO_DMA = 4, RAG_GEMM_SMALL = 5, RAG_GEMM_WIDE = 8,
+       RAG_GEMM_PROBE_NO_SYNC = 9 };
 int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, const void* W,
                   const void* W_lo, const float* bias, int M, int N, int K, void* C,
                   void* C_lo, void* stream);

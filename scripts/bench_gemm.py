@@ -20,7 +20,7 @@ from ragmi.encoders import EPI_F16, EPI_F32, EPI_GELU_F16, linear  # noqa: E402
 
 PEAK = 2.5e15
 VNAME = {0: "auto", 1: "tile", 2: "pipe", 3: "probe_no_mfma", 4: "probe_no_dma", 5: "small",
-         6: "pipe_prio", 7: "pipe_prio_static", 8: "wide"}
+         8: "wide", 9: "probe_no_sync"}
 LAYERS = {
     "small": [("qkv", 1152, 384, EPI_F16), ("o", 384, 384, EPI_F32),
               ("ffn1", 1536, 384, EPI_GELU_F16), ("ffn2", 384, 1536, EPI_F32)],
@@ -65,7 +65,7 @@ def main():
                 wl = (torch.randn((N, K), generator=g, device="cuda") * 1e-5).half() \
                     if prec == "fp16x3" else None
                 for v in variants:
-                    if v in (3, 4) and prec == "fp16x3":
+                    if v in (3, 4, 9) and prec == "fp16x3":
                         continue              # probes are fp16-only
                     ms = timeit(lambda: linear(a, w, bias, epi, al, wl, v))
                     fl = 2.0 * M * N * K
