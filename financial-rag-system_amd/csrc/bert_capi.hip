@@ -48,6 +48,11 @@ struct rag_encoder {
   float *x = nullptr, *y = nullptr;
   _Float16 *xh = nullptr, *qkv = nullptr, *ctx = nullptr, *ff = nullptr;
   _Float16 *xl = nullptr, *qkv_l = nullptr, *ctx_l = nullptr, *ff_l = nullptr;  // fp16x3
+  // last layer on the CLS rows only (B rows; see gather_cls_kernel)
+  int64_t cap_b = 0;
+  float *xc = nullptr, *yc = nullptr;
+  _Float16 *xch = nullptr, *xcl = nullptr, *cc = nullptr, *ccl = nullptr, *ffc = nullptr,
+           *ffcl = nullptr;
   // host-entry staging
   void* stage = nullptr;
   size_t stage_bytes = 0;
@@ -167,6 +172,29 @@ void launch_pipe(const _Float16* A, const _Float16* Al, const _Float16* W, const
       A, Al, W, Wl, bias, M, N, K, C, Clo);
 }
 
+int ensure_cls(rag_encoder* e, int64_t B) {
+  if (B <= e->cap_b) return RAG_OK;
+  for (void* p : {(void*)e->xc, (void*)e->yc, (void*)e->xch, (void*)e->xcl, (void*)e->cc,
+                  (void*)e->ccl, (void*)e->ffc, (void*)e->ffcl})
+    if (p) (void)hipFree(p);
+  e->xc = e->yc = nullptr;
+  e->xch = e->xcl = e->cc = e->ccl = e->ffc = e->ffcl = nullptr;
+  e->cap_b = 0;
+  const int64_t cap = std::max<int64_t>(B, 256), H = e->cfg.hidden, FF = e->cfg.intermediate;
+  RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->xc), cap * H * 4));
+  RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->yc), cap * H * 4));
+  RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->xch), cap * H * 2));
+  RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->cc), cap * H * 2));
+  RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->ffc), cap * FF * 2));
+  if (e->cfg.precision == RAG_PREC_FP16X3) {
+    RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->xcl), cap * H * 2));
+    RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->ccl), cap * H * 2));
+    RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->ffcl), cap * FF * 2));
+  }
+  e->cap_b = cap;
+  return RAG_OK;
+}
+
 template <int EPI>
 void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float16* Wl,
           const float* bias, int M, int N, int K, void* C, _Float16* Clo, hipStream_t st,
@@ -245,37 +273,63 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
   const int NH = H / HD, FF = c.intermediate;
   int rc = ensure_ws(e, T);
   if (rc) return rc;
+  rc = ensure_cls(e, B);
+  if (rc) return rc;
   embed_ln_kernel<H><<<dim3((max_len + 3) / 4, B), dim3(256), 0, st>>>(
       ids, types, cu, e->wemb, e->pemb, e->temb, e->eg, e->eb, c.layer_norm_eps, c.vocab,
       c.type_vocab, c.max_position, e->x, e->xh, e->xl);
   const float scale = 1.0f / sqrtf((float)HD);
-  const unsigned ln_grid = (unsigned)((T + 3) / 4);
   // 1-D grid of (sequence, head) pairs, padded to a multiple of 8 (XCD-aware order in the
   // kernel; gridDim.x / NH = B after the padding is removed there)
   const dim3 agrid((unsigned)((NH * B + 7) / 8 * 8));
   const int planes = e->xl ? 2 : 1;
   const int kc = attn_chunk_keys<HD>(max_len, planes);
   const size_t alds = (size_t)attn_lds_bytes<HD>(kc, planes);
-  for (const Layer& L : e->layers) {
+  const int nl = (int)e->layers.size();
+  for (int l = 0; l < nl; ++l) {
+    const Layer& L = e->layers[l];
+    const bool last = l == nl - 1;                  // CLS rows only after the attention
     gemm<kEpiF16>(e->xh, e->xl, L.wqkv, L.wqkv_l, L.bqkv, T, 3 * H, H, e->qkv, e->qkv_l, st);
+    const int max_qb = last ? 1 : 1 << 20;
     if (e->xl)
       attn_kernel<H, HD, true><<<agrid, dim3(kAttnThreads<true>), alds, st>>>(
-          e->qkv, e->qkv_l, cu, max_len, kc, scale, e->ctx, e->ctx_l);
+          e->qkv, e->qkv_l, cu, max_len, kc, scale, e->ctx, e->ctx_l, max_qb);
     else
       attn_kernel<H, HD, false><<<agrid, dim3(kAttnThreads<false>), alds, st>>>(
-          e->qkv, nullptr, cu, max_len, kc, scale, e->ctx, nullptr);
-    gemm<kEpiF32>(e->ctx, e->ctx_l, L.wo, L.wo_l, L.bo, T, H, H, e->y, nullptr, st);
-    add_ln_kernel<H><<<dim3(ln_grid), dim3(256), 0, st>>>(e->x, e->y, L.g1, L.be1,
-                                                       c.layer_norm_eps, e->xh, e->xl, T);
-    gemm<kEpiGeluF16>(e->xh, e->xl, L.w1, L.w1_l, L.bi1, T, FF, H, e->ff, e->ff_l, st);
-    gemm<kEpiF32>(e->ff, e->ff_l, L.w2, L.w2_l, L.bi2, T, H, FF, e->y, nullptr, st);
-    add_ln_kernel<H><<<dim3(ln_grid), dim3(256), 0, st>>>(e->x, e->y, L.g2, L.be2,
-                                                       c.layer_norm_eps, e->xh, e->xl, T);
+          e->qkv, nullptr, cu, max_len, kc, scale, e->ctx, nullptr, max_qb);
+    // rows the rest of the layer runs on: all T tokens, or the B gathered CLS rows
+    int R = T;
+    float *x = e->x, *y = e->y;
+    _Float16 *xh = e->xh, *xl = e->xl, *ctx = e->ctx, *ctxl = e->ctx_l, *ff = e->ff,
+             *ffl = e->ff_l;
+    if (last) {
+      gather_cls_kernel<H><<<dim3(B), dim3(64), 0, st>>>(e->x, e->ctx, e->ctx_l, cu, e->xc,
+                                                        e->cc, e->xl ? e->ccl : nullptr);
+      R = B;
+      x = e->xc;
+      y = e->yc;
+      xh = e->xch;
+      xl = e->xl ? e->xcl : nullptr;
+      ctx = e->cc;
+      ctxl = e->xl ? e->ccl : nullptr;
+      ff = e->ffc;
+      ffl = e->xl ? e->ffcl : nullptr;
+    }
+    const unsigned lg = (unsigned)((R + 3) / 4);
+    gemm<kEpiF32>(ctx, ctxl, L.wo, L.wo_l, L.bo, R, H, H, y, nullptr, st);
+    add_ln_kernel<H><<<dim3(lg), dim3(256), 0, st>>>(x, y, L.g1, L.be1, c.layer_norm_eps, xh,
+                                                    xl, R);
+    gemm<kEpiGeluF16>(xh, xl, L.w1, L.w1_l, L.bi1, R, FF, H, ff, ffl, st);
+    gemm<kEpiF32>(ff, ffl, L.w2, L.w2_l, L.bi2, R, H, FF, y, nullptr, st);
+    add_ln_kernel<H><<<dim3(lg), dim3(256), 0, st>>>(x, y, L.g2, L.be2, c.layer_norm_eps, xh,
+                                                    xl, R);
   }
+  // the final hidden states of the CLS tokens are rows 0 .. B-1 of e->xc (cu = null)
   if (c.head == RAG_HEAD_CLS_L2)
-    cls_normalize_kernel<H><<<dim3(B), dim3(64), 0, st>>>(e->x, cu, out);
+    cls_normalize_kernel<H><<<dim3(B), dim3(64), 0, st>>>(e->xc, nullptr, out);
   else
-    ce_head_kernel<H><<<dim3(B), dim3(256), 0, st>>>(e->x, cu, e->wp, e->bp, e->wc, e->bc, out);
+    ce_head_kernel<H><<<dim3(B), dim3(256), 0, st>>>(e->xc, nullptr, e->wp, e->bp, e->wc, e->bc,
+                                                     out);
   RAG_HIP(hipGetLastError());
   return RAG_OK;
 }
@@ -404,7 +458,8 @@ int rag_encoder_destroy(rag_encoder_t* e) {
   for (void* p : e->allocs) (void)hipFree(p);
   for (void* p : {(void*)e->x, (void*)e->y, (void*)e->xh, (void*)e->qkv, (void*)e->ctx,
                   (void*)e->ff, (void*)e->xl, (void*)e->qkv_l, (void*)e->ctx_l, (void*)e->ff_l,
-                  e->stage})
+                  e->stage, (void*)e->xc, (void*)e->yc, (void*)e->xch, (void*)e->xcl,
+                  (void*)e->cc, (void*)e->ccl, (void*)e->ffc, (void*)e->ffcl})
     if (p) (void)hipFree(p);
   delete e;
   return RAG_OK;

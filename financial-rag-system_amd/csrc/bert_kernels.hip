@@ -732,7 +732,7 @@ template <int H, int HD, bool SPLIT>
 __global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) void attn_kernel(
     const _Float16* __restrict__ qkv, const _Float16* __restrict__ qkv_lo,
     const int* __restrict__ cu, int max_len, int kc, float scale, _Float16* __restrict__ ctx,
-    _Float16* __restrict__ ctx_lo) {
+    _Float16* __restrict__ ctx_lo, int max_qb) {
   using St = AttnState<HD, SPLIT>;
   constexpr int NP = St::NP, KS = St::KS, DT = St::DT, KROW = HD, KCPR = HD / 8;
   constexpr int NW = kAttnThreads<SPLIT> / 64;
@@ -895,7 +895,7 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) 
     }
   };
 
-  const int nqb = (len + 15) >> 4;
+  const int nqb = min((len + 15) >> 4, max_qb);     // max_qb = 1: the CLS query block only
   if (nch == 1) {
     stage(0, sp);
     __syncthreads();
@@ -925,6 +925,31 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) 
 }
 
 // ----------------------------------------------------------------------------------------
+// last layer, CLS rows only: both heads read only the CLS token's final hidden state
+// (sentence-transformers Pooling(cls); BertPooler takes hidden_states[:, 0]), and a token's
+// row after the last attention depends on the other tokens only through that attention. So
+// the last layer computes Q|K|V for every token (K, V are needed), attention for the first
+// query block of each sequence, and everything after it — O-proj, residual + LN, FFN,
+// residual + LN — on the B gathered CLS rows instead of all T tokens.
+// gather: x_cls[b] = x[cu[b]], ctx_cls[b] = ctx[cu[b]] (+ lo plane); one wave per sequence
+// ----------------------------------------------------------------------------------------
+template <int H>
+__global__ __launch_bounds__(64) void gather_cls_kernel(
+    const float* __restrict__ x, const _Float16* __restrict__ ctx,
+    const _Float16* __restrict__ ctx_lo, const int* __restrict__ cu, float* __restrict__ x_cls,
+    _Float16* __restrict__ ctx_cls, _Float16* __restrict__ ctx_cls_lo) {
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const int64_t r = cu[b];
+#pragma unroll
+  for (int j = 0; j < H / 64; ++j) {
+    const int c = lane + 64 * j;
+    x_cls[(int64_t)b * H + c] = x[r * H + c];
+    ctx_cls[(int64_t)b * H + c] = ctx[r * H + c];
+    if (ctx_lo) ctx_cls_lo[(int64_t)b * H + c] = ctx_lo[r * H + c];
+  }
+}
+
+// ----------------------------------------------------------------------------------------
 // heads
 // ----------------------------------------------------------------------------------------
 // bge (sentence-transformers Pooling(cls) + Normalize): out[b] = x[cls] / max(||x[cls]||, 1e-12)
@@ -933,7 +958,7 @@ __global__ __launch_bounds__(64) void cls_normalize_kernel(const float* __restri
                                                            const int* __restrict__ cu,
                                                            float* __restrict__ out) {
   const int b = blockIdx.x, lane = threadIdx.x;
-  const float* r = x + (int64_t)cu[b] * H;
+  const float* r = x + (cu ? (int64_t)cu[b] : (int64_t)b) * H;   // cu null: x holds CLS rows
   float v[H / 64];
   float s = 0.f;
 #pragma unroll
@@ -960,7 +985,8 @@ __global__ __launch_bounds__(256) void ce_head_kernel(const float* __restrict__ 
   __shared__ float cls[H];
   __shared__ float part[4];
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  for (int c = tid; c < H; c += 256) cls[c] = x[(int64_t)cu[b] * H + c];
+  const int64_t row = cu ? (int64_t)cu[b] : (int64_t)b;   // cu null: x holds CLS rows
+  for (int c = tid; c < H; c += 256) cls[c] = x[row * H + c];
   __syncthreads();
   float acc = 0.f;
   for (int o = tid; o < H; o += 256) {
