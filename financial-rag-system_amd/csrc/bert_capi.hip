@@ -514,6 +514,24 @@ int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, co
   return RAG_OK;
 }
 
+int rag_build_pairs(const int32_t* q_ids, const int32_t* q_cu, int B, const int64_t* rows, int K,
+                    const int16_t* c_toks, int lmax, const int32_t* c_lens, int max_len,
+                    int32_t* ids, int32_t* types, int32_t* cu, int32_t* stats, void* stream) {
+  ragmi::clear_error();
+  if (!q_ids || !q_cu || !rows || !c_toks || !c_lens || !ids || !types || !cu || !stats)
+    return ragmi::fail(RAG_EINVAL, "NULL argument");
+  if (B < 1 || K < 1 || B * K > kPairsMax || lmax < 1 || max_len < 3 || max_len > 4096)
+    return ragmi::fail(RAG_EINVAL, "need 1 <= B*K <= 1024, lmax >= 1, 3 <= max_len <= 4096");
+  auto st = static_cast<hipStream_t>(stream);
+  const int P = B * K;
+  pairs_len_kernel<<<dim3(1), dim3(kPairsMax), 0, st>>>(q_cu, rows, c_lens, P, K, max_len, cu,
+                                                         stats);
+  pairs_fill_kernel<<<dim3(P), dim3(256), 0, st>>>(q_ids, q_cu, rows, c_toks, lmax, c_lens, cu,
+                                                   K, max_len, ids, types);
+  RAG_HIP(hipGetLastError());
+  return RAG_OK;
+}
+
 int rag_encoder_forward_host(rag_encoder_t* e, const int32_t* ids, const int32_t* types,
                              const int32_t* cu, int B, int T, float* out) {
   ragmi::clear_error();

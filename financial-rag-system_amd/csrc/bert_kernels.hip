@@ -950,6 +950,85 @@ __global__ __launch_bounds__(64) void gather_cls_kernel(
 }
 
 // ----------------------------------------------------------------------------------------
+// cross-encoder batch assembly from cached chunk tokens (rag_build_pairs; the torch
+// restatement ragmi.pairs.build_pairs is its CPU-tested twin): pair p = b K + k is
+//   [CLS] q_b [SEP] c_{rows[b][k]} [SEP], token types 0 .. 0 1 .. 1,
+// the chunk cut so the pair fits max_len (longest_first truncation removes chunk tokens for
+// the reference's short queries). pairs_len_kernel: one workgroup, pair lengths -> cu (block
+// scan) + stats {T, longest}; pairs_fill_kernel: one workgroup per pair writes its tokens.
+// ----------------------------------------------------------------------------------------
+constexpr int kPairsMax = 1024;   // B * K per call
+
+__device__ __forceinline__ void pair_parts(const int* __restrict__ q_cu, const int64_t* rows,
+                                           const int* __restrict__ c_lens, int K, int p,
+                                           int max_len, int& ql, int& cl, int64_t& r) {
+  const int b = p / K;
+  ql = q_cu[b + 1] - q_cu[b] - 2;                 // query tokens without its [CLS] / [SEP]
+  r = rows[p] < 0 ? 0 : rows[p];                  // -1 (no hit): row 0, caller masks
+  cl = min(c_lens[r], max_len - 3 - ql);
+}
+
+__global__ __launch_bounds__(kPairsMax) void pairs_len_kernel(
+    const int* __restrict__ q_cu, const int64_t* __restrict__ rows,
+    const int* __restrict__ c_lens, int P, int K, int max_len, int* __restrict__ cu,
+    int* __restrict__ stats) {
+  __shared__ int wsum[kPairsMax / 64];
+  __shared__ int wmax[kPairsMax / 64];
+  const int p = threadIdx.x, lane = p & 63, w = p >> 6;
+  int len = 0;
+  if (p < P) {
+    int ql, cl;
+    int64_t r;
+    pair_parts(q_cu, rows, c_lens, K, p, max_len, ql, cl, r);
+    len = ql + cl + 3;
+  }
+  // inclusive wave scan, then across waves
+  int incl = len, mx = len;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int v = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += v;
+  }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) mx = max(mx, __shfl_xor(mx, d, 64));
+  if (lane == 63) wsum[w] = incl;
+  if (lane == 0) wmax[w] = mx;
+  __syncthreads();
+  int base = 0, gmax = 0;
+  for (int i = 0; i < kPairsMax / 64; ++i) {
+    if (i < w) base += wsum[i];
+    gmax = max(gmax, wmax[i]);
+  }
+  if (p < P) cu[p + 1] = base + incl;
+  if (p == 0) cu[0] = 0;
+  if (p == P - 1) {
+    stats[0] = base + incl;                       // T
+    stats[1] = gmax;                              // longest pair
+  }
+}
+
+__global__ __launch_bounds__(256) void pairs_fill_kernel(
+    const int* __restrict__ q_ids, const int* __restrict__ q_cu,
+    const int64_t* __restrict__ rows, const int16_t* __restrict__ c_toks, int lmax,
+    const int* __restrict__ c_lens, const int* __restrict__ cu, int K, int max_len,
+    int* __restrict__ ids, int* __restrict__ types) {
+  const int p = blockIdx.x;
+  int ql, cl;
+  int64_t r;
+  pair_parts(q_cu, rows, c_lens, K, p, max_len, ql, cl, r);
+  const int n = ql + cl + 3, o = cu[p], qs = q_cu[p / K] + 1;
+  for (int t = threadIdx.x; t < n; t += 256) {
+    int id;
+    if (t == 0) id = 101;                                        // [CLS]
+    else if (t <= ql) id = q_ids[qs + t - 1];
+    else if (t == ql + 1 || t == n - 1) id = 102;                // [SEP]
+    else id = (int)(uint16_t)c_toks[r * lmax + (t - ql - 2)];
+    ids[o + t] = id;
+    types[o + t] = t > ql + 1 ? 1 : 0;
+  }
+}
+
+// ----------------------------------------------------------------------------------------
 // heads
 // ----------------------------------------------------------------------------------------
 // bge (sentence-transformers Pooling(cls) + Normalize): out[b] = x[cls] / max(||x[cls]||, 1e-12)

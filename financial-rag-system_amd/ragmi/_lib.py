@@ -93,6 +93,9 @@ BERT_API = {
                                            ctypes.c_int, c_vp, c_vp]),
     "rag_encoder_forward_host": (ctypes.c_int, [c_vp, c_i32p_, c_i32p_, c_i32p_, ctypes.c_int,
                                                 ctypes.c_int, c_f32p]),
+    "rag_build_pairs": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, c_vp, ctypes.c_int, c_vp,
+                                       ctypes.c_int, c_vp, ctypes.c_int, c_vp, c_vp, c_vp, c_vp,
+                                       c_vp]),
     "rag_bert_gemm": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
                                      ctypes.c_int, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_vp]),
 }

@@ -10,8 +10,13 @@ query, the packed cross-encoder input for all (query, chunk) pairs is built on t
 with the chunk truncated so a pair fits max_len (`longest_first` truncation removes tokens from
 the longer side — the chunk, for the reference's short queries; main.py:241-247 via
 CrossEncoder.predict). Output: packed ids / types (int32 [T]), cu_seqlens (int32 [P+1]) and the
-longest pair, ready for BertEncoder.forward_device. Pure torch ops (works on CPU tensors too,
-which is how tests/test_pairs_cpu.py checks it against a per-pair loop).
+longest pair, ready for BertEncoder.forward_device.
+
+build_pairs_gpu: the production form — two HIP kernels (rag_build_pairs: lengths + scan,
+then one workgroup per pair) and one 8-byte read-back of {T, longest} (the forward's launch
+grids need T on the host). build_pairs: the same assembly in pure torch ops (works on CPU
+tensors too, which is how tests/test_pairs_cpu.py checks it against a per-pair loop; the GPU
+test checks build_pairs_gpu against it bit for bit).
 """
 from __future__ import annotations
 
@@ -50,3 +55,27 @@ def build_pairs(q_ids, q_cu, rows, c_toks, c_lens, max_len: int = 512):
     types = (off > qlp + 1).to(torch.int32)
     return ids.to(torch.int32).contiguous(), types.contiguous(), cu.to(torch.int32), \
         int(plen.max())
+
+
+def build_pairs_gpu(q_ids, q_cu, rows, c_toks, c_lens, max_len: int = 512):
+    """Same contract as build_pairs for cuda tensors (c_toks int16, c_lens int32), through the
+    rag_build_pairs kernels."""
+    from . import _lib
+    dev = rows.device
+    Bq, Kq = rows.shape
+    for t, dt in ((q_ids, torch.int32), (q_cu, torch.int32), (c_toks, torch.int16),
+                  (c_lens, torch.int32), (rows, torch.int64)):
+        if t.dtype != dt or not t.is_cuda or not t.is_contiguous():
+            raise ValueError("q_ids/q_cu int32, rows int64, c_toks int16, c_lens int32: "
+                             "contiguous cuda tensors")
+    P = Bq * Kq
+    ids = torch.empty(P * max_len, dtype=torch.int32, device=dev)
+    types = torch.empty_like(ids)
+    cu = torch.empty(P + 1, dtype=torch.int32, device=dev)
+    stats = torch.empty(2, dtype=torch.int32, device=dev)
+    _lib.check(_lib.load().rag_build_pairs(
+        q_ids.data_ptr(), q_cu.data_ptr(), Bq, rows.data_ptr(), Kq, c_toks.data_ptr(),
+        c_toks.shape[1], c_lens.data_ptr(), max_len, ids.data_ptr(), types.data_ptr(),
+        cu.data_ptr(), stats.data_ptr(), torch.cuda.current_stream(dev).cuda_stream))
+    T, longest = (int(v) for v in stats.cpu())          # one host sync per batch
+    return ids[:T], types[:T], cu, longest

@@ -69,6 +69,18 @@ int rag_encoder_forward(rag_encoder_t* enc, const int32_t* ids_dev, const int32_
 int rag_encoder_forward_host(rag_encoder_t* enc, const int32_t* ids, const int32_t* types,
                              const int32_t* cu_seqlens, int B, int T, float* out);
 
+/* Cross-encoder batch assembly on the device (the batched rerank stage without a host round
+ * trip: main.py:241-247 CrossEncoder.predict([[q, t] ...]) pair encoding
+ * "[CLS] q [SEP] t [SEP]", token types 0/1, chunk truncated to fit max_len). Device pointers,
+ * async on `stream`. q_ids/q_cu: the packed query batch (each query [CLS] ... [SEP]);
+ * rows int64 [B][K]: search hits (-1 = none: row 0 is used, the caller masks); c_toks int16
+ * [rows][lmax] cached chunk WordPiece ids (read as uint16), c_lens int32 [rows].
+ * Outputs: ids/types int32 [<= B*K*max_len], cu int32 [B*K+1], stats int32 [2] = {T, longest
+ * pair}. B*K <= 1024. */
+int rag_build_pairs(const int32_t* q_ids, const int32_t* q_cu, int B, const int64_t* rows, int K,
+                    const int16_t* c_toks, int lmax, const int32_t* c_lens, int max_len,
+                    int32_t* ids, int32_t* types, int32_t* cu, int32_t* stats, void* stream);
+
 /* Diagnostic entry (parity tests and the GEMM benchmark; not called by the reference path):
  * one encoder GEMM C[M,N] = A[M,K] . W[N,K]^T + bias[N] (the nn.Linear of modeling_bert.py
  * BertSelfAttention/BertIntermediate/BertOutput), device pointers, async on `stream`.

@@ -28,7 +28,7 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 import bert_ref as R  # noqa: E402  (seeded weight generator only)
 from ragmi.encoders import HEAD_CLS_L2, HEAD_POOLER_CLS, BertEncoder  # noqa: E402
 from ragmi.index import FlatIndex  # noqa: E402
-from ragmi.pairs import build_pairs  # noqa: E402
+from ragmi.pairs import build_pairs_gpu  # noqa: E402
 
 N, D, B, K, TOPK = 1_000_000, 384, 32, 15, 5
 LC_MAX = 260
@@ -83,7 +83,7 @@ def main():
                 if cfg == 3:                                         # stage 3
                     q_ids = torch.from_numpy(ids).to(dev)
                     q_cu = torch.from_numpy(cu).to(dev)
-                    pid, pty, pcu, mx = build_pairs(q_ids, q_cu, rows, c_toks, c_lens)
+                    pid, pty, pcu, mx = build_pairs_gpu(q_ids, q_cu, rows, c_toks, c_lens)
                     logits = ce.forward_device(pid, pty, pcu, mx).view(B, K)
                     top = torch.topk(logits, TOPK, dim=1).indices
                     _ = torch.gather(rows, 1, top)

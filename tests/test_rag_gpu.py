@@ -138,3 +138,30 @@ def test_end_to_end_retrieval_and_rerank(rag):
         si, ss = rag.rerank_documents(qq, t, 5)
         np.testing.assert_array_equal(bs, ss)
         np.testing.assert_array_equal(bi, si)
+
+
+def test_build_pairs_gpu_matches_torch(gpu):
+    """rag_build_pairs (HIP) == ragmi.pairs.build_pairs (torch, itself CPU-tested against a
+    per-pair loop), bit for bit, incl. truncation to max_len and -1 rows."""
+    import torch
+    from ragmi.pairs import build_pairs, build_pairs_gpu
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    rows_n, lmax = 5000, 300
+    c_toks = torch.randint(0, 65535, (rows_n, lmax), generator=g, device="cuda",
+                           dtype=torch.int32).to(torch.int16)
+    c_lens = torch.randint(1, lmax + 1, (rows_n,), generator=g, device="cuda",
+                           dtype=torch.int32)
+    for B, K, max_len in ((32, 15, 512), (3, 7, 64), (1, 1, 512), (64, 16, 256)):
+        ql = torch.randint(3, 40, (B,), generator=g, device="cuda")
+        q_cu = torch.zeros(B + 1, dtype=torch.int32, device="cuda")
+        q_cu[1:] = torch.cumsum(ql, 0)
+        q_ids = torch.randint(1000, 30000, (int(q_cu[-1]),), generator=g, device="cuda",
+                              dtype=torch.int32)
+        rows = torch.randint(-1, rows_n, (B, K), generator=g, device="cuda")
+        a = build_pairs(q_ids, q_cu, rows, c_toks, c_lens, max_len)
+        b = build_pairs_gpu(q_ids, q_cu, rows, c_toks, c_lens, max_len)
+        torch.cuda.synchronize()
+        for x, y in zip(a[:3], b[:3]):
+            assert torch.equal(x.cpu(), y.cpu())
+        assert a[3] == b[3]
