@@ -761,6 +761,7 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) 
   const _Float16* planes[2] = {qkv, qkv_lo};
   const int g = lane >> 4, ql = lane & 15;
   const float c2 = scale * 1.44269504088896341f;
+  const float rescale_gap = 8.0f / c2;             // deferred-max threshold (score units)
 
   // ---- stage keys [k0, k0 + n) (n multiple of 32; zeros past len): K row-major, V^T permuted
   auto stage = [&](int k0, int n) {
@@ -832,9 +833,23 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) 
       }
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mnew = fmaxf(st.m, mx);
-      const float corr = __builtin_amdgcn_exp2f((st.m - mnew) * c2);
-      const float nm = -mnew * c2;
+      // Deferred rescale: the running max only moves when some query's block max exceeds it
+      // by more than 8 / c2 (P = 2^(s c2 - m c2) then stays <= 2^8, exact in the fp16 MFMA
+      // operand and far from its range limit); otherwise the old max is kept and the
+      // rescale of l and O (an exp2 and DT*4 + 1 multiplies per block) is skipped. The
+      // normalisation divides by l summed from the same P, so the result is unchanged up to
+      // rounding. Wave-uniform branch (ballot).
+      if (__builtin_amdgcn_ballot_w64(mx > st.m + rescale_gap)) {
+        const float mnew = fmaxf(st.m, mx);
+        const float corr = __builtin_amdgcn_exp2f((st.m - mnew) * c2);
+        st.lsum *= corr;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) st.o[dt][r] *= corr;
+        st.m = mnew;
+      }
+      const float nm = -st.m * c2;
       half8 ph, pl;
 #pragma unroll
       for (int j = 0; j < 2; ++j)
@@ -854,12 +869,9 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) 
         if constexpr (SPLIT)
           rs = __builtin_amdgcn_fdot2(half2{pl[2 * e2], pl[2 * e2 + 1]}, one2, rs, false);
       }
-      st.lsum = st.lsum * corr + rs;                  // reduced across g at the end
-      st.m = mnew;
+      st.lsum += rs;                                  // reduced across g at the end
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) st.o[dt][r] *= corr;
         const int vr = (16 * dt + ql) * vrow + kb + 8 * g;
         const half8 v = *reinterpret_cast<const half8*>(vts[0] + vr);
         if constexpr (SPLIT) {
