@@ -53,6 +53,8 @@ struct rag_encoder {
   float *xc = nullptr, *yc = nullptr;
   _Float16 *xch = nullptr, *xcl = nullptr, *cc = nullptr, *ccl = nullptr, *ffc = nullptr,
            *ffcl = nullptr;
+  // residual + LayerNorm fused into the output projections: -1 auto, 0 off, 1 on
+  int fuse_ln = -1;
   // host-entry staging
   void* stage = nullptr;
   size_t stage_bytes = 0;
@@ -165,11 +167,44 @@ bool pipe_ok(int M, int N, int K) {
 template <int EPI, bool SPLIT, typename CFG, int PROBE = 0>
 void launch_pipe(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float16* Wl,
                  const float* bias, int M, int N, int K, void* C, _Float16* Clo, hipStream_t st,
-                 int max_wg) {
+                 int max_wg, const LnArgs& ln = LnArgs{}) {
   const int tiles = (N / CFG::BN) * ((M + CFG::BM - 1) / CFG::BM);
   const dim3 grid((unsigned)std::min(max_wg, (tiles + 7) / 8 * 8));   // multiple of 8
   gemm_pipe_kernel<EPI, SPLIT, CFG, PROBE><<<grid, dim3(CFG::THREADS), 0, st>>>(
-      A, Al, W, Wl, bias, M, N, K, C, Clo);
+      A, Al, W, Wl, bias, M, N, K, C, Clo, ln);
+}
+
+// the fused output projection + residual + LayerNorm (kEpiAddLn on PipeRow tiles)
+bool add_ln_ok(int M, int N, int K) {
+  return N == PipeRow::BN && K % 64 == 0 && (int64_t)M * K * 2 < (int64_t(1) << 31) &&
+         (int64_t)M * N * 4 < (int64_t(1) << 31);
+}
+
+// x[M,N] = LN(x + A . W^T + bias) * gamma + beta (fp32, in place), xh = fp16(x)
+// [, xl = fp16(x - xh)]: BertSelfOutput / BertOutput (dense + dropout(eval) + LayerNorm of
+// the sum with the residual) in one pass over the rows
+void gemm_add_ln(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float16* Wl,
+                 const float* bias, const float* gamma, const float* beta, float eps, int M,
+                 int N, int K, float* x, _Float16* xh, _Float16* xl, hipStream_t st) {
+  LnArgs ln;
+  ln.gamma = gamma;
+  ln.beta = beta;
+  ln.xh = xh;
+  ln.eps = eps;
+  if (Al)
+    launch_pipe<kEpiAddLn, true, PipeRow>(A, Al, W, Wl, bias, M, N, K, x, xl, st, cu_count(), ln);
+  else
+    launch_pipe<kEpiAddLn, false, PipeRow>(A, nullptr, W, nullptr, bias, M, N, K, x, nullptr, st,
+                                           cu_count(), ln);
+}
+
+// fusion mode of the forward: -1 auto (once the 128-row bands cover the CUs), 0 off, 1 on
+int fuse_ln_default() {
+  static int v = [] {
+    const char* s = std::getenv("RAGMI_FUSE_LN");
+    return s ? std::atoi(s) : -1;
+  }();
+  return v;
 }
 
 int ensure_cls(rag_encoder* e, int64_t B) {
@@ -316,13 +351,32 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
       ffl = e->xl ? e->ffcl : nullptr;
     }
     const unsigned lg = (unsigned)((R + 3) / 4);
-    gemm<kEpiF32>(ctx, ctxl, L.wo, L.wo_l, L.bo, R, H, H, y, nullptr, st);
-    add_ln_kernel<H><<<dim3(lg), dim3(256), 0, st>>>(x, y, L.g1, L.be1, c.layer_norm_eps, xh,
-                                                    xl, R);
+    // fused: the projection's epilogue adds the residual and normalises whole 384-wide rows
+    // (saves the fp32 y round trip and add_ln's extra pass). Auto: fp16 mode once the
+    // 128-row bands fill the CUs (rerank batch, 117K tokens: 5.25 -> 4.92 ms). In fp16x3 the
+    // 128x384 two-stage ring loses to the 256x128 three-stage one by what the fusion saves
+    // (10.63 vs 10.67 ms), so auto leaves it off there.
+    const bool fuse = add_ln_ok(R, H, FF) && add_ln_ok(R, H, H) &&
+                      (e->fuse_ln > 0 ||
+                       (e->fuse_ln < 0 && !e->xl &&
+                        (R + PipeRow::BM - 1) / PipeRow::BM >= cu_count()));
+    if (fuse) {
+      gemm_add_ln(ctx, ctxl, L.wo, L.wo_l, L.bo, L.g1, L.be1, c.layer_norm_eps, R, H, H, x, xh,
+                  xl, st);
+    } else {
+      gemm<kEpiF32>(ctx, ctxl, L.wo, L.wo_l, L.bo, R, H, H, y, nullptr, st);
+      add_ln_kernel<H><<<dim3(lg), dim3(256), 0, st>>>(x, y, L.g1, L.be1, c.layer_norm_eps, xh,
+                                                      xl, R);
+    }
     gemm<kEpiGeluF16>(xh, xl, L.w1, L.w1_l, L.bi1, R, FF, H, ff, ffl, st);
-    gemm<kEpiF32>(ff, ffl, L.w2, L.w2_l, L.bi2, R, H, FF, y, nullptr, st);
-    add_ln_kernel<H><<<dim3(lg), dim3(256), 0, st>>>(x, y, L.g2, L.be2, c.layer_norm_eps, xh,
-                                                    xl, R);
+    if (fuse) {
+      gemm_add_ln(ff, ffl, L.w2, L.w2_l, L.bi2, L.g2, L.be2, c.layer_norm_eps, R, H, FF, x, xh,
+                  xl, st);
+    } else {
+      gemm<kEpiF32>(ff, ffl, L.w2, L.w2_l, L.bi2, R, H, FF, y, nullptr, st);
+      add_ln_kernel<H><<<dim3(lg), dim3(256), 0, st>>>(x, y, L.g2, L.be2, c.layer_norm_eps, xh,
+                                                      xl, R);
+    }
   }
   // the final hidden states of the CLS tokens are rows 0 .. B-1 of e->xc (cu = null)
   if (c.head == RAG_HEAD_CLS_L2)
@@ -400,6 +454,7 @@ int rag_encoder_create(const rag_bert_config* cfg, const float* const* w, int n_
   auto* e = new rag_encoder();
   e->cfg = *cfg;
   e->device = device;
+  e->fuse_ln = fuse_ln_default();
   int rc = RAG_OK;
   auto chk = [&](int r) {
     if (r && !rc) rc = r;
@@ -511,6 +566,32 @@ int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, co
     default: return ragmi::fail(RAG_EINVAL, "unknown epilogue");
   }
   RAG_HIP(hipGetLastError());
+  return RAG_OK;
+}
+
+int rag_bert_gemm_add_ln(const void* A, const void* A_lo, const void* W, const void* W_lo,
+                         const float* bias, const float* gamma, const float* beta, float eps,
+                         int M, int N, int K, float* x, void* xh, void* xl, void* stream) {
+  ragmi::clear_error();
+  if (!A || !W || !bias || !gamma || !beta || !x || !xh)
+    return ragmi::fail(RAG_EINVAL, "NULL argument");
+  if ((A_lo == nullptr) != (W_lo == nullptr) || (A_lo != nullptr) != (xl != nullptr))
+    return ragmi::fail(RAG_EINVAL, "A_lo, W_lo and xl: all three (fp16x3) or none (fp16)");
+  if (M < 1 || !add_ln_ok(M, N, K))
+    return ragmi::fail(RAG_EINVAL, "N == 384, K % 64 == 0, M*K*2 and M*N*4 < 2^31 required");
+  gemm_add_ln(static_cast<const _Float16*>(A), static_cast<const _Float16*>(A_lo),
+              static_cast<const _Float16*>(W), static_cast<const _Float16*>(W_lo), bias, gamma,
+              beta, eps, M, N, K, x, static_cast<_Float16*>(xh), static_cast<_Float16*>(xl),
+              static_cast<hipStream_t>(stream));
+  RAG_HIP(hipGetLastError());
+  return RAG_OK;
+}
+
+int rag_encoder_set_fusion(rag_encoder_t* e, int mode) {
+  ragmi::clear_error();
+  if (!e || mode < -1 || mode > 1) return ragmi::fail(RAG_EINVAL, "mode: -1 auto, 0 off, 1 on");
+  std::lock_guard<std::mutex> lk(e->mu);
+  e->fuse_ln = mode;
   return RAG_OK;
 }
 

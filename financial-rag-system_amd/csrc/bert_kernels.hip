@@ -137,7 +137,8 @@ __global__ __launch_bounds__(256) void add_ln_kernel(float* __restrict__ x,
 // v_mfma_f32_16x16x32_f16.
 // Register-staged double-buffered LDS (one barrier per K step), XOR-swizzled 16-B chunks.
 // ----------------------------------------------------------------------------------------
-enum Epi { kEpiF16 = 0, kEpiGeluF16 = 1, kEpiF32 = 2 };
+// kEpiAddLn (gemm_pipe_kernel<PipeRow> only): x = LN(x + A.W^T + bias) on whole rows
+enum Epi { kEpiF16 = 0, kEpiGeluF16 = 1, kEpiF32 = 2, kEpiAddLn = 3 };
 
 constexpr int BM = 128, BN = 128;
 
@@ -357,8 +358,13 @@ struct PipeCfg {
   static constexpr int BM = BM_, BN = BN_, WAVES_M = WAVES_M_, WAVES_N = WAVES_N_, NS = NS_;
   static constexpr int THREADS = 64 * WAVES_M * WAVES_N;
   static constexpr int FM = BM / WAVES_M / 16, FN = BN / WAVES_N / 16;   // 16x16 frags/wave
+  // a K step's fragments all loaded before its MFMAs (the large tiles; see the main loop)
+  static constexpr bool PRELOAD = BM * BN >= 256 * 128;
 };
 using PipeLarge = PipeCfg<256, 128, 4, 2, 3>;
+// whole 384-wide rows per tile (bge-small / MiniLM hidden size): the output projections with
+// residual + LayerNorm fused into the epilogue (kEpiAddLn); 2 x 4 waves of 64 x 96
+using PipeRow = PipeCfg<128, 384, 2, 4, 2>;
 template <bool SPLIT> using PipeSmall = PipeCfg<64, 64, 2, 2, SPLIT ? 3 : 4>;
 // wider N tiles: fewer panel bytes per FLOP (256x256: 128 FLOP/B fp16 vs 85 at 256x128) at
 // the price of a 2-stage ring (one stage in flight)
@@ -412,6 +418,29 @@ __device__ __forceinline__ void wait_ring(int y, bool stored) {
   if constexpr (Y > 0) wait_ring<L, S, Y - 1>(y, stored);
 }
 
+// fp16 out: fragments j, j+1 of a row pair up through one v_permlane16_swap per dword
+// (lanes 16-31 of the j value <-> lanes 0-15 of the j+1 value, same for 48-63 / 32-47), after
+// which every lane holds 8 consecutive columns: 16-B stores, half the store instructions of
+// 8-B ones (the epilogue is store-issue-bound). Lane group g = lane >> 4 then owns columns
+// 16 j + {0, 16, 8, 24}[g] .. +7 (byte offset vo).
+__device__ __forceinline__ void store_f16_pair(half4 xa, half4 xb, __amdgpu_buffer_rsrc_t rsc,
+                                               int vo, int so = 0) {
+  u32x2 a = __builtin_bit_cast(u32x2, xa), b = __builtin_bit_cast(u32x2, xb);
+  const auto r0 = __builtin_amdgcn_permlane16_swap(a[0], b[0], false, false);
+  const auto r1 = __builtin_amdgcn_permlane16_swap(a[1], b[1], false, false);
+  const u32x4 d = {r0[0], r1[0], r0[1], r1[1]};
+  __builtin_amdgcn_raw_buffer_store_b128(d, rsc, vo, so, 0);
+}
+
+// kEpiAddLn operands besides the GEMM's (Cout = the fp32 residual rows x, read and
+// overwritten; Clo = the lo plane of the fp16x3 copy)
+struct LnArgs {
+  const float* gamma = nullptr;
+  const float* beta = nullptr;
+  _Float16* xh = nullptr;       // fp16 copy of the normalised rows (the next GEMM's A)
+  float eps = 0.f;
+};
+
 // PROBE (diagnostic builds only, rag_bert_gemm variants 3/4/9): timing probes of the same
 // kernel with parts removed — 1 = no MFMAs, 2 = no DMAs, 3 = no DMAs and no barriers.
 // (s_setprio around the MFMA clusters / for the younger waves measured +1-2%: not kept.)
@@ -420,7 +449,7 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
     const _Float16* __restrict__ A, const _Float16* __restrict__ Al,
     const _Float16* __restrict__ W, const _Float16* __restrict__ Wl,
     const float* __restrict__ bias, int M, int N, int K, void* __restrict__ Cout,
-    _Float16* __restrict__ Clo) {
+    _Float16* __restrict__ Clo, LnArgs ln) {
   constexpr int BM = CFG::BM, BN = CFG::BN, NS = CFG::NS, TH = CFG::THREADS;
   constexpr int FM = CFG::FM, FN = CFG::FN, WTM = 16 * FM, WTN = 16 * FN;
   constexpr int BK = kBK<SPLIT>, CPR = BK / 8;
@@ -430,10 +459,19 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
   constexpr int LA = A_H8 / TH, LW = W_H8 / TH;          // DMAs per wave per plane
   constexpr int L = NPL * (LA + LW);                      // DMAs per wave per stage
   // epilogue stores per wave: 16 B each; fp16 outputs pair two fragments per store
-  constexpr int S = EPI == kEpiF32 ? FM * FN : FM * FN / 2 * (SPLIT ? 2 : 1);
-  constexpr int OUT_B = EPI == kEpiF32 ? 4 : 2;           // output element bytes
+  // (kEpiAddLn: the fp32 rows and the fp16 copy [+ lo plane], 8-B stores for the latter).
+  // The count is capped at what vmcnt can express: waiting until fewer ops are outstanding
+  // than were issued after the awaited stage is only stricter.
+  constexpr int S_ISSUED = EPI == kEpiF32     ? FM * FN
+                           : EPI == kEpiAddLn ? FM * FN * (SPLIT ? 3 : 2)
+                                              : FM * FN / 2 * (SPLIT ? 2 : 1);
+  constexpr int S = S_ISSUED < 63 - (NS - 2) * L ? S_ISSUED : 63 - (NS - 2) * L;
+  constexpr int OUT_B = EPI == kEpiF32 || EPI == kEpiAddLn ? 4 : 2;   // Cout element bytes
   static_assert(A_H8 % TH == 0 && W_H8 % TH == 0 && FN % 2 == 0, "tile shape");
   static_assert((NS - 2) * L + S <= 63, "vmcnt range");
+  // kEpiAddLn keeps bias | gamma | beta | two [WAVES_N][BM] row-sum tables in the bias area
+  static_assert(EPI != kEpiAddLn || 3 * BN + 2 * CFG::WAVES_N * BM <= kPipeBiasMax,
+                "LN staging");
   // one LDS object (ring | bias): a second __shared__ object beside a DMA target can make
   // hipcc drain vmcnt before every ds_read
   __shared__ half8 lds[NS * STAGE_H8 + kPipeBiasMax / 4];
@@ -450,8 +488,13 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
   const int n_mine = off < n_tiles ? (n_tiles - off + G - 1) / G : 0;
   const int steps = n_mine * nk;
 
-  for (int i = tid * 4; i < N; i += TH * 4)
+  for (int i = tid * 4; i < N; i += TH * 4) {
     *reinterpret_cast<floatx4*>(bias_l + i) = *reinterpret_cast<const floatx4*>(bias + i);
+    if constexpr (EPI == kEpiAddLn) {          // N == BN here (checked by the launcher)
+      *reinterpret_cast<floatx4*>(bias_l + BN + i) = *reinterpret_cast<const floatx4*>(ln.gamma + i);
+      *reinterpret_cast<floatx4*>(bias_l + 2 * BN + i) = *reinterpret_cast<const floatx4*>(ln.beta + i);
+    }
+  }
   __syncthreads();
 
   // per-lane byte offsets inside a panel (launch constants): LDS position q of the
@@ -535,7 +578,7 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
 
     const half8* sa = lds + slot_c * STAGE_H8;
     const half8* sw = sa + NPL * A_H8;
-    if constexpr (PROBE != 1 && CFG::BM >= 256) {
+    if constexpr (PROBE != 1 && CFG::PRELOAD) {
       // every fragment of the K step issued back to back, then the MFMAs (left alone, the
       // compiler loads each fragment just before its first use and waits every few MFMAs;
       // this order measured ~3% faster on the 256-row tiles)
@@ -569,7 +612,7 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
           }
     }
 #pragma unroll
-    for (int ks = 0; ks < (PROBE == 1 || CFG::BM >= 256 ? 0 : BK / 32); ++ks) {
+    for (int ks = 0; ks < (PROBE == 1 || CFG::PRELOAD ? 0 : BK / 32); ++ks) {
       const int ch = ks * 4 + (lane >> 4);
       half8 af[FM], wf[FN];
 #pragma unroll
@@ -607,8 +650,96 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
       const __amdgpu_buffer_rsrc_t rc =
           panel(static_cast<char*>(Cout) + (int64_t)m0 * N * OUT_B, cbytes);
       __amdgpu_buffer_rsrc_t rl = rc;
-      if constexpr (SPLIT && EPI != kEpiF32) rl = panel(Clo + (int64_t)m0 * N, cbytes);
-      if constexpr (EPI == kEpiF32) {
+      if constexpr (SPLIT && EPI != kEpiF32)
+        rl = panel(Clo + (int64_t)m0 * N, (int64_t)(M - m0) * N * 2);
+      if constexpr (EPI == kEpiAddLn) {
+        // x = LN(x + acc + bias) over whole rows (BN == N, n0 = 0). Row statistics: a lane's
+        // 4 FN values -> the 4 lane groups (shuffles) -> the WAVES_N waves of a row band (LDS
+        // tables, one barrier each); two passes, mean then centred squares, as add_ln_kernel.
+        // Every wave runs the same epilogues, so the extra barriers pair up across the
+        // workgroup like the main loop's.
+        const int g = lane >> 4;
+        float* red = bias_l + 3 * BN;                      // [2][WAVES_N][BM]
+        const float* gam = bias_l + BN;
+        const float* bet = bias_l + 2 * BN;
+        const __amdgpu_buffer_rsrc_t rh = panel(ln.xh + (int64_t)m0 * N, (int64_t)(M - m0) * N * 2);
+        // Addressing: a per-lane byte offset per fragment row i (the row must sit in the
+        // voffset: the buffer range check that drops rows past M ignores soffset) plus a
+        // wave-uniform soffset per fragment column j — per-fragment lane offsets would be
+        // hoisted out of the tile loop by the compiler and spilled (96 accumulators live).
+        auto vf = [&](int i) { return ((wr * WTM + i * 16 + (lane & 15)) * N + 4 * g) * 4; };
+        auto sf = [&](int j) { return (wc * WTN + j * 16) * 4; };
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const floatx4 bj = *reinterpret_cast<const floatx4*>(bias_l + wc * WTN + j * 16 + 4 * g);
+#pragma unroll
+          for (int i = 0; i < FM; ++i) {   // rows past M read as zeros (bounded panel)
+            const u32x4 xr = __builtin_amdgcn_raw_buffer_load_b128(rc, vf(i), sf(j), 0);
+            acc[i][j] += bj + __builtin_bit_cast(floatx4, xr);
+          }
+        }
+        float mu[FM], rsd[FM];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) mu[i] = rsd[i] = 0.f;
+#pragma unroll
+        for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+          for (int i = 0; i < FM; ++i) {
+            float s = 0.f;
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const float d = acc[i][j][r] - mu[i];
+                s = pass ? fmaf(d, d, s) : s + d;
+              }
+            s += __shfl_xor(s, 16, 64);
+            s += __shfl_xor(s, 32, 64);
+            if (g == 0) red[(pass * CFG::WAVES_N + wc) * BM + wr * WTM + i * 16 + lane] = s;
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+          asm volatile("" ::: "memory");
+#pragma unroll
+          for (int i = 0; i < FM; ++i) {
+            const int row = wr * WTM + i * 16 + (lane & 15);
+            float s = 0.f;
+#pragma unroll
+            for (int w = 0; w < CFG::WAVES_N; ++w) s += red[(pass * CFG::WAVES_N + w) * BM + row];
+            if (pass == 0) mu[i] = s * (1.0f / BN);
+            else rsd[i] = rsqrtf(s * (1.0f / BN) + ln.eps);
+          }
+        }
+        // fp16 copy [+ lo plane]: 8-B stores straight from the fragment layout (the
+        // permlane16_swap pairing of the plain fp16 epilogue returned wrong dwords for lanes
+        // 12-15 of each 16-lane group in this kernel's fp16x3 instance)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const floatx4 gj = *reinterpret_cast<const floatx4*>(gam + wc * WTN + j * 16 + 4 * g);
+          const floatx4 ej = *reinterpret_cast<const floatx4*>(bet + wc * WTN + j * 16 + 4 * g);
+#pragma unroll
+          for (int i = 0; i < FM; ++i) {
+            floatx4 v;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = (acc[i][j][r] - mu[i]) * rsd[i] * gj[r] + ej[r];
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rc, vf(i),
+                                                   sf(j), 0);
+            half4 h;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) h[r] = (_Float16)v[r];
+            const int vh = vf(i) / 2;                  // same element offsets in fp16
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, h), rh, vh,
+                                                  sf(j) / 2, 0);
+            if constexpr (SPLIT) {
+              half4 l;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) l[r] = lo_part(v[r], h[r]);
+              __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, l), rl, vh,
+                                                    sf(j) / 2, 0);
+            }
+          }
+        }
+      } else if constexpr (EPI == kEpiF32) {
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
           const int nl = wc * WTN + j * 16 + 4 * (lane >> 4);
@@ -622,11 +753,7 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
           }
         }
       } else {
-        // fp16 out: fragments j, j+1 of a row pair up through one v_permlane16_swap per
-        // dword (lanes 16-31 of the j value <-> lanes 0-15 of the j+1 value, same for
-        // 48-63 / 32-47), after which every lane holds 8 consecutive columns: 16-B stores,
-        // half the store instructions of 8-B ones (the epilogue is store-issue-bound).
-        // Lane group g = lane >> 4 then owns columns 16 j + {0, 16, 8, 24}[g] .. +7.
+        // fp16 out, two fragments per 16-B store (store_f16_pair)
         const int g = lane >> 4;
         const int cofs = 8 * ((g & 1) * 2 + (g >> 1));
 #pragma unroll
@@ -651,14 +778,7 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
               ha[r] = (_Float16)va[r];
               hb[r] = (_Float16)vb[r];
             }
-            auto store_pair = [&](half4 xa, half4 xb, __amdgpu_buffer_rsrc_t rsc) {
-              u32x2 a = __builtin_bit_cast(u32x2, xa), b = __builtin_bit_cast(u32x2, xb);
-              const auto r0 = __builtin_amdgcn_permlane16_swap(a[0], b[0], false, false);
-              const auto r1 = __builtin_amdgcn_permlane16_swap(a[1], b[1], false, false);
-              const u32x4 d = {r0[0], r1[0], r0[1], r1[1]};
-              __builtin_amdgcn_raw_buffer_store_b128(d, rsc, vo, 0, 0);
-            };
-            store_pair(ha, hb, rc);
+            store_f16_pair(ha, hb, rc, vo);
             if constexpr (SPLIT) {
               half4 la, lb;
 #pragma unroll
@@ -666,7 +786,7 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
                 la[r] = lo_part(va[r], ha[r]);
                 lb[r] = lo_part(vb[r], hb[r]);
               }
-              store_pair(la, lb, rl);
+              store_f16_pair(la, lb, rl, vo);
             }
           }
         }

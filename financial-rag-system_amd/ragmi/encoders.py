@@ -102,6 +102,31 @@ def linear(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, epilogue: int =
     return (c, c_lo) if c_lo is not None else c
 
 
+def linear_add_ln(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, gamma: torch.Tensor,
+                  beta: torch.Tensor, eps: float, x: torch.Tensor,
+                  a_lo: torch.Tensor | None = None, w_lo: torch.Tensor | None = None):
+    """BertSelfOutput / BertOutput (modeling_bert.py: LayerNorm(dense(h) + x)) through the
+    forward's fused kernel: x fp32 [M, 384] is updated in place to LN(x + a.w^T + bias); returns
+    (x, xh) or (x, xh, xl) with the fp16 copy [+ lo plane] the next GEMM reads."""
+    M, K = a.shape
+    N = w.shape[0]
+    for t, dt in ((a, torch.float16), (w, torch.float16), (bias, torch.float32),
+                  (gamma, torch.float32), (beta, torch.float32), (x, torch.float32)):
+        if t.dtype != dt or not t.is_cuda or not t.is_contiguous():
+            raise ValueError("a, w: contiguous fp16 cuda; bias, gamma, beta, x: fp32 cuda")
+    if x.shape != (M, N):
+        raise ValueError("x must be [M, N]")
+    split = a_lo is not None
+    xh = torch.empty((M, N), dtype=torch.float16, device=a.device)
+    xl = torch.empty_like(xh) if split else None
+    check(_lib.load().rag_bert_gemm_add_ln(
+        a.data_ptr(), a_lo.data_ptr() if split else None, w.data_ptr(),
+        w_lo.data_ptr() if w_lo is not None else None, bias.data_ptr(), gamma.data_ptr(),
+        beta.data_ptr(), float(eps), M, N, K, x.data_ptr(), xh.data_ptr(),
+        xl.data_ptr() if split else None, torch.cuda.current_stream(a.device).cuda_stream))
+    return (x, xh, xl) if split else (x, xh)
+
+
 # ------------------------------------------------------------------ device encoder
 class BertEncoder:
     """One encoder instance in HBM (fp16 GEMM weights, fp32 norms/embeddings)."""
@@ -130,6 +155,10 @@ class BertEncoder:
                                          ctypes.byref(h)))
         self._h = h
         self.out_dim = cfg["hidden"] if head == HEAD_CLS_L2 else 1
+
+    def set_fusion(self, mode: int) -> None:
+        """Residual + LayerNorm fused into the output projections: -1 auto, 0 off, 1 on."""
+        check(self._L.rag_encoder_set_fusion(self._h, int(mode)))
 
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:

@@ -98,6 +98,20 @@ int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, co
                   const void* W_lo, const float* bias, int M, int N, int K, void* C,
                   void* C_lo, void* stream);
 
+/* the output projection of an encoder layer with its residual + LayerNorm fused
+ * (modeling_bert.py BertSelfOutput / BertOutput: LayerNorm(dense(h) + x), eval mode), in place
+ * on the fp32 residual rows: x[M,N] = LN(x + A . W^T + bias) * gamma + beta, xh = fp16(x),
+ * xl = fp16(x - xh) (fp16x3: A_lo, W_lo and xl all given, else all NULL). N == 384 (whole
+ * rows per tile), K % 64 == 0. What rag_encoder_forward runs for large token counts; exported
+ * for parity tests. */
+int rag_bert_gemm_add_ln(const void* A, const void* A_lo, const void* W, const void* W_lo,
+                         const float* bias, const float* gamma, const float* beta, float eps,
+                         int M, int N, int K, float* x, void* xh, void* xl, void* stream);
+
+/* forward's use of rag_bert_gemm_add_ln: -1 auto (default; env RAGMI_FUSE_LN overrides at
+ * create), 0 never (separate GEMM + add-LayerNorm kernels), 1 always where the shape allows */
+int rag_encoder_set_fusion(rag_encoder_t* e, int mode);
+
 #ifdef __cplusplus
 }
 #endif

@@ -181,3 +181,38 @@ def test_text_api_with_local_vocab(gpu, tmp_path):
                       weights=cw, vocab_file=str(voc))
     s = ce.predict([["net income", "apple net income 2023"], ["net income", "iphone margin"]])
     assert s.shape == (2,) and s.dtype == np.float32
+
+
+def test_fused_add_ln_path(bge, ce, golden, prec):
+    """The output projections with residual + LayerNorm fused into the GEMM epilogue
+    (rag_bert_gemm_add_ln; auto-selected only once a batch has >= CUs x 128 tokens) forced on
+    for test-size batches: same oracle bounds as the two-kernel path."""
+    enc_b, wb = bge
+    enc_c, wc = ce
+    rng = np.random.default_rng(11)
+    ids, tt, m = R.random_batch(rng, 32, 32)
+    qi, qt, qm = R.random_batch(rng, 15, 288, pair=True)
+    try:
+        for enc in (enc_b, enc_c):
+            enc.set_fusion(1)
+        out = enc_b.forward_padded(ids, tt, m).cpu().numpy()
+        assert _report(f"[{prec}] bge32 fused", out, R.bge_embed(wb, R.BGE_SMALL, ids, tt, m)) \
+            <= TOL[prec]["bge"]
+        g = golden
+        out = enc_c.forward_padded(g["ids_p"], g["tt_p"], g["m_p"]).cpu().numpy()
+        assert _report(f"[{prec}] ce fused vs transformers", out, g["ce_logits"]) \
+            <= TOL[prec]["ce"]
+        out = enc_c.forward_padded(qi, qt, qm).cpu().numpy()
+        assert _report(f"[{prec}] ce15 fused", out, R.ce_logits(wc, R.MINILM_CE, qi, qt, qm)) \
+            <= TOL[prec]["ce"]
+        enc_c.set_fusion(0)
+        off = enc_c.forward_padded(qi, qt, qm).cpu().numpy()
+        # (fp16 mode: the fp16 rounding of the residual stream differs in ties between the
+        # two paths and the difference propagates like the mode's own error)
+        assert _report(f"[{prec}] ce15 fused vs unfused", out, off) <= \
+            TOL[prec]["ce"] / (10 if prec == "fp16x3" else 2)
+    finally:
+        for enc in (enc_b, enc_c):
+            enc.set_fusion(-1)
+    with pytest.raises(Exception):
+        enc_b.set_fusion(2)

@@ -100,3 +100,57 @@ def test_gemm_rejects_bad_shapes(gpu):
     b = torch.zeros((128,), dtype=torch.float32, device="cuda")
     with pytest.raises(RagmiError):
         linear(a, w, b, EPI_F32, variant=GEMM_PIPE)
+
+
+@pytest.mark.parametrize("shape", [(1, 384), (3001, 1536), (20000, 384), (70001, 1536)],
+                         ids=lambda s: "x".join(map(str, s)))
+@pytest.mark.parametrize("split", [False, True], ids=["fp16", "fp16x3"])
+def test_gemm_add_ln_matches_fp64(gpu, shape, split):
+    """rag_bert_gemm_add_ln: x <- LN(x + a.w^T + bias) * gamma + beta (BertSelfOutput /
+    BertOutput), whole 384-wide rows per tile, against fp64. The pre-LN sum carries the GEMM
+    bound above; normalising by its std (~1.4) keeps it: |x - ref| <= 5e-5 + 5e-6 |ref|.
+    xh must be exactly the fp16 rounding of the returned fp32 x, xl its residual."""
+    from ragmi.encoders import linear_add_ln
+    M, K = shape
+    N = 384
+    a, al, w, wl, bias, a64, w64 = _operands(M, N, K, split, seed=M + K + 1)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(M + 3)
+    # x is the head of a larger buffer: the 130 rows after it must come through untouched
+    # (the last tile's rows past M are dropped by the bounded buffer stores)
+    x_full = torch.randn((M + 130, N), generator=g, device="cuda")
+    tail = x_full[M:].clone()
+    x = x_full[:M]
+    gamma = 1.0 + 0.2 * torch.randn((N,), generator=g, device="cuda")
+    beta = 0.1 * torch.randn((N,), generator=g, device="cuda")
+    eps = 1e-12
+    v = x.double() + a64 @ w64.T + bias.double()
+    mu = v.mean(1, keepdim=True)
+    var = ((v - mu) ** 2).mean(1, keepdim=True)
+    ref = (v - mu) / torch.sqrt(var + eps) * gamma.double() + beta.double()
+    out = linear_add_ln(a, w, bias, gamma, beta, eps, x, al, wl)
+    torch.cuda.synchronize()
+    xo, xh = out[0], out[1]
+    assert xo.data_ptr() == x.data_ptr()
+    assert torch.equal(x_full[M:], tail)
+    assert bool(torch.isfinite(xo).all())
+    err = (xo.double() - ref).abs()
+    bad = err > 5e-5 + 5e-6 * ref.abs()
+    assert not bool(bad.any()), f"{int(bad.sum())} out of bound; max err {float(err.max()):.3g}"
+    assert torch.equal(xh, xo.half())
+    if split:   # xl: x - xh to fp16 precision (the kernel may round it once, from x - xh
+        #         in one mixed-precision op, where torch rounds twice: 1 fp16 ulp apart, rarely)
+        xl = out[2].double()
+        assert float(((xh.double() + xl) - xo.double()).abs().sub(
+            xl.abs() * 2.0 ** -10 + 2.0 ** -24).max()) <= 0
+
+
+def test_gemm_add_ln_rejects_bad_shapes(gpu):
+    from ragmi._lib import RagmiError
+    from ragmi.encoders import linear_add_ln
+    a = torch.zeros((16, 384), dtype=torch.float16, device="cuda")
+    w = torch.zeros((768, 384), dtype=torch.float16, device="cuda")     # N != 384
+    v = torch.zeros((768,), dtype=torch.float32, device="cuda")
+    x = torch.zeros((16, 768), dtype=torch.float32, device="cuda")
+    with pytest.raises(RagmiError):
+        linear_add_ln(a, w, v, v, v, 1e-12, x)
