@@ -235,6 +235,7 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
           const float* bias, int M, int N, int K, void* C, _Float16* Clo, hipStream_t st,
           int variant = RAG_GEMM_AUTO) {
   if (variant == RAG_GEMM_AUTO) variant = gemm_variant_default();
+  const bool auto_pick = variant == RAG_GEMM_AUTO;
   const int pipe_tiles = (N / PBN) * ((M + PBM - 1) / PBM);
   // SMALL while its 64x64 tiles fit about two per CU (every query-batch GEMM; the N = 384
   // ones up to ~5K tokens), PIPE once its 256x128 tiles cover the CUs, TILE in between
@@ -249,6 +250,7 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
               : pipe_tiles >= cu_count()         ? RAG_GEMM_PIPE
                                                  : RAG_GEMM_TILE;
   if (variant != RAG_GEMM_TILE && !pipe_ok(M, N, K)) variant = RAG_GEMM_TILE;
+  if (auto_pick && variant == RAG_GEMM_SMALL && Al) variant = RAG_GEMM_SMALL_BK64;
   if (variant == RAG_GEMM_PROBE_NO_MFMA) {       // diagnostic probes of the PIPE kernel
     launch_pipe<EPI, false, PipeLarge, 1>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st,
                                           cu_count());
@@ -282,8 +284,14 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
                                          cu_count());
     return;
   }
-  if (variant == RAG_GEMM_SMALL) {
-    // fp16: 80 KB LDS -> 2 workgroups per CU; fp16x3: 112 KB -> 1
+  if (variant == RAG_GEMM_SMALL_BK64 && Al) {
+    launch_pipe<EPI, true, PipeSmallSplit64>(A, Al, W, Wl, bias, M, N, K, C, Clo, st, cu_count());
+    return;
+  }
+  if (variant == RAG_GEMM_SMALL || variant == RAG_GEMM_SMALL_BK64) {
+    // fp16: 80 KB LDS -> 2 workgroups per CU; fp16x3 (AUTO's choice is SMALL_BK64, above:
+    // one MiniLM layer's four GEMMs at 782 / 3056 tokens 49.1 -> 46.6 / 96.3 -> 87.5 us):
+    // 112 KB -> 1
     if (Al)
       launch_pipe<EPI, true, PipeSmall<true>>(A, Al, W, Wl, bias, M, N, K, C, Clo, st,
                                               cu_count());
@@ -542,7 +550,8 @@ int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, co
     return ragmi::fail(RAG_EINVAL, "A_lo and W_lo: both (fp16x3) or neither (fp16)");
   if (A_lo && epilogue != kEpiF32 && !C_lo)
     return ragmi::fail(RAG_EINVAL, "fp16x3 fp16-output GEMM needs C_lo");
-  if ((variant == RAG_GEMM_PIPE || variant == RAG_GEMM_SMALL || variant == RAG_GEMM_WIDE) &&
+  if ((variant == RAG_GEMM_PIPE || variant == RAG_GEMM_SMALL || variant == RAG_GEMM_WIDE ||
+       variant == RAG_GEMM_SMALL_BK64) &&
       !pipe_ok(M, N, K))
     return ragmi::fail(RAG_EINVAL, "pipe/small/wide variants need N % 128 == 0, K % 64 == 0, "
                                    "N <= 4096, M*K*2 and M*N*4 < 2^31");
@@ -550,7 +559,7 @@ int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, co
                      variant == RAG_GEMM_PROBE_NO_SYNC;
   const bool known = variant == RAG_GEMM_AUTO || variant == RAG_GEMM_TILE ||
                      variant == RAG_GEMM_PIPE || variant == RAG_GEMM_SMALL ||
-                     variant == RAG_GEMM_WIDE || probe;
+                     variant == RAG_GEMM_WIDE || variant == RAG_GEMM_SMALL_BK64 || probe;
   if (!known || (probe && (A_lo || !pipe_ok(M, N, K))))
     return ragmi::fail(RAG_EINVAL, "unknown GEMM variant (probes: fp16 only)");
   auto* a = static_cast<const _Float16*>(A);

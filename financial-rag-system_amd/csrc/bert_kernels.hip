@@ -353,9 +353,10 @@ __global__ __launch_bounds__(256) void gemm_kernel(const _Float16* __restrict__ 
 // 64x64 tiles, 4 waves of 32x32, a 4-stage ring (fp16: the whole K = 384 of a tile in
 // flight after the prologue), for query batches of a few hundred to a few thousand tokens,
 // where a GEMM is a handful of tiles per CU and latency, not MFMA rate, sets its time.
-template <int BM_, int BN_, int WAVES_M_, int WAVES_N_, int NS_>
+template <int BM_, int BN_, int WAVES_M_, int WAVES_N_, int NS_, int BK_ = 0>
 struct PipeCfg {
   static constexpr int BM = BM_, BN = BN_, WAVES_M = WAVES_M_, WAVES_N = WAVES_N_, NS = NS_;
+  static constexpr int BK = BK_;   // K step; 0 = kBK<SPLIT> (64 fp16 / 32 fp16x3)
   static constexpr int THREADS = 64 * WAVES_M * WAVES_N;
   static constexpr int FM = BM / WAVES_M / 16, FN = BN / WAVES_N / 16;   // 16x16 frags/wave
   // a K step's fragments all loaded before its MFMAs (the large tiles; see the main loop)
@@ -366,6 +367,10 @@ using PipeLarge = PipeCfg<256, 128, 4, 2, 3>;
 // residual + LayerNorm fused into the epilogue (kEpiAddLn); 2 x 4 waves of 64 x 96
 using PipeRow = PipeCfg<128, 384, 2, 4, 2>;
 template <bool SPLIT> using PipeSmall = PipeCfg<64, 64, 2, 2, SPLIT ? 3 : 4>;
+// fp16x3 query-batch GEMMs at BK 64 (4 planes, 4-stage ring, 128 KB LDS, 1 workgroup per
+// CU): half the K steps of PipeSmall<true> — a query-batch GEMM is a few dozen tiles whose
+// time is the serial K loop's per-step latency
+using PipeSmallSplit64 = PipeCfg<64, 64, 2, 2, 4, 64>;
 // wider N tiles: fewer panel bytes per FLOP (256x256: 128 FLOP/B fp16 vs 85 at 256x128) at
 // the price of a 2-stage ring (one stage in flight)
 using PipeWide256 = PipeCfg<256, 256, 4, 2, 2>;
@@ -452,7 +457,7 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
     _Float16* __restrict__ Clo, LnArgs ln) {
   constexpr int BM = CFG::BM, BN = CFG::BN, NS = CFG::NS, TH = CFG::THREADS;
   constexpr int FM = CFG::FM, FN = CFG::FN, WTM = 16 * FM, WTN = 16 * FN;
-  constexpr int BK = kBK<SPLIT>, CPR = BK / 8;
+  constexpr int BK = CFG::BK ? CFG::BK : kBK<SPLIT>, CPR = BK / 8;
   constexpr int NPL = SPLIT ? 2 : 1;                     // planes per operand (hi[, lo])
   constexpr int A_H8 = BM * CPR, W_H8 = BN * CPR;        // half8 per plane per stage
   constexpr int STAGE_H8 = NPL * (A_H8 + W_H8);

@@ -87,13 +87,14 @@ int rag_build_pairs(const int32_t* q_ids, const int32_t* q_cu, int B, const int6
  * A, W fp16 row-major; A_lo/W_lo the fp16x3 residual planes (both NULL = plain fp16).
  * epilogue: RAG_EPI_F16 (C fp16 [+ C_lo]), RAG_EPI_GELU_F16 (erf-GELU, fp16 [+ C_lo]),
  * RAG_EPI_F32 (C fp32). variant: RAG_GEMM_AUTO (what the forward uses), _TILE, _PIPE, _SMALL,
- * _WIDE (_PIPE at 256x256 (N % 256 == 0) or 256x192 (N % 192 == 0, fp16) tiles);
+ * _WIDE (_PIPE at 256x256 (N % 256 == 0) or 256x192 (N % 192 == 0, fp16) tiles),
+ * _SMALL_BK64 (_SMALL with 64-wide K steps in fp16x3; = _SMALL in fp16);
  * _PROBE_* are timing probes of the PIPE kernel with its MFMAs / its loads / its loads and
  * barriers removed (fp16, results meaningless). N % 128 == 0, K % 64 == 0 (PIPE/SMALL also N <= 4096). */
 enum { RAG_EPI_F16 = 0, RAG_EPI_GELU_F16 = 1, RAG_EPI_F32 = 2 };
 enum { RAG_GEMM_AUTO = 0, RAG_GEMM_TILE = 1, RAG_GEMM_PIPE = 2, RAG_GEMM_PROBE_NO_MFMA = 3,
        RAG_GEMM_PROBE_NO_DMA = 4, RAG_GEMM_SMALL = 5, RAG_GEMM_WIDE = 8,
-       RAG_GEMM_PROBE_NO_SYNC = 9 };
+       RAG_GEMM_PROBE_NO_SYNC = 9, RAG_GEMM_SMALL_BK64 = 10 };
 int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, const void* W,
                   const void* W_lo, const float* bias, int M, int N, int K, void* C,
                   void* C_lo, void* stream);
@@ -102,8 +103,8 @@ int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, co
  * (modeling_bert.py BertSelfOutput / BertOutput: LayerNorm(dense(h) + x), eval mode), in place
  * on the fp32 residual rows: x[M,N] = LN(x + A . W^T + bias) * gamma + beta, xh = fp16(x),
  * xl = fp16(x - xh) (fp16x3: A_lo, W_lo and xl all given, else all NULL). N == 384 (whole
- * rows per tile), K % 64 == 0. What rag_encoder_forward runs for large token counts; exported
- * for parity tests. */
+ * rows per tile), K % 64 == 0. What rag_encoder_forward runs for large fp16-mode token
+ * counts (rag_encoder_set_fusion); exported for parity tests. */
 int rag_bert_gemm_add_ln(const void* A, const void* A_lo, const void* W, const void* W_lo,
                          const float* bias, const float* gamma, const float* beta, float eps,
                          int M, int N, int K, float* x, void* xh, void* xl, void* stream);
