@@ -35,15 +35,13 @@ __global__ void f32_to_f16_kernel(const float* __restrict__ in, _Float16* __rest
 
 }  // namespace
 
-struct rag_encoder {
-  rag_bert_config cfg{};
-  int device = 0;
-  std::mutex mu;
-  std::vector<void*> allocs;
-  float *wemb = nullptr, *pemb = nullptr, *temb = nullptr, *eg = nullptr, *eb = nullptr;
-  std::vector<Layer> layers;
-  float *wp = nullptr, *bp = nullptr, *wc = nullptr, *bc = nullptr;
-  // workspace (grown on demand)
+// Activations of one forward in flight (grown on demand). One per HIP stream that calls the
+// encoder: forwards on different streams run concurrently on the GPU (e.g. query batches of
+// a serving loop pipelined over streams), so they must not share activation buffers; forwards
+// on one stream are ordered by the stream and reuse its workspace.
+struct EncWorkspace {
+  hipStream_t stream = nullptr;
+  uint64_t last_use = 0;
   int64_t cap_t = 0;
   float *x = nullptr, *y = nullptr;
   _Float16 *xh = nullptr, *qkv = nullptr, *ctx = nullptr, *ff = nullptr;
@@ -53,6 +51,27 @@ struct rag_encoder {
   float *xc = nullptr, *yc = nullptr;
   _Float16 *xch = nullptr, *xcl = nullptr, *cc = nullptr, *ccl = nullptr, *ffc = nullptr,
            *ffcl = nullptr;
+
+  void release() {
+    for (void* p : {(void*)x, (void*)y, (void*)xh, (void*)qkv, (void*)ctx, (void*)ff, (void*)xl,
+                    (void*)qkv_l, (void*)ctx_l, (void*)ff_l, (void*)xc, (void*)yc, (void*)xch,
+                    (void*)xcl, (void*)cc, (void*)ccl, (void*)ffc, (void*)ffcl})
+      if (p) (void)hipFree(p);
+    *this = EncWorkspace{};
+  }
+};
+
+struct rag_encoder {
+  rag_bert_config cfg{};
+  int device = 0;
+  std::mutex mu;
+  std::vector<void*> allocs;
+  float *wemb = nullptr, *pemb = nullptr, *temb = nullptr, *eg = nullptr, *eb = nullptr;
+  std::vector<Layer> layers;
+  float *wp = nullptr, *bp = nullptr, *wc = nullptr, *bc = nullptr;
+  // per-stream activation workspaces (at most kMaxWorkspaces; see workspace_for)
+  std::vector<EncWorkspace> ws;
+  uint64_t uses = 0;
   // residual + LayerNorm fused into the output projections: -1 auto, 0 off, 1 on
   int fuse_ln = -1;
   // host-entry staging
@@ -105,31 +124,59 @@ int up_f16(rag_encoder* e, _Float16** dst, _Float16** dst_lo,
   return RAG_OK;
 }
 
-int ensure_ws(rag_encoder* e, int64_t T) {
-  if (T <= e->cap_t) return RAG_OK;
-  const int64_t cap = std::max<int64_t>(T, std::max<int64_t>(2 * e->cap_t, 1024));
-  for (void* p : {(void*)e->x, (void*)e->y, (void*)e->xh, (void*)e->qkv, (void*)e->ctx,
-                  (void*)e->ff, (void*)e->xl, (void*)e->qkv_l, (void*)e->ctx_l, (void*)e->ff_l})
+int ensure_ws(const rag_bert_config& cfg, EncWorkspace* w, int64_t T) {
+  if (T <= w->cap_t) return RAG_OK;
+  const int64_t cap = std::max<int64_t>(T, std::max<int64_t>(2 * w->cap_t, 1024));
+  for (void* p : {(void*)w->x, (void*)w->y, (void*)w->xh, (void*)w->qkv, (void*)w->ctx,
+                  (void*)w->ff, (void*)w->xl, (void*)w->qkv_l, (void*)w->ctx_l, (void*)w->ff_l})
     if (p) (void)hipFree(p);
-  e->x = e->y = nullptr;
-  e->xh = e->qkv = e->ctx = e->ff = nullptr;
-  e->xl = e->qkv_l = e->ctx_l = e->ff_l = nullptr;
-  e->cap_t = 0;
-  const int64_t H = e->cfg.hidden, FF = e->cfg.intermediate;
-  if (e->cfg.precision == RAG_PREC_FP16X3) {
-    RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->xl), cap * H * 2));
-    RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->qkv_l), cap * 3 * H * 2));
-    RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->ctx_l), cap * H * 2));
-    RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->ff_l), cap * FF * 2));
+  w->x = w->y = nullptr;
+  w->xh = w->qkv = w->ctx = w->ff = nullptr;
+  w->xl = w->qkv_l = w->ctx_l = w->ff_l = nullptr;
+  w->cap_t = 0;
+  const int64_t H = cfg.hidden, FF = cfg.intermediate;
+  if (cfg.precision == RAG_PREC_FP16X3) {
+    RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->xl), cap * H * 2));
+    RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->qkv_l), cap * 3 * H * 2));
+    RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->ctx_l), cap * H * 2));
+    RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->ff_l), cap * FF * 2));
   }
-  RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->x), cap * H * 4));
-  RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->y), cap * H * 4));
-  RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->xh), cap * H * 2));
-  RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->qkv), cap * 3 * H * 2));
-  RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->ctx), cap * H * 2));
-  RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->ff), cap * FF * 2));
-  e->cap_t = cap;
+  RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->x), cap * H * 4));
+  RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->y), cap * H * 4));
+  RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->xh), cap * H * 2));
+  RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->qkv), cap * 3 * H * 2));
+  RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->ctx), cap * H * 2));
+  RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->ff), cap * FF * 2));
+  w->cap_t = cap;
   return RAG_OK;
+}
+
+constexpr size_t kMaxWorkspaces = 8;
+
+// the workspace of `st` (created on first use); beyond kMaxWorkspaces streams the least
+// recently used one is taken over after a device synchronize (its stream may still be
+// running work that reads it; the stream itself may be gone, so it is not waited on)
+EncWorkspace* workspace_for(rag_encoder* e, hipStream_t st) {
+  ++e->uses;
+  for (auto& w : e->ws)
+    if (w.stream == st) {
+      w.last_use = e->uses;
+      return &w;
+    }
+  if (e->ws.size() < kMaxWorkspaces) {
+    e->ws.emplace_back();
+  } else {
+    auto lru = std::min_element(e->ws.begin(), e->ws.end(),
+                                [](const EncWorkspace& a, const EncWorkspace& b) {
+                                  return a.last_use < b.last_use;
+                                });
+    if (hipDeviceSynchronize() != hipSuccess) return nullptr;
+    std::iter_swap(lru, e->ws.end() - 1);
+  }
+  EncWorkspace& w = e->ws.back();
+  w.stream = st;
+  w.last_use = e->uses;
+  return &w;
 }
 
 // GEMM variants: RAG_GEMM_TILE (gemm_kernel: one 128x128 tile per workgroup, 2 per CU),
@@ -207,26 +254,26 @@ int fuse_ln_default() {
   return v;
 }
 
-int ensure_cls(rag_encoder* e, int64_t B) {
-  if (B <= e->cap_b) return RAG_OK;
-  for (void* p : {(void*)e->xc, (void*)e->yc, (void*)e->xch, (void*)e->xcl, (void*)e->cc,
-                  (void*)e->ccl, (void*)e->ffc, (void*)e->ffcl})
+int ensure_cls(const rag_bert_config& cfg, EncWorkspace* w, int64_t B) {
+  if (B <= w->cap_b) return RAG_OK;
+  for (void* p : {(void*)w->xc, (void*)w->yc, (void*)w->xch, (void*)w->xcl, (void*)w->cc,
+                  (void*)w->ccl, (void*)w->ffc, (void*)w->ffcl})
     if (p) (void)hipFree(p);
-  e->xc = e->yc = nullptr;
-  e->xch = e->xcl = e->cc = e->ccl = e->ffc = e->ffcl = nullptr;
-  e->cap_b = 0;
-  const int64_t cap = std::max<int64_t>(B, 256), H = e->cfg.hidden, FF = e->cfg.intermediate;
-  RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->xc), cap * H * 4));
-  RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->yc), cap * H * 4));
-  RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->xch), cap * H * 2));
-  RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->cc), cap * H * 2));
-  RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->ffc), cap * FF * 2));
-  if (e->cfg.precision == RAG_PREC_FP16X3) {
-    RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->xcl), cap * H * 2));
-    RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->ccl), cap * H * 2));
-    RAG_HIP(hipMalloc(reinterpret_cast<void**>(&e->ffcl), cap * FF * 2));
+  w->xc = w->yc = nullptr;
+  w->xch = w->xcl = w->cc = w->ccl = w->ffc = w->ffcl = nullptr;
+  w->cap_b = 0;
+  const int64_t cap = std::max<int64_t>(B, 256), H = cfg.hidden, FF = cfg.intermediate;
+  RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->xc), cap * H * 4));
+  RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->yc), cap * H * 4));
+  RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->xch), cap * H * 2));
+  RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->cc), cap * H * 2));
+  RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->ffc), cap * FF * 2));
+  if (cfg.precision == RAG_PREC_FP16X3) {
+    RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->xcl), cap * H * 2));
+    RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->ccl), cap * H * 2));
+    RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->ffcl), cap * FF * 2));
   }
-  e->cap_b = cap;
+  w->cap_b = cap;
   return RAG_OK;
 }
 
@@ -314,49 +361,51 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
               int B, int T, int max_len, float* out, hipStream_t st) {
   const rag_bert_config& c = e->cfg;
   const int NH = H / HD, FF = c.intermediate;
-  int rc = ensure_ws(e, T);
+  EncWorkspace* w = workspace_for(e, st);
+  if (!w) return ragmi::fail(RAG_EHIP, "device synchronize failed");
+  int rc = ensure_ws(c, w, T);
   if (rc) return rc;
-  rc = ensure_cls(e, B);
+  rc = ensure_cls(c, w, B);
   if (rc) return rc;
   embed_ln_kernel<H><<<dim3((max_len + 3) / 4, B), dim3(256), 0, st>>>(
       ids, types, cu, e->wemb, e->pemb, e->temb, e->eg, e->eb, c.layer_norm_eps, c.vocab,
-      c.type_vocab, c.max_position, e->x, e->xh, e->xl);
+      c.type_vocab, c.max_position, w->x, w->xh, w->xl);
   const float scale = 1.0f / sqrtf((float)HD);
   // 1-D grid of (sequence, head) pairs, padded to a multiple of 8 (XCD-aware order in the
   // kernel; gridDim.x / NH = B after the padding is removed there)
   const dim3 agrid((unsigned)((NH * B + 7) / 8 * 8));
-  const int planes = e->xl ? 2 : 1;
+  const int planes = w->xl ? 2 : 1;
   const int kc = attn_chunk_keys<HD>(max_len, planes);
   const size_t alds = (size_t)attn_lds_bytes<HD>(kc, planes);
   const int nl = (int)e->layers.size();
   for (int l = 0; l < nl; ++l) {
     const Layer& L = e->layers[l];
     const bool last = l == nl - 1;                  // CLS rows only after the attention
-    gemm<kEpiF16>(e->xh, e->xl, L.wqkv, L.wqkv_l, L.bqkv, T, 3 * H, H, e->qkv, e->qkv_l, st);
+    gemm<kEpiF16>(w->xh, w->xl, L.wqkv, L.wqkv_l, L.bqkv, T, 3 * H, H, w->qkv, w->qkv_l, st);
     const int max_qb = last ? 1 : 1 << 20;
-    if (e->xl)
+    if (w->xl)
       attn_kernel<H, HD, true><<<agrid, dim3(kAttnThreads<true>), alds, st>>>(
-          e->qkv, e->qkv_l, cu, max_len, kc, scale, e->ctx, e->ctx_l, max_qb);
+          w->qkv, w->qkv_l, cu, max_len, kc, scale, w->ctx, w->ctx_l, max_qb);
     else
       attn_kernel<H, HD, false><<<agrid, dim3(kAttnThreads<false>), alds, st>>>(
-          e->qkv, nullptr, cu, max_len, kc, scale, e->ctx, nullptr, max_qb);
+          w->qkv, nullptr, cu, max_len, kc, scale, w->ctx, nullptr, max_qb);
     // rows the rest of the layer runs on: all T tokens, or the B gathered CLS rows
     int R = T;
-    float *x = e->x, *y = e->y;
-    _Float16 *xh = e->xh, *xl = e->xl, *ctx = e->ctx, *ctxl = e->ctx_l, *ff = e->ff,
-             *ffl = e->ff_l;
+    float *x = w->x, *y = w->y;
+    _Float16 *xh = w->xh, *xl = w->xl, *ctx = w->ctx, *ctxl = w->ctx_l, *ff = w->ff,
+             *ffl = w->ff_l;
     if (last) {
-      gather_cls_kernel<H><<<dim3(B), dim3(64), 0, st>>>(e->x, e->ctx, e->ctx_l, cu, e->xc,
-                                                        e->cc, e->xl ? e->ccl : nullptr);
+      gather_cls_kernel<H><<<dim3(B), dim3(64), 0, st>>>(w->x, w->ctx, w->ctx_l, cu, w->xc,
+                                                        w->cc, w->xl ? w->ccl : nullptr);
       R = B;
-      x = e->xc;
-      y = e->yc;
-      xh = e->xch;
-      xl = e->xl ? e->xcl : nullptr;
-      ctx = e->cc;
-      ctxl = e->xl ? e->ccl : nullptr;
-      ff = e->ffc;
-      ffl = e->xl ? e->ffcl : nullptr;
+      x = w->xc;
+      y = w->yc;
+      xh = w->xch;
+      xl = w->xl ? w->xcl : nullptr;
+      ctx = w->cc;
+      ctxl = w->xl ? w->ccl : nullptr;
+      ff = w->ffc;
+      ffl = w->xl ? w->ffcl : nullptr;
     }
     const unsigned lg = (unsigned)((R + 3) / 4);
     // fused: the projection's epilogue adds the residual and normalises whole 384-wide rows
@@ -366,7 +415,7 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
     // (10.63 vs 10.67 ms), so auto leaves it off there.
     const bool fuse = add_ln_ok(R, H, FF) && add_ln_ok(R, H, H) &&
                       (e->fuse_ln > 0 ||
-                       (e->fuse_ln < 0 && !e->xl &&
+                       (e->fuse_ln < 0 && !w->xl &&
                         (R + PipeRow::BM - 1) / PipeRow::BM >= cu_count()));
     if (fuse) {
       gemm_add_ln(ctx, ctxl, L.wo, L.wo_l, L.bo, L.g1, L.be1, c.layer_norm_eps, R, H, H, x, xh,
@@ -386,11 +435,11 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
                                                       xl, R);
     }
   }
-  // the final hidden states of the CLS tokens are rows 0 .. B-1 of e->xc (cu = null)
+  // the final hidden states of the CLS tokens are rows 0 .. B-1 of w->xc (cu = null)
   if (c.head == RAG_HEAD_CLS_L2)
-    cls_normalize_kernel<H><<<dim3(B), dim3(64), 0, st>>>(e->xc, nullptr, out);
+    cls_normalize_kernel<H><<<dim3(B), dim3(64), 0, st>>>(w->xc, nullptr, out);
   else
-    ce_head_kernel<H><<<dim3(B), dim3(256), 0, st>>>(e->xc, nullptr, e->wp, e->bp, e->wc, e->bc,
+    ce_head_kernel<H><<<dim3(B), dim3(256), 0, st>>>(w->xc, nullptr, e->wp, e->bp, e->wc, e->bc,
                                                      out);
   RAG_HIP(hipGetLastError());
   return RAG_OK;
@@ -519,11 +568,8 @@ int rag_encoder_destroy(rag_encoder_t* e) {
   (void)hipSetDevice(e->device);
   (void)hipDeviceSynchronize();
   for (void* p : e->allocs) (void)hipFree(p);
-  for (void* p : {(void*)e->x, (void*)e->y, (void*)e->xh, (void*)e->qkv, (void*)e->ctx,
-                  (void*)e->ff, (void*)e->xl, (void*)e->qkv_l, (void*)e->ctx_l, (void*)e->ff_l,
-                  e->stage, (void*)e->xc, (void*)e->yc, (void*)e->xch, (void*)e->xcl,
-                  (void*)e->cc, (void*)e->ccl, (void*)e->ffc, (void*)e->ffcl})
-    if (p) (void)hipFree(p);
+  for (auto& w : e->ws) w.release();
+  if (e->stage) (void)hipFree(e->stage);
   delete e;
   return RAG_OK;
 }

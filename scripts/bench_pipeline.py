@@ -106,6 +106,36 @@ def main():
                              "rerank_incl_pair_build": round(acc[2] / steps, 3)},
                 "note": "per-batch host sync (stage timing); synthetic weights/tokens"}),
                 flush=True)
+            # pipelined: batch i on stream i % S, no per-batch sync (a serving loop with S
+            # batches in flight; each stream has its own encoder / index workspaces)
+            for S in [int(x) for x in os.environ.get("PIPE_STREAMS", "2,4").split(",")]:
+                streams = [torch.cuda.Stream(dev) for _ in range(S)]
+
+                def run(i, ids, tt, cu):
+                    with torch.cuda.stream(streams[i % S]):
+                        q = bge.forward_packed(ids, tt, cu)
+                        s_, rows = idx.search(q, K)
+                        if cfg == 3:
+                            q_ids = torch.from_numpy(ids).to(dev)
+                            q_cu = torch.from_numpy(cu).to(dev)
+                            pid, pty, pcu, mx = build_pairs_gpu(q_ids, q_cu, rows, c_toks,
+                                                                c_lens)
+                            logits = ce.forward_device(pid, pty, pcu, mx).view(B, K)
+                            top = torch.topk(logits, TOPK, dim=1).indices
+                            return torch.gather(rows, 1, top)
+                        return rows
+                torch.cuda.synchronize()
+                for i in range(3):
+                    run(i, *batches[i])
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for i in range(3, len(batches)):
+                    run(i, *batches[i])
+                torch.cuda.synchronize()
+                el = time.perf_counter() - t0
+                print(json.dumps({"config": cfg, "precision": prec, "batches_in_flight": S,
+                                  "qps": round(B * steps / el, 1),
+                                  "ms_per_batch": round(el / steps * 1e3, 3)}), flush=True)
         bge.close()
         ce.close()
     idx.close()

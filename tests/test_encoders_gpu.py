@@ -216,3 +216,21 @@ def test_fused_add_ln_path(bge, ce, golden, prec):
             enc.set_fusion(-1)
     with pytest.raises(Exception):
         enc_b.set_fusion(2)
+
+
+def test_concurrent_streams_bitwise(ce):
+    """Forwards issued on different HIP streams run concurrently on the GPU, each with its own
+    activation workspace: results equal the one-stream results bit for bit (more streams than
+    the encoder's workspace pool, so a workspace is also taken over)."""
+    enc, w = ce
+    rng = np.random.default_rng(12)
+    batches = [R.random_batch(rng, 15, 200, pair=True) for _ in range(10)]
+    ref = [enc.forward_padded(*b).cpu().numpy() for b in batches]
+    streams = [torch.cuda.Stream() for _ in range(10)]
+    outs = []
+    for b, s in zip(batches, streams):
+        with torch.cuda.stream(s):
+            outs.append(enc.forward_padded(*b))
+    torch.cuda.synchronize()
+    for o, r in zip(outs, ref):
+        np.testing.assert_array_equal(o.cpu().numpy(), r)
