@@ -367,9 +367,26 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
   if (rc) return rc;
   rc = ensure_cls(c, w, B);
   if (rc) return rc;
+  // fused: the output projections' epilogue adds the residual and normalises whole 384-wide
+  // rows (saves the fp32 y round trip and add_ln's extra pass). Auto: fp16 mode once the
+  // 128-row bands fill the CUs (rerank batch, 117K tokens: 5.25 -> 4.92 ms). In fp16x3 the
+  // 128x384 two-stage ring loses to the 256x128 three-stage one by what the fusion saves
+  // (10.63 vs 10.67 ms), so auto leaves it off there.
+  auto fuse_for = [&](int R) {
+    return add_ln_ok(R, H, FF) && add_ln_ok(R, H, H) &&
+           (e->fuse_ln > 0 || (e->fuse_ln < 0 && !w->xl &&
+                               (R + PipeRow::BM - 1) / PipeRow::BM >= cu_count()));
+  };
+  // fp16x3 with the two-kernel projections: the token rows' residual stream is kept as the
+  // operand planes xh + xl alone (add_ln_kernel<XF>), no fp32 copy
+  static const bool xf_on = [] {
+    const char* v = std::getenv("RAGMI_RESIDUAL_F32");      // diagnostic: keep the fp32 copy
+    return !(v && std::atoi(v) == 1);
+  }();
+  const bool xf = xf_on && w->xl && !fuse_for(T);
   embed_ln_kernel<H><<<dim3((max_len + 3) / 4, B), dim3(256), 0, st>>>(
       ids, types, cu, e->wemb, e->pemb, e->temb, e->eg, e->eb, c.layer_norm_eps, c.vocab,
-      c.type_vocab, c.max_position, w->x, w->xh, w->xl);
+      c.type_vocab, c.max_position, xf ? nullptr : w->x, w->xh, w->xl);
   const float scale = 1.0f / sqrtf((float)HD);
   // 1-D grid of (sequence, head) pairs, padded to a multiple of 8 (XCD-aware order in the
   // kernel; gridDim.x / NH = B after the padding is removed there)
@@ -391,12 +408,15 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
           w->qkv, nullptr, cu, max_len, kc, scale, w->ctx, nullptr, max_qb);
     // rows the rest of the layer runs on: all T tokens, or the B gathered CLS rows
     int R = T;
-    float *x = w->x, *y = w->y;
+    float *x = xf ? nullptr : w->x, *y = w->y;
     _Float16 *xh = w->xh, *xl = w->xl, *ctx = w->ctx, *ctxl = w->ctx_l, *ff = w->ff,
              *ffl = w->ff_l;
+    bool row_xf = xf;
     if (last) {
-      gather_cls_kernel<H><<<dim3(B), dim3(64), 0, st>>>(w->x, w->ctx, w->ctx_l, cu, w->xc,
-                                                        w->cc, w->xl ? w->ccl : nullptr);
+      gather_cls_kernel<H><<<dim3(B), dim3(64), 0, st>>>(x, w->xh, w->xl, w->ctx, w->ctx_l, cu,
+                                                        w->xc, w->cc,
+                                                        w->xl ? w->ccl : nullptr);
+      row_xf = false;                                 // the B CLS rows keep an fp32 copy
       R = B;
       x = w->xc;
       y = w->yc;
@@ -408,22 +428,21 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
       ffl = w->xl ? w->ffcl : nullptr;
     }
     const unsigned lg = (unsigned)((R + 3) / 4);
-    // fused: the projection's epilogue adds the residual and normalises whole 384-wide rows
-    // (saves the fp32 y round trip and add_ln's extra pass). Auto: fp16 mode once the
-    // 128-row bands fill the CUs (rerank batch, 117K tokens: 5.25 -> 4.92 ms). In fp16x3 the
-    // 128x384 two-stage ring loses to the 256x128 three-stage one by what the fusion saves
-    // (10.63 vs 10.67 ms), so auto leaves it off there.
-    const bool fuse = add_ln_ok(R, H, FF) && add_ln_ok(R, H, H) &&
-                      (e->fuse_ln > 0 ||
-                       (e->fuse_ln < 0 && !w->xl &&
-                        (R + PipeRow::BM - 1) / PipeRow::BM >= cu_count()));
+    const bool fuse = !row_xf && fuse_for(R);
+    auto add_ln = [&](const float* gam, const float* bet) {
+      if (row_xf)
+        add_ln_kernel<H, true><<<dim3(lg), dim3(256), 0, st>>>(nullptr, y, gam, bet,
+                                                              c.layer_norm_eps, xh, xl, R);
+      else
+        add_ln_kernel<H><<<dim3(lg), dim3(256), 0, st>>>(x, y, gam, bet, c.layer_norm_eps, xh,
+                                                        xl, R);
+    };
     if (fuse) {
       gemm_add_ln(ctx, ctxl, L.wo, L.wo_l, L.bo, L.g1, L.be1, c.layer_norm_eps, R, H, H, x, xh,
                   xl, st);
     } else {
       gemm<kEpiF32>(ctx, ctxl, L.wo, L.wo_l, L.bo, R, H, H, y, nullptr, st);
-      add_ln_kernel<H><<<dim3(lg), dim3(256), 0, st>>>(x, y, L.g1, L.be1, c.layer_norm_eps, xh,
-                                                      xl, R);
+      add_ln(L.g1, L.be1);
     }
     gemm<kEpiGeluF16>(xh, xl, L.w1, L.w1_l, L.bi1, R, FF, H, ff, ffl, st);
     if (fuse) {
@@ -431,8 +450,7 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
                   xl, st);
     } else {
       gemm<kEpiF32>(ff, ffl, L.w2, L.w2_l, L.bi2, R, H, FF, y, nullptr, st);
-      add_ln_kernel<H><<<dim3(lg), dim3(256), 0, st>>>(x, y, L.g2, L.be2, c.layer_norm_eps, xh,
-                                                      xl, R);
+      add_ln(L.g2, L.be2);
     }
   }
   // the final hidden states of the CLS tokens are rows 0 .. B-1 of w->xc (cu = null)
