@@ -547,7 +547,8 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
         rW1 = panel(Wl + (int64_t)n0 * K, wbytes);
       }
     }
-    const uint32_t soff = (uint32_t)kr_i * (BK * 2);
+    // (wave-uniform by construction; readfirstlane keeps it an SGPR in every instance)
+    const uint32_t soff = __builtin_amdgcn_readfirstlane((uint32_t)kr_i * (BK * 2));
     if (++kr_i == nk) kr_i = 0;
     const uint32_t slot = lbase + (uint32_t)slot_i * (STAGE_H8 * 16);
 #pragma unroll
