@@ -5,6 +5,7 @@
 // on the host; every entry point either enqueues on the caller's stream or (for *_host)
 // stages through device memory and synchronises.
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 
 #include <algorithm>
 #include <cstring>
@@ -161,9 +162,22 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
     const dim3 g3(grid * groups), b3(64 * kLdsWaves);
     if (wide) {
       // all groups in every workgroup, one pass over the corpus (scan_wide_kernel)
-      scan_wide_kernel<D><<<dim3(grid), dim3(64 * kWideWaves), 0, st>>>(
-          h->corpus, w.qfrag, (int)h->count, (int)n_tiles, w.seed, w.part_s, w.part_i,
-          w.heads_s, w.heads_i, w.heads_n, groups);
+      static const int wide_mode = [] {
+        const char* v = std::getenv("RAGMI_WIDE_MODE");   // diagnostic timing variants
+        return v ? std::atoi(v) : 0;
+      }();
+      if (wide_mode == 1)
+        scan_wide_kernel<D, 1><<<dim3(grid), dim3(64 * kWideWaves), 0, st>>>(
+            h->corpus, w.qfrag, (int)h->count, (int)n_tiles, w.seed, w.part_s, w.part_i,
+            w.heads_s, w.heads_i, w.heads_n, groups);
+      else if (wide_mode == 2)
+        scan_wide_kernel<D, 2><<<dim3(grid), dim3(64 * kWideWaves), 0, st>>>(
+            h->corpus, w.qfrag, (int)h->count, (int)n_tiles, w.seed, w.part_s, w.part_i,
+            w.heads_s, w.heads_i, w.heads_n, groups);
+      else
+        scan_wide_kernel<D><<<dim3(grid), dim3(64 * kWideWaves), 0, st>>>(
+            h->corpus, w.qfrag, (int)h->count, (int)n_tiles, w.seed, w.part_s, w.part_i,
+            w.heads_s, w.heads_i, w.heads_n, groups);
     } else if (groups == 1) {
       if (filt)
         scan_lds_kernel<D, true, true><<<g3, b3, 0, st>>>(RAG_SCAN_ARGS, groups, w.progress);

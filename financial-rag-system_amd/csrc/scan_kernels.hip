@@ -971,7 +971,9 @@ __device__ __forceinline__ void wtopk_finish(WideTopK& st, int lane, int qt, int
 constexpr int kWideBufs = 4;
 constexpr int kWideWaves = 8;
 
-template <int D>
+// MODE (diagnostic timing variants, RAGMI_WIDE_MODE): 0 production; 1 no top-k (MFMA + a
+// running max); 2 loads and barriers only
+template <int D, int MODE = 0>
 __global__ __launch_bounds__(64 * kWideWaves, 1) void scan_wide_kernel(
     const half8* __restrict__ corpus, const half8* __restrict__ qfrag, int n_rows, int n_tiles,
     const float* __restrict__ seed_thr, float* __restrict__ part_s, int* __restrict__ part_i,
@@ -1038,16 +1040,24 @@ __global__ __launch_bounds__(64 * kWideWaves, 1) void scan_wide_kernel(
     __builtin_amdgcn_s_barrier();   // tile j landed for all; everyone is past tile j-1
     asm volatile("" ::: "memory");  // no LDS read of tile j may be scheduled above it
     issue(j + 3);                   // slot (j+3)%4 == (j-1)%4
-    if (active) {                   // waves of absent groups (B <= 96) only stage and sync
+    if (active && MODE < 2) {       // waves of absent groups (B <= 96) only stage and sync
       const half8* tb = ring + (j % kWideBufs) * TILE + lane;
       floatx4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < S; ++s)
         acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(tb[s * 64], qf[s], acc, 0, 0, 0);
-      wtopk_tile(st, acc, b + j * nb, n_rows, lane);
+      if constexpr (MODE == 0) {
+        wtopk_tile(st, acc, b + j * nb, n_rows, lane);
+      } else {
+        st.thr = fmaxf(st.thr, fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3])));
+      }
     }
   }
-  if (active) wtopk_finish(st, lane, qt, b, nw, part_s, part_i, heads_s, heads_i, heads_n);
+  if constexpr (MODE == 1) {
+    if (active && st.thr == 1e30f) heads_n[0] = 0;    // keeps the MFMAs live
+  }
+  if constexpr (MODE == 0)
+    if (active) wtopk_finish(st, lane, qt, b, nw, part_s, part_i, heads_s, heads_i, heads_n);
 }
 
 // ----------------------------------------------------------------------------------------
@@ -1196,11 +1206,8 @@ __global__ __launch_bounds__(256) void thresh_kernel(const float* __restrict__ s
   seed_thr += blockIdx.y * kQ;
   const float* v = smax + (int64_t)q * n_sample;
   float m = kNegInf;
-  float x[kMaxSample / 256];
-#pragma unroll
-  for (int i = 0; i < kMaxSample / 256; ++i) x[i] = v[min(tid + 256 * i, n_sample - 1)];
-#pragma unroll
-  for (int i = 0; i < kMaxSample / 256; ++i) m = (tid + 256 * i < n_sample) ? fmaxf(m, x[i]) : m;
+#pragma unroll 16
+  for (int i = tid; i < n_sample; i += 256) m = fmaxf(m, v[i]);
   int id = tid;
   bitonic_sort64(m, id, lane);
   if (lane < 32) w_s[wid][lane] = m;
