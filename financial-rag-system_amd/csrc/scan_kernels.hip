@@ -147,15 +147,15 @@ __device__ __forceinline__ void flush_query(const WaveTopK& w, int q, int lane, 
   }
   lds_fence();
   const float nt = __shfl(s, 31, 64);
-  if ((lane & 15) == c) {
-    if (qt == 0) {
-      thr0 = fmaxf(thr0, nt);
-      cnt0 = 0;
-    } else {
-      thr1 = fmaxf(thr1, nt);
-      cnt1 = 0;
-    }
-  }
+  // value selects, not a branch on qt: a qt-dependent choice between the thr0/thr1 (cnt0/cnt1)
+  // references becomes a select of pointers into the caller's state, which keeps that state
+  // in memory (promoted to LDS: a ds_read + lgkmcnt wait on every tile of the scan)
+  const bool mine = (lane & 15) == c;
+  const bool m0 = mine && qt == 0, m1 = mine && qt != 0;
+  thr0 = m0 ? fmaxf(thr0, nt) : thr0;
+  cnt0 = m0 ? 0 : cnt0;
+  thr1 = m1 ? fmaxf(thr1, nt) : thr1;
+  cnt1 = m1 ? 0 : cnt1;
 }
 
 __device__ __forceinline__ void flush_mask(const WaveTopK& w, uint64_t b, int qt, int lane,
@@ -377,7 +377,7 @@ __global__ __launch_bounds__(256, 2) void scan_kernel(
   }
 
   float vmax = kNegInf;   // MODE 1/2: keeps the work alive
-  auto process_v = [&](const half8(&a)[S], int t) {
+  auto process_v = [&](const half8(&a)[S], int t) __attribute__((always_inline)) {
     if constexpr (MODE == 2) {
       half8 x = a[0];
 #pragma unroll
