@@ -318,6 +318,10 @@ int bench_scan(rag_index* h, const float* q, int B, int variant, int reps, doubl
   qprep_kernel<D><<<dim3(kQ), dim3(64), 0, nullptr>>>(q, std::min(B, kQ), nullptr, w.qn,
                                                       w.qfrag, w.filt);
   launch_seed<D, false>(h, w, 1, nullptr);
+  // variant 7: the production kernel with every seed threshold at +inf, i.e. the top-k's
+  // per-tile compares and branches with no candidate ever taken (its fixed cost)
+  if (variant == 7)
+    RAG_HIP(hipMemsetD32(reinterpret_cast<hipDeviceptr_t>(w.seed), 0x7f800000, kQ));
   const int64_t n_tiles = (h->count + 15) / 16;
   int grid = (int)std::min<int64_t>(h->max_wgs, std::max<int64_t>(1, (n_tiles + 3) / 4));
   grid = std::min(grid, kMaxLists / kWavesPerWG);
@@ -332,6 +336,7 @@ int bench_scan(rag_index* h, const float* q, int B, int variant, int reps, doubl
       case 3: launch_variant<D, 3>(h, w, grid, nullptr); break;
       case 4: launch_variant<D, 4>(h, w, grid, nullptr); break;
       case 5: launch_variant<D, 5>(h, w, grid, nullptr); break;
+      case 7: launch_variant<D, 0>(h, w, grid, nullptr); break;
       default: launch_variant<D, 6>(h, w, grid, nullptr); break;
     }
   };
@@ -640,7 +645,7 @@ int rag_merge_topk_packed(const int32_t* in_packed, int n_lists, int B, int k, f
 int rag_bench_scan(rag_index_t* h, const float* queries_dev, int B, int variant, int reps,
                    double* avg_ms) {
   ragmi::clear_error();
-  if (!h || !queries_dev || B < 1 || reps < 1 || !avg_ms || variant < 0 || variant > 6)
+  if (!h || !queries_dev || B < 1 || reps < 1 || !avg_ms || variant < 0 || variant > 7)
     return ragmi::fail(RAG_EINVAL, "bad bench args");
   std::lock_guard<std::mutex> lk(h->mu);
   RAG_HIP(hipSetDevice(h->device));

@@ -222,10 +222,12 @@ __device__ __forceinline__ void topk_tile(ScanTopK& st, const floatx4& acc0, con
   const int rbase = t * kTileRows + 4 * (lane >> 4);
   uint4 tg = {0u, 0u, 0u, 0u};
   if constexpr (FILTER) tg = *reinterpret_cast<const uint4*>(tags + rbase);
+  // every tile but the shard's last is full: no per-row bound check there (wave-uniform)
+  const bool full = (t + 1) * kTileRows <= n_rows;
   float v0[4], v1[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const bool ok = (rbase + r) < n_rows;
+    const bool ok = full || (rbase + r) < n_rows;
     bool ok0 = ok, ok1 = ok;
     if constexpr (FILTER) {
       const uint32_t tr = r == 0 ? tg.x : r == 1 ? tg.y : r == 2 ? tg.z : tg.w;
@@ -559,10 +561,12 @@ __device__ __forceinline__ void rtopk_tile(RegTopK& st, const floatx4& acc0, con
   const int rbase = t * kTileRows + 4 * (lane >> 4);
   uint4 tg = {0u, 0u, 0u, 0u};
   if constexpr (FILTER) tg = *reinterpret_cast<const uint4*>(tags + rbase);
+  // every tile but the shard's last is full: no per-row bound check there (wave-uniform)
+  const bool full = (t + 1) * kTileRows <= n_rows;
   float v0[4], v1[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const bool ok = (rbase + r) < n_rows;
+    const bool ok = full || (rbase + r) < n_rows;
     bool ok0 = ok, ok1 = ok;
     if constexpr (FILTER) {
       const uint32_t tr = r == 0 ? tg.x : r == 1 ? tg.y : r == 2 ? tg.z : tg.w;
