@@ -1210,8 +1210,11 @@ __global__ __launch_bounds__(256) void thresh_kernel(const float* __restrict__ s
   seed_thr += blockIdx.y * kQ;
   const float* v = smax + (int64_t)q * n_sample;
   float m = kNegInf;
-#pragma unroll 16
-  for (int i = tid; i < n_sample; i += 256) m = fmaxf(m, v[i]);
+  float x[kMaxSample / 256];
+#pragma unroll
+  for (int i = 0; i < kMaxSample / 256; ++i) x[i] = v[min(tid + 256 * i, n_sample - 1)];
+#pragma unroll
+  for (int i = 0; i < kMaxSample / 256; ++i) m = (tid + 256 * i < n_sample) ? fmaxf(m, x[i]) : m;
   int id = tid;
   bitonic_sort64(m, id, lane);
   if (lane < 32) w_s[wid][lane] = m;
