@@ -185,7 +185,9 @@ def main():
     # (profiles/r01c_streams.txt), qps by batches in flight 1/2/3/4: 1.25M rows 146K / 177K /
     # 185K / 196K; 2.5M 89K / 99K / - / 103K; 5M 49.8K / 54.1K / - / 53.4K; 10M 26.5K / 27.9K /
     # - / 27.7K. Shards below 4M rows keep 4 in flight, larger ones 2 — except the single-GPU
-    # 10M run (the headline), which keeps 1 so its scan-kernel timing has no overlap.
+    # 10M run (the headline), which keeps 1 so its scan-kernel timing has no overlap. Not
+    # more than 4: a process gets 4 hardware queues (GPU_MAX_HW_QUEUES), and 6 or 8 streams
+    # sharing them measured 149K against 210K qps at 1.25M rows (profiles/r01f_small_shard_streams.jsonl).
     rows_local = hi - lo
     n_streams = args.streams or (4 if rows_local < 4_000_000 else (1 if world == 1 else 2))
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev)
