@@ -150,6 +150,9 @@ def main():
     ap.add_argument("--streams", type=int, default=0,
                     help="batches in flight (0 = by shard size: 4 below 4M rows per GPU, "
                          "else 2; 1 on a single GPU)")
+    ap.add_argument("--scan-order", choices=["auto", "serial", "free"], default="auto",
+                    help="serial: each batch's scan waits for the previous batch's scan "
+                         "(rag_index_set_scan_order); free: scans on different streams overlap")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -184,12 +187,20 @@ def main():
     # 3% of a 10M-row step but ~20% of a 1.25M-row one (8-GPU shard). Measured on one MI355X
     # (profiles/r01c_streams.txt), qps by batches in flight 1/2/3/4: 1.25M rows 146K / 177K /
     # 185K / 196K; 2.5M 89K / 99K / - / 103K; 5M 49.8K / 54.1K / - / 53.4K; 10M 26.5K / 27.9K /
-    # - / 27.7K. Shards below 4M rows keep 4 in flight, larger ones 2 — except the single-GPU
-    # 10M run (the headline), which keeps 1 so its scan-kernel timing has no overlap. Not
-    # more than 4: a process gets 4 hardware queues (GPU_MAX_HW_QUEUES), and 6 or 8 streams
-    # sharing them measured 149K against 210K qps at 1.25M rows (profiles/r01f_small_shard_streams.jsonl).
+    # - / 27.7K. Shards below 4M rows keep 4 in flight, larger ones 2. Not more than 4: a
+    # process gets 4 hardware queues (GPU_MAX_HW_QUEUES), and 6 or 8 streams sharing them
+    # measured 149K against 210K qps at 1.25M rows (profiles/r01f_small_shard_streams.jsonl).
+    # Scan order (rag_index_set_scan_order): at >= 4M rows per GPU the scans are chained
+    # (serial) so only the ~40 us of per-batch prep / seeding / select overlaps another batch's
+    # scan and every scan launch runs alone on HBM — 10M rows, 2 in flight: 27.4K qps with the
+    # scan at 83.2% of the roofline (free order 27.5K but each scan 3% longer; 1 in flight
+    # 26.8K); small shards keep free order, where overlapping scan ramps/tails is the gain
+    # (1.25M rows, 4 in flight: 195K free vs 193K serial) — profiles/r01h_scan_order.jsonl.
     rows_local = hi - lo
-    n_streams = args.streams or (4 if rows_local < 4_000_000 else (1 if world == 1 else 2))
+    n_streams = args.streams or (4 if rows_local < 4_000_000 else 2)
+    serial = args.scan_order == "serial" or (args.scan_order == "auto"
+                                             and rows_local >= 4_000_000)
+    idx.set_scan_order(serial)
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev)
                                                   for _ in range(n_streams - 1)]
     n_step = [0]
@@ -225,9 +236,10 @@ def main():
     scan_avg_ms = scan_ms / max(launches, 1)
     # With several batches in flight a scan launch shares HBM with the other batches' scans,
     # so its duration over the timed region is not the kernel's own rate: time the same
-    # workload once more on ONE stream (after the timed region, not part of `value`).
+    # workload once more on ONE stream (after the timed region, not part of `value`). Serial
+    # scan order already keeps every scan launch alone.
     alone_ms = scan_avg_ms
-    if len(streams) > 1:
+    if len(streams) > 1 and not serial:
         torch.cuda.synchronize()
         idx.profile(True)
         for k in range(min(args.steps, 20)):
@@ -284,7 +296,8 @@ def main():
                                    (" + RCCL all-gather merge" if world > 1 else ""),
                        "corpus_rows": n_total, "dim": D, "batch": B, "k": K_TOP,
                        "rows_per_gpu": local_rows, "parallelism": f"corpus-shard{world}",
-                       "batches_in_flight": n_streams},
+                       "batches_in_flight": n_streams,
+                       "scan_order": "serial" if serial else "free"},
             "recall_at_5": recall5,
             "top15_exact_vs_oracle": exact,
             "roofline": {"bound": "hbm", "achieved": round(achieved / 1e9, 1),

@@ -34,6 +34,19 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_addr) {
       : "memory");
 }
 
+// the same with the non-temporal policy (`nt`): for streams read once per pass that are far
+// larger than the Infinity Cache (MI355X_MICROARCH.md ldsdma-fill: chip 6.4 TB/s default
+// policy, 6.5-6.8 nt)
+__device__ __forceinline__ void glds16_nt(const void* gsrc, uint32_t lds_addr) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_addr)
+      : "memory");
+}
+
 // LDS byte address of a __shared__ pointer (for glds16), made provably wave-uniform
 template <typename T>
 __device__ __forceinline__ uint32_t lds_addr_of(const T* p) {

@@ -68,6 +68,12 @@ struct rag_index {
   void* stage = nullptr;
   size_t stage_bytes = 0;
   // profiling
+  // scan order (rag_index_set_scan_order): when set, every scan launch waits for the
+  // previous one (on whichever stream it ran), so passes on several streams overlap their
+  // query prep / seeding / select with another pass's scan but never two scans
+  bool serial_scans = false;
+  hipEvent_t scan_done = nullptr;
+  hipStream_t scan_last = nullptr;
   int prof = 0;                // 0 off; n > 0: time every n-th scan launch
   int64_t prof_seq = 0;
   std::vector<ProfPair> prof_pairs;
@@ -146,6 +152,10 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
     grid = (int)std::min<int64_t>(h->max_wgs, std::max<int64_t>(1, (n_tiles + 3) / 4));
     grid = std::min(grid, kMaxLists / kWavesPerWG);
   }
+  if (h->serial_scans) {
+    if (!h->scan_done) RAG_HIP(hipEventCreateWithFlags(&h->scan_done, hipEventDisableTiming));
+    if (h->scan_last && h->scan_last != st) RAG_HIP(hipStreamWaitEvent(st, h->scan_done, 0));
+  }
   ProfPair pp{};
   const bool timed = h->prof > 0 && (h->prof_seq++ % h->prof) == 0;
   if (timed) {
@@ -166,18 +176,24 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
         const char* v = std::getenv("RAGMI_WIDE_MODE");   // diagnostic timing variants
         return v ? std::atoi(v) : 0;
       }();
+      // ring loads non-temporal by default (the corpus is read once per pass): 50M x 1024,
+      // B = 128 70.3% -> 71.2% of the HBM roofline, loads-only 80.1% -> 85.8%
+      // (profiles/r01h_wide_nt.jsonl); RAGMI_WIDE_NT=0 restores the default policy
+      static const bool wide_nt = [] {
+        const char* v = std::getenv("RAGMI_WIDE_NT");
+        return v ? std::atoi(v) != 0 : true;
+      }();
+#define RAG_WIDE(MODE, NT)                                                                 \
+  scan_wide_kernel<D, MODE, NT><<<dim3(grid), dim3(64 * kWideWaves), 0, st>>>(             \
+      h->corpus, w.qfrag, (int)h->count, (int)n_tiles, w.seed, w.part_s, w.part_i,         \
+      w.heads_s, w.heads_i, w.heads_n, groups)
       if (wide_mode == 1)
-        scan_wide_kernel<D, 1><<<dim3(grid), dim3(64 * kWideWaves), 0, st>>>(
-            h->corpus, w.qfrag, (int)h->count, (int)n_tiles, w.seed, w.part_s, w.part_i,
-            w.heads_s, w.heads_i, w.heads_n, groups);
+        wide_nt ? RAG_WIDE(1, true) : RAG_WIDE(1, false);
       else if (wide_mode == 2)
-        scan_wide_kernel<D, 2><<<dim3(grid), dim3(64 * kWideWaves), 0, st>>>(
-            h->corpus, w.qfrag, (int)h->count, (int)n_tiles, w.seed, w.part_s, w.part_i,
-            w.heads_s, w.heads_i, w.heads_n, groups);
+        wide_nt ? RAG_WIDE(2, true) : RAG_WIDE(2, false);
       else
-        scan_wide_kernel<D><<<dim3(grid), dim3(64 * kWideWaves), 0, st>>>(
-            h->corpus, w.qfrag, (int)h->count, (int)n_tiles, w.seed, w.part_s, w.part_i,
-            w.heads_s, w.heads_i, w.heads_n, groups);
+        wide_nt ? RAG_WIDE(0, true) : RAG_WIDE(0, false);
+#undef RAG_WIDE
     } else if (groups == 1) {
       if (filt)
         scan_lds_kernel<D, true, true><<<g3, b3, 0, st>>>(RAG_SCAN_ARGS, groups, w.progress);
@@ -200,6 +216,10 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
   if (timed) {
     RAG_HIP(hipEventRecord(pp.b, st));
     h->prof_pairs.push_back(pp);
+  }
+  if (h->serial_scans) {
+    RAG_HIP(hipEventRecord(h->scan_done, st));
+    h->scan_last = st;
   }
   const int n_lists = wide ? grid : grid * (kLdsQ ? kLdsWaves : kWavesPerWG);   // per group
   select_kernel<D><<<dim3(Bq), dim3(256), 0, st>>>(w.part_s, w.part_i, w.heads_s, w.heads_i,
@@ -439,6 +459,7 @@ int rag_index_destroy(rag_index_t* h) {
     (void)hipEventDestroy(p.a);
     (void)hipEventDestroy(p.b);
   }
+  if (h->scan_done) (void)hipEventDestroy(h->scan_done);
   if (h->corpus) (void)hipFree(h->corpus);
   if (h->tags) (void)hipFree(h->tags);
   if (h->stage) (void)hipFree(h->stage);
@@ -659,6 +680,15 @@ int rag_profile_enable(rag_index_t* h, int enable) {
   std::lock_guard<std::mutex> lk(h->mu);
   h->prof = enable < 0 ? 0 : enable;
   h->prof_seq = 0;
+  return RAG_OK;
+}
+
+int rag_index_set_scan_order(rag_index_t* h, int serial) {
+  ragmi::clear_error();
+  if (!h) return ragmi::fail(RAG_EINVAL, "index is NULL");
+  std::lock_guard<std::mutex> lk(h->mu);
+  h->serial_scans = serial != 0;
+  h->scan_last = nullptr;
   return RAG_OK;
 }
 

@@ -976,8 +976,8 @@ constexpr int kWideBufs = 4;
 constexpr int kWideWaves = 8;
 
 // MODE (diagnostic timing variants, RAGMI_WIDE_MODE): 0 production; 1 no top-k (MFMA + a
-// running max); 2 loads and barriers only
-template <int D, int MODE = 0>
+// running max); 2 loads and barriers only. NT: ring loads with the non-temporal policy.
+template <int D, int MODE = 0, bool NT = false>
 __global__ __launch_bounds__(64 * kWideWaves, 1) void scan_wide_kernel(
     const half8* __restrict__ corpus, const half8* __restrict__ qfrag, int n_rows, int n_tiles,
     const float* __restrict__ seed_thr, float* __restrict__ part_s, int* __restrict__ part_i,
@@ -1027,7 +1027,12 @@ __global__ __launch_bounds__(64 * kWideWaves, 1) void scan_wide_kernel(
       const char* src = cbase + (int64_t)t * (S * 1024) + wid_u * 4096 + lane * 16;
       const uint32_t dst = ring_addr + (j % kWideBufs) * (TILE * 16) + wid_u * 4096;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) glds16(src + i * 1024, dst + i * 1024);
+      for (int i = 0; i < 4; ++i) {
+        if constexpr (NT)
+          glds16_nt(src + i * 1024, dst + i * 1024);
+        else
+          glds16(src + i * 1024, dst + i * 1024);
+      }
     }
   };
   issue(0);

@@ -69,6 +69,7 @@ INDEX_API = {
                                              c_vp, c_vp, c_vp]),
     "rag_bench_scan": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                       ctypes.POINTER(ctypes.c_double)]),
+    "rag_index_set_scan_order": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "rag_profile_enable": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "rag_profile_scan_ms": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_double), c_i64p]),
 }

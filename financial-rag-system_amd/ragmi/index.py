@@ -199,6 +199,11 @@ class FlatIndex:
                                             out.ctypes.data_as(_lib.c_u32p)))
         return out
 
+    def set_scan_order(self, serial: bool) -> None:
+        """serial=True: each pass's scan waits for the previous pass's scan on any stream
+        (rag_index_set_scan_order); prep / seeding / select still overlap across streams."""
+        check(self._L.rag_index_set_scan_order(self._h, int(bool(serial))))
+
     # ---------------------------------------------------------------- profiling
     def profile(self, every: int | bool) -> None:
         """Time every `every`-th scan launch with HIP events (0/False: off, True: every one)."""

@@ -134,6 +134,15 @@ int rag_merge_topk(const float* in_scores_dev, const int64_t* in_ids_dev, int n_
 int rag_merge_topk_packed(const int32_t* in_packed_dev, int n_lists, int B, int k,
                           float* out_scores_dev, int64_t* out_ids_dev, void* stream);
 
+/* Scan order across streams. serial != 0: each search pass's scan launch waits for the
+ * previous pass's scan, whichever stream that ran on (one HIP event per handle), so passes
+ * issued on several streams overlap their query prep, seed sampling and select with another
+ * pass's scan while the HBM-bound scans themselves run one at a time. serial = 0 (default):
+ * passes on different streams are unordered. No reference counterpart: the reference issues
+ * one HTTP search per query (main.py:232-237); this is serving-loop plumbing for
+ * main2.py:281-295's batch processor with several batches in flight. */
+int rag_index_set_scan_order(rag_index_t* index, int serial);
+
 /* Kernel timing hook for bench.py: average device time (ms) of `rag_index_search` scan-kernel
  * launches measured with HIP events on the launch stream. enable = 0 off; enable = n > 0 records
  * an event pair around every n-th scan launch (each record costs a few us of device idle

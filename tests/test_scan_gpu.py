@@ -230,6 +230,37 @@ def test_one_million_rows_planted_and_exact(gpu):
         np.testing.assert_array_equal(res[t][1], i)
 
 
+@pytest.mark.parametrize("dim,b", [(384, 32), (1024, 128)])
+def test_serial_scan_order_across_streams(gpu, dim, b):
+    """rag_index_set_scan_order(1): batches issued round-robin on 3 streams without host
+    syncs, every scan chained behind the previous one by the handle's event; each batch's
+    result equals the oracle's (and the unordered mode gives the same)."""
+    rng = np.random.default_rng(dim + b)
+    n = 20_000
+    x = rng.standard_normal((n, dim)).astype(np.float32)
+    idx = make_index(gpu, x)
+    enc = idx.export_rows()
+    qs = [x[rng.choice(n, b)] + 0.05 * rng.standard_normal((b, dim)).astype(np.float32)
+          for _ in range(6)]
+    want = [O.search(enc, q, 15) for q in qs]
+    qd = [torch.from_numpy(q).to(gpu) for q in qs]
+    streams = [torch.cuda.Stream(gpu) for _ in range(3)]
+    for serial in (True, False):
+        idx.set_scan_order(serial)
+        torch.cuda.synchronize()
+        outs = []
+        for j, q in enumerate(qd):
+            st = streams[j % 3]
+            st.wait_stream(torch.cuda.current_stream(gpu))
+            with torch.cuda.stream(st):
+                outs.append(idx.search(q, 15))
+        torch.cuda.synchronize()
+        for (s, i), (s2, i2) in zip(outs, want):
+            np.testing.assert_array_equal(i.cpu().numpy(), i2)
+            np.testing.assert_array_equal(s.cpu().numpy(), s2)
+    idx.close()
+
+
 # ---- D = 1024 (config 5: bge-large vectors; queries in LDS, scan_lds_kernel)
 @pytest.mark.parametrize("n,b,k", [(5003, 32, 15), (4096, 128, 15), (777, 45, 16), (33, 3, 5)])
 def test_search_d1024_vs_oracle(gpu, n, b, k):
