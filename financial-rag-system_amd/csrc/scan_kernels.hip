@@ -974,9 +974,12 @@ __device__ __forceinline__ void wtopk_finish(WideTopK& st, int lane, int qt, int
 // next load reuses). The loop issues no VMEM besides the ring loads, so the counts are exact.
 constexpr int kWideBufs = 4;
 constexpr int kWideWaves = 8;
+constexpr int kWidePre = 8;   // tile-fragment LDS reads in flight ahead of the MFMA chain
 
 // MODE (diagnostic timing variants, RAGMI_WIDE_MODE): 0 production; 1 no top-k (MFMA + a
-// running max); 2 loads and barriers only. NT: ring loads with the non-temporal policy.
+// running max); 2 loads and barriers only; 3 production with an infinite threshold (the
+// per-tile check runs, no candidate is ever taken: results invalid). NT: ring loads with the
+// non-temporal policy.
 template <int D, int MODE = 0, bool NT = false>
 __global__ __launch_bounds__(64 * kWideWaves, 1) void scan_wide_kernel(
     const half8* __restrict__ corpus, const half8* __restrict__ qfrag, int n_rows, int n_tiles,
@@ -1007,6 +1010,7 @@ __global__ __launch_bounds__(64 * kWideWaves, 1) void scan_wide_kernel(
   }
   WideTopK st;
   wtopk_init(st, keep + wid * TK, lane, active ? seed_thr + g * kQ + qt * 16 : nullptr);
+  if constexpr (MODE == 3) st.thr = __builtin_inff();
   const int nw = nb;                                             // lists per group
   part_s += (int64_t)g * nw * (kQ * kKS);
   part_i += (int64_t)g * nw * (kQ * kKS);
@@ -1049,13 +1053,27 @@ __global__ __launch_bounds__(64 * kWideWaves, 1) void scan_wide_kernel(
     __builtin_amdgcn_s_barrier();   // tile j landed for all; everyone is past tile j-1
     asm volatile("" ::: "memory");  // no LDS read of tile j may be scheduled above it
     issue(j + 3);                   // slot (j+3)%4 == (j-1)%4
-    if (active && MODE < 2) {       // waves of absent groups (B <= 96) only stage and sync
+    if (active && MODE != 2) {       // waves of absent groups (B <= 96) only stage and sync
       const half8* tb = ring + (j % kWideBufs) * TILE + lane;
       floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+      // Tile fragments read kWidePre steps ahead of the MFMA chain. Left to itself hipcc
+      // keeps only two reads in flight, so every MFMA waits out a full (contended) LDS
+      // latency: 32 of those per tile per wave outlast the tile's HBM time. The MFMA order
+      // (and so every fp32 sum) is unchanged.
+      half8 a[S];
+#pragma unroll
+      for (int s = 0; s < S; ++s) a[s] = tb[s * 64];
 #pragma unroll
       for (int s = 0; s < S; ++s)
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(tb[s * 64], qf[s], acc, 0, 0, 0);
-      if constexpr (MODE == 0) {
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[s], qf[s], acc, 0, 0, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, kWidePre, 0);    // DS reads
+#pragma unroll
+      for (int s = 0; s < S - kWidePre; ++s) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);         // one MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);         // one DS read
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, kWidePre, 0);
+      if constexpr (MODE == 0 || MODE == 3) {
         wtopk_tile(st, acc, b + j * nb, n_rows, lane);
       } else {
         st.thr = fmaxf(st.thr, fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3])));
@@ -1065,7 +1083,7 @@ __global__ __launch_bounds__(64 * kWideWaves, 1) void scan_wide_kernel(
   if constexpr (MODE == 1) {
     if (active && st.thr == 1e30f) heads_n[0] = 0;    // keeps the MFMAs live
   }
-  if constexpr (MODE == 0)
+  if constexpr (MODE == 0 || MODE == 3)
     if (active) wtopk_finish(st, lane, qt, b, nw, part_s, part_i, heads_s, heads_i, heads_n);
 }
 
