@@ -120,7 +120,11 @@ void launch_seed(rag_index* h, Workspace& w, int groups, hipStream_t st) {
   using namespace ragmi;
   const int n_tiles = (int)((h->count + 15) / 16);
   if (n_tiles == 0) return;   // the scan visits no tile; seeds are never read
-  const int n_sample = std::min({n_tiles, std::max(256, n_tiles / 128), kMaxSample});
+  static const int div = [] {
+    const char* v = std::getenv("RAGMI_SAMPLE_DIV");   // tuning knob: 1 / sampled fraction
+    return v ? std::max(1, std::atoi(v)) : 128;
+  }();
+  const int n_sample = std::min({n_tiles, std::max(256, n_tiles / div), kMaxSample});
   sample_kernel<D, FILTER><<<dim3((n_sample + 7) / 8, groups), dim3(256), 0, st>>>(
       h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, n_tiles, n_sample, w.smax);
   thresh_kernel<<<dim3(kQ, groups), dim3(256), 0, st>>>(w.smax, n_sample, w.seed);
