@@ -124,10 +124,13 @@ void launch_seed(rag_index* h, Workspace& w, int groups, hipStream_t st) {
     const char* v = std::getenv("RAGMI_SAMPLE_DIV");   // tuning knob: 1 / sampled fraction
     return v ? std::max(1, std::atoi(v)) : 128;
   }();
-  const int n_sample = std::min({n_tiles, std::max(256, n_tiles / div), kMaxSample});
+  // D = 1024 tiles are 32 KB and config 5 shards hold up to 3.1M of them: a 4096-tile cap
+  // would sample 0.13% of a 50M-row shard and let ~25K rows per query past the seed
+  constexpr int kCap = D > 384 ? kMaxSampleWide : kMaxSample;
+  const int n_sample = std::min({n_tiles, std::max(256, n_tiles / div), kCap});
   sample_kernel<D, FILTER><<<dim3((n_sample + 7) / 8, groups), dim3(256), 0, st>>>(
       h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, n_tiles, n_sample, w.smax);
-  thresh_kernel<<<dim3(kQ, groups), dim3(256), 0, st>>>(w.smax, n_sample, w.seed);
+  thresh_kernel<kCap><<<dim3(kQ, groups), dim3(256), 0, st>>>(w.smax, n_sample, w.seed);
 }
 
 template <int D>
@@ -420,7 +423,8 @@ int rag_index_create(int dim, int64_t capacity_rows, int device, rag_index_t** o
                   hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&w.filt), G * Q * 2 * 4) == hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&w.smax),
-                        G * ragmi::kMaxSample * Q * 4) == hipSuccess &&
+                        G * (dim > 384 ? ragmi::kMaxSampleWide : ragmi::kMaxSample) * Q * 4) ==
+                  hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&w.heads_s),
                         G * ragmi::kMaxLists * Q * 4) == hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&w.heads_i),

@@ -1219,9 +1219,11 @@ __global__ __launch_bounds__(256) void sample_kernel(const half8* __restrict__ c
 // not exceed an exact score it stands for: the bound is lowered by kSeedMargin (relative +
 // absolute) to cover the MFMA-vs-exact difference (fp16 query rounding, fp32 accumulation).
 constexpr float kSeedMargin = 1e-3f;
-constexpr int kMaxSample = 4096;
+constexpr int kMaxSample = 4096;        // sample tiles per query group, D <= 384
+constexpr int kMaxSampleWide = 16384;   // D = 1024 (32 KB tiles: 50M rows = 3.1M tiles)
 constexpr int kCandCap = 256;   // select: compacted heads at/above the lane-max threshold
 
+template <int MAXS>
 __global__ __launch_bounds__(256) void thresh_kernel(const float* __restrict__ smax,
                                                      int n_sample, float* __restrict__ seed_thr) {
   // Each lane takes the max over its group of sample tiles (disjoint groups), each wave
@@ -1233,11 +1235,11 @@ __global__ __launch_bounds__(256) void thresh_kernel(const float* __restrict__ s
   seed_thr += blockIdx.y * kQ;
   const float* v = smax + (int64_t)q * n_sample;
   float m = kNegInf;
-  float x[kMaxSample / 256];
+  float x[MAXS / 256];
 #pragma unroll
-  for (int i = 0; i < kMaxSample / 256; ++i) x[i] = v[min(tid + 256 * i, n_sample - 1)];
+  for (int i = 0; i < MAXS / 256; ++i) x[i] = v[min(tid + 256 * i, n_sample - 1)];
 #pragma unroll
-  for (int i = 0; i < kMaxSample / 256; ++i) m = (tid + 256 * i < n_sample) ? fmaxf(m, x[i]) : m;
+  for (int i = 0; i < MAXS / 256; ++i) m = (tid + 256 * i < n_sample) ? fmaxf(m, x[i]) : m;
   int id = tid;
   bitonic_sort64(m, id, lane);
   if (lane < 32) w_s[wid][lane] = m;
