@@ -128,8 +128,12 @@ void launch_seed(rag_index* h, Workspace& w, int groups, hipStream_t st) {
   // would sample 0.13% of a 50M-row shard and let ~25K rows per query past the seed
   constexpr int kCap = D > 384 ? kMaxSampleWide : kMaxSample;
   const int n_sample = std::min({n_tiles, std::max(256, n_tiles / div), kCap});
-  sample_kernel<D, FILTER><<<dim3((n_sample + 7) / 8, groups), dim3(256), 0, st>>>(
-      h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, n_tiles, n_sample, w.smax);
+  if constexpr (D > 384)   // every query group in one pass over each sample tile
+    sample_wide_kernel<D, FILTER><<<dim3((n_sample + 7) / 8), dim3(256), 0, st>>>(
+        h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, n_tiles, n_sample, w.smax, groups);
+  else
+    sample_kernel<D, FILTER><<<dim3((n_sample + 7) / 8, groups), dim3(256), 0, st>>>(
+        h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, n_tiles, n_sample, w.smax);
   thresh_kernel<kCap><<<dim3(kQ, groups), dim3(256), 0, st>>>(w.smax, n_sample, w.seed);
 }
 

@@ -1094,6 +1094,59 @@ __global__ __launch_bounds__(64 * kWideWaves, 1) void scan_wide_kernel(
 // smax[w][q]. The 32nd largest of these per-wave maxima comes from 32 distinct rows, so it
 // is a lower bound of the global 32nd-best score: thresh_kernel turns it into seed_thr.
 // ----------------------------------------------------------------------------------------
+// per-query maxima of one wave's two sample tiles (sc[tile][query half]) -> smax[q][j]
+template <bool FILTER>
+__device__ __forceinline__ void sample_epilogue(const floatx4 (&sc)[2][2], int t0, int t1,
+                                                bool two, int j0, int lane,
+                                                const uint32_t* __restrict__ tags,
+                                                const uint32_t* __restrict__ filt, int n_rows,
+                                                int n_sample, float* __restrict__ smax) {
+  uint32_t fm0 = 0, fv0 = 0, fm1 = 0, fv1 = 0;
+  if constexpr (FILTER) {
+    fm0 = filt[2 * (lane & 15)];
+    fv0 = filt[2 * (lane & 15) + 1];
+    fm1 = filt[2 * (16 + (lane & 15))];
+    fv1 = filt[2 * (16 + (lane & 15)) + 1];
+  }
+  float mx[2][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int t = u == 0 ? t0 : t1;
+    const floatx4 acc0 = sc[u][0], acc1 = sc[u][1];
+    const int rbase = t * kTileRows + 4 * (lane >> 4);
+    uint4 tg = {0u, 0u, 0u, 0u};
+    if constexpr (FILTER) tg = *reinterpret_cast<const uint4*>(tags + rbase);
+    float m0 = kNegInf, m1 = kNegInf;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const bool ok = (rbase + r) < n_rows;
+      bool ok0 = ok, ok1 = ok;
+      if constexpr (FILTER) {
+        const uint32_t tr = r == 0 ? tg.x : r == 1 ? tg.y : r == 2 ? tg.z : tg.w;
+        ok0 = ok0 && ((tr & fm0) == fv0);
+        ok1 = ok1 && ((tr & fm1) == fv1);
+      }
+      m0 = ok0 ? fmaxf(m0, acc0[r]) : m0;
+      m1 = ok1 ? fmaxf(m1, acc1[r]) : m1;
+    }
+    // lanes l, l^16, l^32, l^48 hold the same queries
+    m0 = fmaxf(m0, __shfl_xor(m0, 16, 64));
+    m0 = fmaxf(m0, __shfl_xor(m0, 32, 64));
+    m1 = fmaxf(m1, __shfl_xor(m1, 16, 64));
+    m1 = fmaxf(m1, __shfl_xor(m1, 32, 64));
+    mx[u][0] = m0;
+    mx[u][1] = m1;
+  }
+  if (lane < 16) {
+    smax[(int64_t)lane * n_sample + j0] = mx[0][0];
+    smax[(int64_t)(16 + lane) * n_sample + j0] = mx[0][1];
+    if (two) {
+      smax[(int64_t)lane * n_sample + j0 + 1] = mx[1][0];
+      smax[(int64_t)(16 + lane) * n_sample + j0 + 1] = mx[1][1];
+    }
+  }
+}
+
 template <int D, bool FILTER>
 __global__ __launch_bounds__(256) void sample_kernel(const half8* __restrict__ corpus,
                                                      const uint32_t* __restrict__ tags,
@@ -1167,50 +1220,70 @@ __global__ __launch_bounds__(256) void sample_kernel(const half8* __restrict__ c
       sc[u][1] = acc1;
     }
   }
-  uint32_t fm0 = 0, fv0 = 0, fm1 = 0, fv1 = 0;
-  if constexpr (FILTER) {
-    fm0 = filt[2 * (lane & 15)];
-    fv0 = filt[2 * (lane & 15) + 1];
-    fm1 = filt[2 * (16 + (lane & 15))];
-    fv1 = filt[2 * (16 + (lane & 15)) + 1];
-  }
-  float mx[2][2];
+  sample_epilogue<FILTER>(sc, t0, t1, two, j0, lane, tags, filt, n_rows, n_sample, smax);
+}
+
+constexpr int kSampleGroups = 4;   // query groups of 32 per wide pass (index_capi kMaxGroups)
+
+// D = 1024 with several query groups: one pass over each sample tile for ALL groups (the
+// grouped sample_kernel re-read every tile once per group: 4x the bytes at B = 128). Same MFMA
+// order per (tile, group, query half) as sample_kernel, so the same maxima.
+template <int D, bool FILTER>
+__global__ __launch_bounds__(256) void sample_wide_kernel(const half8* __restrict__ corpus,
+                                                          const uint32_t* __restrict__ tags,
+                                                          const uint32_t* __restrict__ filt,
+                                                          const half8* __restrict__ qfrag,
+                                                          int n_rows, int n_tiles, int n_sample,
+                                                          float* __restrict__ smax, int groups) {
+  constexpr int S = steps<D>();
+  constexpr int CH = 8;
+  static_assert(S % CH == 0, "sample_wide: D must be a multiple of 256");
+  const int lane = threadIdx.x & 63;
+  const int w = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int j0 = 2 * w;
+  if (j0 >= n_sample) return;
+  const bool two = j0 + 1 < n_sample;
+  const int t0 = (int)(((int64_t)j0 * n_tiles) / n_sample);
+  const int t1 = two ? (int)(((int64_t)(j0 + 1) * n_tiles) / n_sample) : t0;
+  const half8* p0 = corpus + (int64_t)t0 * (S * 64) + lane;
+  const half8* p1 = corpus + (int64_t)t1 * (S * 64) + lane;
+  floatx4 acc[kSampleGroups][2][2];
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int t = u == 0 ? t0 : t1;
-    const floatx4 acc0 = sc[u][0], acc1 = sc[u][1];
-    const int rbase = t * kTileRows + 4 * (lane >> 4);
-    uint4 tg = {0u, 0u, 0u, 0u};
-    if constexpr (FILTER) tg = *reinterpret_cast<const uint4*>(tags + rbase);
-    float m0 = kNegInf, m1 = kNegInf;
+  for (int g = 0; g < kSampleGroups; ++g)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const bool ok = (rbase + r) < n_rows;
-      bool ok0 = ok, ok1 = ok;
-      if constexpr (FILTER) {
-        const uint32_t tr = r == 0 ? tg.x : r == 1 ? tg.y : r == 2 ? tg.z : tg.w;
-        ok0 = ok0 && ((tr & fm0) == fv0);
-        ok1 = ok1 && ((tr & fm1) == fv1);
+    for (int u = 0; u < 2; ++u) acc[g][u][0] = acc[g][u][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int c = 0; c < S / CH; ++c) {
+    half8 a0[CH], a1[CH];
+#pragma unroll
+    for (int s = 0; s < CH; ++s) {
+      a0[s] = __builtin_nontemporal_load(p0 + (c * CH + s) * 64);
+      a1[s] = __builtin_nontemporal_load(p1 + (c * CH + s) * 64);
+    }
+#pragma unroll
+    for (int g = 0; g < kSampleGroups; ++g) {
+      if (g < groups) {
+        const half8* qg = qfrag + g * (2 * S * 64);
+        half8 b0[CH], b1[CH];
+#pragma unroll
+        for (int s = 0; s < CH; ++s) {
+          b0[s] = qg[(c * CH + s) * 64 + lane];
+          b1[s] = qg[(S + c * CH + s) * 64 + lane];
+        }
+#pragma unroll
+        for (int s = 0; s < CH; ++s) {
+          acc[g][0][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0[s], b0[s], acc[g][0][0], 0, 0, 0);
+          acc[g][0][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0[s], b1[s], acc[g][0][1], 0, 0, 0);
+          acc[g][1][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[s], b0[s], acc[g][1][0], 0, 0, 0);
+          acc[g][1][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[s], b1[s], acc[g][1][1], 0, 0, 0);
+        }
       }
-      m0 = ok0 ? fmaxf(m0, acc0[r]) : m0;
-      m1 = ok1 ? fmaxf(m1, acc1[r]) : m1;
-    }
-    // lanes l, l^16, l^32, l^48 hold the same queries
-    m0 = fmaxf(m0, __shfl_xor(m0, 16, 64));
-    m0 = fmaxf(m0, __shfl_xor(m0, 32, 64));
-    m1 = fmaxf(m1, __shfl_xor(m1, 16, 64));
-    m1 = fmaxf(m1, __shfl_xor(m1, 32, 64));
-    mx[u][0] = m0;
-    mx[u][1] = m1;
-  }
-  if (lane < 16) {
-    smax[(int64_t)lane * n_sample + j0] = mx[0][0];
-    smax[(int64_t)(16 + lane) * n_sample + j0] = mx[0][1];
-    if (two) {
-      smax[(int64_t)lane * n_sample + j0 + 1] = mx[1][0];
-      smax[(int64_t)(16 + lane) * n_sample + j0 + 1] = mx[1][1];
     }
   }
+#pragma unroll
+  for (int g = 0; g < kSampleGroups; ++g)
+    if (g < groups)
+      sample_epilogue<FILTER>(acc[g], t0, t1, two, j0, lane, tags, filt + g * (2 * kQ), n_rows,
+                              n_sample, smax + (int64_t)g * kQ * n_sample);
 }
 
 // thresh: one 256-thread workgroup per query slot: seed_thr[q] = 32nd largest of
