@@ -204,6 +204,8 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
         wide_nt ? RAG_WIDE(2, true) : RAG_WIDE(2, false);
       else if (wide_mode == 3)
         wide_nt ? RAG_WIDE(3, true) : RAG_WIDE(3, false);
+      else if (wide_mode == 4)
+        wide_nt ? RAG_WIDE(4, true) : RAG_WIDE(4, false);
       else
         wide_nt ? RAG_WIDE(0, true) : RAG_WIDE(0, false);
 #undef RAG_WIDE

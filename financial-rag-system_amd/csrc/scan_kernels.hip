@@ -978,7 +978,8 @@ constexpr int kWidePre = 8;   // tile-fragment LDS reads in flight ahead of the 
 
 // MODE (diagnostic timing variants, RAGMI_WIDE_MODE): 0 production; 1 no top-k (MFMA + a
 // running max); 2 loads and barriers only; 3 production with an infinite threshold (the
-// per-tile check runs, no candidate is ever taken: results invalid). NT: ring loads with the
+// per-tile check runs, no candidate is ever taken: results invalid); 4 loads, barriers and
+// the tile-fragment LDS reads, no MFMA. NT: ring loads with the
 // non-temporal policy.
 template <int D, int MODE = 0, bool NT = false>
 __global__ __launch_bounds__(64 * kWideWaves, 1) void scan_wide_kernel(
@@ -1063,6 +1064,13 @@ __global__ __launch_bounds__(64 * kWideWaves, 1) void scan_wide_kernel(
       half8 a[S];
 #pragma unroll
       for (int s = 0; s < S; ++s) a[s] = tb[s * 64];
+      if constexpr (MODE == 4) {   // the LDS reads without the MFMAs (diagnostic)
+        uint32_t x = 0;
+#pragma unroll
+        for (int s = 0; s < S; ++s) x ^= __builtin_bit_cast(uint4, a[s]).x;
+        st.cnt ^= (int)x;
+        continue;
+      }
 #pragma unroll
       for (int s = 0; s < S; ++s)
         acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[s], qf[s], acc, 0, 0, 0);
@@ -1082,6 +1090,9 @@ __global__ __launch_bounds__(64 * kWideWaves, 1) void scan_wide_kernel(
   }
   if constexpr (MODE == 1) {
     if (active && st.thr == 1e30f) heads_n[0] = 0;    // keeps the MFMAs live
+  }
+  if constexpr (MODE == 4) {
+    if (active && st.cnt == 0x1234567) heads_n[0] = 0;  // keeps the LDS reads live
   }
   if constexpr (MODE == 0 || MODE == 3)
     if (active) wtopk_finish(st, lane, qt, b, nw, part_s, part_i, heads_s, heads_i, heads_n);
