@@ -41,6 +41,12 @@ struct Workspace {
   int* heads_i = nullptr;
   int* heads_n = nullptr;
   int* progress = nullptr;      // [lists][groups] shared-group scan throttle words
+  float* eps = nullptr;         // [groups][32] per-query |MFMA - exact| score bound (qprep)
+  float* fb_L = nullptr;        // [groups][32] tier-2 rescan floors (select; +inf = none)
+  float* fb_E = nullptr;        // [groups][32] exact k-th candidate scores
+  int* fb_flag = nullptr;       // any tier-2 request in this pass
+  int* fb_tier = nullptr;       // [groups][32] certifying path per query of the last pass
+  unsigned long long* fb_cnt = nullptr;   // [2] tier-1 / tier-2 totals since creation
   hipStream_t owner = nullptr;  // stream of the last pass that used this slot
   bool used = false;
   uint64_t tick = 0;            // last use (LRU rebinding)
@@ -64,6 +70,8 @@ struct rag_index {
   std::mutex mu;
   Workspace ws[kRing];
   uint64_t ws_tick = 0;
+  Workspace* last_ws = nullptr;   // workspace of the most recent search pass
+  int last_bq = 0;                // its query count
   // host staging for *_host entry points
   void* stage = nullptr;
   size_t stage_bytes = 0;
@@ -134,7 +142,7 @@ void launch_seed(rag_index* h, Workspace& w, int groups, hipStream_t st) {
   else
     sample_kernel<D, FILTER><<<dim3((n_sample + 7) / 8, groups), dim3(256), 0, st>>>(
         h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, n_tiles, n_sample, w.smax);
-  thresh_kernel<kCap><<<dim3(kQ, groups), dim3(256), 0, st>>>(w.smax, n_sample, w.seed);
+  thresh_kernel<kCap><<<dim3(kQ, groups), dim3(256), 0, st>>>(w.smax, n_sample, w.eps, w.seed);
 }
 
 template <int D>
@@ -144,7 +152,8 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
   using namespace ragmi;
   // Bq <= 32 * h->groups queries: `groups` query groups of 32 (one for D <= 384)
   const int groups = (Bq + kQ - 1) / kQ;
-  qprep_kernel<D><<<dim3(groups * kQ), dim3(64), 0, st>>>(q, Bq, filt, w.qn, w.qfrag, w.filt);
+  qprep_kernel<D><<<dim3(groups * kQ), dim3(64), 0, st>>>(q, Bq, filt, w.qn, w.qfrag, w.filt,
+                                                          w.eps, w.fb_flag);
   if (filt)
     launch_seed<D, true>(h, w, groups, st);
   else
@@ -183,32 +192,12 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
     const dim3 g3(grid * groups), b3(64 * kLdsWaves);
     if (wide) {
       // all groups in every workgroup, one pass over the corpus (scan_wide_kernel)
-      static const int wide_mode = [] {
-        const char* v = std::getenv("RAGMI_WIDE_MODE");   // diagnostic timing variants
-        return v ? std::atoi(v) : 0;
-      }();
-      // ring loads non-temporal by default (the corpus is read once per pass): 50M x 1024,
-      // B = 128 70.3% -> 71.2% of the HBM roofline, loads-only 80.1% -> 85.8%
-      // (profiles/r01h_wide_nt.jsonl); RAGMI_WIDE_NT=0 restores the default policy
-      static const bool wide_nt = [] {
-        const char* v = std::getenv("RAGMI_WIDE_NT");
-        return v ? std::atoi(v) != 0 : true;
-      }();
-#define RAG_WIDE(MODE, NT)                                                                 \
-  scan_wide_kernel<D, MODE, NT><<<dim3(grid), dim3(64 * kWideWaves), 0, st>>>(             \
-      h->corpus, w.qfrag, (int)h->count, (int)n_tiles, w.seed, w.part_s, w.part_i,         \
-      w.heads_s, w.heads_i, w.heads_n, groups)
-      if (wide_mode == 1)
-        wide_nt ? RAG_WIDE(1, true) : RAG_WIDE(1, false);
-      else if (wide_mode == 2)
-        wide_nt ? RAG_WIDE(2, true) : RAG_WIDE(2, false);
-      else if (wide_mode == 3)
-        wide_nt ? RAG_WIDE(3, true) : RAG_WIDE(3, false);
-      else if (wide_mode == 4)
-        wide_nt ? RAG_WIDE(4, true) : RAG_WIDE(4, false);
-      else
-        wide_nt ? RAG_WIDE(0, true) : RAG_WIDE(0, false);
-#undef RAG_WIDE
+      // ring loads non-temporal (the corpus is read once per pass): 50M x 1024, B = 128
+      // 70.3% -> 71.2% of the HBM roofline, loads-only 80.1% -> 85.8%
+      // (profiles/r01h_wide_nt.jsonl). The diagnostic variants run only via rag_bench_scan.
+      scan_wide_kernel<D, 0, true><<<dim3(grid), dim3(64 * kWideWaves), 0, st>>>(
+          h->corpus, w.qfrag, (int)h->count, (int)n_tiles, w.seed, w.part_s, w.part_i,
+          w.heads_s, w.heads_i, w.heads_n, groups);
     } else if (groups == 1) {
       if (filt)
         scan_lds_kernel<D, true, true><<<g3, b3, 0, st>>>(RAG_SCAN_ARGS, groups, w.progress);
@@ -237,9 +226,27 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
     h->scan_last = st;
   }
   const int n_lists = wide ? grid : grid * (kLdsQ ? kLdsWaves : kWavesPerWG);   // per group
-  select_kernel<D><<<dim3(Bq), dim3(256), 0, st>>>(w.part_s, w.part_i, w.heads_s, w.heads_i,
-                                                   w.heads_n, n_lists, h->corpus, w.qn, k, id_offset,
-                                                   out_s, out_i, out_packed);
+  const Fallback fb{w.fb_L, w.fb_E, w.fb_flag, w.fb_tier, w.fb_cnt};
+  select_kernel<D, false><<<dim3(Bq), dim3(256), 0, st>>>(
+      w.part_s, w.part_i, w.heads_s, w.heads_i, w.heads_n, n_lists, h->corpus, w.qn, k, w.eps,
+      w.seed, fb, id_offset, out_s, out_i, out_packed);
+  // Tier-2 exactness fallback (select_kernel): a rescan over the whole shard for the queries
+  // whose approximate top-32 could not certify the exact top-k, then select over its exact
+  // lists. Both launches exit in their first instructions unless select raised fb_flag
+  // (no host round trip on the hot path).
+  const int rgrid = (int)std::min<int64_t>(std::min(h->max_wgs / 2, kMaxLists / kWavesPerWG),
+                                           std::max<int64_t>(1, (n_tiles + 3) / 4));
+  if (filt)
+    rescan_kernel<D, true><<<dim3(rgrid, groups), dim3(256), 0, st>>>(
+        h->corpus, h->tags, w.filt, w.qfrag, w.qn, w.eps, fb, (int)h->count, (int)n_tiles,
+        w.part_s, w.part_i, w.heads_s, w.heads_i, w.heads_n);
+  else
+    rescan_kernel<D, false><<<dim3(rgrid, groups), dim3(256), 0, st>>>(
+        h->corpus, h->tags, w.filt, w.qfrag, w.qn, w.eps, fb, (int)h->count, (int)n_tiles,
+        w.part_s, w.part_i, w.heads_s, w.heads_i, w.heads_n);
+  select_kernel<D, true><<<dim3(Bq), dim3(256), 0, st>>>(
+      w.part_s, w.part_i, w.heads_s, w.heads_i, w.heads_n, rgrid * kWavesPerWG, h->corpus, w.qn,
+      k, w.eps, w.seed, fb, id_offset, out_s, out_i, out_packed);
   RAG_HIP(hipGetLastError());
   return RAG_OK;
 }
@@ -311,6 +318,8 @@ int search_locked(rag_index* h, const float* q, int B, int k, const uint32_t* fi
     w.owner = st;
     w.tick = ++h->ws_tick;
     int rc;
+    h->last_ws = &w;
+    h->last_bq = Bq;
     if (h->dim == 384)
       rc = launch_search_pass<384>(
           h, w, q + (int64_t)b0 * h->dim, Bq, k, filt ? filt + 2 * b0 : nullptr, id_offset,
@@ -351,7 +360,7 @@ int bench_scan(rag_index* h, const float* q, int B, int variant, int reps, doubl
   Workspace& w = h->ws[0];
   RAG_HIP(hipDeviceSynchronize());
   qprep_kernel<D><<<dim3(kQ), dim3(64), 0, nullptr>>>(q, std::min(B, kQ), nullptr, w.qn,
-                                                      w.qfrag, w.filt);
+                                                      w.qfrag, w.filt, w.eps, w.fb_flag);
   launch_seed<D, false>(h, w, 1, nullptr);
   // variant 7: the production kernel with every seed threshold at +inf, i.e. the top-k's
   // per-tile compares and branches with no candidate ever taken (its fixed cost)
@@ -375,6 +384,51 @@ int bench_scan(rag_index* h, const float* q, int B, int variant, int reps, doubl
       default: launch_variant<D, 6>(h, w, grid, nullptr); break;
     }
   };
+  one();  // warm
+  RAG_HIP(hipEventRecord(a, nullptr));
+  for (int r = 0; r < reps; ++r) one();
+  RAG_HIP(hipEventRecord(b, nullptr));
+  RAG_HIP(hipEventSynchronize(b));
+  float ms = 0.f;
+  RAG_HIP(hipEventElapsedTime(&ms, a, b));
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  RAG_HIP(hipGetLastError());
+  *avg_ms = ms / reps;
+  return RAG_OK;
+}
+
+// Diagnostic A/B of the wide (D = 1024, 33..128 queries, unfiltered) scan's variants
+// (scan_wide_kernel MODE 0..4; 0 is production). Returns avg device ms/launch.
+template <int D>
+int bench_wide(rag_index* h, const float* q, int B, int mode, int reps, double* avg_ms) {
+  using namespace ragmi;
+  Workspace& w = h->ws[0];
+  const int groups = (std::min(B, kQ * kMaxGroups) + kQ - 1) / kQ;
+  if (groups < 2) return ragmi::fail(RAG_EINVAL, "wide scan variants need 33..128 queries");
+  RAG_HIP(hipDeviceSynchronize());
+  qprep_kernel<D><<<dim3(groups * kQ), dim3(64), 0, nullptr>>>(
+      q, std::min(B, groups * kQ), nullptr, w.qn, w.qfrag, w.filt, w.eps, w.fb_flag);
+  launch_seed<D, false>(h, w, groups, nullptr);
+  const int64_t n_tiles = (h->count + 15) / 16;
+  const int grid = (int)std::min<int64_t>(h->max_wgs / 2, std::max<int64_t>(1, n_tiles));
+  auto one = [&]() {
+#define RAG_WIDE(MODE)                                                                     \
+  scan_wide_kernel<D, MODE, true><<<dim3(grid), dim3(64 * kWideWaves), 0, nullptr>>>(      \
+      h->corpus, w.qfrag, (int)h->count, (int)n_tiles, w.seed, w.part_s, w.part_i,         \
+      w.heads_s, w.heads_i, w.heads_n, groups)
+    switch (mode) {
+      case 1: RAG_WIDE(1); break;
+      case 2: RAG_WIDE(2); break;
+      case 3: RAG_WIDE(3); break;
+      case 4: RAG_WIDE(4); break;
+      default: RAG_WIDE(0); break;
+    }
+#undef RAG_WIDE
+  };
+  hipEvent_t a, b;
+  RAG_HIP(hipEventCreate(&a));
+  RAG_HIP(hipEventCreate(&b));
   one();  // warm
   RAG_HIP(hipEventRecord(a, nullptr));
   for (int r = 0; r < reps; ++r) one();
@@ -443,7 +497,15 @@ int rag_index_create(int dim, int64_t capacity_rows, int device, rag_index_t** o
               hipMalloc(reinterpret_cast<void**>(&w.part_i),
                         G * max_lists * Q * ragmi::kKS * 4) == hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&w.progress),
-                        G * ragmi::kMaxLists * 4) == hipSuccess;
+                        G * ragmi::kMaxLists * 4) == hipSuccess &&
+              hipMalloc(reinterpret_cast<void**>(&w.eps), G * Q * 4) == hipSuccess &&
+              hipMalloc(reinterpret_cast<void**>(&w.fb_L), G * Q * 4) == hipSuccess &&
+              hipMalloc(reinterpret_cast<void**>(&w.fb_E), G * Q * 4) == hipSuccess &&
+              hipMalloc(reinterpret_cast<void**>(&w.fb_flag), 16) == hipSuccess &&
+              hipMalloc(reinterpret_cast<void**>(&w.fb_tier), G * Q * 4) == hipSuccess &&
+              hipMalloc(reinterpret_cast<void**>(&w.fb_cnt), 16) == hipSuccess &&
+              hipMemset(w.fb_cnt, 0, 16) == hipSuccess &&
+              hipMemset(w.fb_tier, 0, G * Q * 4) == hipSuccess;
     if (!ok) {
       rag_index_destroy(h);
       return ragmi::fail(RAG_ENOMEM, "workspace allocation failed");
@@ -470,6 +532,12 @@ int rag_index_destroy(rag_index_t* h) {
     if (w.part_s) (void)hipFree(w.part_s);
     if (w.part_i) (void)hipFree(w.part_i);
     if (w.progress) (void)hipFree(w.progress);
+    if (w.eps) (void)hipFree(w.eps);
+    if (w.fb_L) (void)hipFree(w.fb_L);
+    if (w.fb_E) (void)hipFree(w.fb_E);
+    if (w.fb_flag) (void)hipFree(w.fb_flag);
+    if (w.fb_tier) (void)hipFree(w.fb_tier);
+    if (w.fb_cnt) (void)hipFree(w.fb_cnt);
   }
   for (auto& p : h->prof_pairs) {
     (void)hipEventDestroy(p.a);
@@ -686,8 +754,37 @@ int rag_bench_scan(rag_index_t* h, const float* queries_dev, int B, int variant,
     return ragmi::fail(RAG_EINVAL, "bad bench args");
   std::lock_guard<std::mutex> lk(h->mu);
   RAG_HIP(hipSetDevice(h->device));
-  if (h->dim != 384) return ragmi::fail(RAG_EINVAL, "bench variants built for dim 384");
+  if (h->dim == 1024) {
+    if (variant > 4) return ragmi::fail(RAG_EINVAL, "dim 1024: wide scan variants 0..4");
+    return bench_wide<1024>(h, queries_dev, B, variant, reps, avg_ms);
+  }
   return bench_scan<384>(h, queries_dev, B, variant, reps, avg_ms);
+}
+
+int rag_index_exactness_stats(rag_index_t* h, int64_t* tier1, int64_t* tier2,
+                               int32_t* last_tiers, int n_last) {
+  ragmi::clear_error();
+  if (!h || !tier1 || !tier2 || n_last < 0 || (n_last > 0 && !last_tiers))
+    return ragmi::fail(RAG_EINVAL, "bad exactness stats args");
+  std::lock_guard<std::mutex> lk(h->mu);
+  RAG_HIP(hipSetDevice(h->device));
+  RAG_HIP(hipDeviceSynchronize());
+  unsigned long long t1 = 0, t2 = 0;
+  for (auto& w : h->ws) {
+    unsigned long long c[2];
+    RAG_HIP(hipMemcpy(c, w.fb_cnt, sizeof(c), hipMemcpyDeviceToHost));
+    t1 += c[0];
+    t2 += c[1];
+  }
+  *tier1 = (int64_t)t1;
+  *tier2 = (int64_t)t2;
+  if (n_last > 0) {
+    const int n = h->last_ws ? std::min(n_last, h->last_bq) : 0;
+    for (int i = n; i < n_last; ++i) last_tiers[i] = -1;
+    if (n > 0)
+      RAG_HIP(hipMemcpy(last_tiers, h->last_ws->fb_tier, (size_t)n * 4, hipMemcpyDeviceToHost));
+  }
+  return RAG_OK;
 }
 
 int rag_profile_enable(rag_index_t* h, int enable) {

@@ -61,13 +61,29 @@ __global__ __launch_bounds__(64) void upsert_kernel(const float* __restrict__ ve
 //   qfrag [2][D/32][64] half8: B-operand fragments, lane l -> query 16*qt + (l&15),
 //         dims 32s + 8(l>>4) .. +7
 //   filt  [32][2] (tag mask, tag value) per query slot
+//   eps   [32] bound on |MFMA score - exact score| over every stored row (see below)
+//   fb_flag  cleared: no query of this pass needs the tier-2 rescan yet (select sets it)
+//
+// Error bound. Stored rows c are fp16 roundings of unit vectors (||c||_2 <= kRowNorm); the
+// scan scores a = MFMA(c, h) with h = fp16(qn) and fp32 accumulation over D products (each
+// product exact in fp32), the exact score is e = fp32(sum c_k qn_k). Then
+//   |a - e| <= ||c|| ||h - qn||            (query rounding, Cauchy-Schwarz)
+//            + D 2^-23 ||c|| ||h||          (<= D roundings of the fp32 accumulator, each
+//                                            <= 1 ulp: holds for any internal MFMA order)
+//            + 2^-23                        (e's own fp32 rounding)
+// inflated by 2^-10 relative + 2^-22 absolute so the fp32 comparisons that use it in select
+// stay conservative.
 // ----------------------------------------------------------------------------------------
+constexpr double kRowNorm = 1.001;   // fp16(unit vector): ||c|| <= 1 + 2^-11 + sqrt(D) 2^-25
+
 template <int D>
 __global__ __launch_bounds__(64) void qprep_kernel(const float* __restrict__ q, int B,
                                                    const uint32_t* __restrict__ filt_in,
                                                    float* __restrict__ qn,
                                                    half8* __restrict__ qfrag,
-                                                   uint32_t* __restrict__ filt) {
+                                                   uint32_t* __restrict__ filt,
+                                                   float* __restrict__ eps,
+                                                   int* __restrict__ fb_flag) {
   const int b = blockIdx.x;
   const int lane = threadIdx.x;
   const bool live = b < B;
@@ -75,10 +91,12 @@ __global__ __launch_bounds__(64) void qprep_kernel(const float* __restrict__ q, 
     // per-query payload filter (mask, value); padding / unfiltered queries match every row
     filt[2 * b] = (live && filt_in) ? filt_in[2 * b] : 0u;
     filt[2 * b + 1] = (live && filt_in) ? filt_in[2 * b + 1] : 0u;
+    if (b == 0) *fb_flag = 0;
   }
   double norm = 0.0;
   if (live) norm = sqrt(canon_sumsq<D>(q + (int64_t)b * D, lane));
   const int qt = b >> 4, c16 = b & 15;
+  double dq2 = 0.0, hh2 = 0.0;   // ||h - qn||^2, ||h||^2 (lane partials)
   for (int c = lane; c < D / 8; c += 64) {
     half8 h;
 #pragma unroll
@@ -86,9 +104,22 @@ __global__ __launch_bounds__(64) void qprep_kernel(const float* __restrict__ q, 
       const float y = live ? canon_scale(q[(int64_t)b * D + 8 * c + j], norm) : 0.0f;
       qn[b * D + 8 * c + j] = y;
       h[j] = f32_to_f16(y);
+      const double hd = (double)h[j], dd = hd - (double)y;
+      dq2 = fma(dd, dd, dq2);
+      hh2 = fma(hd, hd, hh2);
     }
     const int s = c >> 2, hh = c & 3;
     qfrag[(qt * steps<D>() + s) * 64 + hh * 16 + c16] = h;
+  }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) {
+    dq2 += __shfl_xor(dq2, d, 64);
+    hh2 += __shfl_xor(hh2, d, 64);
+  }
+  if (lane == 0) {
+    double e = kRowNorm * sqrt(dq2) + (double)D * 0x1p-23 * kRowNorm * sqrt(hh2) + 0x1p-23;
+    e = e * (1.0 + 0x1p-10) + 0x1p-22;
+    eps[b] = live ? (float)(e * (1.0 + 0x1p-20)) : 0.0f;   // rounded up past fp32's RNE
   }
 }
 
@@ -976,7 +1007,7 @@ constexpr int kWideBufs = 4;
 constexpr int kWideWaves = 8;
 constexpr int kWidePre = 8;   // tile-fragment LDS reads in flight ahead of the MFMA chain
 
-// MODE (diagnostic timing variants, RAGMI_WIDE_MODE): 0 production; 1 no top-k (MFMA + a
+// MODE (diagnostic timing variants, rag_bench_scan at dim 1024): 0 production; 1 no top-k (MFMA + a
 // running max); 2 loads and barriers only; 3 production with an infinite threshold (the
 // per-tile check runs, no candidate is ever taken: results invalid); 4 loads, barriers and
 // the tile-fragment LDS reads, no MFMA. NT: ring loads with the
@@ -1298,10 +1329,12 @@ __global__ __launch_bounds__(256) void sample_wide_kernel(const half8* __restric
 }
 
 // thresh: one 256-thread workgroup per query slot: seed_thr[q] = 32nd largest of
-// smax[0..n_waves)[q] (-inf if fewer than 32 are finite). MFMA-rounded scores are used only
-// to prune, never to rank, so their rounding is harmless... except that a pruning bound must
-// not exceed an exact score it stands for: the bound is lowered by kSeedMargin (relative +
-// absolute) to cover the MFMA-vs-exact difference (fp16 query rounding, fp32 accumulation).
+// smax[0..n_waves)[q] (-inf if fewer than 32 are finite). The sample scores come from the
+// scan's own MFMA arithmetic (same operands, same accumulation order), so T is a lower bound
+// of the 32nd-best scan score and pruning below it never loses a row of the approximate
+// top-32. The seed is lowered further, by max(kSeedMargin (1 + |T|), 3 eps_q), so that the
+// rows select's tier-1 exactness fallback needs (approximate score >= e_k - eps_q >= T -
+// 2 eps_q) were never pruned: select checks L >= seed and otherwise takes the rescan.
 constexpr float kSeedMargin = 1e-3f;
 constexpr int kMaxSample = 4096;        // sample tiles per query group, D <= 384
 constexpr int kMaxSampleWide = 16384;   // D = 1024 (32 KB tiles: 50M rows = 3.1M tiles)
@@ -1309,7 +1342,8 @@ constexpr int kCandCap = 256;   // select: compacted heads at/above the lane-max
 
 template <int MAXS>
 __global__ __launch_bounds__(256) void thresh_kernel(const float* __restrict__ smax,
-                                                     int n_sample, float* __restrict__ seed_thr) {
+                                                     int n_sample, const float* __restrict__ eps,
+                                                     float* __restrict__ seed_thr) {
   // Each lane takes the max over its group of sample tiles (disjoint groups), each wave
   // sorts its 64 group maxima, wave 0 merges the four top-32s: the 32nd best of the group
   // maxima is attained by 32 distinct rows, so it is a valid lower bound.
@@ -1317,6 +1351,7 @@ __global__ __launch_bounds__(256) void thresh_kernel(const float* __restrict__ s
   const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   smax += (int64_t)blockIdx.y * kQ * n_sample;   // query group
   seed_thr += blockIdx.y * kQ;
+  eps += blockIdx.y * kQ;
   const float* v = smax + (int64_t)q * n_sample;
   float m = kNegInf;
   float x[MAXS / 256];
@@ -1340,7 +1375,9 @@ __global__ __launch_bounds__(256) void thresh_kernel(const float* __restrict__ s
     }
     const float t32 = __shfl(s, 31, 64);
     if (lane == 0)
-      seed_thr[q] = t32 == kNegInf ? kNegInf : t32 - kSeedMargin * (1.0f + fabsf(t32));
+      seed_thr[q] = t32 == kNegInf
+                        ? kNegInf
+                        : t32 - fmaxf(kSeedMargin * (1.0f + fabsf(t32)), 3.0f * eps[q]);
   }
 }
 
@@ -1349,14 +1386,16 @@ __global__ __launch_bounds__(256) void thresh_kernel(const float* __restrict__ s
 // lane l accumulates the 8-element chunks c = l, l+64, ... with fp64 fma in order, then a
 // xor butterfly (32..1) in fp64; lane 0's sum rounded to fp32. oracle/scan_ref.c
 // (orc_exact_score) restates this order bit for bit.
+// NC (row, query) pairs at once: every row chunk is loaded before any arithmetic, so the
+// wave pays one memory round trip instead of NC dependent ones. rows[i] < 0 => out[i] = -inf.
+// Query i is qn + qoff[i] (wave-uniform offsets).
 // ----------------------------------------------------------------------------------------
 template <int D, int NC>
-__device__ __forceinline__ void exact_scores_wave(const half8* __restrict__ corpus,
-                                                  const int (&rows)[NC],
-                                                  const float* __restrict__ qq, int lane,
-                                                  float (&out)[NC]) {
-  // NC candidates at once: every row chunk is loaded before any arithmetic, so the wave pays
-  // one memory round trip instead of NC dependent ones. rows[i] < 0 => out[i] = -inf.
+__device__ __forceinline__ void exact_scores_pairs(const half8* __restrict__ corpus,
+                                                   const int (&rows)[NC],
+                                                   const int (&qoff)[NC],
+                                                   const float* __restrict__ qn, int lane,
+                                                   float (&out)[NC]) {
   constexpr int S = steps<D>();
   double acc[NC];
 #pragma unroll
@@ -1368,10 +1407,11 @@ __device__ __forceinline__ void exact_scores_wave(const half8* __restrict__ corp
       const int row = rows[i] < 0 ? 0 : rows[i];
       h[i] = corpus[(int64_t)(row >> 4) * (S * 64) + (c >> 2) * 64 + (c & 3) * 16 + (row & 15)];
     }
-    const float4 qa = *reinterpret_cast<const float4*>(qq + 8 * c);
-    const float4 qb = *reinterpret_cast<const float4*>(qq + 8 * c + 4);
 #pragma unroll
     for (int i = 0; i < NC; ++i) {
+      const float* qq = qn + qoff[i];
+      const float4 qa = *reinterpret_cast<const float4*>(qq + 8 * c);
+      const float4 qb = *reinterpret_cast<const float4*>(qq + 8 * c + 4);
       double x = acc[i];
       x = fma((double)h[i][0], (double)qa.x, x);
       x = fma((double)h[i][1], (double)qa.y, x);
@@ -1394,6 +1434,34 @@ __device__ __forceinline__ void exact_scores_wave(const half8* __restrict__ corp
     out[i] = rows[i] < 0 ? kNegInf : (float)__shfl(acc[i], 0, 64);
 }
 
+// the same, every pair against one query
+template <int D, int NC>
+__device__ __forceinline__ void exact_scores_wave(const half8* __restrict__ corpus,
+                                                  const int (&rows)[NC],
+                                                  const float* __restrict__ qq, int lane,
+                                                  float (&out)[NC]) {
+  int qoff[NC];
+#pragma unroll
+  for (int i = 0; i < NC; ++i) qoff[i] = 0;
+  exact_scores_pairs<D, NC>(corpus, rows, qoff, qq, lane, out);
+}
+
+// ----------------------------------------------------------------------------------------
+// Exactness fallback state of one search pass (written by select, read by the rescan):
+//   fb_L[q]  approximate-score floor of the tier-2 rescan for query q (+inf: not needed)
+//   fb_E[q]  exact score of the k-th candidate (every true top-k row scores >= it)
+//   *fb_flag 1 if any query of the pass needs the rescan (cleared by qprep)
+//   tier[q]  the path that certified query q's result: 0 check, 1 tier 1, 2 tier 2
+//   cnt[2]   running totals of tier-1 / tier-2 queries (rag_index_exactness_stats)
+// ----------------------------------------------------------------------------------------
+struct Fallback {
+  float* L;
+  float* E;
+  int* flag;
+  int* tier;
+  unsigned long long* cnt;
+};
+
 // ----------------------------------------------------------------------------------------
 // select: one 256-thread workgroup per query merges the n_lists sorted per-wave top-32
 // lists (approximate MFMA scores) into the exact top-k.
@@ -1401,11 +1469,23 @@ __device__ __forceinline__ void exact_scores_wave(const half8* __restrict__ corp
 //     heads is beaten by those 32 heads, so the global top-32 lies inside the 32 selected
 //     lists. (Threshold from lane maxima -> compaction -> small sort; exact column-sort
 //     fallback when ties push more than kCandCap heads past the threshold.)
-//  2. each wave merges 8 of the selected lists (prefetched) -> wave 0 merges the 4 results.
+//  2. each wave merges 8 of the selected lists (prefetched) -> wave 0 merges the 4 results:
+//     A = the approximate top-32, a_32 its last score.
 //  3. exact rescoring of the 32 candidates (exact_score_wave), 8 per wave.
-//  4. sort by (exact score desc, row asc), emit k.
+//  4. sort by (exact score desc, row asc); e_k = the k-th exact score.
+//  5. exactness check. Every row r outside A has a(r) <= a_32, so e(r) <= a_32 + eps_q
+//     (qprep's bound). If e_k > a_32 + eps_q (or A holds every matching row), the k best of
+//     A are the exact top-k: emit. Otherwise every true top-k row has e >= e_k, hence
+//     a >= L = e_k - eps_q, and:
+//     tier 1 (here): if L >= the scan's seed (no such row was pruned) and no per-wave list
+//       whose tail is >= L is full (none dropped one), every row with a >= L sits in some
+//       list: rescore all of them exactly and emit their top-k.
+//     tier 2: otherwise record (L, e_k) in fb and raise fb_flag; rescan_kernel streams the
+//       shard again and select in EXACT_LISTS mode overwrites this query's output.
+// EXACT_LISTS: the lists hold exact scores (rescan_kernel); queries without a tier-2 request
+// return at once; no rescoring, no check.
 // ----------------------------------------------------------------------------------------
-template <int D>
+template <int D, bool EXACT_LISTS>
 __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ part_s,
                                                      const int* __restrict__ part_i,
                                                      const float* __restrict__ heads_s,
@@ -1414,7 +1494,9 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
                                                      int n_lists,
                                                      const half8* __restrict__ corpus,
                                                      const float* __restrict__ qn, int k,
-                                                     int64_t id_offset,
+                                                     const float* __restrict__ eps,
+                                                     const float* __restrict__ seed_thr,
+                                                     Fallback fb, int64_t id_offset,
                                                      float* __restrict__ out_s,
                                                      int64_t* __restrict__ out_i,
                                                      int32_t* __restrict__ out_packed) {
@@ -1430,9 +1512,16 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
   __shared__ int c_i[4][32];
   __shared__ float e_s[32];
   __shared__ int e_i[32];
+  __shared__ int qlist[kMaxLists];   // tier 1: lists whose head is >= L
+  __shared__ int n_q;
+  __shared__ int verdict;            // 0 exact, 1 tier 1, 2 tier 2
+  __shared__ float floor_L, floor_E;
   // query bq of the batch = slot b of query group grp (the scan's per-group lists)
   const int bq = blockIdx.x, grp = bq / kQ, b = bq % kQ;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if constexpr (EXACT_LISTS) {
+    if (!(fb.L[bq] < __builtin_inff())) return;   // no tier-2 request (uniform per group)
+  }
   part_s += (int64_t)grp * n_lists * (kQ * kKS);
   part_i += (int64_t)grp * n_lists * (kQ * kKS);
   heads_s += (int64_t)grp * kQ * n_lists;
@@ -1470,7 +1559,11 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
     bitonic_sort64(m, id, lane);
     if (lane < 32) w_s[wid][lane] = m;
   }
-  if (tid == 0) n_cand = 0;
+  if (tid == 0) {
+    n_cand = 0;
+    n_q = 0;
+    verdict = 0;
+  }
   __syncthreads();
   if (wid == 0) {
     float m = lane < 32 ? w_s[0][lane] : kNegInf;
@@ -1615,9 +1708,14 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
   }
   __syncthreads();
 
-  // ---- 3. exact rescoring, 8 candidates per wave (one round trip)
-  {
-    const float* qq = qn + (int64_t)bq * D;
+  const float* qq = qn + (int64_t)bq * D;
+  // ---- 3. exact rescoring, 8 candidates per wave (one round trip); exact lists as they are
+  if constexpr (EXACT_LISTS) {
+    if (tid < 32) {
+      e_s[tid] = c_s[0][tid];
+      e_i[tid] = c_s[0][tid] != kNegInf ? c_i[0][tid] : kIdNone32;
+    }
+  } else {
     int rows[8];
     float es[8];
 #pragma unroll
@@ -1636,11 +1734,7 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
   }
   __syncthreads();
 
-  // ---- 4. final order by exact score
-  if (wid == 0) {
-    float s = lane < 32 ? e_s[lane] : kNegInf;
-    int id = lane < 32 ? e_i[lane] : kIdNone32;
-    bitonic_sort64(s, id, lane);
+  auto emit = [&](float s, int id) {   // wave 0, lanes < k: (s, id) sorted best-first
     if (lane < k) {
       const bool ok = s != kNegInf;
       if (out_packed) {
@@ -1652,7 +1746,266 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
         out_i[(int64_t)bq * k + lane] = ok ? (int64_t)id + id_offset : (int64_t)-1;
       }
     }
+  };
+
+  // ---- 4. order by exact score; 5. exactness check
+  if (wid == 0) {
+    float s = lane < 32 ? e_s[lane] : kNegInf;
+    int id = lane < 32 ? e_i[lane] : kIdNone32;
+    bitonic_sort64(s, id, lane);
+    int v = 0;
+    if constexpr (!EXACT_LISTS) {
+      const float ek = __shfl(s, k - 1, 64);
+      const float a32 = c_s[0][kKS - 1];
+      const float e = eps[bq];
+      float L = 0.0f;
+      // a32 == -inf: fewer than 32 finite candidates, i.e. A holds every matching row (a
+      // finite seed implies >= 32 rows above it)
+      if (!(a32 == kNegInf || ek > a32 + e)) {
+        L = ek - e;
+        v = (L >= seed_thr[bq]) ? 1 : 2;
+      }
+      if (lane == 0) {
+        verdict = v;
+        floor_L = L;
+        floor_E = ek;
+        fb.L[bq] = v == 2 ? L : __builtin_inff();   // tier 1 may still escalate below
+        fb.E[bq] = ek;
+        fb.tier[bq] = v;
+        if (v == 2) {
+          *fb.flag = 1;
+          atomicAdd(&fb.cnt[1], 1ull);
+        }
+      }
+    }
+    if (v != 1) emit(s, id);   // tier 2: provisional, overwritten by the EXACT_LISTS pass
   }
+  if constexpr (EXACT_LISTS) return;
+  __syncthreads();
+  if (verdict != 1) return;
+
+  // ---- tier 1: every row with approximate score >= L is in a list (checked below)
+  const float L = floor_L;
+  for (int l = tid; l < n_lists; l += 256) {
+    const float h = heads_s[(int64_t)b * n_lists + l];
+    if (h != kNegInf && h >= L) {
+      const int n = heads_n[(int64_t)b * n_lists + l];
+      if (n >= kKS && part_s[at(l, kKS - 1)] >= L) verdict = 2;   // full list: may have dropped one
+      const int p = atomicAdd(&n_q, 1);
+      qlist[p] = l;
+    }
+  }
+  __syncthreads();
+  if (verdict == 2) {
+    if (tid == 0) {
+      fb.L[bq] = L;
+      fb.E[bq] = floor_E;
+      fb.tier[bq] = 2;
+      *fb.flag = 1;
+      atomicAdd(&fb.cnt[1], 1ull);
+    }
+    if (wid == 0) {   // provisional result (the exact pass overwrites it)
+      float s = lane < 32 ? e_s[lane] : kNegInf;
+      int id = lane < 32 ? e_i[lane] : kIdNone32;
+      bitonic_sort64(s, id, lane);
+      emit(s, id);
+    }
+    return;
+  }
+  if (tid == 0) atomicAdd(&fb.cnt[0], 1ull);
+  // each wave: its share of the qualifying lists, entries >= L (a prefix of each sorted
+  // list) rescored 8 at a time into a running exact top-32 (lanes 0..31)
+  float rs = kNegInf;
+  int ri = kIdNone32;
+  const int nql = n_q;
+  for (int i = wid; i < nql; i += 4) {
+    const int l = qlist[i];
+    const int n = heads_n[(int64_t)b * n_lists + l];
+    float s = kNegInf;
+    int id = kIdNone32;
+    if (lane < kKS && lane < n) {
+      s = part_s[at(l, lane)];
+      id = part_i[at(l, lane)];
+    }
+    const int m = __popcll(__ballot(lane < kKS && lane < n && s >= L));
+    for (int c0 = 0; c0 < m; c0 += 8) {
+      int rows[8];
+      float es[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int r = __shfl(id, min(c0 + j, 63), 64);
+        rows[j] = c0 + j < m ? r : -1;
+      }
+      exact_scores_wave<D, 8>(corpus, rows, qq, lane, es);
+      float ns = kNegInf;
+      int ni = kIdNone32;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (lane == 32 + j && rows[j] >= 0) {
+          ns = es[j];
+          ni = rows[j];
+        }
+      }
+      if (lane >= 32) {
+        rs = ns;
+        ri = ni;
+      }
+      bitonic_sort64(rs, ri, lane);
+    }
+  }
+  if (lane < 32) {
+    c_s[wid][lane] = rs;
+    c_i[wid][lane] = ri;
+  }
+  __syncthreads();
+  if (wid == 0) {
+    float s = lane < 32 ? c_s[0][lane] : kNegInf;
+    int id = lane < 32 ? c_i[0][lane] : kIdNone32;
+    for (int v = 1; v < 4; ++v) {
+      if (lane >= 32) {
+        s = c_s[v][63 - lane];
+        id = c_i[v][63 - lane];
+      }
+      bitonic_merge64(s, id, lane);
+    }
+    emit(s, id);
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// rescan (tier-2 exactness fallback): for the queries select flagged (fb.L finite), stream
+// the shard again, keep rows whose approximate score is >= max(L_q, thr - eps_q), score them
+// exactly (canonical arithmetic) and keep per-wave top-32 lists BY EXACT SCORE (thresholds in
+// the exact domain, starting at pred(E_q): every true top-k row scores >= E_q). A true top-k
+// row is in its wave's exact top-32 (k <= 32), so select<EXACT_LISTS> over these lists is the
+// exact top-k. Launched after every select; exits at once unless fb.flag is set.
+// One 4-wave workgroup per CU: query B-fragments staged in LDS, tiles t = gw, gw + nw, ...
+// (the interleave select uses to map a row to its list).
+// ----------------------------------------------------------------------------------------
+template <int D, bool FILTER>
+__global__ __launch_bounds__(256, 1) void rescan_kernel(
+    const half8* __restrict__ corpus, const uint32_t* __restrict__ tags,
+    const uint32_t* __restrict__ filt, const half8* __restrict__ qfrag,
+    const float* __restrict__ qn, const float* __restrict__ eps, Fallback fb, int n_rows,
+    int n_tiles, float* __restrict__ part_s, int* __restrict__ part_i,
+    float* __restrict__ heads_s, int* __restrict__ heads_i, int* __restrict__ heads_n) {
+  constexpr int S = steps<D>();
+  constexpr int CH = S % 8 == 0 ? 8 : (S % 4 == 0 ? 4 : 1);
+  __shared__ int lds[kWavesPerWG * kLdsPerWave];
+  __shared__ half8 qb[2 * S * 64];
+  if (__builtin_amdgcn_readfirstlane(*fb.flag) == 0) return;
+  const int g = blockIdx.y;
+  const float* Lq = fb.L + g * kQ;
+  const float* Eq = fb.E + g * kQ;
+  // any tier-2 query in this group?
+  {
+    const int lane0 = threadIdx.x & 63;
+    const bool any = __ballot(lane0 < kQ && Lq[lane0 & 31] < __builtin_inff()) != 0;
+    if (!any) return;
+  }
+  qfrag += g * (2 * S * 64);
+  filt += g * (2 * kQ);
+  qn += (int64_t)g * kQ * D;
+  eps += g * kQ;
+  const int nw = gridDim.x * kWavesPerWG;
+  part_s += (int64_t)g * nw * (kQ * kKS);
+  part_i += (int64_t)g * nw * (kQ * kKS);
+  heads_s += (int64_t)g * kQ * nw;
+  heads_i += (int64_t)g * kQ * nw;
+  heads_n += (int64_t)g * kQ * nw;
+  for (int i = threadIdx.x; i < 2 * S * 64; i += 256) qb[i] = qfrag[i];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  ScanTopK st;
+  topk_init<FILTER>(st, lds, wid, lane, nullptr, filt);
+  const int c0 = lane & 15, c1 = 16 + (lane & 15);
+  const float L0 = Lq[c0], L1 = Lq[c1];
+  const float ep0 = eps[c0], ep1 = eps[c1];
+  const float inf = __builtin_inff();
+  st.thr0 = L0 < inf ? nextafterf(Eq[c0], kNegInf) : inf;
+  st.thr1 = L1 < inf ? nextafterf(Eq[c1], kNegInf) : inf;
+  __syncthreads();
+
+  const int gw = blockIdx.x * kWavesPerWG + __builtin_amdgcn_readfirstlane(wid);
+  int t_first, t_step, n_mine;
+  tile_sequence<true>(gw, nw, n_tiles, t_first, t_step, n_mine);
+  for (int j = 0; j < n_mine; ++j) {
+    const int t = t_first + j * t_step;
+    const half8* tp = corpus + (int64_t)t * (S * 64) + lane;
+    floatx4 acc0 = {0.f, 0.f, 0.f, 0.f};
+    floatx4 acc1 = {0.f, 0.f, 0.f, 0.f};
+    for (int s0 = 0; s0 < S; s0 += CH) {
+      half8 a[CH];
+#pragma unroll
+      for (int s = 0; s < CH; ++s) a[s] = tp[(s0 + s) * 64];
+#pragma unroll
+      for (int s = 0; s < CH; ++s) {
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[s], qb[(s0 + s) * 64 + lane], acc0, 0,
+                                                      0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[s], qb[(S + s0 + s) * 64 + lane], acc1,
+                                                      0, 0, 0);
+      }
+    }
+    const int rbase = t * kTileRows + 4 * (lane >> 4);
+    uint4 tg = {0u, 0u, 0u, 0u};
+    if constexpr (FILTER) tg = *reinterpret_cast<const uint4*>(tags + rbase);
+    const float f0 = fmaxf(L0, st.thr0 - ep0), f1 = fmaxf(L1, st.thr1 - ep1);
+    bool pass[8];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const bool ok = (rbase + r) < n_rows;
+      bool ok0 = ok, ok1 = ok;
+      if constexpr (FILTER) {
+        const uint32_t tr = r == 0 ? tg.x : r == 1 ? tg.y : r == 2 ? tg.z : tg.w;
+        ok0 = ok0 && ((tr & st.fm0) == st.fv0);
+        ok1 = ok1 && ((tr & st.fm1) == st.fv1);
+      }
+      pass[r] = ok0 && acc0[r] >= f0;
+      pass[4 + r] = ok1 && acc1[r] >= f1;
+    }
+    bool any = false;
+#pragma unroll
+    for (int p = 0; p < 8; ++p) any = any || pass[p];
+    if (!__ballot(any)) continue;
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      uint64_t m = __ballot(pass[p]);
+      while (m) {
+        int ln[8], rows[8], qoff[8];
+        float es[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          ln[i] = m ? (int)__builtin_ctzll(m) : -1;
+          if (m) m &= m - 1;
+          rows[i] = ln[i] >= 0 ? t * kTileRows + 4 * (ln[i] >> 4) + (p & 3) : -1;
+          qoff[i] = ln[i] >= 0 ? ((p >> 2) * 16 + (ln[i] & 15)) * D : 0;
+        }
+        exact_scores_pairs<D, 8>(corpus, rows, qoff, qn, lane, es);
+        float e = kNegInf;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) e = lane == ln[i] ? es[i] : e;
+        if (p < 4) {
+          if (e > st.thr0) {
+            st.w.pend_s[st.cnt0 * 64 + lane] = e;
+            st.w.pend_i[st.cnt0 * 64 + lane] = rbase + (p & 3);
+            ++st.cnt0;
+          }
+        } else {
+          if (e > st.thr1) {
+            st.w.pend_s[(kP + st.cnt1) * 64 + lane] = e;
+            st.w.pend_i[(kP + st.cnt1) * 64 + lane] = rbase + (p & 3);
+            ++st.cnt1;
+          }
+        }
+      }
+    }
+    lds_fence();
+    const uint64_t b0 = __ballot(st.cnt0 > kP - 4);
+    const uint64_t b1 = __ballot(st.cnt1 > kP - 4);
+    if (b0) flush_mask(st.w, b0, 0, lane, st.thr0, st.cnt0, st.thr1, st.cnt1);
+    if (b1) flush_mask(st.w, b1, 1, lane, st.thr0, st.cnt0, st.thr1, st.cnt1);
+  }
+  topk_finish(st, lane, gw, nw, part_s, part_i, heads_s, heads_i, heads_n);
 }
 
 // ----------------------------------------------------------------------------------------

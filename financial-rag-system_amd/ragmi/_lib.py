@@ -70,6 +70,7 @@ INDEX_API = {
     "rag_bench_scan": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                       ctypes.POINTER(ctypes.c_double)]),
     "rag_index_set_scan_order": (ctypes.c_int, [c_vp, ctypes.c_int]),
+    "rag_index_exactness_stats": (ctypes.c_int, [c_vp, c_i64p, c_i64p, c_i32p, ctypes.c_int]),
     "rag_profile_enable": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "rag_profile_scan_ms": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_double), c_i64p]),
 }

@@ -204,6 +204,18 @@ class FlatIndex:
         (rag_index_set_scan_order); prep / seeding / select still overlap across streams."""
         check(self._L.rag_index_set_scan_order(self._h, int(bool(serial))))
 
+    def exactness_stats(self, n_last: int = 0):
+        """(tier1 total, tier2 total, tiers of the last pass's first n_last queries): which
+        path certified each top-k (0 error-bound check, 1 list re-scoring, 2 second pass);
+        rag_index_exactness_stats. Synchronises the device."""
+        t1 = ctypes.c_int64()
+        t2 = ctypes.c_int64()
+        last = np.empty((max(n_last, 0),), dtype=np.int32)
+        check(self._L.rag_index_exactness_stats(
+            self._h, ctypes.byref(t1), ctypes.byref(t2),
+            last.ctypes.data_as(_lib.c_i32p) if n_last > 0 else None, int(n_last)))
+        return int(t1.value), int(t2.value), last
+
     # ---------------------------------------------------------------- profiling
     def profile(self, every: int | bool) -> None:
         """Time every `every`-th scan launch with HIP events (0/False: off, True: every one)."""

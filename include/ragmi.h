@@ -53,11 +53,15 @@ enum {
   RAG_ERANGE = -4,   /* row slot beyond capacity, k too large, ... */
 };
 
-/* Largest k a single search may ask for (the reference uses limit=15, main.py:215). The scan
- * keeps the 32 best rows by MFMA score and re-ranks them exactly, so the result is the exact
- * top-k whenever fewer than 33-k rows sit within MFMA error (~1e-5 at D=384, a few 1e-5 at
- * D=1024) of the k-th exact score: always in practice for k <= 16, a boundary effect for
- * k close to 32. */
+/* Largest k a single search may ask for (the reference uses limit=15, main.py:215).
+ * Exactness is unconditional for every k <= RAG_MAX_K: the result is always the exact top-k
+ * by (canonical score desc, row asc). The scan ranks rows by MFMA score (fp16 query, fp32
+ * accumulation) and re-scores its approximate top-32 exactly; a per-query bound eps on
+ * |MFMA score - exact score| (computed at query prep) certifies the result when the k-th
+ * exact score exceeds the 32nd approximate score + eps. When it does not (near-duplicate
+ * rows, k close to 32), every row whose MFMA score is >= (k-th exact score - eps) is
+ * re-scored exactly, from the scan's per-wave lists when they provably hold all of them,
+ * otherwise by a second pass over the shard (see rag_index_exactness_stats). */
 #define RAG_MAX_K 32
 /* Queries handled per scan pass; larger batches run ceil(B/32) passes. */
 #define RAG_QUERY_TILE 32
@@ -133,6 +137,15 @@ int rag_merge_topk(const float* in_scores_dev, const int64_t* in_ids_dev, int n_
  * rag_index_search_packed) gathered from all shards. */
 int rag_merge_topk_packed(const int32_t* in_packed_dev, int n_lists, int B, int k,
                           float* out_scores_dev, int64_t* out_ids_dev, void* stream);
+
+/* Exactness bookkeeping (tests, bench): tier1 / tier2 = number of queries, since the index
+ * was created, whose top-k was certified by the list re-scoring fallback / needed the second
+ * pass over the shard (all other queries passed the error-bound check directly).
+ * last_tiers (host, may be NULL when n_last == 0) receives, for the first n_last queries of
+ * the most recent search pass, 0 / 1 / 2 = the path that certified them (-1 past the pass's
+ * query count). Synchronises the device. */
+int rag_index_exactness_stats(rag_index_t* index, int64_t* tier1, int64_t* tier2,
+                              int32_t* last_tiers, int n_last);
 
 /* Scan order across streams. serial != 0: each search pass's scan launch waits for the
  * previous pass's scan, whichever stream that ran on (one HIP event per handle), so passes

@@ -107,25 +107,35 @@ def rescore(corpus16: np.ndarray, qn: np.ndarray, cand: np.ndarray) -> np.ndarra
     return sc
 
 
+def _blas_scores(corpus16, qn, r0, chunk, tags, mask, value, use_filter):
+    c = corpus16[r0:r0 + chunk].view(np.float16).astype(np.float32)
+    s = qn @ c.T  # [b, chunk]
+    if use_filter:
+        t = tags[r0:r0 + chunk]
+        s[:, (t & mask) != value] = -np.inf
+    return s
+
+
 def search_fast(corpus16: np.ndarray, queries: np.ndarray, k: int, margin: int = 64,
                 chunk: int = 1 << 20, tags: np.ndarray | None = None, mask: int = 0,
-                value: int = 0, use_filter: bool = False):
-    """Same result as search() for large corpora: numpy fp32 BLAS shortlist of k+margin
-    candidates per query (chunked), then canonical exact rescoring and (score desc, row asc)
-    ordering. Exact unless more than `margin` rows lie within fp32-BLAS error of the k-th."""
+                value: int = 0, use_filter: bool = False, stats: dict | None = None):
+    """Same result as search() for large corpora, with a certificate: numpy fp32 BLAS
+    shortlist of k+margin candidates per query (chunked), canonical exact rescoring, (score
+    desc, row asc) ordering. |BLAS - exact| <= delta (fp32 accumulation over D terms of
+    unit-norm operands), so the result is certified when the k-th exact score exceeds the
+    last shortlisted BLAS score + delta; otherwise every row with BLAS score >= (k-th exact
+    - delta) is rescored exactly (the oracle's own exactness fallback, counted in
+    stats["widened"])."""
     queries = np.ascontiguousarray(queries, dtype=np.float32)
     qn = normalize(queries)
     n, d = corpus16.shape
     b = qn.shape[0]
     m = min(k + margin, n)
+    delta = np.float32(2.0 * d * 2.0 ** -24 * 1.01 + 2.0 ** -20)
     best_s = np.full((b, 0), -np.inf, dtype=np.float32)
     best_i = np.zeros((b, 0), dtype=np.int64)
     for r0 in range(0, n, chunk):
-        c = corpus16[r0:r0 + chunk].view(np.float16).astype(np.float32)
-        s = qn @ c.T  # [b, chunk]
-        if use_filter:
-            t = tags[r0:r0 + chunk]
-            s[:, (t & mask) != value] = -np.inf
+        s = _blas_scores(corpus16, qn, r0, chunk, tags, mask, value, use_filter)
         mm = min(m, s.shape[1])
         part = np.argpartition(-s, mm - 1, axis=1)[:, :mm]
         ps = np.take_along_axis(s, part, axis=1)
@@ -139,12 +149,31 @@ def search_fast(corpus16: np.ndarray, queries: np.ndarray, k: int, margin: int =
     ex = rescore(corpus16, qn, cand)
     out_s = np.full((b, k), -np.inf, dtype=np.float32)
     out_i = np.full((b, k), -1, dtype=np.int64)
+    widen = []
     for q in range(b):
         valid = cand[q] >= 0
         ids, sc = cand[q][valid], ex[q][valid]
         order = np.lexsort((ids, -sc.astype(np.float64)))[:k]
         out_s[q, :len(order)] = sc[order]
         out_i[q, :len(order)] = ids[order]
+        # certificate: rows outside the shortlist have BLAS score <= its last one
+        if valid.sum() >= m and len(order) == k:
+            s_m = best_s[q][valid].min()
+            if not sc[order[-1]] > s_m + delta:
+                widen.append(q)
+    for q in widen:
+        floor = np.float32(out_s[q, k - 1] - delta)
+        ids = []
+        for r0 in range(0, n, chunk):
+            s = _blas_scores(corpus16, qn[q:q + 1], r0, chunk, tags, mask, value, use_filter)[0]
+            ids.append(np.nonzero(s >= floor)[0] + r0)
+        ids = np.concatenate(ids)
+        sc = rescore(corpus16, qn[q:q + 1], ids[None, :])[0]
+        order = np.lexsort((ids, -sc.astype(np.float64)))[:k]
+        out_s[q] = sc[order]
+        out_i[q] = ids[order]
+    if stats is not None:
+        stats["widened"] = stats.get("widened", 0) + len(widen)
     return out_s, out_i
 
 
