@@ -55,6 +55,10 @@ class UnsupportedFilter(NotImplementedError):
     pass
 
 
+class LimitTooLarge(ValueError):
+    """query_points(limit > RAG_MAX_K): refused loudly, never answered with empty points."""
+
+
 class PayloadTags:
     """Dictionary-codes up to two keyword payload fields into a per-row uint32 tag
     (16 bits per field, code 0 = field absent) and compiles Qdrant `must` filters on those
@@ -181,9 +185,10 @@ class Collection:
             B = len(filters)
             if limit < 1:
                 return [[] for _ in range(B)]
-            k = min(limit, MAX_K)
             if limit > MAX_K:
-                raise ValueError(f"limit > {MAX_K} is not supported by the GPU top-k")
+                raise LimitTooLarge(f"limit {limit} > {MAX_K} is not supported by the GPU "
+                                    f"top-k (the reference uses limit=15, main.py:215)")
+            k = limit
             live = [i for i, f in enumerate(filters) if f is not None]
             out = [[] for _ in range(B)]
             if not live or self.index.count == 0:

@@ -115,6 +115,12 @@ def _filter(ticker, document_type=None):
 def retrieve_from_qdrant(query_vector, ticker, document_type=None, limit=RETRIEVE_LIMIT):
     if _testing():
         return type("obj", (object,), {"points": []})
+    from .index import MAX_K
+    if int(limit) > MAX_K:
+        # outside the reference's swallow-to-empty (main.py:238-239): an unsupported limit
+        # must not look like "no matching documents"
+        from .qdrant import LimitTooLarge
+        raise LimitTooLarge(f"limit {limit} > {MAX_K} (RAG_MAX_K)")
     try:
         return get_qdrant().query_points(collection_name=COLLECTION_NAME, query=query_vector,
                                          limit=limit,
@@ -151,7 +157,10 @@ def rerank_batch(queries, texts_lists, top_k):
     for i, (q, texts) in enumerate(zip(queries, texts_lists)):
         pairs += [[q, t] for t in texts]
         owner += [i] * len(texts)
-    scores = get_reranker().predict(pairs) if pairs else np.zeros(0, np.float32)
+    # batch_size = all pairs: ONE packed forward (CrossEncoder.predict's default of 32 would
+    # split a 32 x 15 micro-batch into 15 forwards)
+    scores = (get_reranker().predict(pairs, batch_size=len(pairs)) if pairs
+              else np.zeros(0, np.float32))
     out, pos = [], 0
     for i, texts in enumerate(texts_lists):
         s = scores[pos:pos + len(texts)]

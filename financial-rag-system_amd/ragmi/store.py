@@ -42,6 +42,12 @@ def save_index(index, path: str, chunk_rows: int = CHUNK_ROWS) -> None:
     """Write FlatIndex `index` (rows [0, count)) to shard directory `path`."""
     os.makedirs(path, exist_ok=True)
     n, d = index.count, index.dim
+    # meta.json marks a complete save: drop it before the arrays are rewritten in place, so a
+    # crash mid-save leaves an incomplete directory (load refuses it), never a stale meta.json
+    # over partially written rows
+    meta = os.path.join(path, "meta.json")
+    if os.path.exists(meta):
+        os.remove(meta)
     vec = np.lib.format.open_memmap(os.path.join(path, "vectors.f16.npy"), mode="w+",
                                     dtype=np.float16, shape=(n, d))
     tags = np.lib.format.open_memmap(os.path.join(path, "tags.u32.npy"), mode="w+",

@@ -15,7 +15,8 @@
  * reference never changes a valid token's output, so packing is exact.
  * Outputs: RAG_HEAD_CLS_L2 -> fp32 [B][hidden] (L2-normalised CLS vector);
  *          RAG_HEAD_POOLER_CLS -> fp32 [B] (raw logit, identity activation).
- * Built shapes: hidden 384, heads 12 (head_dim 32), intermediate 1536, max_pos <= 512.
+ * Built shapes: hidden/heads 384/12 (bge-small, MiniLM-L6), 768/12 (bge-base) and 1024/16
+ * (bge-large, config 5); head_dim 32 or 64; intermediate = 4 x hidden; max_pos <= 512.
  * Numerics: fp16 (or split fp16x3) GEMM/attention operands, fp32 accumulation / residual
  * stream / LayerNorm / softmax statistics.
  */

@@ -177,6 +177,39 @@ def search_fast(corpus16: np.ndarray, queries: np.ndarray, k: int, margin: int =
     return out_s, out_i
 
 
+def blas_delta(d: int) -> np.float32:
+    """Bound on |numpy fp32 BLAS score - canonical exact score| for unit-norm operands."""
+    return np.float32(2.0 * d * 2.0 ** -24 * 1.01 + 2.0 ** -20)
+
+
+def candidates_above(corpus16: np.ndarray, qn: np.ndarray, floor: np.ndarray,
+                     chunk: int = 1 << 17, row_offset: int = 0):
+    """Every row whose canonical exact score against normalised query q is >= floor[q]:
+    a BLAS pass keeps rows with fp32 score >= floor - delta (a superset), which are then
+    rescored exactly. Returns per query (ids + row_offset, exact scores), unordered. Used to
+    CERTIFY a top-k: with floor = the k-th best exact score among any k returned rows (a
+    lower bound of the true k-th score), the true top-k is inside the result."""
+    qn = np.ascontiguousarray(qn, dtype=np.float32)
+    n, d = corpus16.shape
+    b = qn.shape[0]
+    thr = (np.asarray(floor, np.float32) - blas_delta(d))[:, None]
+    hits = [[] for _ in range(b)]
+    for r0 in range(0, n, chunk):
+        c = corpus16[r0:r0 + chunk].view(np.float16).astype(np.float32)
+        s = qn @ c.T
+        qq, rr = np.nonzero(s >= thr)
+        for q in np.unique(qq):
+            hits[q].append(rr[qq == q] + r0)
+    out = []
+    for q in range(b):
+        ids = np.concatenate(hits[q]) if hits[q] else np.zeros(0, np.int64)
+        sc = rescore(corpus16, qn[q:q + 1], ids[None, :].astype(np.int64))[0] if len(ids) \
+            else np.zeros(0, np.float32)
+        keep = sc >= floor[q]
+        out.append((ids[keep].astype(np.int64) + row_offset, sc[keep]))
+    return out
+
+
 def search_f64_reference(corpus16: np.ndarray, queries: np.ndarray, k: int):
     """Independent numpy formulation used to pin the C oracle in tests: float64 matmul on
     the fp16 corpus against canonically normalised queries, rounded to fp32, full lexsort.

@@ -1,0 +1,130 @@
+"""Config 3 at its real size (BASELINE.json configs[2]): the stage-2 rerank of a 32-query
+micro-batch — 32 x 15 = 480 (query, chunk) pairs of ~220-290 tokens, ~117K packed tokens —
+through the production path the pipeline bench measures: pairs assembled on the GPU from
+cached chunk tokens (rag_build_pairs), ONE packed MiniLM-L6 forward (AUTO GEMM selection:
+the persistent PIPE / WIDE kernels at this token count; fused residual + LayerNorm in fp16,
+forced on once in fp16x3), top-5 per query. Reference: rerank_documents, main.py:241-247
+(main2.py:242 per request); CrossEncoder.predict -> BertForSequenceClassification.
+
+Also the a4 shape: /embed of 64 chunks x ~200-260 tokens through the 12-layer bge-small
+forward (ingest.embed_chunks, ingest.py:52-66; EMBED_BATCH = 64).
+
+Oracle: oracle/bert_ref.py (numpy fp32 restatement pinned to transformers 5.15), computed in
+sub-batches of 32 sequences padded to their longest. Bounds: logits <= 1e-3 (north_star's
+rerank tolerance) and embeddings <= 5e-5 in fp16x3; fp16 fast mode 2e-2 / 2e-3.
+"""
+import numpy as np
+import pytest
+import torch
+
+import bert_ref as R
+
+pytestmark = pytest.mark.gpu
+
+B, K, TOPK = 32, 15, 5
+TOL = {"fp16x3": dict(ce=1e-3, bge=5e-5), "fp16": dict(ce=2e-2, bge=2e-3)}
+
+
+def _padded(ids, types, cu, lo, hi):
+    """Packed sequences [lo, hi) -> right-padded [n, S] ids / types / mask (HF layout)."""
+    lens = np.diff(cu)[lo:hi]
+    S = int(lens.max())
+    n = hi - lo
+    pi = np.zeros((n, S), np.int64)
+    pt = np.zeros((n, S), np.int64)
+    pm = np.zeros((n, S), np.int64)
+    for j in range(n):
+        a, b = cu[lo + j], cu[lo + j + 1]
+        pi[j, :b - a] = ids[a:b]
+        pt[j, :b - a] = types[a:b]
+        pm[j, :b - a] = 1
+    return pi, pt, pm
+
+
+def _oracle(fn, w, cfg, ids, types, cu, sub=32):
+    n = len(cu) - 1
+    return np.concatenate([fn(w, cfg, *_padded(ids, types, cu, lo, min(n, lo + sub)))
+                           for lo in range(0, n, sub)])
+
+
+@pytest.fixture(scope="module")
+def batch(gpu):
+    """32 queries (16-32 tokens, own [CLS]/[SEP]) x 15 retrieved chunks (180-260 tokens)."""
+    from ragmi.pairs import build_pairs, build_pairs_gpu
+    rng = np.random.default_rng(30)
+    lens = rng.integers(16, 33, B)
+    q_ids = np.concatenate([np.r_[101, rng.integers(1000, 30000, L - 2), 102] for L in lens])
+    q_cu = np.r_[0, np.cumsum(lens)].astype(np.int32)
+    n_rows = 2000
+    c_toks = rng.integers(1000, 30000, (n_rows, 260)).astype(np.int16)
+    c_lens = rng.integers(180, 261, n_rows).astype(np.int32)
+    rows = np.stack([rng.choice(n_rows, K, replace=False) for _ in range(B)]).astype(np.int64)
+    args = [torch.from_numpy(a).to(gpu) for a in (q_ids.astype(np.int32), q_cu, rows, c_toks,
+                                                  c_lens)]
+    ids, types, cu, mx = build_pairs_gpu(*args)
+    ids2, types2, cu2, mx2 = build_pairs(*args)
+    torch.testing.assert_close(ids, ids2, rtol=0, atol=0)     # device assembly == torch twin
+    torch.testing.assert_close(types, types2, rtol=0, atol=0)
+    assert mx == mx2 and cu.numel() == B * K + 1
+    T = int(cu[-1])
+    assert 100_000 < T < 140_000, T                           # ~117K tokens, config 3's size
+    return ids, types, cu, mx
+
+
+@pytest.fixture(scope="module")
+def ce_ref(batch):
+    w = R.make_weights(R.MINILM_CE, 2)
+    ids, types, cu, _ = (t.cpu().numpy() if isinstance(t, torch.Tensor) else t for t in batch)
+    return w, _oracle(R.ce_logits, w, R.MINILM_CE, ids, types, cu)
+
+
+@pytest.mark.parametrize("prec", ["fp16x3", "fp16"])
+def test_rerank_480_pairs_vs_oracle(gpu, batch, ce_ref, prec):
+    from ragmi.encoders import HEAD_POOLER_CLS, BertEncoder
+    w, ref = ce_ref
+    ids, types, cu, mx = batch
+    enc = BertEncoder(R.MINILM_CE, w, HEAD_POOLER_CLS, gpu, prec)
+    modes = [-1, 1] if prec == "fp16x3" else [-1]        # AUTO; fused add-LN forced on
+    try:
+        for fusion in modes:
+            enc.set_fusion(fusion)
+            out = enc.forward_device(ids, types, cu, mx).cpu().numpy()
+            d = np.abs(out - ref)
+            print(f"[{prec} fusion={fusion}] 480 pairs: max|d|={d.max():.3e} "
+                  f"mean|d|={d.mean():.3e}")
+            assert d.max() <= TOL[prec]["ce"]
+            # per-query top-5 exactly as main.py:246, wherever the oracle's top-6 scores are
+            # separated by more than twice the measured max deviation (closer pairs may swap
+            # within the tolerance: a tie at this precision)
+            got, want = out.reshape(B, K), ref.reshape(B, K)
+            checked = 0
+            for b in range(B):
+                srt = np.sort(want[b])[::-1]
+                if np.min(np.abs(np.diff(srt[:TOPK + 1]))) > 2 * d.max():
+                    np.testing.assert_array_equal(R.rerank_order(got[b], TOPK),
+                                                  R.rerank_order(want[b], TOPK))
+                    checked += 1
+            assert checked >= B // 4, checked
+    finally:
+        enc.set_fusion(-1)
+        enc.close()
+
+
+@pytest.mark.parametrize("prec", ["fp16x3", "fp16"])
+def test_embed_chunks_64x256_vs_oracle(gpu, prec):
+    """a4: one /embed call of EMBED_BATCH = 64 chunks (~200-260 tokens) through the 12-layer
+    bge-small forward."""
+    from ragmi.encoders import HEAD_CLS_L2, BertEncoder
+    rng = np.random.default_rng(31)
+    lens = rng.integers(200, 261, 64)
+    ids = np.concatenate([np.r_[101, rng.integers(1000, 30000, L - 2), 102] for L in lens])
+    cu = np.r_[0, np.cumsum(lens)].astype(np.int32)
+    types = np.zeros(len(ids), np.int32)
+    w = R.make_weights(R.BGE_SMALL, 1)
+    enc = BertEncoder(R.BGE_SMALL, w, HEAD_CLS_L2, gpu, prec)
+    out = enc.forward_packed(ids.astype(np.int32), types, cu).cpu().numpy()
+    ref = _oracle(R.bge_embed, w, R.BGE_SMALL, ids, types, cu)
+    d = np.abs(out - ref)
+    print(f"[{prec}] embed 64 chunks: max|d|={d.max():.3e}")
+    assert d.max() <= TOL[prec]["bge"]
+    enc.close()

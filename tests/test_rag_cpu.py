@@ -84,3 +84,35 @@ def test_reference_model_constructors():
     assert p.payload["ticker"] == "A"
     fc = m.FieldCondition(key="ticker", match=m.MatchValue(value="AAPL"))
     assert m.Filter(must=[fc]).must[0].match.value == "AAPL"
+
+
+def test_limit_above_max_k_fails_loudly(monkeypatch):
+    """limit > RAG_MAX_K is refused before the reference's swallow-to-empty wrapper
+    (main.py:238-239): an unsupported limit must not read as 'no documents'."""
+    monkeypatch.setenv("TESTING", "False")
+    import ragmi.rag as rag
+    rag = importlib.reload(rag)
+    from ragmi.qdrant import LimitTooLarge
+    with pytest.raises(LimitTooLarge):
+        rag.retrieve_from_qdrant([0.0] * 384, "aapl", limit=33)
+
+
+def test_rerank_batch_is_one_forward(monkeypatch):
+    """rerank_batch packs every (query, chunk) pair of a micro-batch into ONE predict call
+    (batch_size = all pairs), then splits per request like rerank_documents."""
+    monkeypatch.setenv("TESTING", "False")
+    import ragmi.rag as rag
+    rag = importlib.reload(rag)
+    calls = []
+
+    class FakeCE:
+        def predict(self, pairs, batch_size=32):
+            calls.append((len(pairs), batch_size))
+            return np.arange(len(pairs), dtype=np.float32)[::-1].copy()
+
+    monkeypatch.setattr(rag, "get_reranker", lambda: FakeCE())
+    qs = [f"q{i}" for i in range(32)]
+    texts = [[f"t{i}_{j}" for j in range(15)] for i in range(32)]
+    out = rag.rerank_batch(qs, texts, 5)
+    assert calls == [(480, 480)]
+    assert len(out) == 32 and list(out[0][0]) == [0, 1, 2, 3, 4]

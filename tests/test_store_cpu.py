@@ -160,3 +160,27 @@ def test_sharded_save_world2_load_world3(tmp_path):
                        start_method="spawn")
     res = sorted(q.get(timeout=60) for _ in range(3))
     assert res == [(0, True), (1, True), (2, True)]
+
+
+def test_save_drops_stale_meta_before_rewriting(tmp_path):
+    """A save over an existing shard removes meta.json first: if the rewrite dies midway the
+    directory is refused by load instead of pairing the old meta with partial rows."""
+    _paths()
+    from ragmi import store
+    idx = HostIndex(8, 64)
+    idx.import_rows(np.arange(40 * 8, dtype=np.uint16).reshape(40, 8), 0, None, 40)
+    d = str(tmp_path / "s")
+    store.save_index(idx, d)
+    assert os.path.exists(os.path.join(d, "meta.json"))
+
+    class Boom(HostIndex):
+        def export_rows(self, r0, n):
+            raise RuntimeError("crash mid-save")
+
+    bad = Boom(8, 64)
+    bad.count = 40
+    with pytest.raises(RuntimeError):
+        store.save_index(bad, d)
+    assert not os.path.exists(os.path.join(d, "meta.json"))
+    with pytest.raises(FileNotFoundError):
+        store.read_meta(d)
