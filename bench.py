@@ -206,7 +206,20 @@ def main():
     ap.add_argument("--scan-order", choices=["auto", "serial", "free"], default="auto",
                     help="serial: each batch's scan waits for the previous batch's scan "
                          "(rag_index_set_scan_order); free: scans on different streams overlap")
+    ap.add_argument("--config", choices=["4", "2", "3", "5", "filtered"], default="4",
+                    help="4 (default): the headline 10M x 384 line (BASELINE configs[3] at N "
+                         "GPUs); 2 / 3: encode + search (+ rerank) pipeline over 1M x 384; "
+                         "5: 50M x 1024 at batch 128; filtered: 10M x 384 with per-query "
+                         "ticker filters (scripts/bench_modes.py)")
+    ap.add_argument("--precision", choices=["fp16x3", "fp16"], default="fp16x3",
+                    help="encoder precision for --config 2/3 (fp16x3 = the 1e-3 contract)")
     args = ap.parse_args()
+    if args.config != "4":
+        sys.path.insert(0, os.path.join(ROOT, "scripts"))
+        import bench_modes
+        if args.rows == 10_000_000:
+            args.rows = 0            # each mode's own default size
+        return bench_modes.run(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -1,0 +1,567 @@
+"""bench.py --config modes: one driver-parsable JSON line per BASELINE.json config beside the
+headline (config 4's 10M x 384 line, bench.py's default).
+
+  --config 2        batch of 32 queries -> bge-small encode -> top-15 over 1M x 384 fp16
+  --config 3        ... -> MiniLM-L6 cross-encoder rerank of the 32 x 15 pairs -> top-5
+                    (main.py:_ask_impl stages 1-3 = main2.batch_processor, batched)
+  --config 5        cosine top-15 over 50M x 1024 fp16 at batch 128 (bge-large width)
+  --config filtered 10M x 384 with a 16-ticker payload tag, every query filtered on one ticker
+                    (the reference always filters: main.py:218-236, main2.py:161-163)
+
+Every mode: W untimed warmup steps, K timed steps bracketed by barrier + synchronize, MAX over
+ranks, rank 0 prints the line. Inputs are resident in HBM when the timed region starts.
+Synthetic data (no datasets or checkpoints offline): torch randn corpora in 1M-row chunks,
+seeded synthetic encoder weights of the exact architectures, random token ids.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (os.path.join(ROOT, "financial-rag-system_amd"), os.path.join(ROOT, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+K_TOP, TOPK, B = 15, 5, 32
+CHUNK = 1_000_000
+HBM_PEAK = 8.0e12
+MFMA_PEAK_F16 = 2.5e15       # dense fp16 MFMA, MI355X_MICROARCH.md (no sparsity)
+
+
+def _world():
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")))
+
+
+def _max_over_ranks(vals, dev):
+    world, _ = _world()
+    if world == 1:
+        return vals
+    t = torch.tensor(vals, device=dev, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(v) for v in t]
+
+
+def _sync(dev):
+    torch.cuda.synchronize(dev)
+    if _world()[0] > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+
+
+def gen_chunk(c, dev, rows, dim, seed0):
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed0 + c)
+    return torch.randn((rows, dim), generator=g, device=dev, dtype=torch.float32)
+
+
+def build_shard(idx, lo, hi, n, dim, seed0, dev, tags_fn=None):
+    for c in range(lo // CHUNK, (hi - 1) // CHUNK + 1):
+        rows_c = min(CHUNK, n - c * CHUNK)
+        x = gen_chunk(c, dev, rows_c, dim, seed0)
+        a, b = max(lo, c * CHUNK), min(hi, c * CHUNK + rows_c)
+        rows = torch.arange(a - lo, b - lo, device=dev, dtype=torch.int64)
+        t = tags_fn(np.arange(a, b)) if tags_fn else None
+        idx.upsert(x[a - c * CHUNK:b - c * CHUNK], rows, t, new_count=max(idx.count, b - lo))
+        del x
+    torch.cuda.synchronize(dev)
+
+
+def planted_queries(nb, batch, n, dim, seed0, dev, qseed):
+    """corpus row + 0.05 N(0,1); every 4th batch pure random. Returns (queries, source rows)."""
+    rng = np.random.default_rng(qseed)
+    picks = rng.integers(0, n, (nb, batch))
+    rows = {}
+    for c in sorted(set((picks // CHUNK).ravel().tolist())):
+        x = gen_chunk(c, dev, min(CHUNK, n - c * CHUNK), dim, seed0)
+        for r in np.unique(picks[(picks // CHUNK) == c]):
+            rows[int(r)] = x[int(r) - c * CHUNK].clone()
+        del x
+    g = torch.Generator(device=dev)
+    g.manual_seed(qseed + 1)
+    qs = []
+    for i in range(nb):
+        base = torch.stack([rows[int(r)] for r in picks[i]])
+        noise = torch.randn((batch, dim), generator=g, device=dev)
+        qs.append((base + 0.05 * noise if i % 4 != 3 else noise).contiguous())
+    return qs, picks
+
+
+def _line(metric, value, unit, args, elapsed, world, dtype, data, config, **extra):
+    d = {"metric": metric, "value": round(value, 3), "unit": unit, "n_gpus": world,
+         "steps": args.steps, "warmup": args.warmup,
+         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+         "scaling": "strong" if config.get("corpus_rows") else "weak", "vs_baseline": None,
+         "dtype": dtype, "data": data, "config": config}
+    d.update(extra)
+    return d
+
+
+# ---------------------------------------------------------------------------- configs 2 / 3
+def _ce_flops(cu: np.ndarray, cfg) -> float:
+    """Reference forward FLOPs of a packed batch: every token through every layer (GEMMs
+    2 * (4 H^2 + 2 H FF) per token per layer + attention 4 L^2 H per sequence per layer)."""
+    H, FF, nl = cfg["hidden"], cfg["inter"], cfg["layers"]
+    L = np.diff(cu).astype(np.float64)
+    return float(nl * (2 * (4 * H * H + 2 * H * FF) * L.sum() + 4 * H * (L ** 2).sum()))
+
+
+def _cpu_pipeline_baseline(cfg_id, budget_s, corpus16_sample, n_total, R, bge_w, ce_w,
+                           q_batch, pair_batch):
+    """The reference's CPU stack restated on the host cores: transformers
+    BertModel / BertForSequenceClassification fp32 (the library sentence-transformers runs
+    on) for stage 1 (32 queries) and stage 3 (a bounded sample of the 480 pairs, scaled),
+    numpy fp32 Q.C^T + argpartition top-15 over a 1M-row sample (scaled) for stage 2."""
+    from transformers import BertConfig, BertForSequenceClassification, BertModel
+    torch.set_num_threads(min(16, os.cpu_count() or 16))
+    cores = torch.get_num_threads()
+
+    def hf(cfgd, w, cls):
+        # the same construction as tests/golden/make_golden_bert.py (local config, seeded
+        # weights, eager attention)
+        c = BertConfig(vocab_size=cfgd["vocab"], hidden_size=cfgd["hidden"],
+                       num_hidden_layers=cfgd["layers"], num_attention_heads=cfgd["heads"],
+                       intermediate_size=cfgd["inter"], max_position_embeddings=cfgd["max_pos"],
+                       type_vocab_size=cfgd["type_vocab"], layer_norm_eps=cfgd["eps"],
+                       hidden_act="gelu", hidden_dropout_prob=0.0,
+                       attention_probs_dropout_prob=0.0, num_labels=1,
+                       attn_implementation="eager")
+        seq = cls is BertForSequenceClassification
+        m = cls(c) if seq else cls(c, add_pooling_layer=False)
+        sd = {(k if not seq or k.startswith("classifier") else "bert." + k): torch.from_numpy(v)
+              for k, v in w.items()}
+        m.load_state_dict(sd, strict=False)
+        return m.eval()
+
+    def padded(ids, types, cu):
+        lens = np.diff(cu)
+        S = int(lens.max())
+        pi = np.zeros((len(lens), S), np.int64)
+        pt = np.zeros_like(pi)
+        pm = np.zeros_like(pi)
+        for j in range(len(lens)):
+            a, b = cu[j], cu[j + 1]
+            pi[j, :b - a], pt[j, :b - a], pm[j, :b - a] = ids[a:b], types[a:b], 1
+        return [torch.from_numpy(t) for t in (pi, pt, pm)]
+
+    def timed(fn):
+        fn()
+        t0, reps = time.perf_counter(), 0
+        while True:
+            fn()
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= budget_s / (3 if cfg_id == 3 else 2):
+                return el / reps, reps
+
+    bge = hf(R.BGE_SMALL, bge_w, BertModel)
+    qi, qt, qm = padded(*q_batch)
+    with torch.no_grad():
+        t_enc, r_enc = timed(lambda: bge(input_ids=qi, token_type_ids=qt, attention_mask=qm))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_scan as O
+    c32 = corpus16_sample.view(np.float16).astype(np.float32)
+    qn = np.random.default_rng(0).standard_normal((B, c32.shape[1])).astype(np.float32)
+    qn /= np.linalg.norm(qn, axis=1, keepdims=True)
+
+    def search():
+        s = qn @ c32.T
+        part = np.argpartition(-s, K_TOP - 1, axis=1)[:, :K_TOP]
+        np.take_along_axis(part, np.argsort(-np.take_along_axis(s, part, 1), 1), 1)
+    t_s, r_s = timed(search)
+    t_s *= n_total / c32.shape[0]
+    t_ce, r_ce, frac = 0.0, 0, 0.0
+    if cfg_id == 3:
+        ce = hf(R.MINILM_CE, ce_w, BertForSequenceClassification)
+        ids, types, cu = pair_batch
+        sub = 32                                     # pairs per sample forward
+        ci, ct, cm = padded(ids, types, cu[:sub + 1])
+        with torch.no_grad():
+            t_ce, r_ce = timed(lambda: ce(input_ids=ci, token_type_ids=ct, attention_mask=cm))
+        frac = sub / (len(cu) - 1)
+        t_ce /= frac
+    total = t_enc + t_s + t_ce
+    return {"value": round(B / total, 3), "unit": "queries/s", "cores": int(cores),
+            "kind": "port",
+            "sample": (f"transformers 5.15 BertModel fp32 on 32 queries ({r_enc} reps, "
+                       f"{t_enc * 1e3:.0f} ms/batch); numpy fp32 top-15 over "
+                       f"{c32.shape[0]} of {n_total} rows scaled ({t_s * 1e3:.0f} ms/batch)" +
+                       (f"; transformers BertForSequenceClassification fp32 on {sub} of "
+                        f"{len(cu) - 1} pairs ({r_ce} reps) scaled to the batch "
+                        f"({t_ce * 1e3:.0f} ms/batch)" if cfg_id == 3 else ""))}
+
+
+def run_pipeline(args, cfg_id):
+    import bert_ref as R
+    from ragmi.encoders import HEAD_CLS_L2, HEAD_POOLER_CLS, BertEncoder
+    from ragmi.index import FlatIndex
+    from ragmi.pairs import build_pairs_gpu
+    world, rank = _world()
+    dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+    torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    n, D, prec = args.rows or 1_000_000, 384, args.precision
+    idx = FlatIndex(dim=D, capacity=n, device=dev)
+    build_shard(idx, 0, n, n, D, 1000, dev)
+    g = torch.Generator(device=dev)
+    g.manual_seed(77)
+    c_toks = torch.randint(1000, 30000, (n, 260), generator=g, device=dev,
+                           dtype=torch.int32).to(torch.int16)
+    c_lens = torch.randint(180, 261, (n,), generator=g, device=dev, dtype=torch.int32)
+    rng = np.random.default_rng(3 + rank)
+    batches = []
+    for _ in range(args.warmup + args.steps):
+        lens = rng.integers(16, 33, B)
+        ids = np.concatenate([np.r_[101, rng.integers(1000, 30000, L - 2), 102] for L in lens])
+        batches.append((ids.astype(np.int32), np.zeros(len(ids), np.int32),
+                        np.r_[0, np.cumsum(lens)].astype(np.int32)))
+    bge_w, ce_w = R.make_weights(R.BGE_SMALL, 1), R.make_weights(R.MINILM_CE, 2)
+    bge = BertEncoder(R.BGE_SMALL, bge_w, HEAD_CLS_L2, dev, prec)
+    ce = BertEncoder(R.MINILM_CE, ce_w, HEAD_POOLER_CLS, dev, prec)
+    S = args.streams or 2
+    streams = [torch.cuda.Stream(dev) for _ in range(S)]
+    ev_every = 4                        # CE forward events on every 4th batch (sampled)
+    evs, flops = [], []
+
+    def step(i, timed):
+        ids, tt, cu = batches[i]
+        st = streams[i % S]
+        with torch.cuda.stream(st):
+            q = bge.forward_packed(ids, tt, cu)
+            _, rows = idx.search(q, K_TOP)
+            if cfg_id == 2:
+                return rows, None
+            q_ids = torch.from_numpy(ids).to(dev, non_blocking=True)
+            q_cu = torch.from_numpy(cu).to(dev, non_blocking=True)
+            pid, pty, pcu, mx = build_pairs_gpu(q_ids, q_cu, rows, c_toks, c_lens)
+            rec = timed and i % ev_every == 0
+            if rec:
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(st)
+            logits = ce.forward_device(pid, pty, pcu, mx).view(B, K_TOP)
+            if rec:
+                b.record(st)
+                evs.append((a, b))
+                flops.append(pcu)
+            top = torch.topk(logits, TOPK, dim=1).indices
+            return torch.gather(rows, 1, top), (pid, pty, pcu, logits)
+
+    for i in range(args.warmup):
+        step(i, False)
+    _sync(dev)
+    t0 = time.perf_counter()
+    outs = [step(args.warmup + k, True) for k in range(args.steps)]
+    _sync(dev)
+    elapsed = time.perf_counter() - t0
+    ce_ms = float(np.mean([a.elapsed_time(b) for a, b in evs])) if evs else None
+    flops = [_ce_flops(c.cpu().numpy(), R.MINILM_CE) for c in flops]
+    ce_alone = None
+    if cfg_id == 3:
+        # the same forward re-timed alone on one stream (with S batches in flight the
+        # timed-region events include the other batches' overlapping kernels)
+        pid, pty, pcu, _ = outs[0][1]
+        mx = int(np.diff(pcu.cpu().numpy()).max())
+        ce.forward_device(pid, pty, pcu, mx)
+        torch.cuda.synchronize(dev)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(5):
+            ce.forward_device(pid, pty, pcu, mx)
+        b.record()
+        torch.cuda.synchronize(dev)
+        ce_alone = a.elapsed_time(b) / 5
+    elapsed, = _max_over_ranks([elapsed], dev)
+
+    # parity legs (after the timed region): search top-15 of the first timed batch certified
+    # against the oracle; CE logits of its first query's 15 pairs vs bert_ref
+    import oracle_scan as O
+    extra = {}
+    if not args.no_recall and rank == 0:
+        ids, tt, cu = batches[args.warmup]
+        q = bge.forward_packed(ids, tt, cu)
+        s, rows = idx.search(q, K_TOP)
+        enc = idx.export_rows()
+        qh = q.cpu().numpy()
+        qn = O.normalize(qh)
+        g_i = rows.cpu().numpy()
+        floor = O.rescore(enc, qn, g_i).min(axis=1)
+        cand = O.candidates_above(enc, qn, floor)
+        ok = 0
+        for j, (ci, cs) in enumerate(cand):
+            o = np.lexsort((ci, -cs.astype(np.float64)))[:K_TOP]
+            ok += int(np.array_equal(ci[o], g_i[j]) and np.array_equal(cs[o], s[j].cpu().numpy()))
+        extra["search_top15_exact_queries"] = f"{ok}/{B}"
+        if cfg_id == 3:
+            pid, pty, pcu, logits = outs[0][1]
+            pcu_h = pcu.cpu().numpy()
+            hi = int(pcu_h[K_TOP])
+            sub_cu = pcu_h[:K_TOP + 1]
+            ids_h, ty_h = pid.cpu().numpy()[:hi], pty.cpu().numpy()[:hi]
+            lens = np.diff(sub_cu)
+            Smax = int(lens.max())
+            pi = np.zeros((K_TOP, Smax), np.int64)
+            pt, pm = np.zeros_like(pi), np.zeros_like(pi)
+            for j in range(K_TOP):
+                a, b = sub_cu[j], sub_cu[j + 1]
+                pi[j, :b - a], pt[j, :b - a], pm[j, :b - a] = ids_h[a:b], ty_h[a:b], 1
+            ref = R.ce_logits(ce_w, R.MINILM_CE, pi, pt, pm)
+            extra["rerank_max_abs_diff_vs_oracle"] = float(
+                np.abs(logits[0].cpu().numpy() - ref).max())
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        ids, tt, cu = batches[args.warmup]
+        pb = None
+        if cfg_id == 3:
+            pid, pty, pcu, _ = outs[0][1]
+            pb = (pid.cpu().numpy(), pty.cpu().numpy(), pcu.cpu().numpy())
+        cpu = _cpu_pipeline_baseline(cfg_id, args.cpu_budget, idx.export_rows(0, min(n, CHUNK)),
+                                     n, R, bge_w, ce_w, (ids, tt, cu), pb)
+    if rank == 0:
+        qps = B * args.steps / elapsed * world
+        roof = None
+        if cfg_id == 3 and ce_ms:
+            fl = float(np.mean(flops))
+            ach = fl / (ce_ms * 1e-3)
+            pipe = 3 if prec == "fp16x3" else 1
+            roof = {"bound": "mfma", "achieved": round(ach / 1e12, 2),
+                    "peak": MFMA_PEAK_F16 / 1e12, "unit": "TFLOP/s",
+                    "frac": round(ach / MFMA_PEAK_F16, 4), "traffic": None,
+                    "kernel": f"MiniLM-L6 cross-encoder forward (480 pairs, {prec}; GEMM + "
+                              f"attention + LayerNorm kernels, one packed batch)",
+                    "avg_ms": round(ce_ms, 4), "algorithmic_flops_per_launch": fl,
+                    "mfma_pipe_frac": round(pipe * ach / MFMA_PEAK_F16, 4),
+                    "standalone_avg_ms": round(ce_alone, 4),
+                    "standalone_frac": round(fl / (ce_alone * 1e-3) / MFMA_PEAK_F16, 4),
+                    "standalone_mfma_pipe_frac": round(pipe * fl / (ce_alone * 1e-3) /
+                                                       MFMA_PEAK_F16, 4),
+                    "note": "achieved = reference forward FLOPs (every token, every layer) / "
+                            "event-timed forward; fp16x3 issues 3 MFMAs per product "
+                            "(mfma_pipe_frac)"}
+        line = _line(
+            f"queries/sec, batch=32: bge-small encode + top-15 over {n}x384 fp16" +
+            (" + MiniLM-L6 rerank of 32x15 pairs -> top-5" if cfg_id == 3 else "") +
+            f" (config {cfg_id})", qps, "queries/s", args, elapsed, world, prec,
+            "synthetic (torch randn corpus seeded 1000+c; seeded synthetic weights of the "
+            "bge-small / MiniLM-L6 architectures; random token ids: queries 16-32, chunks "
+            "180-260 tokens)",
+            {"workload": f"config {cfg_id}: 32 queries -> bge-small ({prec}) -> top-15 of "
+                         f"{n}x384" + (" -> CE rerank 480 pairs -> top-5" if cfg_id == 3
+                                       else ""),
+             "batch": B, "k": K_TOP, "rerank_top_k": TOPK if cfg_id == 3 else None,
+             "precision": prec, "batches_in_flight": S,
+             "parallelism": f"replicas{world}" if world > 1 else "1 GPU"},
+            roofline=roof, cpu_baseline=cpu, **extra)
+        line["scaling"] = "weak"
+        print(json.dumps(line), flush=True)
+    idx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+# ---------------------------------------------------------------------------- search configs
+def _filtered_check(idx, q, g_s, g_i, filt, tags_all, lo):
+    """Certified exactness of filtered results (oracle.candidates_above over the rows that
+    pass each query's filter; queries grouped by filter so each row subset is cut once)."""
+    import oracle_scan as O
+    enc = idx.export_rows()
+    qn = O.normalize(q)
+    own = (g_i >= lo) & (g_i < lo + enc.shape[0])
+    e = O.rescore(enc, qn, np.where(own, g_i - lo, -1))
+    floor = e.min(axis=1)
+    ok = 0
+    r5 = np.zeros(len(q))
+    keys = [tuple(f) for f in filt.tolist()]
+    for key in sorted(set(keys)):
+        js = [j for j, kk in enumerate(keys) if kk == key]
+        sub = np.nonzero((tags_all & key[0]) == key[1])[0]
+        cand = O.candidates_above(enc[sub], qn[js], floor[js])
+        for j, (ci, cs) in zip(js, cand):
+            ci = sub[ci] + lo
+            o = np.lexsort((ci, -cs.astype(np.float64)))[:K_TOP]
+            ok += int(np.array_equal(ci[o], g_i[j]) and np.array_equal(cs[o], g_s[j]))
+            r5[j] = len(set(g_i[j, :5].tolist()) & set(ci[o][:5].tolist())) / 5
+    return ok, float(r5.mean()), float(r5.min())
+
+
+def _cpu_search_baseline(sample16, q, n_total, k, budget_s, tags=None, filt=None):
+    """The reference CPU search restated: numpy fp32 Q.C^T (+ the payload filter
+    as a -inf mask) + argpartition top-k over a bounded corpus sample, scaled to n_total."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_scan as O
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([p.get("num_threads", 1) for p in threadpool_info()
+                     if p.get("user_api") == "blas"] or [os.cpu_count()])
+    except Exception:
+        cores = os.cpu_count()
+    c32 = sample16.view(np.float16).astype(np.float32)
+    qn = O.normalize(q)
+    bad = None
+    if filt is not None:
+        bad = (tags[None, :] & filt[:, :1]) != filt[:, 1:2]
+    t0, reps = time.perf_counter(), 0
+    while True:
+        s = qn @ c32.T
+        if bad is not None:
+            s[bad] = -np.inf
+        part = np.argpartition(-s, k - 1, axis=1)[:, :k]
+        np.take_along_axis(part, np.argsort(-np.take_along_axis(s, part, 1), 1), 1)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    t_full = el / reps * (n_total / c32.shape[0])
+    return {"value": round(len(q) / t_full, 3), "unit": "queries/s", "cores": int(cores),
+            "kind": "port",
+            "sample": f"{c32.shape[0]} of {n_total} rows x {len(q)} queries, {reps} reps "
+                      f"({el:.1f} s), numpy fp32 matmul" + (" + ticker mask" if bad is not None
+                                                            else "") +
+                      f" + argpartition top-{k}, scaled linearly to {n_total} rows"}
+
+
+def run_search(args, mode):
+    from ragmi.dist import ShardedIndex
+    world, rank = _world()
+    dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+    torch.cuda.set_device(dev)
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        dist.init_process_group("nccl", device_id=dev)
+    if mode == "5":
+        n, D, batch, seed0, qseed = args.rows or 50_000_000, 1024, 128, 5000, 7
+    else:
+        n, D, batch, seed0, qseed = args.rows or 10_000_000, 384, B, 1000, 1
+    n_tick = 16
+
+    def tags_fn(rows):            # ticker code 1..16 per global row (PayloadTags code space)
+        return ((rows * 2654435761) % (1 << 32) // 7 % n_tick + 1).astype(np.uint32)
+
+    sh = ShardedIndex(n, dim=D, device=dev)
+    idx, lo, hi = sh.local, sh.lo, sh.hi
+    t_b = time.perf_counter()
+    build_shard(idx, lo, hi, n, D, seed0, dev, tags_fn if mode == "filtered" else None)
+    t_b = time.perf_counter() - t_b
+    nb = args.warmup + args.steps
+    qs, picks = planted_queries(nb, batch, n, D, seed0, dev, qseed)
+    filts = None
+    if mode == "filtered":
+        # planted queries filter on their source row's ticker, pure-random ones on a random one
+        rng = np.random.default_rng(11)
+        filts = []
+        for i in range(nb):
+            tick = tags_fn(picks[i]) if i % 4 != 3 else rng.integers(1, n_tick + 1, batch)
+            f = np.stack([np.full(batch, 0xFFFF, np.uint32), tick.astype(np.uint32)], 1)
+            filts.append(torch.from_numpy(f.view(np.int32)).to(dev))
+    n_streams = args.streams or (4 if hi - lo < 4_000_000 else 2)
+    serial = hi - lo >= 4_000_000
+    idx.set_scan_order(serial)
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev)
+                                                  for _ in range(n_streams - 1)]
+    for s in streams[1:]:
+        s.wait_stream(streams[0])
+
+    def step(i):
+        with torch.cuda.stream(streams[i % n_streams]):
+            return sh.search(qs[i], K_TOP, filters=filts[i] if filts else None)
+
+    for i in range(args.warmup):
+        step(i)
+    _sync(dev)
+    idx.profile(4)
+    t0 = time.perf_counter()
+    outs = [step(args.warmup + k) for k in range(args.steps)]
+    _sync(dev)
+    elapsed = time.perf_counter() - t0
+    idx.profile(0)
+    scan_ms, launches = idx.profile_scan_ms()
+    scan_avg = scan_ms / max(launches, 1)
+    elapsed, scan_avg = _max_over_ranks([elapsed, scan_avg], dev)
+    extra = {}
+    if not args.no_recall and world == 1:
+        # the first timed planted batch and the first timed pure-random one (every 4th)
+        ks = [k for k in range(args.steps) if (args.warmup + k) % 4 != 3][:1] + \
+             [k for k in range(args.steps) if (args.warmup + k) % 4 == 3][:1]
+        if mode == "filtered":
+            tags_all = tags_fn(np.arange(lo, hi))
+            oks, r5s, r5m = [], [], []
+            for k in ks:
+                g_s, g_i = (t.cpu().numpy() for t in outs[k])
+                f0 = filts[args.warmup + k].cpu().numpy().view(np.uint32)
+                ok, r5, r5min = _filtered_check(idx, qs[args.warmup + k].cpu().numpy(), g_s,
+                                                g_i, f0, tags_all, lo)
+                oks.append(ok)
+                r5s.append(r5)
+                r5m.append(r5min)
+            g_i = outs[ks[0]][1].cpu().numpy()
+            extra.update({"top15_exact_queries": f"{sum(oks)}/{batch * len(ks)}",
+                          "checked_batches": "1 planted + 1 pure random",
+                          "recall_at_5": float(np.mean(r5s)),
+                          "recall_at_5_min_query": float(np.min(r5m)),
+                          "planted_found_first": f"{int((g_i[:, 0] == picks[args.warmup + ks[0]]).sum())}/{batch}"})
+        else:
+            # config 5: recall@5 vs an fp32 scoring of the fp16 rows (GPU torch, streamed),
+            # as in round 1
+            from bench_config5 import reference_top
+            r5 = []
+            for k in ks:
+                g_i = outs[k][1].cpu().numpy()
+                rs, ri = reference_top(qs[args.warmup + k], lo, hi, n, dev)
+                ref = ri.cpu().numpy()
+                r5 += [len(set(g_i[b, :5]) & set(ref[b, :5])) / 5 for b in range(batch)]
+            g_i = outs[ks[0]][1].cpu().numpy()
+            extra["recall_at_5_vs_fp32"] = float(np.mean(r5))
+            extra["checked_batches"] = "1 planted + 1 pure random"
+            extra["planted_found_first"] = \
+                f"{int((g_i[:, 0] == picks[args.warmup + ks[0]]).sum())}/{batch}"
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        m = min(hi - lo, CHUNK if D == 384 else CHUNK // 4)
+        cpu = _cpu_search_baseline(
+            idx.export_rows(0, m), qs[args.warmup].cpu().numpy(), n, K_TOP, args.cpu_budget,
+            tags_fn(np.arange(lo, lo + m)) if mode == "filtered" else None,
+            filts[args.warmup].cpu().numpy().view(np.uint32) if mode == "filtered" else None)
+    if rank == 0:
+        per_row = D * 2 + (4 if mode == "filtered" else 0)
+        algo = (hi - lo) * per_row
+        ach = algo / (scan_avg * 1e-3)
+        kern = ("scan_wide_kernel<1024,0,true>" if mode == "5" else
+                "scan_kernel<384,true>")
+        metric = ("queries/sec + recall@5, batch=128 over 50Mx1024 corpus (config 5)"
+                  if mode == "5" else
+                  "queries/sec + recall@5, batch=32 over 10Mx384 corpus, per-query ticker "
+                  "filter (16 tickers)")
+        line = _line(
+            metric, batch * args.steps / elapsed, "queries/s", args, elapsed, world, "fp16",
+            "synthetic (torch randn corpus, 1M-row chunks seeded %d+c; planted queries = "
+            "corpus row + 0.05 N(0,1), every 4th batch pure random%s)" % (
+                seed0, "; ticker tag = hash(row) % 16, planted queries filter on their "
+                       "source row's ticker" if mode == "filtered" else ""),
+            {"workload": f"cosine top-{K_TOP} over {n}x{D} fp16, batch={batch}, "
+                         f"{world} shard(s)" + (", filtered" if mode == "filtered" else ""),
+             "corpus_rows": n, "dim": D, "batch": batch, "k": K_TOP, "rows_per_gpu": hi - lo,
+             "parallelism": f"corpus-shard{world}", "batches_in_flight": n_streams,
+             "scan_order": "serial" if serial else "free"},
+            roofline={"bound": "hbm", "achieved": round(ach / 1e9, 1), "peak": HBM_PEAK / 1e9,
+                      "unit": "GB/s", "frac": round(ach / HBM_PEAK, 4), "traffic": None,
+                      "kernel": kern, "avg_ms": round(scan_avg, 4),
+                      "algorithmic_bytes_per_launch": algo,
+                      "bytes_per_row": per_row,
+                      "step_frac": round(algo / (elapsed / args.steps) / HBM_PEAK, 4)},
+            cpu_baseline=cpu, build_s=round(t_b, 1), **extra)
+        print(json.dumps(line), flush=True)
+    idx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def run(args):
+    if args.config in ("2", "3"):
+        return run_pipeline(args, int(args.config))
+    return run_search(args, args.config)
