@@ -660,6 +660,40 @@ int rag_bert_gemm_add_ln(const void* A, const void* A_lo, const void* W, const v
   return RAG_OK;
 }
 
+int rag_bert_gemm_add_ln_probe(int probe, const void* A, const void* A_lo, const void* W,
+                               const void* W_lo, const float* bias, const float* gamma,
+                               const float* beta, float eps, int M, int N, int K, float* x,
+                               void* xh, void* xl, void* stream) {
+  ragmi::clear_error();
+  if (probe != 4 && probe != 5) return ragmi::fail(RAG_EINVAL, "probe: 4 or 5");
+  if (!A || !W || !bias || !gamma || !beta || !x || !xh)
+    return ragmi::fail(RAG_EINVAL, "NULL argument");
+  if ((A_lo == nullptr) != (W_lo == nullptr) || (A_lo != nullptr) != (xl != nullptr))
+    return ragmi::fail(RAG_EINVAL, "A_lo, W_lo and xl: all three (fp16x3) or none (fp16)");
+  if (M < 1 || !add_ln_ok(M, N, K))
+    return ragmi::fail(RAG_EINVAL, "N == 384, K % 64 == 0, M*K*2 and M*N*4 < 2^31 required");
+  LnArgs ln;
+  ln.gamma = gamma;
+  ln.beta = beta;
+  ln.xh = static_cast<_Float16*>(xh);
+  ln.eps = eps;
+  const auto* a = static_cast<const _Float16*>(A);
+  const auto* al = static_cast<const _Float16*>(A_lo);
+  const auto* w = static_cast<const _Float16*>(W);
+  const auto* wl = static_cast<const _Float16*>(W_lo);
+  auto* l = static_cast<_Float16*>(xl);
+  const auto st = static_cast<hipStream_t>(stream);
+  if (probe == 4) {
+    if (al) launch_pipe<kEpiAddLn, true, PipeRow, 4>(a, al, w, wl, bias, M, N, K, x, l, st, cu_count(), ln);
+    else launch_pipe<kEpiAddLn, false, PipeRow, 4>(a, nullptr, w, nullptr, bias, M, N, K, x, nullptr, st, cu_count(), ln);
+  } else {
+    if (al) launch_pipe<kEpiAddLn, true, PipeRow, 5>(a, al, w, wl, bias, M, N, K, x, l, st, cu_count(), ln);
+    else launch_pipe<kEpiAddLn, false, PipeRow, 5>(a, nullptr, w, nullptr, bias, M, N, K, x, nullptr, st, cu_count(), ln);
+  }
+  RAG_HIP(hipGetLastError());
+  return RAG_OK;
+}
+
 int rag_encoder_set_fusion(rag_encoder_t* e, int mode) {
   ragmi::clear_error();
   if (!e || mode < -1 || mode > 1) return ragmi::fail(RAG_EINVAL, "mode: -1 auto, 0 off, 1 on");

@@ -452,6 +452,10 @@ struct LnArgs {
 
 // PROBE (diagnostic builds only, rag_bert_gemm variants 3/4/9): timing probes of the same
 // kernel with parts removed — 1 = no MFMAs, 2 = no DMAs, 3 = no DMAs and no barriers.
+// kEpiAddLn only (rag_bert_gemm_add_ln_probe): 4 = the fp16 copy [+ lo plane] stored with
+// the plain epilogue's paired 16-B stores (store_f16_pair) and a store count S matching
+// them; 5 = the same stores with S still counting the 8-B stores (more than are issued: the
+// post-epilogue vmcnt wait then passes before the next ring stage has landed).
 // (s_setprio around the MFMA clusters / for the younger waves measured +1-2%: not kept.)
 template <int EPI, bool SPLIT, typename CFG, int PROBE = 0>
 __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
@@ -472,7 +476,8 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
   // The count is capped at what vmcnt can express: waiting until fewer ops are outstanding
   // than were issued after the awaited stage is only stricter.
   constexpr int S_ISSUED = EPI == kEpiF32     ? FM * FN
-                           : EPI == kEpiAddLn ? FM * FN * (SPLIT ? 3 : 2)
+                           : EPI == kEpiAddLn ? (PROBE == 4 ? FM * FN + FM * FN / 2 * (SPLIT ? 2 : 1)
+                                                            : FM * FN * (SPLIT ? 3 : 2))
                                               : FM * FN / 2 * (SPLIT ? 2 : 1);
   constexpr int S = S_ISSUED < 63 - (NS - 2) * L ? S_ISSUED : 63 - (NS - 2) * L;
   constexpr int OUT_B = EPI == kEpiF32 || EPI == kEpiAddLn ? 4 : 2;   // Cout element bytes
@@ -531,7 +536,7 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
   __amdgpu_buffer_rsrc_t rA0 = panel(A, 0), rA1 = rA0, rW0 = rA0, rW1 = rA0;
   auto issue_next = [&]() {
     if (it_i >= n_mine) return;
-    if constexpr (PROBE >= 2) {
+    if constexpr (PROBE == 2 || PROBE == 3) {
       if (++kt_i == nk) { kt_i = 0; ++it_i; }
       return;
     }
@@ -579,7 +584,7 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
   for (int g = 0; g < steps; ++g) {
     // stages issued after step g: min(NS - 2, steps - 1 - g); plus the last epilogue's
     // stores when it ran at the end of step g-1
-    if constexpr (PROBE < 3) {
+    if constexpr (PROBE != 3) {
       wait_ring<L, S, NS - 2>(min(NS - 2, steps - 1 - g), g > 0 && kt_c == 0);
       __builtin_amdgcn_s_barrier();   // step g landed for all waves; all are past step g-1
     }
@@ -720,9 +725,49 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
             else rsd[i] = rsqrtf(s * (1.0f / BN) + ln.eps);
           }
         }
-        // fp16 copy [+ lo plane]: 8-B stores straight from the fragment layout (the
-        // permlane16_swap pairing of the plain fp16 epilogue returned wrong dwords for lanes
-        // 12-15 of each 16-lane group in this kernel's fp16x3 instance)
+        // fp16 copy [+ lo plane]: 8-B stores straight from the fragment layout. (Paired 16-B
+        // stores — PROBE 4 — issue fewer stores than the 8-B count S; with S unchanged the
+        // next tile's first ring stage was read before it landed: wrong dwords. PROBE 5.)
+        if constexpr (PROBE == 4 || PROBE == 5) {
+          const int cofs = 8 * ((g & 1) * 2 + (g >> 1));
+#pragma unroll
+          for (int jp = 0; jp < FN; jp += 2) {
+            const floatx4 ga = *reinterpret_cast<const floatx4*>(gam + wc * WTN + jp * 16 + 4 * g);
+            const floatx4 ea = *reinterpret_cast<const floatx4*>(bet + wc * WTN + jp * 16 + 4 * g);
+            const floatx4 gb = *reinterpret_cast<const floatx4*>(gam + wc * WTN + jp * 16 + 16 + 4 * g);
+            const floatx4 eb = *reinterpret_cast<const floatx4*>(bet + wc * WTN + jp * 16 + 16 + 4 * g);
+#pragma unroll
+            for (int i = 0; i < FM; ++i) {
+              floatx4 va, vb;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                va[r] = (acc[i][jp][r] - mu[i]) * rsd[i] * ga[r] + ea[r];
+                vb[r] = (acc[i][jp + 1][r] - mu[i]) * rsd[i] * gb[r] + eb[r];
+              }
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, va), rc, vf(i),
+                                                     sf(jp), 0);
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, vb), rc, vf(i),
+                                                     sf(jp + 1), 0);
+              half4 ha, hb;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                ha[r] = (_Float16)va[r];
+                hb[r] = (_Float16)vb[r];
+              }
+              const int vo = ((wr * WTM + i * 16 + (lane & 15)) * N + wc * WTN + jp * 16 + cofs) * 2;
+              store_f16_pair(ha, hb, rh, vo);
+              if constexpr (SPLIT) {
+                half4 la, lb;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                  la[r] = lo_part(va[r], ha[r]);
+                  lb[r] = lo_part(vb[r], hb[r]);
+                }
+                store_f16_pair(la, lb, rl, vo);
+              }
+            }
+          }
+        } else
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
           const floatx4 gj = *reinterpret_cast<const floatx4*>(gam + wc * WTN + j * 16 + 4 * g);

@@ -110,6 +110,14 @@ int rag_bert_gemm_add_ln(const void* A, const void* A_lo, const void* W, const v
                          const float* bias, const float* gamma, const float* beta, float eps,
                          int M, int N, int K, float* x, void* xh, void* xl, void* stream);
 
+/* Diagnostic (tests only): rag_bert_gemm_add_ln with the fp16 copy stored by the plain
+ * epilogue's paired 16-B stores — probe 4 with the ring's post-epilogue vmcnt budget counting
+ * them, probe 5 with it counting the production 8-B stores (too many: the wait passes early). */
+int rag_bert_gemm_add_ln_probe(int probe, const void* A, const void* A_lo, const void* W,
+                               const void* W_lo, const float* bias, const float* gamma,
+                               const float* beta, float eps, int M, int N, int K, float* x,
+                               void* xh, void* xl, void* stream);
+
 /* forward's use of rag_bert_gemm_add_ln: -1 auto (default; env RAGMI_FUSE_LN overrides at
  * create), 0 never (separate GEMM + add-LayerNorm kernels), 1 always where the shape allows */
 int rag_encoder_set_fusion(rag_encoder_t* e, int mode);
