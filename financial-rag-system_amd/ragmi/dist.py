@@ -62,6 +62,22 @@ def _gpu_merge(s, i, k):
     return merge_topk(s, i, k)
 
 
+def _gpu_merge_packed(p, k):
+    from .index import merge_topk_packed
+    return merge_topk_packed(p, k)
+
+
+def all_gather_packed(p: torch.Tensor, group=None) -> torch.Tensor:
+    """[B, k, 2] int32 per rank -> [world, B, k, 2] on every rank in ONE collective (RCCL
+    over xGMI on device tensors; gloo on host tensors). The concatenated output form
+    ([world * B, k, 2], the same bytes) is the one every backend implements."""
+    world = dist.get_world_size(group)
+    out = torch.empty((world * p.shape[0],) + tuple(p.shape[1:]), dtype=p.dtype,
+                      device=p.device)
+    dist.all_gather_into_tensor(out, p.contiguous(), group=group)
+    return out.view((world,) + tuple(p.shape))
+
+
 class ShardedIndex:
     """A collection of n_total rows sharded over the process group's ranks.
 
@@ -72,7 +88,7 @@ class ShardedIndex:
     """
 
     def __init__(self, n_total: int, local=None, dim: int = 384, device=None, group=None,
-                 merge: Callable | None = None):
+                 merge: Callable | None = None, merge_packed: Callable | None = None):
         self.group = group
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -83,11 +99,13 @@ class ShardedIndex:
             local = FlatIndex(dim=dim, capacity=max(self.hi - self.lo, 16), device=device)
         self.local = local
         self.merge = merge or _gpu_merge
-        # packed exchange (one collective): device-resident FlatIndex shards over RCCL with
-        # the default GPU merge and global rows < 2^31
-        self.packed = (merge is None and hasattr(local, "search_packed") and
-                       self.n_total < 2 ** 31 and dist.is_initialized() and
-                       dist.get_backend(group) == "nccl")
+        self.merge_packed = merge_packed or _gpu_merge_packed
+        # packed exchange (one collective of (score bits, int32 row) pairs) whenever the
+        # local shard offers it and global rows fit int32: the production path on RCCL, and
+        # on gloo with a host-side merge_packed (tests/test_dist_cpu.py)
+        self.packed = ((merge is None or merge_packed is not None) and
+                       hasattr(local, "search_packed") and self.n_total < 2 ** 31 and
+                       dist.is_initialized())
 
     @property
     def rows(self) -> int:
@@ -107,12 +125,9 @@ class ShardedIndex:
 
     def search(self, queries, k: int, filters=None):
         if self.world > 1 and self.packed:
-            # one RCCL all-gather of the packed (score bits, int32 row) lists instead of two
+            # one all-gather of the packed (score bits, int32 row) lists instead of two
             p = self.local.search_packed(queries, k, filters=filters, id_offset=self.lo)
-            out = torch.empty((self.world,) + tuple(p.shape), dtype=p.dtype, device=p.device)
-            dist.all_gather_into_tensor(out, p, group=self.group)
-            from .index import merge_topk_packed
-            return merge_topk_packed(out, k)
+            return self.merge_packed(all_gather_packed(p, self.group), k)
         s, i = self.local.search(queries, k, filters=filters, id_offset=self.lo)
         if self.world == 1:
             return s, i

@@ -23,6 +23,7 @@ from __future__ import annotations
 import os
 import shutil
 import threading
+import time
 import uuid
 from typing import Any, Iterable
 
@@ -122,6 +123,88 @@ class PayloadTags:
         return (mask, value)
 
 
+class _Req:
+    __slots__ = ("q", "limit", "filt", "result", "exc", "wake", "lead")
+
+    def __init__(self, q, limit, filt):
+        self.q, self.limit, self.filt = q, limit, filt
+        self.result = self.exc = None
+        self.wake = threading.Event()
+        self.lead = False
+
+
+class Coalescer:
+    """Rides concurrent single-query searches on one GPU scan.
+
+    The reference's batched service still searches per request: main2.py's batch_processor
+    fans a micro-batch out to process_independently tasks that each call
+    retrieve_from_qdrant -> query_points from an asyncio.to_thread worker (<= 25 at once,
+    main2.py:52-53,218,228). Unchanged, that is one full-corpus scan per query. Here the
+    first caller becomes the LEADER and searches; callers arriving while a search runs queue
+    up, and the next leader (the oldest queued request) searches all of them in ONE batched
+    scan (per-query payload filters ride inside the kernel). With no concurrency a request
+    runs at once (no added latency); `window_s` > 0 additionally holds a leader back for up
+    to that long to gather more callers. Results are bit-identical to individual calls: every
+    query's top-k is exact, independent of its batch-mates (tests/test_qdrant_gpu.py)."""
+
+    def __init__(self, col: "Collection", window_s: float = 0.0, max_batch: int = 32):
+        self.col = col
+        self.window = float(window_s)
+        self.max_batch = int(max_batch)
+        self.lock = threading.Lock()
+        self.pending: list[_Req] = []
+        self.leader_active = False
+        self.batches = 0            # scans issued (stats)
+        self.requests = 0
+
+    def search(self, q: np.ndarray, limit: int, filt):
+        req = _Req(q, int(limit), filt)
+        with self.lock:
+            self.pending.append(req)
+            self.requests += 1
+            if not self.leader_active:
+                self.leader_active = True
+                req.lead = True
+        if not req.lead:
+            req.wake.wait()
+            if not req.lead:                       # served by another leader
+                if req.exc is not None:
+                    raise req.exc
+                return req.result
+        if self.window > 0:
+            t_end = time.perf_counter() + self.window
+            while time.perf_counter() < t_end:
+                with self.lock:
+                    if len(self.pending) >= self.max_batch:
+                        break
+                time.sleep(min(5e-5, self.window / 4))
+        with self.lock:
+            batch = self.pending[:self.max_batch]
+            del self.pending[:self.max_batch]
+            self.batches += 1
+        try:
+            hits = self.col.search(np.stack([r.q for r in batch]),
+                                   max(r.limit for r in batch), [r.filt for r in batch])
+            for r, h in zip(batch, hits):
+                r.result = h[:r.limit]
+        except Exception as e:                     # every rider sees the failure
+            for r in batch:
+                r.exc = e
+        with self.lock:
+            if self.pending:                       # hand leadership to the oldest waiter
+                nxt = self.pending[0]
+                nxt.lead = True
+                nxt.wake.set()
+            else:
+                self.leader_active = False
+        for r in batch:
+            if r is not req:
+                r.wake.set()
+        if req.exc is not None:
+            raise req.exc
+        return req.result
+
+
 class Collection:
     """One COSINE collection: FlatIndex in HBM + host-side id/payload maps."""
 
@@ -137,6 +220,8 @@ class Collection:
         self.versions: list[int] = []
         self.op = 0
         self.lock = threading.RLock()
+        # 32 queries per scan pass at D = 384, 4 groups of 32 at D = 1024 (ragmi.h)
+        self.coalescer = Coalescer(self, 0.0, 32 if dim <= 384 else 128)
 
     def compile_filter(self, flt):
         return self.tags.compile(flt)
@@ -217,10 +302,14 @@ class QdrantClient:
     """In-process, GPU-resident replacement for qdrant_client.QdrantClient."""
 
     def __init__(self, url: str | None = None, *args, device=None, path: str | None = None,
-                 **kwargs):
+                 coalesce: bool = True, coalesce_window_s: float = 0.0, **kwargs):
         self.url = url
         self.device = device
         self.path = path
+        # concurrent query_points calls share GPU scans (Coalescer); coalesce=False searches
+        # every call on its own
+        self.coalesce = bool(coalesce)
+        self.coalesce_window_s = float(coalesce_window_s)
         self._collections: dict[str, Collection] = {}
         self._lock = threading.Lock()
         if path is not None and os.path.isdir(path):
@@ -229,6 +318,7 @@ class QdrantClient:
                 d = os.path.join(path, name)
                 if os.path.isfile(os.path.join(d, "collection.json")):
                     col = load_collection(d, device)
+                    col.coalescer.window = self.coalesce_window_s
                     self._collections[col.name] = col
 
     def save(self, path: str | None = None) -> None:
@@ -266,9 +356,10 @@ class QdrantClient:
         with self._lock:
             if collection_name in self._collections:
                 raise ValueError(f"collection {collection_name!r} already exists")
-            self._collections[collection_name] = Collection(
-                collection_name, int(vectors_config.size), self.device,
-                tuple(payload_tag_fields), capacity)
+            col = Collection(collection_name, int(vectors_config.size), self.device,
+                             tuple(payload_tag_fields), capacity)
+            col.coalescer.window = self.coalesce_window_s
+            self._collections[collection_name] = col
         return True
 
     def recreate_collection(self, collection_name: str, vectors_config, **kwargs) -> bool:
@@ -322,9 +413,19 @@ class QdrantClient:
                      query_filter: models.Filter | None = None, with_payload=True,
                      with_vectors=False, **kwargs) -> models.QueryResponse:
         col = self._col(collection_name)
-        q = query if isinstance(query, torch.Tensor) else np.asarray(query, dtype=np.float32)
-        q = q.reshape(1, -1)
-        hits = col.search(q, int(limit), [col.compile_filter(query_filter)])[0]
+        flt = col.compile_filter(query_filter)
+        if self.coalesce and 1 <= int(limit) <= MAX_K:
+            q = (query.detach().float().cpu().numpy() if isinstance(query, torch.Tensor)
+                 else np.asarray(query, dtype=np.float32))
+            if q.shape != (col.dim,):
+                q = q.reshape(-1)
+                if q.shape != (col.dim,):
+                    raise ValueError(f"query must be one {col.dim}-dim vector")
+            hits = col.coalescer.search(q, int(limit), flt)
+        else:
+            q = query if isinstance(query, torch.Tensor) else np.asarray(query, dtype=np.float32)
+            q = q.reshape(1, -1)
+            hits = col.search(q, int(limit), [flt])[0]
         return models.QueryResponse(points=[col.point(r, s, with_payload, with_vectors)
                                             for r, s in hits])
 

@@ -1,9 +1,11 @@
 """CPU (gloo) tests of the N > 1 path: contiguous row shards, per-shard top-k
 with global id offsets, all-gather, merge by (score desc, id asc) == unsharded result.
 
-The per-shard search here is the oracle (the GPU scan cannot run on CPU) and the merge is a
-numpy restatement of rag_merge_topk; what is under test is ragmi.dist's sharding, id offset
-and all-gather plumbing with world_size 2 and 3 over gloo on 127.0.0.1."""
+The per-shard search here is the oracle (the GPU scan cannot run on CPU) and the merges are
+numpy restatements of rag_merge_topk / rag_merge_topk_packed; what is under test is
+ragmi.dist's sharding, id offsets and exchange plumbing with world_size 2 and 3 over gloo on
+127.0.0.1 — including the production packed exchange (search_packed -> ONE all-gather of
+[B, k, 2] int32 (score bits, global row) -> packed merge), the exact bytes RCCL carries."""
 import os
 import socket
 import sys
@@ -41,6 +43,32 @@ class OracleShard:
         i = np.where(i >= 0, i + id_offset, -1)
         return torch.from_numpy(s), torch.from_numpy(i)
 
+    def search_packed(self, q, k, filters=None, id_offset=0):
+        """rag_index_search_packed's exchange format: int32 [B, k, 2] = (fp32 score bits,
+        global row; -1 = none)."""
+        s, i = self.search(q, k, filters, id_offset)
+        p = np.empty(tuple(s.shape) + (2,), np.int32)
+        p[..., 0] = s.numpy().view(np.int32)
+        p[..., 1] = np.where(i.numpy() >= 0, i.numpy(), -1).astype(np.int32)
+        return torch.from_numpy(p)
+
+
+def np_merge_packed(p, k):
+    """numpy restatement of merge_exact_kernel<PACKED> (csrc/scan_kernels.hip): the union of
+    the gathered lists' valid entries (row >= 0), ordered by (score desc, row asc), first k."""
+    p = p.numpy()
+    W, B = p.shape[:2]
+    out_s = np.full((B, k), -np.inf, np.float32)
+    out_i = np.full((B, k), -1, np.int64)
+    for b in range(B):
+        s = p[:, b, :, 0].ravel().view(np.float32)
+        i = p[:, b, :, 1].ravel().astype(np.int64)
+        keep = i >= 0
+        s, i = s[keep], i[keep]
+        o = np.lexsort((i, -s.astype(np.float64)))[:k]
+        out_s[b, :len(o)], out_i[b, :len(o)] = s[o], i[o]
+    return torch.from_numpy(out_s), torch.from_numpy(out_i)
+
 
 def np_merge(gs, gi, k):
     gs, gi = gs.numpy(), gi.numpy()
@@ -57,7 +85,7 @@ def np_merge(gs, gi, k):
     return torch.from_numpy(out_s), torch.from_numpy(out_i)
 
 
-def _worker(rank, world, port, n, q, x, tags, filt, result_q):
+def _worker(rank, world, port, n, q, x, tags, filt, result_q, packed=False):
     _paths()
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -67,7 +95,12 @@ def _worker(rank, world, port, n, q, x, tags, filt, result_q):
         from ragmi.dist import ShardedIndex, shard_bounds
         lo, hi = shard_bounds(n, rank, world)
         shard = OracleShard(O.encode_rows(x[lo:hi]), tags[lo:hi])
-        sh = ShardedIndex(n, local=shard, merge=np_merge)
+        if packed:
+            sh = ShardedIndex(n, local=shard, merge_packed=np_merge_packed)
+            assert sh.packed
+        else:
+            sh = ShardedIndex(n, local=shard, merge=np_merge)
+            assert not sh.packed
         assert (sh.lo, sh.hi) == (lo, hi)
         s, i = sh.search(torch.from_numpy(q), 15)
         sf, i_f = sh.search(torch.from_numpy(q), 15, filters=filt)
@@ -83,12 +116,13 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_search_equals_unsharded_gloo(world):
+@pytest.mark.parametrize("packed", [False, True], ids=["lists", "packed"])
+@pytest.mark.parametrize("world,n", [(2, 1001), (3, 1001), (3, 25)])
+def test_sharded_search_equals_unsharded_gloo(world, n, packed):
+    """n = 25 at world 3: shards of 8-9 rows, fewer than k = 15 (-1 entries in the exchange)."""
     _paths()
     import oracle_scan as O
     rng = np.random.default_rng(world)
-    n = 1001
     x = rng.standard_normal((n, 384)).astype(np.float32)
     tags = rng.integers(1, 4, n).astype(np.uint32)
     q = x[rng.choice(n, 6)] + 0.05 * rng.standard_normal((6, 384)).astype(np.float32)
@@ -97,7 +131,8 @@ def test_sharded_search_equals_unsharded_gloo(world):
     ctx = mp.get_context("spawn")
     result_q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, q, x, tags, filt, result_q))
+    procs = [ctx.Process(target=_worker,
+                         args=(r, world, port, n, q, x, tags, filt, result_q, packed))
              for r in range(world)]
     [p.start() for p in procs]
     s, i, sf, i_f = result_q.get(timeout=240)
