@@ -369,10 +369,30 @@ int bench_scan(rag_index* h, const float* q, int B, int variant, int reps, doubl
   const int64_t n_tiles = (h->count + 15) / 16;
   int grid = (int)std::min<int64_t>(h->max_wgs, std::max<int64_t>(1, (n_tiles + 3) / 4));
   grid = std::min(grid, kMaxLists / kWavesPerWG);
+  // variant 8: the v_dot2 VALU ablation over a row-group-major copy of the corpus
+  half8* rows64 = nullptr;
+  half8* qc = nullptr;
+  const int n_groups = (int)((h->count + 63) / 64);
+  if (variant == 8) {
+    RAG_HIP(hipMalloc(reinterpret_cast<void**>(&rows64), (size_t)n_groups * 64 * D * 2));
+    RAG_HIP(hipMalloc(reinterpret_cast<void**>(&qc), (size_t)kQ * D * 2));
+    RAG_HIP(hipMemset(rows64, 0, (size_t)n_groups * 64 * D * 2));
+    const int64_t total = h->count * (D / 8);
+    rows64_kernel<D><<<dim3((unsigned)((total + 255) / 256)), dim3(256), 0, nullptr>>>(
+        h->corpus, h->count, rows64);
+    qchunk_kernel<D><<<dim3(kQ), dim3(64), 0, nullptr>>>(w.qn, qc);
+  }
+  const int vgrid = std::min(h->max_wgs, std::max(1, (n_groups + 3) / 4));
   hipEvent_t a, b;
   RAG_HIP(hipEventCreate(&a));
   RAG_HIP(hipEventCreate(&b));
   auto one = [&]() {
+    if (variant == 8) {
+      scan_valu_kernel<D><<<dim3(vgrid), dim3(256), 0, nullptr>>>(
+          rows64, qc, (int)h->count, n_groups, w.seed, w.part_s, w.part_i, w.heads_s,
+          w.heads_i, w.heads_n);
+      return;
+    }
     switch (variant) {
       case 0: launch_variant<D, 0>(h, w, grid, nullptr); break;
       case 1: launch_variant<D, 1>(h, w, grid, nullptr); break;
@@ -393,6 +413,8 @@ int bench_scan(rag_index* h, const float* q, int B, int variant, int reps, doubl
   RAG_HIP(hipEventElapsedTime(&ms, a, b));
   (void)hipEventDestroy(a);
   (void)hipEventDestroy(b);
+  if (rows64) (void)hipFree(rows64);
+  if (qc) (void)hipFree(qc);
   RAG_HIP(hipGetLastError());
   *avg_ms = ms / reps;
   return RAG_OK;
@@ -750,7 +772,7 @@ int rag_merge_topk_packed(const int32_t* in_packed, int n_lists, int B, int k, f
 int rag_bench_scan(rag_index_t* h, const float* queries_dev, int B, int variant, int reps,
                    double* avg_ms) {
   ragmi::clear_error();
-  if (!h || !queries_dev || B < 1 || reps < 1 || !avg_ms || variant < 0 || variant > 7)
+  if (!h || !queries_dev || B < 1 || reps < 1 || !avg_ms || variant < 0 || variant > 8)
     return ragmi::fail(RAG_EINVAL, "bad bench args");
   std::lock_guard<std::mutex> lk(h->mu);
   RAG_HIP(hipSetDevice(h->device));

@@ -1130,6 +1130,121 @@ __global__ __launch_bounds__(64 * kWideWaves, 1) void scan_wide_kernel(
 }
 
 // ----------------------------------------------------------------------------------------
+// VALU ablation of the scan (rag_bench_scan variant 8; north_star's literal "MFMA only for
+// the encoders' GEMMs"): the same 32-query dot products with v_dot2_f32_f16 (2 fp16 MACs per
+// lane per instruction) instead of MFMA. Lane = row: a wave takes 64-row groups g = gw,
+// gw + nw, ... of a row-group-major copy of the corpus (rows64[(g*C + c)*64 + lane] = the
+// 8-dim chunk c of row 64g + lane: every load is one coalesced 1 KB wave read), while the
+// 32 queries' chunk c is wave-uniform, read by scalar loads from qc[c][32]. 128 dot2 per
+// chunk per lane, no cross-lane reduction. The 64 x 32 scores are then transposed through LDS
+// into the MFMA accumulator layout so the production top-k (topk_tile, seeded thresholds)
+// runs unchanged. Diagnostic only (results are not selected).
+// ----------------------------------------------------------------------------------------
+template <int D>
+__global__ void rows64_kernel(const half8* __restrict__ corpus, int64_t n_rows,
+                              half8* __restrict__ rows64) {
+  constexpr int C = D / 8, S = steps<D>();
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // (row, chunk)
+  if (idx >= n_rows * C) return;
+  const int64_t r = idx / C;
+  const int c = (int)(idx % C);
+  rows64[((r >> 6) * C + c) * 64 + (r & 63)] =
+      corpus[(r >> 4) * (S * 64) + (c >> 2) * 64 + (c & 3) * 16 + (r & 15)];
+}
+
+template <int D>
+__global__ __launch_bounds__(64) void qchunk_kernel(const float* __restrict__ qn,
+                                                    half8* __restrict__ qc) {
+  constexpr int C = D / 8;
+  const int q = blockIdx.x;
+  for (int c = threadIdx.x; c < C; c += 64) {
+    half8 h;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) h[j] = f32_to_f16(qn[q * D + 8 * c + j]);
+    qc[c * kQ + q] = h;
+  }
+}
+
+typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+
+template <int D>
+__global__ __launch_bounds__(256, 2) void scan_valu_kernel(
+    const half8* __restrict__ rows64, const half8* __restrict__ qc, int n_rows, int n_groups,
+    const float* __restrict__ seed_thr, float* __restrict__ part_s, int* __restrict__ part_i,
+    float* __restrict__ heads_s, int* __restrict__ heads_i, int* __restrict__ heads_n) {
+  constexpr int C = D / 8, PF = 8;
+  static_assert(C % PF == 0, "chunks");
+  __shared__ int lds[kWavesPerWG * kLdsPerWave];
+  __shared__ float tr[kWavesPerWG][kQ / 2][64];   // 4 KB per wave: two WGs per CU
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  ScanTopK st;
+  topk_init<false>(st, lds, wid, lane, seed_thr, nullptr);
+  const int gw = blockIdx.x * kWavesPerWG + __builtin_amdgcn_readfirstlane(wid);
+  const int nw = gridDim.x * kWavesPerWG;
+  for (int g = gw; g < n_groups; g += nw) {
+    const half8* rp = rows64 + (int64_t)g * C * 64 + lane;
+    half8 ring[PF];
+#pragma unroll
+    for (int u = 0; u < PF; ++u) ring[u] = __builtin_nontemporal_load(rp + u * 64);
+    float acc[kQ];
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) acc[q] = 0.f;
+    for (int c0 = 0; c0 < C; c0 += PF) {
+#pragma unroll
+      for (int u = 0; u < PF; ++u) {
+        const half8 a = ring[u];
+        // prefetch PF chunks ahead (clamped: the last chunk is re-read, an L1/L2 hit, instead
+        // of a branch around the load)
+        ring[u] = __builtin_nontemporal_load(rp + min(c0 + PF + u, C - 1) * 64);
+        // 8 queries' chunks (32 SGPRs of scalar loads) at a time. The empty asm takes the
+        // group's sums as inputs and "rewrites" a zero offset of the query address, so the
+        // next group's scalar loads depend on this group's dot products: without it the
+        // scheduler hoists every group's loads to the top and spills SGPRs through VGPR
+        // lanes. (The offset, not the pointer: a pointer out of an asm loses the const
+        // provenance that lets the loads be scalar.)
+        int zo = 0;
+#pragma unroll
+        for (int q0 = 0; q0 < kQ; q0 += 8) {
+#pragma unroll
+          for (int q = q0; q < q0 + 8; ++q) {
+            const half8 b = qc[(c0 + u) * kQ + q + zo];   // wave-uniform: scalar loads
+            float x = acc[q];
+            x = __builtin_amdgcn_fdot2(half2v{a[0], a[1]}, half2v{b[0], b[1]}, x, false);
+            x = __builtin_amdgcn_fdot2(half2v{a[2], a[3]}, half2v{b[2], b[3]}, x, false);
+            x = __builtin_amdgcn_fdot2(half2v{a[4], a[5]}, half2v{b[4], b[5]}, x, false);
+            x = __builtin_amdgcn_fdot2(half2v{a[6], a[7]}, half2v{b[6], b[7]}, x, false);
+            acc[q] = x;
+          }
+          asm volatile("" : "+s"(zo)
+                       : "v"(acc[q0]), "v"(acc[q0 + 1]), "v"(acc[q0 + 2]), "v"(acc[q0 + 3]),
+                         "v"(acc[q0 + 4]), "v"(acc[q0 + 5]), "v"(acc[q0 + 6]), "v"(acc[q0 + 7]));
+        }
+      }
+    }
+    floatx4 a0[4], a1[4];       // the 4 tiles' scores in the MFMA accumulator layout
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int q = 0; q < kQ / 2; ++q) tr[wid][q][lane] = acc[h * 16 + q];
+      lds_fence();
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) {
+        const floatx4 v = *reinterpret_cast<const floatx4*>(&tr[wid][lane & 15][16 * tt + 4 * (lane >> 4)]);
+        if (h == 0) a0[tt] = v; else a1[tt] = v;
+      }
+      lds_fence();
+    }
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt) {
+      const int t = 4 * g + tt;
+      if (t * kTileRows >= n_rows) break;
+      topk_tile<false>(st, a0[tt], a1[tt], t, n_rows, nullptr, lane);
+    }
+  }
+  topk_finish(st, lane, gw, nw, part_s, part_i, heads_s, heads_i, heads_n);
+}
+
+// ----------------------------------------------------------------------------------------
 // sample: seed thresholds for the scan. Sample wave w scores the corpus tiles
 //   t = (j * n_tiles) / n_sample, j = w, w + n_waves, ...   (spread over the shard)
 // and writes, per query, the max score over its (valid, filter-passing) rows to

@@ -166,7 +166,10 @@ int rag_profile_scan_ms(rag_index_t* index, double* total_ms, int64_t* launches)
 /* Diagnostic: average device ms of `reps` launches of scan variant `variant` on the current
  * corpus with the first min(B,32) queries (dim 384 only). Variants: 0 production (seeded
  * thresholds), 1 unseeded, 2 contiguous per-wave tile ranges, 3 MFMA without top-k,
- * 4 loads only, 5 without non-temporal loads, 6 without the load sched-barrier. */
+ * 4 loads only, 5 without non-temporal loads, 6 without the load sched-barrier, 7 production
+ * with every seed at +inf (top-k compares only), 8 the VALU ablation: v_dot2_f32_f16 instead
+ * of MFMA over a row-group-major copy of the corpus, same top-k. dim 1024: variants 0-4 of
+ * the wide (33-128 query) scan. */
 int rag_bench_scan(rag_index_t* index, const float* queries_dev, int B, int variant, int reps,
                    double* avg_ms);
 

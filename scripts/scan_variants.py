@@ -16,7 +16,8 @@ import bench  # noqa: E402
 from ragmi.index import FlatIndex  # noqa: E402
 
 NAMES = {0: "prod (seeded, interleaved, nt, sched-barrier)", 1: "unseeded", 2: "contiguous",
-         3: "mfma-only", 4: "loads-only", 5: "no-nt", 6: "no-sb", 7: "top-k never taken"}
+         3: "mfma-only", 4: "loads-only", 5: "no-nt", 6: "no-sb", 7: "top-k never taken",
+         8: "VALU v_dot2_f32_f16 (no MFMA), same loads and top-k"}
 
 
 def main():
