@@ -42,9 +42,6 @@ struct Workspace {
   int* heads_n = nullptr;
   int* progress = nullptr;      // [lists][groups] shared-group scan throttle words
   float* eps = nullptr;         // [groups][32] per-query |MFMA - exact| score bound (qprep)
-  float* fb_L = nullptr;        // [groups][32] tier-2 rescan floors (select; +inf = none)
-  float* fb_E = nullptr;        // [groups][32] exact k-th candidate scores
-  int* fb_flag = nullptr;       // any tier-2 request in this pass
   int* fb_tier = nullptr;       // [groups][32] certifying path per query of the last pass
   unsigned long long* fb_cnt = nullptr;   // [2] tier-1 / tier-2 totals since creation
   hipStream_t owner = nullptr;  // stream of the last pass that used this slot
@@ -153,7 +150,7 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
   // Bq <= 32 * h->groups queries: `groups` query groups of 32 (one for D <= 384)
   const int groups = (Bq + kQ - 1) / kQ;
   qprep_kernel<D><<<dim3(groups * kQ), dim3(64), 0, st>>>(q, Bq, filt, w.qn, w.qfrag, w.filt,
-                                                          w.eps, w.fb_flag);
+                                                          w.eps);
   if (filt)
     launch_seed<D, true>(h, w, groups, st);
   else
@@ -226,27 +223,19 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
     h->scan_last = st;
   }
   const int n_lists = wide ? grid : grid * (kLdsQ ? kLdsWaves : kWavesPerWG);   // per group
-  const Fallback fb{w.fb_L, w.fb_E, w.fb_flag, w.fb_tier, w.fb_cnt};
-  select_kernel<D, false><<<dim3(Bq), dim3(256), 0, st>>>(
-      w.part_s, w.part_i, w.heads_s, w.heads_i, w.heads_n, n_lists, h->corpus, w.qn, k, w.eps,
-      w.seed, fb, id_offset, out_s, out_i, out_packed);
-  // Tier-2 exactness fallback (select_kernel): a rescan over the whole shard for the queries
-  // whose approximate top-32 could not certify the exact top-k, then select over its exact
-  // lists. Both launches exit in their first instructions unless select raised fb_flag
-  // (no host round trip on the hot path).
-  const int rgrid = (int)std::min<int64_t>(std::min(h->max_wgs / 2, kMaxLists / kWavesPerWG),
-                                           std::max<int64_t>(1, (n_tiles + 3) / 4));
+  const ExactStats fb{w.fb_tier, w.fb_cnt};
+  // select certifies every query's top-k; its fallbacks (list re-scoring, a workgroup-local
+  // second pass over the shard) run inside the same launch
+#define RAG_SELECT(F)                                                                          \
+  select_kernel<D, F><<<dim3(Bq), dim3(256), 0, st>>>(                                         \
+      w.part_s, w.part_i, w.heads_s, w.heads_i, w.heads_n, n_lists, h->corpus, h->tags,      \
+      w.filt, w.qfrag, (int)h->count, w.qn, k, w.eps, w.seed, fb, id_offset, out_s, out_i,   \
+      out_packed)
   if (filt)
-    rescan_kernel<D, true><<<dim3(rgrid, groups), dim3(256), 0, st>>>(
-        h->corpus, h->tags, w.filt, w.qfrag, w.qn, w.eps, fb, (int)h->count, (int)n_tiles,
-        w.part_s, w.part_i, w.heads_s, w.heads_i, w.heads_n);
+    RAG_SELECT(true);
   else
-    rescan_kernel<D, false><<<dim3(rgrid, groups), dim3(256), 0, st>>>(
-        h->corpus, h->tags, w.filt, w.qfrag, w.qn, w.eps, fb, (int)h->count, (int)n_tiles,
-        w.part_s, w.part_i, w.heads_s, w.heads_i, w.heads_n);
-  select_kernel<D, true><<<dim3(Bq), dim3(256), 0, st>>>(
-      w.part_s, w.part_i, w.heads_s, w.heads_i, w.heads_n, rgrid * kWavesPerWG, h->corpus, w.qn,
-      k, w.eps, w.seed, fb, id_offset, out_s, out_i, out_packed);
+    RAG_SELECT(false);
+#undef RAG_SELECT
   RAG_HIP(hipGetLastError());
   return RAG_OK;
 }
@@ -360,7 +349,7 @@ int bench_scan(rag_index* h, const float* q, int B, int variant, int reps, doubl
   Workspace& w = h->ws[0];
   RAG_HIP(hipDeviceSynchronize());
   qprep_kernel<D><<<dim3(kQ), dim3(64), 0, nullptr>>>(q, std::min(B, kQ), nullptr, w.qn,
-                                                      w.qfrag, w.filt, w.eps, w.fb_flag);
+                                                      w.qfrag, w.filt, w.eps);
   launch_seed<D, false>(h, w, 1, nullptr);
   // variant 7: the production kernel with every seed threshold at +inf, i.e. the top-k's
   // per-tile compares and branches with no candidate ever taken (its fixed cost)
@@ -430,7 +419,7 @@ int bench_wide(rag_index* h, const float* q, int B, int mode, int reps, double* 
   if (groups < 2) return ragmi::fail(RAG_EINVAL, "wide scan variants need 33..128 queries");
   RAG_HIP(hipDeviceSynchronize());
   qprep_kernel<D><<<dim3(groups * kQ), dim3(64), 0, nullptr>>>(
-      q, std::min(B, groups * kQ), nullptr, w.qn, w.qfrag, w.filt, w.eps, w.fb_flag);
+      q, std::min(B, groups * kQ), nullptr, w.qn, w.qfrag, w.filt, w.eps);
   launch_seed<D, false>(h, w, groups, nullptr);
   const int64_t n_tiles = (h->count + 15) / 16;
   const int grid = (int)std::min<int64_t>(h->max_wgs / 2, std::max<int64_t>(1, n_tiles));
@@ -521,9 +510,6 @@ int rag_index_create(int dim, int64_t capacity_rows, int device, rag_index_t** o
               hipMalloc(reinterpret_cast<void**>(&w.progress),
                         G * ragmi::kMaxLists * 4) == hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&w.eps), G * Q * 4) == hipSuccess &&
-              hipMalloc(reinterpret_cast<void**>(&w.fb_L), G * Q * 4) == hipSuccess &&
-              hipMalloc(reinterpret_cast<void**>(&w.fb_E), G * Q * 4) == hipSuccess &&
-              hipMalloc(reinterpret_cast<void**>(&w.fb_flag), 16) == hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&w.fb_tier), G * Q * 4) == hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&w.fb_cnt), 16) == hipSuccess &&
               hipMemset(w.fb_cnt, 0, 16) == hipSuccess &&
@@ -555,9 +541,6 @@ int rag_index_destroy(rag_index_t* h) {
     if (w.part_i) (void)hipFree(w.part_i);
     if (w.progress) (void)hipFree(w.progress);
     if (w.eps) (void)hipFree(w.eps);
-    if (w.fb_L) (void)hipFree(w.fb_L);
-    if (w.fb_E) (void)hipFree(w.fb_E);
-    if (w.fb_flag) (void)hipFree(w.fb_flag);
     if (w.fb_tier) (void)hipFree(w.fb_tier);
     if (w.fb_cnt) (void)hipFree(w.fb_cnt);
   }

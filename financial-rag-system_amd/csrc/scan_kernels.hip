@@ -16,6 +16,7 @@
 namespace ragmi {
 
 constexpr int kTileRows = 16;
+typedef _Float16 half2v __attribute__((ext_vector_type(2)));
 constexpr int kQ = 32;            // queries per pass
 constexpr int kKS = 32;           // candidates kept per (wave, query)
 constexpr int kP = 8;             // pending slots per (lane, query tile)
@@ -62,7 +63,6 @@ __global__ __launch_bounds__(64) void upsert_kernel(const float* __restrict__ ve
 //         dims 32s + 8(l>>4) .. +7
 //   filt  [32][2] (tag mask, tag value) per query slot
 //   eps   [32] bound on |MFMA score - exact score| over every stored row (see below)
-//   fb_flag  cleared: no query of this pass needs the tier-2 rescan yet (select sets it)
 //
 // Error bound. Stored rows c are fp16 roundings of unit vectors (||c||_2 <= kRowNorm); the
 // scan scores a = MFMA(c, h) with h = fp16(qn) and fp32 accumulation over D products (each
@@ -82,8 +82,7 @@ __global__ __launch_bounds__(64) void qprep_kernel(const float* __restrict__ q, 
                                                    float* __restrict__ qn,
                                                    half8* __restrict__ qfrag,
                                                    uint32_t* __restrict__ filt,
-                                                   float* __restrict__ eps,
-                                                   int* __restrict__ fb_flag) {
+                                                   float* __restrict__ eps) {
   const int b = blockIdx.x;
   const int lane = threadIdx.x;
   const bool live = b < B;
@@ -91,7 +90,6 @@ __global__ __launch_bounds__(64) void qprep_kernel(const float* __restrict__ q, 
     // per-query payload filter (mask, value); padding / unfiltered queries match every row
     filt[2 * b] = (live && filt_in) ? filt_in[2 * b] : 0u;
     filt[2 * b + 1] = (live && filt_in) ? filt_in[2 * b + 1] : 0u;
-    if (b == 0) *fb_flag = 0;
   }
   double norm = 0.0;
   if (live) norm = sqrt(canon_sumsq<D>(q + (int64_t)b * D, lane));
@@ -1165,8 +1163,6 @@ __global__ __launch_bounds__(64) void qchunk_kernel(const float* __restrict__ qn
   }
 }
 
-typedef _Float16 half2v __attribute__((ext_vector_type(2)));
-
 template <int D>
 __global__ __launch_bounds__(256, 2) void scan_valu_kernel(
     const half8* __restrict__ rows64, const half8* __restrict__ qc, int n_rows, int n_groups,
@@ -1562,17 +1558,11 @@ __device__ __forceinline__ void exact_scores_wave(const half8* __restrict__ corp
 }
 
 // ----------------------------------------------------------------------------------------
-// Exactness fallback state of one search pass (written by select, read by the rescan):
-//   fb_L[q]  approximate-score floor of the tier-2 rescan for query q (+inf: not needed)
-//   fb_E[q]  exact score of the k-th candidate (every true top-k row scores >= it)
-//   *fb_flag 1 if any query of the pass needs the rescan (cleared by qprep)
+// Exactness bookkeeping of a search pass (rag_index_exactness_stats):
 //   tier[q]  the path that certified query q's result: 0 check, 1 tier 1, 2 tier 2
-//   cnt[2]   running totals of tier-1 / tier-2 queries (rag_index_exactness_stats)
+//   cnt[2]   running totals of tier-1 / tier-2 queries
 // ----------------------------------------------------------------------------------------
-struct Fallback {
-  float* L;
-  float* E;
-  int* flag;
+struct ExactStats {
   int* tier;
   unsigned long long* cnt;
 };
@@ -1595,12 +1585,17 @@ struct Fallback {
 //     tier 1 (here): if L >= the scan's seed (no such row was pruned) and no per-wave list
 //       whose tail is >= L is full (none dropped one), every row with a >= L sits in some
 //       list: rescore all of them exactly and emit their top-k.
-//     tier 2: otherwise record (L, e_k) in fb and raise fb_flag; rescan_kernel streams the
-//       shard again and select in EXACT_LISTS mode overwrites this query's output.
-// EXACT_LISTS: the lists hold exact scores (rescan_kernel); queries without a tier-2 request
-// return at once; no rescoring, no check.
+//     tier 2 (here too): otherwise this workgroup streams the shard once more for its query:
+//       approximate scores by v_dot2 over the query's fp16 fragment (error within eps_q,
+//       like the scan's), rows with a >= max(L, thr - eps_q) scored exactly into each wave's
+//       running exact top-32 (thr = its 32nd, starting just below e_k), merged, emitted.
+//       Only inputs with more than 32 in-band rows inside one wave's share of the tiles (or
+//       a seed above L) get here; it costs a single-CU pass over the shard, and no launch
+//       at all when unused (a separate always-launched rescan kernel cost ~5% of the
+//       small-shard throughput: its workgroups cannot start beside another stream's
+//       full-occupancy scan).
 // ----------------------------------------------------------------------------------------
-template <int D, bool EXACT_LISTS>
+template <int D, bool FILTER>
 __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ part_s,
                                                      const int* __restrict__ part_i,
                                                      const float* __restrict__ heads_s,
@@ -1608,10 +1603,14 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
                                                      const int* __restrict__ heads_n,
                                                      int n_lists,
                                                      const half8* __restrict__ corpus,
+                                                     const uint32_t* __restrict__ tags,
+                                                     const uint32_t* __restrict__ filt,
+                                                     const half8* __restrict__ qfrag,
+                                                     int n_rows,
                                                      const float* __restrict__ qn, int k,
                                                      const float* __restrict__ eps,
                                                      const float* __restrict__ seed_thr,
-                                                     Fallback fb, int64_t id_offset,
+                                                     ExactStats fb, int64_t id_offset,
                                                      float* __restrict__ out_s,
                                                      int64_t* __restrict__ out_i,
                                                      int32_t* __restrict__ out_packed) {
@@ -1634,9 +1633,6 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
   // query bq of the batch = slot b of query group grp (the scan's per-group lists)
   const int bq = blockIdx.x, grp = bq / kQ, b = bq % kQ;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  if constexpr (EXACT_LISTS) {
-    if (!(fb.L[bq] < __builtin_inff())) return;   // no tier-2 request (uniform per group)
-  }
   part_s += (int64_t)grp * n_lists * (kQ * kKS);
   part_i += (int64_t)grp * n_lists * (kQ * kKS);
   heads_s += (int64_t)grp * kQ * n_lists;
@@ -1824,13 +1820,8 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
   __syncthreads();
 
   const float* qq = qn + (int64_t)bq * D;
-  // ---- 3. exact rescoring, 8 candidates per wave (one round trip); exact lists as they are
-  if constexpr (EXACT_LISTS) {
-    if (tid < 32) {
-      e_s[tid] = c_s[0][tid];
-      e_i[tid] = c_s[0][tid] != kNegInf ? c_i[0][tid] : kIdNone32;
-    }
-  } else {
+  // ---- 3. exact rescoring, 8 candidates per wave (one round trip)
+  {
     int rows[8];
     float es[8];
 #pragma unroll
@@ -1869,7 +1860,7 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
     int id = lane < 32 ? e_i[lane] : kIdNone32;
     bitonic_sort64(s, id, lane);
     int v = 0;
-    if constexpr (!EXACT_LISTS) {
+    {
       const float ek = __shfl(s, k - 1, 64);
       const float a32 = c_s[0][kKS - 1];
       const float e = eps[bq];
@@ -1884,23 +1875,19 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
         verdict = v;
         floor_L = L;
         floor_E = ek;
-        fb.L[bq] = v == 2 ? L : __builtin_inff();   // tier 1 may still escalate below
-        fb.E[bq] = ek;
-        fb.tier[bq] = v;
-        if (v == 2) {
-          *fb.flag = 1;
-          atomicAdd(&fb.cnt[1], 1ull);
-        }
       }
     }
-    if (v != 1) emit(s, id);   // tier 2: provisional, overwritten by the EXACT_LISTS pass
+    if (v == 0) {
+      emit(s, id);
+      if (lane == 0) fb.tier[bq] = 0;
+    }
   }
-  if constexpr (EXACT_LISTS) return;
   __syncthreads();
-  if (verdict != 1) return;
+  if (verdict == 0) return;
 
   // ---- tier 1: every row with approximate score >= L is in a list (checked below)
   const float L = floor_L;
+  if (verdict == 1)
   for (int l = tid; l < n_lists; l += 256) {
     const float h = heads_s[(int64_t)b * n_lists + l];
     if (h != kNegInf && h >= L) {
@@ -1911,27 +1898,78 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
     }
   }
   __syncthreads();
+  float rs = kNegInf;   // each wave's running exact top-32 (lanes 0..31, best first)
+  int ri = kIdNone32;
   if (verdict == 2) {
+    // ---- tier 2: stream the shard (tiles t = wid, wid + 4, ...: rows increase per wave)
+    constexpr int S = steps<D>();
+    const float e = eps[bq];
+    uint32_t fm = 0, fv = 0;
+    if constexpr (FILTER) {
+      fm = filt[2 * bq];
+      fv = filt[2 * bq + 1];
+    }
+    const int hh = lane >> 4, rr = lane & 15;
+    // lane (hh, rr): dims 32 s + 8 hh .. + 7 of row 16 t + rr and of query b (qprep's
+    // B-fragment of query tile b >> 4, column b & 15)
+    const half8* qf = qfrag + grp * (2 * S * 64) + ((b >> 4) * S) * 64 + hh * 16 + (b & 15);
+    float thr = nextafterf(floor_E, kNegInf);   // every true top-k row scores >= e_k
+    const int n_tiles = (n_rows + kTileRows - 1) / kTileRows;
+    for (int t = wid; t < n_tiles; t += 4) {
+      const half8* tp = corpus + (int64_t)t * (S * 64) + hh * 16 + rr;
+      float a = 0.f;
+#pragma unroll 4
+      for (int s2 = 0; s2 < S; ++s2) {
+        const half8 x = tp[s2 * 64], y = qf[s2 * 64];
+        a = __builtin_amdgcn_fdot2(half2v{x[0], x[1]}, half2v{y[0], y[1]}, a, false);
+        a = __builtin_amdgcn_fdot2(half2v{x[2], x[3]}, half2v{y[2], y[3]}, a, false);
+        a = __builtin_amdgcn_fdot2(half2v{x[4], x[5]}, half2v{y[4], y[5]}, a, false);
+        a = __builtin_amdgcn_fdot2(half2v{x[6], x[7]}, half2v{y[6], y[7]}, a, false);
+      }
+      a += __shfl_xor(a, 16, 64);
+      a += __shfl_xor(a, 32, 64);
+      const int row = t * kTileRows + rr;
+      bool ok = lane < 16 && row < n_rows;
+      if constexpr (FILTER) ok = ok && ((tags[row < n_rows ? row : 0] & fm) == fv);
+      uint64_t m = __ballot(ok && a >= fmaxf(L, thr - e));
+      while (m) {
+        int rows[8];
+        float es[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int ln = m ? (int)__builtin_ctzll(m) : -1;
+          if (m) m &= m - 1;
+          rows[j] = ln >= 0 ? t * kTileRows + ln : -1;
+        }
+        exact_scores_wave<D, 8>(corpus, rows, qq, lane, es);
+        float ns = kNegInf;
+        int ni = kIdNone32;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (lane == 32 + j && rows[j] >= 0 && es[j] > thr) {
+            ns = es[j];
+            ni = rows[j];
+          }
+        }
+        if (lane >= 32) {
+          rs = ns;
+          ri = ni;
+        }
+        bitonic_sort64(rs, ri, lane);
+        thr = fmaxf(thr, __shfl(rs, 31, 64));
+      }
+    }
     if (tid == 0) {
-      fb.L[bq] = L;
-      fb.E[bq] = floor_E;
       fb.tier[bq] = 2;
-      *fb.flag = 1;
       atomicAdd(&fb.cnt[1], 1ull);
     }
-    if (wid == 0) {   // provisional result (the exact pass overwrites it)
-      float s = lane < 32 ? e_s[lane] : kNegInf;
-      int id = lane < 32 ? e_i[lane] : kIdNone32;
-      bitonic_sort64(s, id, lane);
-      emit(s, id);
-    }
-    return;
+  } else {   // tier 1
+  if (tid == 0) {
+    fb.tier[bq] = 1;
+    atomicAdd(&fb.cnt[0], 1ull);
   }
-  if (tid == 0) atomicAdd(&fb.cnt[0], 1ull);
   // each wave: its share of the qualifying lists, entries >= L (a prefix of each sorted
-  // list) rescored 8 at a time into a running exact top-32 (lanes 0..31)
-  float rs = kNegInf;
-  int ri = kIdNone32;
+  // list) rescored 8 at a time into the running exact top-32
   const int nql = n_q;
   for (int i = wid; i < nql; i += 4) {
     const int l = qlist[i];
@@ -1968,6 +2006,7 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
       bitonic_sort64(rs, ri, lane);
     }
   }
+  }   // tier 1
   if (lane < 32) {
     c_s[wid][lane] = rs;
     c_i[wid][lane] = ri;
@@ -1985,142 +2024,6 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
     }
     emit(s, id);
   }
-}
-
-// ----------------------------------------------------------------------------------------
-// rescan (tier-2 exactness fallback): for the queries select flagged (fb.L finite), stream
-// the shard again, keep rows whose approximate score is >= max(L_q, thr - eps_q), score them
-// exactly (canonical arithmetic) and keep per-wave top-32 lists BY EXACT SCORE (thresholds in
-// the exact domain, starting at pred(E_q): every true top-k row scores >= E_q). A true top-k
-// row is in its wave's exact top-32 (k <= 32), so select<EXACT_LISTS> over these lists is the
-// exact top-k. Launched after every select; exits at once unless fb.flag is set.
-// One 4-wave workgroup per CU: query B-fragments staged in LDS, tiles t = gw, gw + nw, ...
-// (the interleave select uses to map a row to its list).
-// ----------------------------------------------------------------------------------------
-template <int D, bool FILTER>
-__global__ __launch_bounds__(256, 1) void rescan_kernel(
-    const half8* __restrict__ corpus, const uint32_t* __restrict__ tags,
-    const uint32_t* __restrict__ filt, const half8* __restrict__ qfrag,
-    const float* __restrict__ qn, const float* __restrict__ eps, Fallback fb, int n_rows,
-    int n_tiles, float* __restrict__ part_s, int* __restrict__ part_i,
-    float* __restrict__ heads_s, int* __restrict__ heads_i, int* __restrict__ heads_n) {
-  constexpr int S = steps<D>();
-  constexpr int CH = S % 8 == 0 ? 8 : (S % 4 == 0 ? 4 : 1);
-  __shared__ int lds[kWavesPerWG * kLdsPerWave];
-  __shared__ half8 qb[2 * S * 64];
-  if (__builtin_amdgcn_readfirstlane(*fb.flag) == 0) return;
-  const int g = blockIdx.y;
-  const float* Lq = fb.L + g * kQ;
-  const float* Eq = fb.E + g * kQ;
-  // any tier-2 query in this group?
-  {
-    const int lane0 = threadIdx.x & 63;
-    const bool any = __ballot(lane0 < kQ && Lq[lane0 & 31] < __builtin_inff()) != 0;
-    if (!any) return;
-  }
-  qfrag += g * (2 * S * 64);
-  filt += g * (2 * kQ);
-  qn += (int64_t)g * kQ * D;
-  eps += g * kQ;
-  const int nw = gridDim.x * kWavesPerWG;
-  part_s += (int64_t)g * nw * (kQ * kKS);
-  part_i += (int64_t)g * nw * (kQ * kKS);
-  heads_s += (int64_t)g * kQ * nw;
-  heads_i += (int64_t)g * kQ * nw;
-  heads_n += (int64_t)g * kQ * nw;
-  for (int i = threadIdx.x; i < 2 * S * 64; i += 256) qb[i] = qfrag[i];
-  const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
-  ScanTopK st;
-  topk_init<FILTER>(st, lds, wid, lane, nullptr, filt);
-  const int c0 = lane & 15, c1 = 16 + (lane & 15);
-  const float L0 = Lq[c0], L1 = Lq[c1];
-  const float ep0 = eps[c0], ep1 = eps[c1];
-  const float inf = __builtin_inff();
-  st.thr0 = L0 < inf ? nextafterf(Eq[c0], kNegInf) : inf;
-  st.thr1 = L1 < inf ? nextafterf(Eq[c1], kNegInf) : inf;
-  __syncthreads();
-
-  const int gw = blockIdx.x * kWavesPerWG + __builtin_amdgcn_readfirstlane(wid);
-  int t_first, t_step, n_mine;
-  tile_sequence<true>(gw, nw, n_tiles, t_first, t_step, n_mine);
-  for (int j = 0; j < n_mine; ++j) {
-    const int t = t_first + j * t_step;
-    const half8* tp = corpus + (int64_t)t * (S * 64) + lane;
-    floatx4 acc0 = {0.f, 0.f, 0.f, 0.f};
-    floatx4 acc1 = {0.f, 0.f, 0.f, 0.f};
-    for (int s0 = 0; s0 < S; s0 += CH) {
-      half8 a[CH];
-#pragma unroll
-      for (int s = 0; s < CH; ++s) a[s] = tp[(s0 + s) * 64];
-#pragma unroll
-      for (int s = 0; s < CH; ++s) {
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[s], qb[(s0 + s) * 64 + lane], acc0, 0,
-                                                      0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[s], qb[(S + s0 + s) * 64 + lane], acc1,
-                                                      0, 0, 0);
-      }
-    }
-    const int rbase = t * kTileRows + 4 * (lane >> 4);
-    uint4 tg = {0u, 0u, 0u, 0u};
-    if constexpr (FILTER) tg = *reinterpret_cast<const uint4*>(tags + rbase);
-    const float f0 = fmaxf(L0, st.thr0 - ep0), f1 = fmaxf(L1, st.thr1 - ep1);
-    bool pass[8];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const bool ok = (rbase + r) < n_rows;
-      bool ok0 = ok, ok1 = ok;
-      if constexpr (FILTER) {
-        const uint32_t tr = r == 0 ? tg.x : r == 1 ? tg.y : r == 2 ? tg.z : tg.w;
-        ok0 = ok0 && ((tr & st.fm0) == st.fv0);
-        ok1 = ok1 && ((tr & st.fm1) == st.fv1);
-      }
-      pass[r] = ok0 && acc0[r] >= f0;
-      pass[4 + r] = ok1 && acc1[r] >= f1;
-    }
-    bool any = false;
-#pragma unroll
-    for (int p = 0; p < 8; ++p) any = any || pass[p];
-    if (!__ballot(any)) continue;
-#pragma unroll
-    for (int p = 0; p < 8; ++p) {
-      uint64_t m = __ballot(pass[p]);
-      while (m) {
-        int ln[8], rows[8], qoff[8];
-        float es[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          ln[i] = m ? (int)__builtin_ctzll(m) : -1;
-          if (m) m &= m - 1;
-          rows[i] = ln[i] >= 0 ? t * kTileRows + 4 * (ln[i] >> 4) + (p & 3) : -1;
-          qoff[i] = ln[i] >= 0 ? ((p >> 2) * 16 + (ln[i] & 15)) * D : 0;
-        }
-        exact_scores_pairs<D, 8>(corpus, rows, qoff, qn, lane, es);
-        float e = kNegInf;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) e = lane == ln[i] ? es[i] : e;
-        if (p < 4) {
-          if (e > st.thr0) {
-            st.w.pend_s[st.cnt0 * 64 + lane] = e;
-            st.w.pend_i[st.cnt0 * 64 + lane] = rbase + (p & 3);
-            ++st.cnt0;
-          }
-        } else {
-          if (e > st.thr1) {
-            st.w.pend_s[(kP + st.cnt1) * 64 + lane] = e;
-            st.w.pend_i[(kP + st.cnt1) * 64 + lane] = rbase + (p & 3);
-            ++st.cnt1;
-          }
-        }
-      }
-    }
-    lds_fence();
-    const uint64_t b0 = __ballot(st.cnt0 > kP - 4);
-    const uint64_t b1 = __ballot(st.cnt1 > kP - 4);
-    if (b0) flush_mask(st.w, b0, 0, lane, st.thr0, st.cnt0, st.thr1, st.cnt1);
-    if (b1) flush_mask(st.w, b1, 1, lane, st.thr0, st.cnt0, st.thr1, st.cnt1);
-  }
-  topk_finish(st, lane, gw, nw, part_s, part_i, heads_s, heads_i, heads_n);
 }
 
 // ----------------------------------------------------------------------------------------
