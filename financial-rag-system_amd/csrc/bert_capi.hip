@@ -323,6 +323,16 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
     }
     return;
   }
+  if (variant == RAG_GEMM_BIG && N % 256 == 0) {
+    if (Al) launch_pipe<EPI, true, PipeBig>(A, Al, W, Wl, bias, M, N, K, C, Clo, st, cu_count());
+    else launch_pipe<EPI, false, PipeBig>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st, cu_count());
+    return;
+  }
+  if (variant == RAG_GEMM_BIG128 || variant == RAG_GEMM_BIG) {
+    if (Al) launch_pipe<EPI, true, PipeBig128>(A, Al, W, Wl, bias, M, N, K, C, Clo, st, cu_count());
+    else launch_pipe<EPI, false, PipeBig128>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st, cu_count());
+    return;
+  }
   if (variant == RAG_GEMM_PIPE || variant == RAG_GEMM_WIDE) {
     if (Al)
       launch_pipe<EPI, true, PipeLarge>(A, Al, W, Wl, bias, M, N, K, C, Clo, st, cu_count());
@@ -615,7 +625,7 @@ int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, co
   if (A_lo && epilogue != kEpiF32 && !C_lo)
     return ragmi::fail(RAG_EINVAL, "fp16x3 fp16-output GEMM needs C_lo");
   if ((variant == RAG_GEMM_PIPE || variant == RAG_GEMM_SMALL || variant == RAG_GEMM_WIDE ||
-       variant == RAG_GEMM_SMALL_BK64) &&
+       variant == RAG_GEMM_SMALL_BK64 || variant == RAG_GEMM_BIG || variant == RAG_GEMM_BIG128) &&
       !pipe_ok(M, N, K))
     return ragmi::fail(RAG_EINVAL, "pipe/small/wide variants need N % 128 == 0, K % 64 == 0, "
                                    "N <= 4096, M*K*2 and M*N*4 < 2^31");
@@ -623,7 +633,8 @@ int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, co
                      variant == RAG_GEMM_PROBE_NO_SYNC;
   const bool known = variant == RAG_GEMM_AUTO || variant == RAG_GEMM_TILE ||
                      variant == RAG_GEMM_PIPE || variant == RAG_GEMM_SMALL ||
-                     variant == RAG_GEMM_WIDE || variant == RAG_GEMM_SMALL_BK64 || probe;
+                     variant == RAG_GEMM_WIDE || variant == RAG_GEMM_SMALL_BK64 ||
+                     variant == RAG_GEMM_BIG || variant == RAG_GEMM_BIG128 || probe;
   if (!known || (probe && (A_lo || !pipe_ok(M, N, K))))
     return ragmi::fail(RAG_EINVAL, "unknown GEMM variant (probes: fp16 only)");
   auto* a = static_cast<const _Float16*>(A);

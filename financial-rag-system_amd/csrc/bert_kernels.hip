@@ -378,6 +378,11 @@ using PipeSmallSplit64 = PipeCfg<64, 64, 2, 2, 4, 64>;
 // wider N tiles: fewer panel bytes per FLOP (256x256: 128 FLOP/B fp16 vs 85 at 256x128) at
 // the price of a 2-stage ring (one stage in flight)
 using PipeWide256 = PipeCfg<256, 256, 4, 2, 2>;
+// register-blocked shapes (round 2): 4 waves, each 128 x 128 (BIG) or 128 x 64 (BIG128) —
+// half / three quarters of the LDS fragment bytes per MFMA of the 64 x 64-per-wave tiles,
+// one wave per SIMD (256 / 128 accumulator registers)
+using PipeBig = PipeCfg<256, 256, 2, 2, 2>;
+using PipeBig128 = PipeCfg<256, 128, 2, 2, 3>;
 using PipeWide192 = PipeCfg<256, 192, 4, 2, 2>;
 constexpr int PBM = PipeLarge::BM, PBN = PipeLarge::BN;
 constexpr int kPipeThreads = PipeLarge::THREADS;

@@ -1615,11 +1615,11 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
                                                      int64_t* __restrict__ out_i,
                                                      int32_t* __restrict__ out_packed) {
   __shared__ float w_s[4][32];
-  __shared__ int w_i[4][32];
+  __shared__ int64_t w_i[4][32];
   __shared__ int sel[32];
   __shared__ int sel_n[32];
   __shared__ float cand_s[kCandCap];
-  __shared__ int cand_i[kCandCap];
+  __shared__ int64_t cand_i[kCandCap];
   __shared__ int n_cand;
   __shared__ float head_t;
   __shared__ float c_s[4][32];
@@ -1640,18 +1640,23 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
   heads_n += (int64_t)grp * kQ * n_lists;
   auto at = [&](int l, int pos) { return ((int64_t)l * kQ + b) * kKS + pos; };
 
-  // ---- 1. the 32 best list heads (a list = one scan wave; under the interleaved tile order
-  //      the wave of row r is (r >> 4) % n_lists, so the row alone identifies the list).
+  // ---- 1. the 32 best list heads (a list = one scan wave). Heads are ranked by (score desc,
+  //      row asc) with the list index carried in the low bits of a 64-bit id (row << 11 |
+  //      list): select needs no knowledge of which tiles a wave scanned (static interleave,
+  //      dynamic tile queue or the rescan's own order).
   constexpr int kCols = kMaxLists / 256;
+  static_assert(kMaxLists <= 2048, "list index packs into 11 bits");
+  auto hid = [](int row, int l) { return ((int64_t)row << 11) | (int64_t)l; };
+  constexpr int64_t kId64None = INT64_MAX;
   float hs[kCols];
-  int hr[kCols];
+  int64_t hr[kCols];
   // unconditional (clamped) loads, selects afterwards: a load under a data-dependent branch
   // makes hipcc wait vmcnt(0) per element (one round trip each)
 #pragma unroll
   for (int j = 0; j < kCols; ++j) {
     const int l = min((j * 4 + wid) * 64 + lane, n_lists - 1);
     hs[j] = heads_s[(int64_t)b * n_lists + l];
-    hr[j] = heads_i[(int64_t)b * n_lists + l];
+    hr[j] = hid(heads_i[(int64_t)b * n_lists + l], l);
   }
   float lmax = kNegInf;
 #pragma unroll
@@ -1659,7 +1664,7 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
     const int l = (j * 4 + wid) * 64 + lane;
     const bool ok = l < n_lists && hs[j] != kNegInf;
     hs[j] = ok ? hs[j] : kNegInf;
-    hr[j] = ok ? hr[j] : kIdNone32;
+    hr[j] = ok ? hr[j] : kId64None;
     lmax = fmaxf(lmax, hs[j]);
   }
   // 1a. T = 32nd largest lane maximum (the maxima of 32 distinct lanes are 32 distinct heads,
@@ -1709,7 +1714,7 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
   if (nc <= kCandCap) {
     // 1c. top-32 of the compacted heads: each wave sorts 64 of them, wave 0 merges
     float m = kNegInf;
-    int id = kIdNone32;
+    int64_t id = kId64None;
     if (64 * wid + lane < nc) {
       m = cand_s[64 * wid + lane];
       id = cand_i[64 * wid + lane];
@@ -1722,15 +1727,16 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
   } else {
     // 1c'. adversarial ties (more than kCandCap heads at the threshold): exact column sort
     float cs = kNegInf;
-    int ci = kIdNone32;
+    int64_t ci = kId64None;
 #pragma unroll
     for (int j = 0; j < kCols; ++j) {
       if (!__ballot(hs[j] != kNegInf)) continue;   // wave-uniform: empty column
       float x = hs[j];
-      int id = hr[j];
+      int64_t id = hr[j];
       bitonic_sort64(x, id, lane);
       const float rx = __shfl(x, 63 - lane, 64);
-      const int ri = __shfl(id, 63 - lane, 64);
+      const int64_t ri = (int64_t)(((uint64_t)(uint32_t)__shfl((int)(id >> 32), 63 - lane, 64) << 32) |
+                                   (uint32_t)__shfl((int)id, 63 - lane, 64));
       if (lane >= 32) {
         cs = rx;
         ci = ri;
@@ -1738,7 +1744,7 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
       bitonic_merge64(cs, ci, lane);
       if (lane >= 32) {
         cs = kNegInf;
-        ci = kIdNone32;
+        ci = kId64None;
       }
     }
     if (lane < 32) {
@@ -1749,7 +1755,7 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
   __syncthreads();
   if (wid == 0) {
     float x = lane < 32 ? w_s[0][lane] : kNegInf;
-    int id = lane < 32 ? w_i[0][lane] : kIdNone32;
+    int64_t id = lane < 32 ? w_i[0][lane] : kId64None;
     for (int v = 1; v < 4; ++v) {
       if (lane >= 32) {
         x = w_s[v][63 - lane];
@@ -1758,7 +1764,7 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
       bitonic_merge64(x, id, lane);
     }
     if (lane < 32) {
-      const int l = (x != kNegInf) ? (int)(((uint32_t)id >> 4) % (uint32_t)n_lists) : -1;
+      const int l = (x != kNegInf) ? (int)(id & 2047) : -1;
       sel[lane] = l;
       sel_n[lane] = l >= 0 ? heads_n[(int64_t)b * n_lists + l] : 0;
     }

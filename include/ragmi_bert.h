@@ -95,7 +95,8 @@ int rag_build_pairs(const int32_t* q_ids, const int32_t* q_cu, int B, const int6
 enum { RAG_EPI_F16 = 0, RAG_EPI_GELU_F16 = 1, RAG_EPI_F32 = 2 };
 enum { RAG_GEMM_AUTO = 0, RAG_GEMM_TILE = 1, RAG_GEMM_PIPE = 2, RAG_GEMM_PROBE_NO_MFMA = 3,
        RAG_GEMM_PROBE_NO_DMA = 4, RAG_GEMM_SMALL = 5, RAG_GEMM_WIDE = 8,
-       RAG_GEMM_PROBE_NO_SYNC = 9, RAG_GEMM_SMALL_BK64 = 10 };
+       RAG_GEMM_PROBE_NO_SYNC = 9, RAG_GEMM_SMALL_BK64 = 10, RAG_GEMM_BIG = 11,
+       RAG_GEMM_BIG128 = 12 };
 int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, const void* W,
                   const void* W_lo, const float* bias, int M, int N, int K, void* C,
                   void* C_lo, void* stream);

@@ -20,7 +20,7 @@ from ragmi.encoders import EPI_F16, EPI_F32, EPI_GELU_F16, linear  # noqa: E402
 
 PEAK = 2.5e15
 VNAME = {0: "auto", 1: "tile", 2: "pipe", 3: "probe_no_mfma", 4: "probe_no_dma", 5: "small",
-         8: "wide", 9: "probe_no_sync", 10: "small_bk64"}
+         8: "wide", 9: "probe_no_sync", 10: "small_bk64", 11: "big", 12: "big128"}
 LAYERS = {
     "small": [("qkv", 1152, 384, EPI_F16), ("o", 384, 384, EPI_F32),
               ("ffn1", 1536, 384, EPI_GELU_F16), ("ffn2", 384, 1536, EPI_F32)],

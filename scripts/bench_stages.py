@@ -104,8 +104,12 @@ def main():
               ("rerank", R.MINILM_CE, HEAD_POOLER_CLS, (480, 200, 288, True)),
               # config 5 query encoder: bge-large-en-v1.5 shape, 128 queries
               ("encode_q_large", R.BGE_LARGE, HEAD_CLS_L2, (128, 16, 32, False))]
-    for prec in ("fp16", "fp16x3"):
+    only = os.environ.get("STAGES")          # e.g. STAGES=rerank PRECS=fp16x3
+    precs = os.environ.get("PRECS", "fp16,fp16x3").split(",")
+    for prec in precs:
         for name, cfg, head, (B, lo, hi, pair) in stages:
+            if only and name not in only.split(","):
+                continue
             w = R.make_weights(cfg, 1)
             enc = BertEncoder(cfg, w, head, dev, prec)
             ids, tt, cu = batch(rng, B, lo, hi, pair)

@@ -26,7 +26,8 @@ def _grid(g, shape, den, kmax):
 @pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "x".join(map(str, s)))
 @pytest.mark.parametrize("epi", [0, 2], ids=["f16", "f32"])
 @pytest.mark.parametrize("split", [False, True], ids=["fp16", "fp16x3"])
-@pytest.mark.parametrize("variant", [1, 2, 5, 8, 10], ids=["tile", "pipe", "small", "wide", "small64"])
+@pytest.mark.parametrize("variant", [1, 2, 5, 8, 10, 11, 12],
+                         ids=["tile", "pipe", "small", "wide", "small64", "big", "big128"])
 def test_gemm_epilogue_bit_exact(gpu, shape, epi, split, variant):
     from ragmi.encoders import linear
     M, N, K = shape
