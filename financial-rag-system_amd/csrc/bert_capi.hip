@@ -6,6 +6,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/ragmi_bert.h"
@@ -221,6 +222,15 @@ void launch_pipe(const _Float16* A, const _Float16* Al, const _Float16* W, const
       A, Al, W, Wl, bias, M, N, K, C, Clo, ln);
 }
 
+template <int EPI, bool SPLIT, typename CFG, int PROBE = 0, int AUX = 0>
+void launch_ws(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float16* Wl,
+               const float* bias, int M, int N, int K, void* C, _Float16* Clo, hipStream_t st) {
+  const int tiles = (N / CFG::BN) * ((M + CFG::BM - 1) / CFG::BM);
+  const dim3 grid((unsigned)std::min(cu_count(), (tiles + 7) / 8 * 8));
+  gemm_ws_kernel<EPI, SPLIT, CFG, PROBE, AUX><<<grid, dim3(CFG::THREADS + 256), 0, st>>>(
+      A, Al, W, Wl, bias, M, N, K, C, Clo);
+}
+
 // the fused output projection + residual + LayerNorm (kEpiAddLn on PipeRow tiles)
 bool add_ln_ok(int M, int N, int K) {
   return N == PipeRow::BN && K % 64 == 0 && (int64_t)M * K * 2 < (int64_t(1) << 31) &&
@@ -285,32 +295,41 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
   const bool auto_pick = variant == RAG_GEMM_AUTO;
   const int pipe_tiles = (N / PBN) * ((M + PBM - 1) / PBM);
   // SMALL while its 64x64 tiles fit about two per CU (every query-batch GEMM; the N = 384
-  // ones up to ~5K tokens), PIPE once its 256x128 tiles cover the CUs, TILE in between
-  // (WIDE, 256x256, for N % 256 == 0 once it has two tiles per CU: rerank-size FFN1,
-  // measured 0.236 -> 0.217 ms at 117K x 1536 x 384 fp16; below that PIPE is faster)
+  // ones up to ~5K tokens), then WS (the loader-specialised pipe) once its 256x128 tiles reach
+  // half the CUs, TILE in between. Measured per layer (QKV + O + FFN1 + FFN2, scripts/
+  // bench_gemm.py, profiles/r02_gemm_ws.jsonl): 117K tokens fp16x3 WS 1.337 ms vs PIPE 1.447,
+  // WIDE 1.416, TILE 1.547; 14.8K fp16x3 0.190 vs 0.216 / 0.223 / 0.216; at 4K tokens the
+  // N = 384 GEMMs (48 tiles) run faster as TILE
   const int small_tiles = (N / 64) * ((M + 63) / 64);
-  const int wide_tiles = N % 256 == 0 ? (N / 256) * ((M + 255) / 256) : 0;
   if (variant == RAG_GEMM_AUTO)
     variant = !pipe_ok(M, N, K)                  ? RAG_GEMM_TILE
               : small_tiles <= 2 * cu_count()    ? RAG_GEMM_SMALL
-              : wide_tiles >= 2 * cu_count()     ? RAG_GEMM_WIDE
-              : pipe_tiles >= cu_count()         ? RAG_GEMM_PIPE
+              : 2 * pipe_tiles >= cu_count()     ? RAG_GEMM_WS
                                                  : RAG_GEMM_TILE;
   if (variant != RAG_GEMM_TILE && !pipe_ok(M, N, K)) variant = RAG_GEMM_TILE;
   if (auto_pick && variant == RAG_GEMM_SMALL && Al) variant = RAG_GEMM_SMALL_BK64;
-  if (variant == RAG_GEMM_PROBE_NO_MFMA) {       // diagnostic probes of the PIPE kernel
-    launch_pipe<EPI, false, PipeLarge, 1>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st,
-                                          cu_count());
-    return;
-  }
-  if (variant == RAG_GEMM_PROBE_NO_SYNC) {
-    launch_pipe<EPI, false, PipeLarge, 3>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr,
-                                          st, cu_count());
-    return;
-  }
-  if (variant == RAG_GEMM_PROBE_NO_DMA) {
-    launch_pipe<EPI, false, PipeLarge, 2>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st,
-                                          cu_count());
+  // diagnostic probes of the PIPE kernel (parts removed; bert_kernels.hip PROBE)
+  const int probe = variant == RAG_GEMM_PROBE_NO_MFMA           ? 1
+                    : variant == RAG_GEMM_PROBE_NO_DMA          ? 2
+                    : variant == RAG_GEMM_PROBE_NO_SYNC         ? 3
+                    : variant == RAG_GEMM_PROBE_NO_STORE        ? 6
+                    : variant == RAG_GEMM_PROBE_MFMA_ONLY       ? 7
+                    : variant == RAG_GEMM_PROBE_DMA_ONLY        ? 8
+                                                                : 0;
+  if (probe) {
+    auto go = [&](auto pc) {
+      constexpr int P = decltype(pc)::value;
+      if (Al) launch_pipe<EPI, true, PipeLarge, P>(A, Al, W, Wl, bias, M, N, K, C, Clo, st, cu_count());
+      else launch_pipe<EPI, false, PipeLarge, P>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st, cu_count());
+    };
+    switch (probe) {
+      case 1: go(std::integral_constant<int, 1>{}); break;
+      case 2: go(std::integral_constant<int, 2>{}); break;
+      case 3: go(std::integral_constant<int, 3>{}); break;
+      case 6: go(std::integral_constant<int, 6>{}); break;
+      case 7: go(std::integral_constant<int, 7>{}); break;
+      default: go(std::integral_constant<int, 8>{}); break;
+    }
     return;
   }
   // (256x192 fp16x3 would split a stage's W rows unevenly over the waves: fp16 only)
@@ -320,6 +339,32 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
       else launch_pipe<EPI, false, PipeWide256>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st, cu_count());
     } else {
       launch_pipe<EPI, false, PipeWide192>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st, cu_count());
+    }
+    return;
+  }
+  if (variant == RAG_GEMM_WS || variant == RAG_GEMM_WS_MFMA_ONLY ||
+      variant == RAG_GEMM_WS_NO_STORE || variant == RAG_GEMM_WS_DMA_ONLY ||
+      variant == RAG_GEMM_WS_L2_STORE || variant == RAG_GEMM_WS_NT) {
+    auto go = [&](auto pc) {
+      constexpr int P = decltype(pc)::value;
+      if (Al) launch_ws<EPI, true, PipeLarge, P>(A, Al, W, Wl, bias, M, N, K, C, Clo, st);
+      else launch_ws<EPI, false, PipeLarge, P>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st);
+    };
+    if (variant == RAG_GEMM_WS) {
+      // non-temporal stores for the fp16 outputs (QKV / FFN1: 117K x 1152 fp16x3 0.354 ->
+      // 0.310 ms, the streamed 540 MB no longer evicting the A panels the n-tiles of an XCD
+      // share); the fp32 ones (O / FFN2, read back at once by add_ln) keep the default policy
+      constexpr int AX = EPI == kEpiF32 ? 0 : 2;
+      if (Al) launch_ws<EPI, true, PipeLarge, 0, AX>(A, Al, W, Wl, bias, M, N, K, C, Clo, st);
+      else launch_ws<EPI, false, PipeLarge, 0, AX>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st);
+    }
+    else if (variant == RAG_GEMM_WS_MFMA_ONLY) go(std::integral_constant<int, 7>{});
+    else if (variant == RAG_GEMM_WS_NO_STORE) go(std::integral_constant<int, 6>{});
+    else if (variant == RAG_GEMM_WS_L2_STORE) go(std::integral_constant<int, 9>{});
+    else if (variant == RAG_GEMM_WS_DMA_ONLY) go(std::integral_constant<int, 8>{});
+    else if (variant == RAG_GEMM_WS_NT) {
+      if (Al) launch_ws<EPI, true, PipeLarge, 0, 2>(A, Al, W, Wl, bias, M, N, K, C, Clo, st);
+      else launch_ws<EPI, false, PipeLarge, 0, 2>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st);
     }
     return;
   }
@@ -625,18 +670,23 @@ int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, co
   if (A_lo && epilogue != kEpiF32 && !C_lo)
     return ragmi::fail(RAG_EINVAL, "fp16x3 fp16-output GEMM needs C_lo");
   if ((variant == RAG_GEMM_PIPE || variant == RAG_GEMM_SMALL || variant == RAG_GEMM_WIDE ||
-       variant == RAG_GEMM_SMALL_BK64 || variant == RAG_GEMM_BIG || variant == RAG_GEMM_BIG128) &&
+       variant == RAG_GEMM_SMALL_BK64 || variant == RAG_GEMM_BIG || variant == RAG_GEMM_BIG128 ||
+       variant == RAG_GEMM_WS || variant == RAG_GEMM_WS_NT) &&
       !pipe_ok(M, N, K))
     return ragmi::fail(RAG_EINVAL, "pipe/small/wide variants need N % 128 == 0, K % 64 == 0, "
                                    "N <= 4096, M*K*2 and M*N*4 < 2^31");
   const bool probe = variant == RAG_GEMM_PROBE_NO_MFMA || variant == RAG_GEMM_PROBE_NO_DMA ||
-                     variant == RAG_GEMM_PROBE_NO_SYNC;
+                     variant == RAG_GEMM_PROBE_NO_SYNC || variant == RAG_GEMM_PROBE_NO_STORE ||
+                     variant == RAG_GEMM_PROBE_MFMA_ONLY || variant == RAG_GEMM_PROBE_DMA_ONLY ||
+                     variant == RAG_GEMM_WS_MFMA_ONLY || variant == RAG_GEMM_WS_NO_STORE ||
+                     variant == RAG_GEMM_WS_DMA_ONLY || variant == RAG_GEMM_WS_L2_STORE;
   const bool known = variant == RAG_GEMM_AUTO || variant == RAG_GEMM_TILE ||
                      variant == RAG_GEMM_PIPE || variant == RAG_GEMM_SMALL ||
                      variant == RAG_GEMM_WIDE || variant == RAG_GEMM_SMALL_BK64 ||
-                     variant == RAG_GEMM_BIG || variant == RAG_GEMM_BIG128 || probe;
-  if (!known || (probe && (A_lo || !pipe_ok(M, N, K))))
-    return ragmi::fail(RAG_EINVAL, "unknown GEMM variant (probes: fp16 only)");
+                     variant == RAG_GEMM_BIG || variant == RAG_GEMM_BIG128 ||
+                     variant == RAG_GEMM_WS || variant == RAG_GEMM_WS_NT || probe;
+  if (!known || (probe && !pipe_ok(M, N, K)))
+    return ragmi::fail(RAG_EINVAL, "unknown GEMM variant, or a probe on a non-pipe shape");
   auto* a = static_cast<const _Float16*>(A);
   auto* al = static_cast<const _Float16*>(A_lo);
   auto* w = static_cast<const _Float16*>(W);

@@ -437,13 +437,90 @@ __device__ __forceinline__ void wait_ring(int y, bool stored) {
 // which every lane holds 8 consecutive columns: 16-B stores, half the store instructions of
 // 8-B ones (the epilogue is store-issue-bound). Lane group g = lane >> 4 then owns columns
 // 16 j + {0, 16, 8, 24}[g] .. +7 (byte offset vo).
+template <int AUX = 0>
 __device__ __forceinline__ void store_f16_pair(half4 xa, half4 xb, __amdgpu_buffer_rsrc_t rsc,
                                                int vo, int so = 0) {
   u32x2 a = __builtin_bit_cast(u32x2, xa), b = __builtin_bit_cast(u32x2, xb);
   const auto r0 = __builtin_amdgcn_permlane16_swap(a[0], b[0], false, false);
   const auto r1 = __builtin_amdgcn_permlane16_swap(a[1], b[1], false, false);
   const u32x4 d = {r0[0], r1[0], r0[1], r1[1]};
-  __builtin_amdgcn_raw_buffer_store_b128(d, rsc, vo, so, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(d, rsc, vo, so, AUX);
+}
+
+// the plain epilogues (kEpiF16 / kEpiGeluF16 / kEpiF32) of one wave's FM x FN accumulator
+// fragments of the tile at column n0 (rc / rl: the output panels from the tile's row m0):
+// bias (staged in LDS), GELU, then fp32 16-B stores or fp16 [+ lo plane] paired 16-B stores
+// straight from registers — exactly pipe_plain_stores<EPI, SPLIT, CFG>() stores per wave (the
+// ring's vmcnt accounting counts them). NO_STORE: timing probe, nothing written. AUX: the
+// stores' cache policy (buffer-op aux bits; 2 = nt).
+template <int EPI, bool SPLIT, typename CFG>
+constexpr int pipe_plain_stores() {
+  return EPI == kEpiF32 ? CFG::FM * CFG::FN : CFG::FM * CFG::FN / 2 * (SPLIT ? 2 : 1);
+}
+
+// one fragment pair (i, jp), (i, jp + 1) of it
+template <int EPI, bool SPLIT, typename CFG, bool NO_STORE, int AUX = 0>
+__device__ __forceinline__ void pipe_epi_pair(const floatx4& a0, const floatx4& a1, int i, int jp,
+                                              const float* bias_l, __amdgpu_buffer_rsrc_t rc,
+                                              __amdgpu_buffer_rsrc_t rl, int N, int n0, int wr,
+                                              int wc, int lane) {
+  constexpr int WTM = 16 * CFG::FM, WTN = 16 * CFG::FN;
+  const int g = lane >> 4;
+  const int ml = wr * WTM + i * 16 + (lane & 15);
+  if constexpr (EPI == kEpiF32) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int nl = wc * WTN + (jp + h) * 16 + 4 * g;
+      const floatx4 v = (h ? a1 : a0) + *reinterpret_cast<const floatx4*>(bias_l + n0 + nl);
+      if (!NO_STORE || v[0] == 1234.5f)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rc,
+                                               (ml * N + n0 + nl) * 4, 0, AUX);
+    }
+  } else {
+    // fp16 out, two fragments per 16-B store (store_f16_pair)
+    const int cofs = 8 * ((g & 1) * 2 + (g >> 1));
+    const floatx4 b0 = *reinterpret_cast<const floatx4*>(bias_l + n0 + wc * WTN + jp * 16 + 4 * g);
+    const floatx4 b1 = *reinterpret_cast<const floatx4*>(bias_l + n0 + wc * WTN + jp * 16 + 16 + 4 * g);
+    const int vo = (ml * N + n0 + wc * WTN + jp * 16 + cofs) * 2;
+    floatx4 va = a0 + b0, vb = a1 + b1;
+    if constexpr (EPI == kEpiGeluF16) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        va[r] = gelu_erf(va[r]);
+        vb[r] = gelu_erf(vb[r]);
+      }
+    }
+    half4 ha, hb;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      ha[r] = (_Float16)va[r];
+      hb[r] = (_Float16)vb[r];
+    }
+    if (!NO_STORE || va[0] == 1234.5f) store_f16_pair<AUX>(ha, hb, rc, vo);
+    if constexpr (SPLIT) {
+      half4 la, lb;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        la[r] = lo_part(va[r], ha[r]);
+        lb[r] = lo_part(vb[r], hb[r]);
+      }
+      if (!NO_STORE || vb[0] == 1234.5f) store_f16_pair<AUX>(la, lb, rl, vo);
+    }
+  }
+}
+
+template <int EPI, bool SPLIT, typename CFG, bool NO_STORE, int AUX = 0>
+__device__ __forceinline__ void pipe_plain_epilogue(const floatx4 (&acc)[CFG::FM][CFG::FN],
+                                                    const float* bias_l,
+                                                    __amdgpu_buffer_rsrc_t rc,
+                                                    __amdgpu_buffer_rsrc_t rl, int N, int n0,
+                                                    int wr, int wc, int lane) {
+#pragma unroll
+  for (int jp = 0; jp < CFG::FN; jp += 2)
+#pragma unroll
+    for (int i = 0; i < CFG::FM; ++i)
+      pipe_epi_pair<EPI, SPLIT, CFG, NO_STORE, AUX>(acc[i][jp], acc[i][jp + 1], i, jp, bias_l, rc,
+                                                   rl, N, n0, wr, wc, lane);
 }
 
 // kEpiAddLn operands besides the GEMM's (Cout = the fp32 residual rows x, read and
@@ -457,6 +534,9 @@ struct LnArgs {
 
 // PROBE (diagnostic builds only, rag_bert_gemm variants 3/4/9): timing probes of the same
 // kernel with parts removed — 1 = no MFMAs, 2 = no DMAs, 3 = no DMAs and no barriers.
+// 6 = epilogue without its stores (bias, GELU and conversions run; nothing is written):
+// the cost of the epilogue's store stream; 7 = no DMAs and no stores (MFMAs, LDS reads and
+// barriers only); 8 = no MFMAs and no stores (the DMA ring alone).
 // kEpiAddLn only (rag_bert_gemm_add_ln_probe): 4 = the fp16 copy [+ lo plane] stored with
 // the plain epilogue's paired 16-B stores (store_f16_pair) and a store count S matching
 // them; 5 = the same stores with S still counting the 8-B stores (more than are issued: the
@@ -480,7 +560,11 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
   // (kEpiAddLn: the fp32 rows and the fp16 copy [+ lo plane], 8-B stores for the latter).
   // The count is capped at what vmcnt can express: waiting until fewer ops are outstanding
   // than were issued after the awaited stage is only stricter.
-  constexpr int S_ISSUED = EPI == kEpiF32     ? FM * FN
+  constexpr bool P_NO_MFMA = PROBE == 1 || PROBE == 8;
+  constexpr bool P_NO_DMA = PROBE == 2 || PROBE == 3 || PROBE == 7;
+  constexpr bool P_NO_STORE = PROBE == 6 || PROBE == 7 || PROBE == 8;
+  constexpr int S_ISSUED = P_NO_STORE           ? 0
+                           : EPI == kEpiF32     ? FM * FN
                            : EPI == kEpiAddLn ? (PROBE == 4 ? FM * FN + FM * FN / 2 * (SPLIT ? 2 : 1)
                                                             : FM * FN * (SPLIT ? 3 : 2))
                                               : FM * FN / 2 * (SPLIT ? 2 : 1);
@@ -541,7 +625,7 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
   __amdgpu_buffer_rsrc_t rA0 = panel(A, 0), rA1 = rA0, rW0 = rA0, rW1 = rA0;
   auto issue_next = [&]() {
     if (it_i >= n_mine) return;
-    if constexpr (PROBE == 2 || PROBE == 3) {
+    if constexpr (P_NO_DMA) {
       if (++kt_i == nk) { kt_i = 0; ++it_i; }
       return;
     }
@@ -598,7 +682,7 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
 
     const half8* sa = lds + slot_c * STAGE_H8;
     const half8* sw = sa + NPL * A_H8;
-    if constexpr (PROBE != 1 && CFG::PRELOAD) {
+    if constexpr (!P_NO_MFMA && CFG::PRELOAD) {
       // every fragment of the K step issued back to back, then the MFMAs (left alone, the
       // compiler loads each fragment just before its first use and waits every few MFMAs;
       // this order measured ~3% faster on the 256-row tiles)
@@ -632,7 +716,7 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
           }
     }
 #pragma unroll
-    for (int ks = 0; ks < (PROBE == 1 || CFG::PRELOAD ? 0 : BK / 32); ++ks) {
+    for (int ks = 0; ks < (P_NO_MFMA || CFG::PRELOAD ? 0 : BK / 32); ++ks) {
       const int ch = ks * 4 + (lane >> 4);
       half8 af[FM], wf[FN];
 #pragma unroll
@@ -799,58 +883,203 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
             }
           }
         }
-      } else if constexpr (EPI == kEpiF32) {
-#pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          const int nl = wc * WTN + j * 16 + 4 * (lane >> 4);
-          const floatx4 bj = *reinterpret_cast<const floatx4*>(bias_l + n0 + nl);
-#pragma unroll
-          for (int i = 0; i < FM; ++i) {
-            const int ml = wr * WTM + i * 16 + (lane & 15);
-            const floatx4 v = acc[i][j] + bj;
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rc,
-                                                   (ml * N + n0 + nl) * 4, 0, 0);
-          }
-        }
       } else {
-        // fp16 out, two fragments per 16-B store (store_f16_pair)
-        const int g = lane >> 4;
-        const int cofs = 8 * ((g & 1) * 2 + (g >> 1));
+        pipe_plain_epilogue<EPI, SPLIT, CFG, P_NO_STORE>(acc, bias_l, rc, rl, N, n0, wr, wc, lane);
+      }
 #pragma unroll
-        for (int jp = 0; jp < FN; jp += 2) {
-          const floatx4 b0 = *reinterpret_cast<const floatx4*>(bias_l + n0 + wc * WTN + jp * 16 + 4 * g);
-          const floatx4 b1 = *reinterpret_cast<const floatx4*>(bias_l + n0 + wc * WTN + jp * 16 + 16 + 4 * g);
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
-          for (int i = 0; i < FM; ++i) {
-            const int ml = wr * WTM + i * 16 + (lane & 15);
-            const int vo = (ml * N + n0 + wc * WTN + jp * 16 + cofs) * 2;
-            floatx4 va = acc[i][jp] + b0, vb = acc[i][jp + 1] + b1;
-            if constexpr (EPI == kEpiGeluF16) {
+        for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// GEMM, loader-specialised pipe (gemm_ws_kernel; round 2): gemm_pipe_kernel's tiles and ring
+// with the DMAs moved to 4 loader waves (one per SIMD), beside the 8 MFMA waves.
+// Probes of gemm_pipe_kernel at 117K x 1152 x 384 fp16x3 (rag_bert_gemm variants 13-15):
+// MFMAs + LDS reads + barriers 0.206 ms, DMAs alone 0.163 ms (~28 B/clk/CU of LDS-DMA intake),
+// both 0.260 ms, + the epilogue stores 0.373 ms — the parts add instead of overlapping. Two
+// couplings cause it: an LDS-DMA issue holds its wave for ~60-185 cycles (MI355X_MICROARCH
+// price list), so the 6 DMAs every wave issued per step stalled the MFMA issue of both waves of
+// a SIMD together (they leave the barrier in lockstep); and loads and stores share one
+// in-order vmcnt, so a tile's stores had to complete before the next-but-one ring wait passed.
+// Here the loader waves issue every DMA and wait only for DMAs (exact counts, no stores), and
+// the MFMA waves issue only LDS reads, MFMAs and the epilogue's stores and never wait on
+// vmcnt. One s_barrier per K step is the hand-off: the loaders pass it once stage g has
+// landed, the MFMA waves once they are done reading stage g-1 (whose slot the loaders refill
+// right after it). 12 waves: 3 per SIMD, <= 168 VGPRs each (the MFMA path needs ~145).
+// ----------------------------------------------------------------------------------------
+template <int EPI, bool SPLIT, typename CFG, int PROBE = 0, int AUX = 0>
+__global__ __launch_bounds__(CFG::THREADS + 256, 1) void gemm_ws_kernel(
+    const _Float16* __restrict__ A, const _Float16* __restrict__ Al,
+    const _Float16* __restrict__ W, const _Float16* __restrict__ Wl,
+    const float* __restrict__ bias, int M, int N, int K, void* __restrict__ Cout,
+    _Float16* __restrict__ Clo) {
+  static_assert(EPI != kEpiAddLn && CFG::PRELOAD, "plain epilogues, large tiles");
+  constexpr int BM = CFG::BM, BN = CFG::BN, NS = CFG::NS, TH = CFG::THREADS;
+  constexpr int LTH = 256;                         // loader threads (4 waves)
+  constexpr int FM = CFG::FM, FN = CFG::FN, WTM = 16 * FM, WTN = 16 * FN;
+  constexpr int BK = CFG::BK ? CFG::BK : kBK<SPLIT>, CPR = BK / 8, KSN = BK / 32;
+  constexpr int NPL = SPLIT ? 2 : 1;
+  constexpr int A_H8 = BM * CPR, W_H8 = BN * CPR;
+  constexpr int STAGE_H8 = NPL * (A_H8 + W_H8);
+  constexpr int LA = A_H8 / LTH, LW = W_H8 / LTH;  // DMAs per loader wave per plane
+  constexpr int L = NPL * (LA + LW);               // DMAs per loader wave per stage
+  constexpr bool P_NO_MFMA = PROBE == 1 || PROBE == 8;
+  constexpr bool P_NO_DMA = PROBE == 2 || PROBE == 7;
+  constexpr bool P_NO_STORE = PROBE == 6 || PROBE == 7 || PROBE == 8;
+  constexpr int OUT_B = EPI == kEpiF32 ? 4 : 2;
+  static_assert(A_H8 % LTH == 0 && W_H8 % LTH == 0 && FN % 2 == 0, "tile shape");
+  static_assert((NS - 2) * L <= 63, "vmcnt range");
+  __shared__ half8 lds[NS * STAGE_H8 + kPipeBiasMax / 4];
+  float* bias_l = reinterpret_cast<float*>(lds + NS * STAGE_H8);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t lbase = lds_addr_of(lds);
+  const int nN = N / BN, nM = (M + BM - 1) / BM, n_tiles = nM * nN;
+  const int nk = K / BK;
+  const int G = gridDim.x, per_xcd = G >> 3;
+  const int off = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+  const int n_mine = off < n_tiles ? (n_tiles - off + G - 1) / G : 0;
+  const int steps = n_mine * nk;
+
+  for (int i = tid * 4; i < N; i += (TH + LTH) * 4)
+    *reinterpret_cast<floatx4*>(bias_l + i) = *reinterpret_cast<const floatx4*>(bias + i);
+  __syncthreads();
+
+  if (wid >= TH / 64) {
+    // ---- loader waves: stage g+NS-1 issued after the barrier of step g ----
+    const int lw = wid - TH / 64;
+    uint32_t voA[LA], voW[LW];
 #pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                va[r] = gelu_erf(va[r]);
-                vb[r] = gelu_erf(vb[r]);
-              }
-            }
-            half4 ha, hb;
+    for (int i = 0; i < LA; ++i) {
+      const int q = (lw * LA + i) * 64 + lane, r = q / CPR, cs = q % CPR;
+      voA[i] = (uint32_t)(r * K + swz_chunk<CPR>(r, cs) * 8) * 2u;
+    }
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              ha[r] = (_Float16)va[r];
-              hb[r] = (_Float16)vb[r];
-            }
-            store_f16_pair(ha, hb, rc, vo);
-            if constexpr (SPLIT) {
-              half4 la, lb;
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                la[r] = lo_part(va[r], ha[r]);
-                lb[r] = lo_part(vb[r], hb[r]);
-              }
-              store_f16_pair(la, lb, rl, vo);
-            }
-          }
+    for (int i = 0; i < LW; ++i) {
+      const int q = (lw * LW + i) * 64 + lane, r = q / CPR, cs = q % CPR;
+      voW[i] = (uint32_t)(r * K + swz_chunk<CPR>(r, cs) * 8) * 2u;
+    }
+    int it_i = 0, kt_i = 0, kr_i = 0, slot_i = 0;
+    __amdgpu_buffer_rsrc_t rA0 = panel(A, 0), rA1 = rA0, rW0 = rA0, rW1 = rA0;
+    auto issue_next = [&]() __attribute__((always_inline)) {
+      if (it_i >= n_mine) return;
+      if constexpr (P_NO_DMA) {
+        if (++kt_i == nk) { kt_i = 0; ++it_i; }
+        return;
+      }
+      if (kt_i == 0) {
+        const int tile = it_i * G + off;
+        const int m0 = (tile / nN) * BM, n0 = (tile % nN) * BN;
+        kr_i = (tile % nN) % nk;   // rotated K order (gemm_pipe_kernel)
+        const int64_t abytes = (int64_t)(M - m0) * K * 2, wbytes = (int64_t)BN * K * 2;
+        rA0 = panel(A + (int64_t)m0 * K, abytes);
+        rW0 = panel(W + (int64_t)n0 * K, wbytes);
+        if constexpr (SPLIT) {
+          rA1 = panel(Al + (int64_t)m0 * K, abytes);
+          rW1 = panel(Wl + (int64_t)n0 * K, wbytes);
         }
       }
+      const uint32_t soff = __builtin_amdgcn_readfirstlane((uint32_t)kr_i * (BK * 2));
+      if (++kr_i == nk) kr_i = 0;
+      const uint32_t slot = lbase + (uint32_t)slot_i * (STAGE_H8 * 16);
+#pragma unroll
+      for (int i = 0; i < LA; ++i) {
+        const uint32_t d = slot + (uint32_t)((lw * LA + i) * 64 * 16);
+        blds16(rA0, voA[i], soff, d);
+        if constexpr (SPLIT) blds16(rA1, voA[i], soff, d + A_H8 * 16);
+      }
+#pragma unroll
+      for (int i = 0; i < LW; ++i) {
+        const uint32_t d = slot + (uint32_t)((NPL * A_H8 + (lw * LW + i) * 64) * 16);
+        blds16(rW0, voW[i], soff, d);
+        if constexpr (SPLIT) blds16(rW1, voW[i], soff, d + W_H8 * 16);
+      }
+      if (++kt_i == nk) { kt_i = 0; ++it_i; }
+      if (++slot_i == NS) slot_i = 0;
+    };
+#pragma unroll
+    for (int p = 0; p < NS - 1; ++p) issue_next();
+    for (int g = 0; g < steps; ++g) {
+      wait_ring<L, 0, NS - 2>(min(NS - 2, steps - 1 - g), false);   // stage g landed
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      issue_next();                     // stage g+NS-1 -> slot (g-1) % NS
+    }
+    return;
+  }
+
+  // ---- MFMA waves ----
+  const int wr = wid / CFG::WAVES_N, wc = wid % CFG::WAVES_N;
+  floatx4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  int kt_c = 0, it_c = 0, slot_c = 0;
+  for (int g = 0; g < steps; ++g) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // done reading stage g-1
+    __builtin_amdgcn_s_barrier();                        // stage g landed
+    asm volatile("" ::: "memory");
+    const half8* sa = lds + slot_c * STAGE_H8;
+    const half8* sw = sa + NPL * A_H8;
+    half8 af[KSN][NPL][FM], wf[KSN][NPL][FN];
+    auto read_a = [&](int i) __attribute__((always_inline)) {
+#pragma unroll
+      for (int ks = 0; ks < KSN; ++ks)
+#pragma unroll
+        for (int p = 0; p < NPL; ++p)
+          af[ks][p][i] = sa[p * A_H8 + swz<CPR>(wr * WTM + i * 16 + (lane & 15), ks * 4 + (lane >> 4))];
+    };
+    auto read_w = [&]() __attribute__((always_inline)) {
+#pragma unroll
+      for (int ks = 0; ks < KSN; ++ks)
+#pragma unroll
+        for (int p = 0; p < NPL; ++p)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            wf[ks][p][j] = sw[p * W_H8 + swz<CPR>(wc * WTN + j * 16 + (lane & 15), ks * 4 + (lane >> 4))];
+    };
+    auto mma = [&](int ks, int i, int j) __attribute__((always_inline)) {
+      if constexpr (!P_NO_MFMA) {
+        if constexpr (SPLIT) {   // small terms first: W_lo A_hi + W_hi A_lo + W_hi A_hi
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[ks][1][j], af[ks][0][i], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[ks][0][j], af[ks][1][i], acc[i][j], 0, 0, 0);
+        }
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[ks][0][j], af[ks][0][i], acc[i][j], 0, 0, 0);
+      }
+    };
+    {
+      if constexpr (!P_NO_MFMA) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i) read_a(i);
+        read_w();
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int ks = 0; ks < KSN; ++ks)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) mma(ks, i, j);
+    }
+    if (++slot_c == NS) slot_c = 0;
+    if (++kt_c == nk) {               // tile done (stores never waited on)
+      kt_c = 0;
+      const int tile = it_c * G + off;
+      ++it_c;
+      // (PROBE 9: every tile stored over the first row band — L2-resident writes)
+      const int m0 = PROBE == 9 ? 0 : (tile / nN) * BM, n0 = (tile % nN) * BN;
+      const __amdgpu_buffer_rsrc_t rc =
+          panel(static_cast<char*>(Cout) + (int64_t)m0 * N * OUT_B, (int64_t)(M - m0) * N * OUT_B);
+      __amdgpu_buffer_rsrc_t rl = rc;
+      if constexpr (SPLIT && EPI != kEpiF32)
+        rl = panel(Clo + (int64_t)m0 * N, (int64_t)(M - m0) * N * 2);
+      pipe_plain_epilogue<EPI, SPLIT, CFG, P_NO_STORE, AUX>(acc, bias_l, rc, rl, N, n0, wr, wc,
+                                                            lane);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll

@@ -90,13 +90,21 @@ int rag_build_pairs(const int32_t* q_ids, const int32_t* q_cu, int B, const int6
  * RAG_EPI_F32 (C fp32). variant: RAG_GEMM_AUTO (what the forward uses), _TILE, _PIPE, _SMALL,
  * _WIDE (_PIPE at 256x256 (N % 256 == 0) or 256x192 (N % 192 == 0, fp16) tiles),
  * _SMALL_BK64 (_SMALL with 64-wide K steps in fp16x3; = _SMALL in fp16);
- * _PROBE_* are timing probes of the PIPE kernel with its MFMAs / its loads / its loads and
- * barriers removed (fp16, results meaningless). N % 128 == 0, K % 64 == 0 (PIPE/SMALL also N <= 4096). */
+ * _BIG / _BIG128 register-blocked PIPE shapes (diagnostic); _PROBE_* are timing probes of the
+ * PIPE kernel, fp16 or fp16x3, with parts removed (results meaningless): its MFMAs / its loads /
+ * its loads and barriers / its epilogue stores / loads and stores (_MFMA_ONLY) / MFMAs and
+ * stores (_DMA_ONLY). _WS: PIPE's tiles with the DMAs on 4 loader waves beside the 8 MFMA
+ * waves; _WS_NT the same with non-temporal output stores; _WS_* probes as the PIPE ones, and
+ * _WS_L2_STORE with every tile stored over the first row band (L2-resident writes).
+ * N % 128 == 0, K % 64 == 0 (PIPE/SMALL also N <= 4096). */
 enum { RAG_EPI_F16 = 0, RAG_EPI_GELU_F16 = 1, RAG_EPI_F32 = 2 };
 enum { RAG_GEMM_AUTO = 0, RAG_GEMM_TILE = 1, RAG_GEMM_PIPE = 2, RAG_GEMM_PROBE_NO_MFMA = 3,
        RAG_GEMM_PROBE_NO_DMA = 4, RAG_GEMM_SMALL = 5, RAG_GEMM_WIDE = 8,
        RAG_GEMM_PROBE_NO_SYNC = 9, RAG_GEMM_SMALL_BK64 = 10, RAG_GEMM_BIG = 11,
-       RAG_GEMM_BIG128 = 12 };
+       RAG_GEMM_BIG128 = 12, RAG_GEMM_PROBE_NO_STORE = 13, RAG_GEMM_PROBE_MFMA_ONLY = 14,
+       RAG_GEMM_PROBE_DMA_ONLY = 15, RAG_GEMM_WS = 19, RAG_GEMM_WS_MFMA_ONLY = 20,
+       RAG_GEMM_WS_NO_STORE = 21, RAG_GEMM_WS_DMA_ONLY = 22, RAG_GEMM_WS_L2_STORE = 23,
+       RAG_GEMM_WS_NT = 24 };
 int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, const void* W,
                   const void* W_lo, const float* bias, int M, int N, int K, void* C,
                   void* C_lo, void* stream);

@@ -20,7 +20,10 @@ from ragmi.encoders import EPI_F16, EPI_F32, EPI_GELU_F16, linear  # noqa: E402
 
 PEAK = 2.5e15
 VNAME = {0: "auto", 1: "tile", 2: "pipe", 3: "probe_no_mfma", 4: "probe_no_dma", 5: "small",
-         8: "wide", 9: "probe_no_sync", 10: "small_bk64", 11: "big", 12: "big128"}
+         8: "wide", 9: "probe_no_sync", 10: "small_bk64", 11: "big", 12: "big128",
+         13: "probe_no_store", 14: "probe_mfma_only", 15: "probe_dma_only",
+         19: "ws", 20: "ws_mfma_only",
+         21: "ws_no_store", 22: "ws_dma_only", 23: "ws_l2_store", 24: "ws_nt"}
 LAYERS = {
     "small": [("qkv", 1152, 384, EPI_F16), ("o", 384, 384, EPI_F32),
               ("ffn1", 1536, 384, EPI_GELU_F16), ("ffn2", 384, 1536, EPI_F32)],
@@ -65,8 +68,6 @@ def main():
                 wl = (torch.randn((N, K), generator=g, device="cuda") * 1e-5).half() \
                     if prec == "fp16x3" else None
                 for v in variants:
-                    if v in (3, 4, 9) and prec == "fp16x3":
-                        continue              # probes are fp16-only
                     ms = timeit(lambda: linear(a, w, bias, epi, al, wl, v))
                     fl = 2.0 * M * N * K
                     pipe_fl = fl * (3 if prec == "fp16x3" else 1)

@@ -1,5 +1,5 @@
 """Bit-exact layout test of every encoder GEMM epilogue (rag_bert_gemm: TILE, PIPE, SMALL,
-WIDE, SMALL-BK64; fp16 and fp16x3; fp32 and fp16 [+ lo plane] outputs).
+WIDE, SMALL-BK64, BIG, BIG128, WS, WS-NT; fp16 and fp16x3; fp32 and fp16 [+ lo plane] outputs).
 
 Operands sit on a coarse dyadic grid (hi planes k/16, |k| <= 4; lo planes k/2048, |k| <= 2;
 bias k/256) so every product and every partial sum is exactly representable in fp32: the
@@ -26,8 +26,8 @@ def _grid(g, shape, den, kmax):
 @pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "x".join(map(str, s)))
 @pytest.mark.parametrize("epi", [0, 2], ids=["f16", "f32"])
 @pytest.mark.parametrize("split", [False, True], ids=["fp16", "fp16x3"])
-@pytest.mark.parametrize("variant", [1, 2, 5, 8, 10, 11, 12],
-                         ids=["tile", "pipe", "small", "wide", "small64", "big", "big128"])
+@pytest.mark.parametrize("variant", [1, 2, 5, 8, 10, 11, 12, 19, 24],
+                         ids=["tile", "pipe", "small", "wide", "small64", "big", "big128", "ws", "ws_nt"])
 def test_gemm_epilogue_bit_exact(gpu, shape, epi, split, variant):
     from ragmi.encoders import linear
     M, N, K = shape
