@@ -25,9 +25,8 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "financial-rag-system_amd"))
-sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
-import bert_ref as R  # noqa: E402  (seeded weights only)
+from ragmi import synth as R  # noqa: E402  (model shapes, seeded weights)
 
 WORDS = ("apple iphone revenue services margin risk supply chain china tariffs cash flow "
          "dividend buyback microsoft azure cloud gaming licence windows office growth "

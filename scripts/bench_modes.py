@@ -198,7 +198,7 @@ def _cpu_pipeline_baseline(cfg_id, budget_s, corpus16_sample, n_total, R, bge_w,
 
 
 def run_pipeline(args, cfg_id):
-    import bert_ref as R
+    from ragmi import synth as R          # model shapes, seeded weights (product-side data)
     from ragmi.encoders import HEAD_CLS_L2, HEAD_POOLER_CLS, BertEncoder
     from ragmi.index import FlatIndex
     from ragmi.pairs import build_pairs_gpu
@@ -311,7 +311,8 @@ def run_pipeline(args, cfg_id):
             for j in range(K_TOP):
                 a, b = sub_cu[j], sub_cu[j + 1]
                 pi[j, :b - a], pt[j, :b - a], pm[j, :b - a] = ids_h[a:b], ty_h[a:b], 1
-            ref = R.ce_logits(ce_w, R.MINILM_CE, pi, pt, pm)
+            import bert_ref                    # the checker (oracle) leg only
+            ref = bert_ref.ce_logits(ce_w, R.MINILM_CE, pi, pt, pm)
             extra["rerank_max_abs_diff_vs_oracle"] = float(
                 np.abs(logits[0].cpu().numpy() - ref).max())
     cpu = None

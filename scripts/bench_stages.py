@@ -20,9 +20,8 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "financial-rag-system_amd"))
-sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
-import bert_ref as R  # noqa: E402  (weights + batch generator only)
+from ragmi import synth as R  # noqa: E402  (model shapes, seeded weights)
 from ragmi.encoders import HEAD_CLS_L2, HEAD_POOLER_CLS, BertEncoder  # noqa: E402
 
 PEAK_F16 = 2.5e15   # dense fp16 MFMA, MI355X_MICROARCH.md

@@ -8,8 +8,7 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "financial-rag-system_amd"))
-sys.path.insert(0, os.path.join(ROOT, "oracle"))
-import bert_ref as R  # noqa: E402
+from ragmi import synth as R  # noqa: E402  (model shapes, seeded weights)
 from ragmi.encoders import HEAD_POOLER_CLS, BertEncoder  # noqa: E402
 
 prec = os.environ.get("PREC", "fp16")
