@@ -28,9 +28,10 @@ __global__ void f32_to_f16_kernel(const float* __restrict__ in, _Float16* __rest
                                   _Float16* __restrict__ out_lo, int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) {
-    const _Float16 h = (_Float16)in[i];
+    _Float16 h, l;
+    { const half2 s16_ = split16(in[i]); h = s16_[0]; l = s16_[1]; }
     out[i] = h;
-    if (out_lo) out_lo[i] = lo_part(in[i], h);
+    if (out_lo) out_lo[i] = l;
   }
 }
 
@@ -726,6 +727,56 @@ int rag_bert_gemm_add_ln(const void* A, const void* A_lo, const void* W, const v
               static_cast<hipStream_t>(stream));
   RAG_HIP(hipGetLastError());
   return RAG_OK;
+}
+
+// attention alone (bge-small / MiniLM shape: hidden 384, head_dim 32), variant = the
+// attn_kernel VAR bit mask (0..7; kAttnVar is the forward's): for A/B timing and tests
+int rag_bert_attention(int variant, const void* qkv, const void* qkv_lo, const int32_t* cu,
+                       int B, int max_len, void* ctx, void* ctx_lo, void* stream) {
+  ragmi::clear_error();
+  if (!qkv || !cu || !ctx || B < 1 || max_len < 1 || max_len > 512)
+    return ragmi::fail(RAG_EINVAL, "qkv, cu, ctx required; 1 <= B, 1 <= max_len <= 512");
+  if ((qkv_lo == nullptr) != (ctx_lo == nullptr))
+    return ragmi::fail(RAG_EINVAL, "qkv_lo and ctx_lo: both (fp16x3) or neither (fp16)");
+  if (variant == -1) variant = kAttnVar;
+  if (variant < 0 || variant > 7) return ragmi::fail(RAG_EINVAL, "variant: -1 or 0..7");
+  constexpr int H = 384, HD = 32, NH = H / HD;
+  const int planes = qkv_lo ? 2 : 1;
+  const int kc = attn_chunk_keys<HD>(max_len, planes);
+  const size_t alds = (size_t)attn_lds_bytes<HD>(kc, planes);
+  const dim3 agrid((unsigned)((NH * B + 7) / 8 * 8));
+  const float scale = 1.0f / sqrtf((float)HD);
+  auto st = static_cast<hipStream_t>(stream);
+  auto q = static_cast<const _Float16*>(qkv);
+  auto ql = static_cast<const _Float16*>(qkv_lo);
+  auto c = static_cast<_Float16*>(ctx);
+  auto cl = static_cast<_Float16*>(ctx_lo);
+  auto go = [&](auto vc) -> int {
+    constexpr int V = decltype(vc)::value;
+    if (qkv_lo) {
+      RAG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_kernel<H, HD, true, V>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, kAttnLdsMax));
+      attn_kernel<H, HD, true, V><<<agrid, dim3(kAttnThreads<true>), alds, st>>>(
+          q, ql, cu, max_len, kc, scale, c, cl, 1 << 20);
+    } else {
+      RAG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_kernel<H, HD, false, V>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, kAttnLdsMax));
+      attn_kernel<H, HD, false, V><<<agrid, dim3(kAttnThreads<false>), alds, st>>>(
+          q, nullptr, cu, max_len, kc, scale, c, nullptr, 1 << 20);
+    }
+    RAG_HIP(hipGetLastError());
+    return RAG_OK;
+  };
+  switch (variant) {
+    case 0: return go(std::integral_constant<int, 0>{});
+    case 1: return go(std::integral_constant<int, 1>{});
+    case 2: return go(std::integral_constant<int, 2>{});
+    case 3: return go(std::integral_constant<int, 3>{});
+    case 4: return go(std::integral_constant<int, 4>{});
+    case 5: return go(std::integral_constant<int, 5>{});
+    case 6: return go(std::integral_constant<int, 6>{});
+    default: return go(std::integral_constant<int, 7>{});
+  }
 }
 
 int rag_bert_gemm_add_ln_probe(int probe, const void* A, const void* A_lo, const void* W,

@@ -25,7 +25,17 @@ typedef _Float16 half2 __attribute__((ext_vector_type(2)));
 
 // fp16x3 split: v = hi + lo with hi = fp16(v), lo = fp16(v - hi); a*b ~ ah*bh + ah*bl + al*bh
 // (relative error ~2^-22) on the fp16 MFMA pipe.
-__device__ __forceinline__ _Float16 lo_part(float v, _Float16 hi) { return (_Float16)(v - (float)hi); }
+// v is pinned as an fp32 register value before either conversion: under -ffp-contract=fast
+// the compiler may fuse the operation that produced v into the hi conversion (one rounding of
+// the unrounded product / sum straight to fp16, v_fma_mix*_f16) while lo subtracts hi from
+// the fp32-rounded v — where an fp16 rounding midpoint falls between the two, hi and lo
+// disagree and hi + lo is off by one fp16 ulp (measured: 1-4 of ~1e5 attention outputs, every
+// error exactly one ulp; tests/test_attention_gpu.py).
+__device__ __forceinline__ half2 split16(float v) {   // {hi, lo}
+  asm("" : "+v"(v));
+  const _Float16 hi = (_Float16)v;
+  return half2{hi, (_Float16)(v - (float)hi)};
+}
 
 // erf-GELU, 0.5 x (1 + erf(x / sqrt 2)), with erfc(|z|) from Abramowitz & Stegun 7.1.26
 // (|error of erf| <= 1.5e-7 absolute, i.e. at fp32 rounding level for the GELU output):
@@ -84,9 +94,10 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(
     const int c = lane + 64 * j;
     const float y = (v[j] - mu) * rs * g[c] + bt[c];
     if (x) x[t * H + c] = y;                 // (null: fp16x3 residual kept as xh + xl only)
-    const _Float16 yh = (_Float16)y;
+    _Float16 yh, yl;
+    { const half2 s16_ = split16(y); yh = s16_[0]; yl = s16_[1]; }
     xh[t * H + c] = yh;
-    if (xl) xl[t * H + c] = lo_part(y, yh);
+    if (xl) xl[t * H + c] = yl;
   }
 }
 
@@ -129,9 +140,10 @@ __global__ __launch_bounds__(256) void add_ln_kernel(float* __restrict__ x,
     const int c = lane + 64 * j;
     const float o = (v[j] - mu) * rs * g[c] + bt[c];
     if constexpr (!XF) x[t * H + c] = o;
-    const _Float16 oh = (_Float16)o;
+    _Float16 oh, ol;
+    { const half2 s16_ = split16(o); oh = s16_[0]; ol = s16_[1]; }
     xh[t * H + c] = oh;
-    if (xl) xl[t * H + c] = lo_part(o, oh);
+    if (xl) xl[t * H + c] = ol;
   }
 }
 
@@ -313,8 +325,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(const _Float16* __restrict__ 
           half8 h, l;
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            h[e] = (_Float16)v[e];
-            if constexpr (SPLIT) l[e] = lo_part(v[e], h[e]);
+            if constexpr (SPLIT) { const half2 s16_ = split16(v[e]); h[e] = s16_[0]; l[e] = s16_[1]; }
+            else h[e] = (_Float16)v[e];
           }
           *reinterpret_cast<half8*>(static_cast<_Float16*>(Cout) + (int64_t)m * N + gn) = h;
           if constexpr (SPLIT) *reinterpret_cast<half8*>(Clo + (int64_t)m * N + gn) = l;
@@ -490,22 +502,20 @@ __device__ __forceinline__ void pipe_epi_pair(const floatx4& a0, const floatx4& 
         vb[r] = gelu_erf(vb[r]);
       }
     }
-    half4 ha, hb;
+    half4 ha, hb, la, lb;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      ha[r] = (_Float16)va[r];
-      hb[r] = (_Float16)vb[r];
+      if constexpr (SPLIT) {
+        { const half2 s16_ = split16(va[r]); ha[r] = s16_[0]; la[r] = s16_[1]; }
+        { const half2 s16_ = split16(vb[r]); hb[r] = s16_[0]; lb[r] = s16_[1]; }
+      } else {
+        ha[r] = (_Float16)va[r];
+        hb[r] = (_Float16)vb[r];
+      }
     }
     if (!NO_STORE || va[0] == 1234.5f) store_f16_pair<AUX>(ha, hb, rc, vo);
-    if constexpr (SPLIT) {
-      half4 la, lb;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        la[r] = lo_part(va[r], ha[r]);
-        lb[r] = lo_part(vb[r], hb[r]);
-      }
+    if constexpr (SPLIT)
       if (!NO_STORE || vb[0] == 1234.5f) store_f16_pair<AUX>(la, lb, rl, vo);
-    }
   }
 }
 
@@ -837,23 +847,15 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
                                                      sf(jp), 0);
               __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, vb), rc, vf(i),
                                                      sf(jp + 1), 0);
-              half4 ha, hb;
+              half4 ha, hb, la, lb;
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
-                ha[r] = (_Float16)va[r];
-                hb[r] = (_Float16)vb[r];
+                { const half2 s16_ = split16(va[r]); ha[r] = s16_[0]; la[r] = s16_[1]; }
+                { const half2 s16_ = split16(vb[r]); hb[r] = s16_[0]; lb[r] = s16_[1]; }
               }
               const int vo = ((wr * WTM + i * 16 + (lane & 15)) * N + wc * WTN + jp * 16 + cofs) * 2;
               store_f16_pair(ha, hb, rh, vo);
-              if constexpr (SPLIT) {
-                half4 la, lb;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                  la[r] = lo_part(va[r], ha[r]);
-                  lb[r] = lo_part(vb[r], hb[r]);
-                }
-                store_f16_pair(la, lb, rl, vo);
-              }
+              if constexpr (SPLIT) store_f16_pair(la, lb, rl, vo);
             }
           }
         } else
@@ -868,19 +870,18 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
             for (int r = 0; r < 4; ++r) v[r] = (acc[i][j][r] - mu[i]) * rsd[i] * gj[r] + ej[r];
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rc, vf(i),
                                                    sf(j), 0);
-            half4 h;
+            half4 h, l;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) h[r] = (_Float16)v[r];
+            for (int r = 0; r < 4; ++r) {
+              if constexpr (SPLIT) { const half2 s16_ = split16(v[r]); h[r] = s16_[0]; l[r] = s16_[1]; }
+              else h[r] = (_Float16)v[r];
+            }
             const int vh = vf(i) / 2;                  // same element offsets in fp16
             __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, h), rh, vh,
                                                   sf(j) / 2, 0);
-            if constexpr (SPLIT) {
-              half4 l;
-#pragma unroll
-              for (int r = 0; r < 4; ++r) l[r] = lo_part(v[r], h[r]);
+            if constexpr (SPLIT)
               __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, l), rl, vh,
                                                     sf(j) / 2, 0);
-            }
           }
         }
       } else {
@@ -1120,11 +1121,17 @@ __global__ __launch_bounds__(CFG::THREADS + 256, 1) void gemm_ws_kernel(
 // The MFMA C layout puts query q = lane&15 in every lane's column, so the softmax running
 // max / sum and the O rescale are per-lane scalars; the P^T fragment slot 8g+j (g = lane>>4)
 // holds key 4g+j (j<4) or 16+4g+(j-4) (j>=4) of the block, i.e. exactly the lane's two S^T
-// accumulators — V^T is stored in LDS with its keys permuted the same way.
+// accumulators. V stays row-major in LDS ([key][HD], 16-B copies from the Q|K|V rows) and
+// the V^T fragment is gathered by two ds_read_b64_tr_b16 (gfx950 transposed LDS read: per
+// 16-lane group, 4 rows x 16 columns delivered column-major): rows 4g..4g+3 and 16+4g..
+// 16+4g+3 of the block — the P^T slot order, so no key permutation is stored anywhere.
+// (Round 1 staged V^T with eight 2-byte LDS stores per 16-B chunk: SQ_LDS_BANK_CONFLICT
+// 1.9e7 cycles per launch against 1.24e7 active LDS cycles at rerank size.)
 // qkv: fp16 [T][3H] (Q | K | V; head h = columns h*HD .. +HD-1 of each); ctx: fp16 [T][H].
 // LDS (dynamic) per plane: K [cap][HD] (16-B chunks swizzled as the GEMM images, swz_chunk)
-// + V^T [HD][cap+8] halves, cap = keys staged at once. The unpadded K lets two fp16x3
-// workgroups share a CU up to ~300 keys.
+// + V [cap][HD] (16-B chunk c of row r at c ^ attn_vsw(r), which spreads the 8 rows a 32-lane
+// half reads over all 64 banks), cap = keys staged at once. Two fp16x3 workgroups share a CU
+// up to ~300 keys.
 // ----------------------------------------------------------------------------------------
 template <bool SPLIT> constexpr int kAttnThreads = 512;   // 2 waves per SIMD per workgroup
 constexpr int kAttnLdsMax = 160 * 1024;
@@ -1136,7 +1143,7 @@ template <int HD, bool SPLIT> constexpr int kAttnWavesPerEU = HD == 32 ? (SPLIT 
 
 template <int HD>
 __host__ __device__ constexpr int attn_lds_bytes(int cap, int planes) {
-  return planes * (cap * HD + HD * (cap + 8)) * 2;
+  return planes * 2 * cap * HD * 2;
 }
 // keys staged per chunk (multiple of 32): all of them if they fit, else the most that fit
 template <int HD>
@@ -1147,8 +1154,18 @@ __host__ __device__ constexpr int attn_chunk_keys(int max_len, int planes) {
   return kc;
 }
 
-__device__ __forceinline__ int vperm(int k) {       // key k of a 32-block -> P^T slot
-  return 8 * ((k & 15) >> 2) + (k & 3) + ((k >> 4) << 2);
+// V image chunk swizzle: a transposed read takes 32 B (16 columns) of each of 8 rows per
+// 32-lane half (rows 4g + q, g = two groups); rows 128 / HD apart share a bank window, so the
+// chunk pair is XORed by the row's window index
+template <int HD>
+__device__ __forceinline__ int attn_vsw(int r) {
+  return ((r / (128 / HD)) & (HD / 16 - 1)) << 1;
+}
+
+typedef short short4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ half4 lds_read_tr16(const _Float16* p) {
+  return __builtin_bit_cast(half4, __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) short4v*)(p)));
 }
 
 template <int HD, bool SPLIT>
@@ -1156,10 +1173,20 @@ struct AttnState {
   static constexpr int DT = HD / 16, KS = HD / 32, NP = SPLIT ? 2 : 1;
   half8 qf[KS][NP];
   floatx4 o[DT];
-  float m, lsum;
+  // row sums of P: fp16x3 by MFMA against a ones fragment (every element = l(q)); fp16 by
+  // v_dot2 into l[0] (lane-partial, reduced across the lane groups at the end)
+  floatx4 l;
+  float m;
 };
 
-template <int H, int HD, bool SPLIT>
+// VAR (bit mask; rag_bert_attention A/Bs them): 1 = rolling Q prefetch, 2 = fp16x3 row sums
+// by MFMA (else v_dot2), 4 = software-pipelined scores (block kb+1's K.Q^T MFMAs issued
+// before block kb's softmax, so they run in the matrix pipe under its vector work).
+// Measured at the rerank shape (scripts/bench_attn.py, profiles/r02_attn_variants.jsonl):
+// fp16x3 0.270-0.283 ms over all eight, 2 the fastest; fp16 0.140 ms without 4, 0.19-0.21
+// with it (64-VGPR budget). The kernel's time is not in these (staging / latency bound).
+constexpr int kAttnVar = 2;
+template <int H, int HD, bool SPLIT, int VAR = kAttnVar>
 __global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) void attn_kernel(
     const _Float16* __restrict__ qkv, const _Float16* __restrict__ qkv_lo,
     const int* __restrict__ cu, int max_len, int kc, float scale, _Float16* __restrict__ ctx,
@@ -1186,50 +1213,63 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) 
   const int sp = (len + 31) & ~31;
   const int cap = min(sp, kc);                      // keys per staged chunk
   const int nch = (sp + cap - 1) / cap;
-  const int vrow = cap + 8;
-  _Float16* kls[2] = {alds, alds + cap * KROW + HD * vrow};
-  _Float16* vts[2] = {alds + cap * KROW, alds + 2 * cap * KROW + HD * vrow};
+  _Float16* kls[2] = {alds, alds + 2 * cap * KROW};
+  _Float16* vls[2] = {alds + cap * KROW, alds + 3 * cap * KROW};
   const _Float16* planes[2] = {qkv, qkv_lo};
   const int g = lane >> 4, ql = lane & 15;
   const float c2 = scale * 1.44269504088896341f;
   const float rescale_gap = 8.0f / c2;             // deferred-max threshold (score units)
 
-  // ---- stage keys [k0, k0 + n) (n multiple of 32; zeros past len): K row-major, V^T permuted
+  // ---- stage keys [k0, k0 + n) (n multiple of 32; zeros past len): K and V row-major,
+  // 16-B chunks (swizzled: swz_chunk for K's row reads, attn_vsw for V's transposed reads)
   auto stage = [&](int k0, int n) {
     for (int c = tid; c < n * (HD / 8); c += kAttnThreads<SPLIT>) {
-      const int kl = c / (HD / 8), dc = (c % (HD / 8)) * 8, key = k0 + kl;
+      const int kl = c / (HD / 8), ch = c % (HD / 8), key = k0 + kl;
 #pragma unroll
       for (int p = 0; p < NP; ++p) {
         half8 kv = {}, vv = {};
         if (key < len) {
-          const _Float16* src = planes[p] + (int64_t)(base + key) * (3 * H) + h * HD + dc;
+          const _Float16* src = planes[p] + (int64_t)(base + key) * (3 * H) + h * HD + 8 * ch;
           kv = *reinterpret_cast<const half8*>(src + H);
           vv = *reinterpret_cast<const half8*>(src + 2 * H);
         }
-        *reinterpret_cast<half8*>(kls[p] + kl * KROW + 8 * swz_chunk<KCPR>(kl, dc / 8)) = kv;
-        const int pos = (kl & ~31) + vperm(kl & 31);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) vts[p][(dc + e) * vrow + pos] = vv[e];
+        *reinterpret_cast<half8*>(kls[p] + kl * KROW + 8 * swz_chunk<KCPR>(kl, ch)) = kv;
+        *reinterpret_cast<half8*>(vls[p] + kl * HD + 8 * (ch ^ attn_vsw<HD>(kl))) = vv;
       }
     }
   };
-  auto init = [&](St& st, int qb) {
+  // this lane's transposed-read offset (halves) for V^T fragment dt of a 32-key block at
+  // row 0: lane 4q + pp of 16-lane group g supplies row 4g + q, columns 16 dt + 4 pp .. + 3
+  // (the second read: rows + 16; the swizzle is the same for both and for every block)
+  const int vq = (lane & 15) >> 2, vpp = lane & 3;
+  auto voff = [&](int dt) {
+    const int r = 4 * g + vq;
+    return r * HD + 8 * ((2 * dt + (vpp >> 1)) ^ attn_vsw<HD>(r)) + 4 * (vpp & 1);
+  };
+  auto load_q = [&](half8 (&qf)[KS][NP], int qb) {
     const int r = min(qb * 16 + ql, len - 1);
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
       for (int p = 0; p < NP; ++p)
-        st.qf[ks][p] = *reinterpret_cast<const half8*>(
+        qf[ks][p] = *reinterpret_cast<const half8*>(
             planes[p] + (int64_t)(base + r) * (3 * H) + h * HD + 32 * ks + 8 * g);
+  };
+  auto reset = [&](St& st) {
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) st.o[dt] = floatx4{0.f, 0.f, 0.f, 0.f};
+    st.l = floatx4{0.f, 0.f, 0.f, 0.f};
     st.m = kNegInf;
-    st.lsum = 0.f;
   };
-  // keys [k0, k0 + n) of the staged chunk (LDS positions 0 .. n-1)
-  auto attend = [&](St& st, int k0, int n) {
-    for (int kb = 0; kb < n; kb += 32) {
-      floatx4 sc[2];
+  auto init = [&](St& st, int qb) {
+    load_q(st.qf, qb);
+    reset(st);
+  };
+  half8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (_Float16)1.0f;
+  // S^T of the 32-key block at LDS position kb
+  auto qk = [&](const St& st, int kb, floatx4 (&sc)[2]) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         sc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -1246,6 +1286,9 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) 
           }
         }
       }
+  };
+  // softmax update and P.V for the block at LDS position kb (keys k0 + kb ..)
+  auto softmax_pv = [&](St& st, int k0, int kb, floatx4 (&sc)[2]) {
       // lane: S^T[key k0 + kb + 16j + 4g + r][q]. Softmax in base 2 with the 1/sqrt(d) scale
       // folded into one FMA: p = 2^(s*c - m*c), c = scale*log2(e) > 0 (max commutes).
       float mx;
@@ -1273,7 +1316,8 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) 
       if (__builtin_amdgcn_ballot_w64(mx > st.m + rescale_gap)) {
         const float mnew = fmaxf(st.m, mx);
         const float corr = __builtin_amdgcn_exp2f((st.m - mnew) * c2);
-        st.lsum *= corr;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) st.l[r] *= corr;
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
@@ -1287,37 +1331,65 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) 
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float e = __builtin_amdgcn_exp2f(fmaf(sc[j][r], c2, nm));
-          const _Float16 eh = (_Float16)e;
-          ph[4 * j + r] = eh;
-          if constexpr (SPLIT) pl[4 * j + r] = lo_part(e, eh);
+          if constexpr (SPLIT) { const half2 s16_ = split16(e); ph[4 * j + r] = s16_[0]; pl[4 * j + r] = s16_[1]; }
+          else ph[4 * j + r] = (_Float16)e;
         }
-      // lane-partial row sum of P exactly as the MFMA sees it (hi [+ lo]), fp32 dot2
-      float rs = 0.f;
-      const half2 one2 = {(_Float16)1.0f, (_Float16)1.0f};
+      // row sum of P exactly as the MFMA sees it (hi [+ lo]). fp16x3: the same MFMA against
+      // a ones fragment (the MFMA pipe has the slack there, the vector ALU does not: 2 MFMAs
+      // for 8 v_dot2, and every lane ends up with its query's whole sum); fp16: v_dot2 (the
+      // 64-VGPR budget of 8 waves per SIMD has no room for the fragment and accumulator)
+      if constexpr (SPLIT && (VAR & 2)) {
+        st.l = __builtin_amdgcn_mfma_f32_16x16x32_f16(ones, pl, st.l, 0, 0, 0);
+        st.l = __builtin_amdgcn_mfma_f32_16x16x32_f16(ones, ph, st.l, 0, 0, 0);
+      } else {
+        const half2 one2 = {(_Float16)1.0f, (_Float16)1.0f};
 #pragma unroll
-      for (int e2 = 0; e2 < 4; ++e2) {
-        rs = __builtin_amdgcn_fdot2(half2{ph[2 * e2], ph[2 * e2 + 1]}, one2, rs, false);
-        if constexpr (SPLIT)
-          rs = __builtin_amdgcn_fdot2(half2{pl[2 * e2], pl[2 * e2 + 1]}, one2, rs, false);
+        for (int e2 = 0; e2 < 4; ++e2) {
+          st.l[0] = __builtin_amdgcn_fdot2(half2{ph[2 * e2], ph[2 * e2 + 1]}, one2, st.l[0], false);
+          if constexpr (SPLIT)
+            st.l[0] = __builtin_amdgcn_fdot2(half2{pl[2 * e2], pl[2 * e2 + 1]}, one2, st.l[0], false);
+        }
       }
-      st.lsum += rs;                                  // reduced across g at the end
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
-        const int vr = (16 * dt + ql) * vrow + kb + 8 * g;
-        const half8 v = *reinterpret_cast<const half8*>(vts[0] + vr);
+        const int vr = kb * HD + voff(dt);
+        const half8 v = __builtin_shufflevector(lds_read_tr16(vls[0] + vr),
+                                                lds_read_tr16(vls[0] + vr + 16 * HD),
+                                                0, 1, 2, 3, 4, 5, 6, 7);
         if constexpr (SPLIT) {
-          const half8 vl = *reinterpret_cast<const half8*>(vts[1] + vr);
+          const half8 vl = __builtin_shufflevector(lds_read_tr16(vls[1] + vr),
+                                                   lds_read_tr16(vls[1] + vr + 16 * HD),
+                                                   0, 1, 2, 3, 4, 5, 6, 7);
           st.o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vl, ph, st.o[dt], 0, 0, 0);
           st.o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(v, pl, st.o[dt], 0, 0, 0);
         }
         st.o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(v, ph, st.o[dt], 0, 0, 0);
       }
+  };
+  // keys [k0, k0 + n) of the staged chunk (LDS positions 0 .. n-1)
+  auto attend = [&](St& st, int k0, int n) {
+    if constexpr ((VAR & 4) != 0) {
+      floatx4 sn[2];
+      qk(st, 0, sn);
+      for (int kb = 0; kb < n; kb += 32) {
+        floatx4 sc[2] = {sn[0], sn[1]};
+        if (kb + 32 < n) qk(st, kb + 32, sn);
+        softmax_pv(st, k0, kb, sc);
+      }
+    } else {
+      for (int kb = 0; kb < n; kb += 32) {
+        floatx4 sc[2];
+        qk(st, kb, sc);
+        softmax_pv(st, k0, kb, sc);
+      }
     }
   };
   auto finish = [&](St& st, int qb) {
-    float l = st.lsum;
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
+    float l = st.l[0];
+    if constexpr (!(SPLIT && (VAR & 2))) {
+      l += __shfl_xor(l, 16, 64);
+      l += __shfl_xor(l, 32, 64);
+    }
     const int q = qb * 16 + ql;
     if (q < len) {
       // lane: O^T[d = 16dt + 4g + r][q]
@@ -1329,8 +1401,8 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) 
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float x = st.o[dt][r] * inv;
-          a[r] = (_Float16)x;
-          if constexpr (SPLIT) al[r] = lo_part(x, a[r]);
+          if constexpr (SPLIT) { const half2 s16_ = split16(x); a[r] = s16_[0]; al[r] = s16_[1]; }
+          else a[r] = (_Float16)x;
         }
         *reinterpret_cast<half4*>(ctx + off + 16 * dt) = a;
         if constexpr (SPLIT) *reinterpret_cast<half4*>(ctx_lo + off + 16 * dt) = al;
@@ -1340,11 +1412,32 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) 
 
   const int nqb = min((len + 15) >> 4, max_qb);     // max_qb = 1: the CLS query block only
   if (nch == 1) {
+    // rolling Q prefetch: a wave's first QPF query blocks are loaded before the K/V staging
+    // (their latency hides behind it), and each later one while the block QPF ahead computes
+    // (fp16 at head_dim 32 runs 8 waves per SIMD in 64 VGPRs: one block ahead fits)
+    constexpr int QPF = (VAR & 1) == 0 ? 0 : SPLIT || HD > 32 ? 3 : 1;
+    half8 qpre[QPF > 0 ? QPF : 1][KS][NP];
+#pragma unroll
+    for (int i = 0; i < QPF; ++i)
+      if (wid + i * NW < nqb) load_q(qpre[i], wid + i * NW);
     stage(0, sp);
     __syncthreads();
     for (int qb = wid; qb < nqb; qb += NW) {
       St st;
-      init(st, qb);
+      if constexpr (QPF > 0) {
+        reset(st);
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+          for (int p = 0; p < NP; ++p) {
+            st.qf[ks][p] = qpre[0][ks][p];
+#pragma unroll
+            for (int i = 0; i + 1 < QPF; ++i) qpre[i][ks][p] = qpre[i + 1][ks][p];
+          }
+        if (qb + QPF * NW < nqb) load_q(qpre[QPF - 1], qb + QPF * NW);
+      } else {
+        init(st, qb);
+      }
       attend(st, 0, sp);
       finish(st, qb);
     }

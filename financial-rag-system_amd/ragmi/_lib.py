@@ -108,6 +108,8 @@ BERT_API = {
                                                   c_vp, c_vp, ctypes.c_float, ctypes.c_int,
                                                   ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_vp,
                                                   c_vp]),
+    "rag_bert_attention": (ctypes.c_int, [ctypes.c_int, c_vp, c_vp, c_vp, ctypes.c_int,
+                                          ctypes.c_int, c_vp, c_vp, c_vp]),
 }
 
 

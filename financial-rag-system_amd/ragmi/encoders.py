@@ -102,6 +102,29 @@ def linear(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, epilogue: int =
     return (c, c_lo) if c_lo is not None else c
 
 
+def attention(qkv: torch.Tensor, cu: torch.Tensor, max_len: int,
+              qkv_lo: torch.Tensor | None = None, variant: int | None = None):
+    """The forward's attention kernel alone (hidden 384, head_dim 32: bge-small / MiniLM-L6;
+    modeling_bert.py eager attention, no mask beyond the packed sequence bounds): qkv fp16
+    [T, 1152] (Q | K | V) [+ lo plane], cu int32 [B+1] packed row offsets -> ctx fp16 [T, 384]
+    [+ lo plane]. variant: the kernel's VAR bit mask (None = the forward's). Diagnostic entry
+    for parity tests and A/B timing."""
+    if qkv.dtype != torch.float16 or qkv.dim() != 2 or qkv.shape[1] != 1152 or not qkv.is_cuda:
+        raise ValueError("qkv: fp16 cuda [T, 1152]")
+    if cu.dtype != torch.int32 or not cu.is_cuda:
+        raise ValueError("cu: int32 cuda [B+1]")
+    split = qkv_lo is not None
+    T = qkv.shape[0]
+    ctx = torch.empty((T, 384), dtype=torch.float16, device=qkv.device)
+    ctx_lo = torch.empty_like(ctx) if split else None
+    check(_lib.load().rag_bert_attention(
+        -1 if variant is None else int(variant), qkv.data_ptr(),
+        qkv_lo.data_ptr() if split else None, cu.data_ptr(), cu.numel() - 1, int(max_len),
+        ctx.data_ptr(), ctx_lo.data_ptr() if split else None,
+        torch.cuda.current_stream(qkv.device).cuda_stream))
+    return (ctx, ctx_lo) if split else ctx
+
+
 def linear_add_ln(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, gamma: torch.Tensor,
                   beta: torch.Tensor, eps: float, x: torch.Tensor,
                   a_lo: torch.Tensor | None = None, w_lo: torch.Tensor | None = None):

@@ -1,0 +1,70 @@
+"""The encoder attention kernel alone (rag_bert_attention: hidden 384, head_dim 32) against a
+plain torch fp32 reference of modeling_bert.py's eager attention, softmax(Q K^T / sqrt(d)) V
+per (sequence, head) over packed variable-length sequences, for every kernel variant (the
+VAR bit mask: Q prefetch, fp16x3 row sums by MFMA, software-pipelined scores) and both
+precisions. Ragged lengths cover the masked tail blocks (len % 32 != 0), a 1-token sequence,
+sequences past 256 keys, and more query blocks per wave than the Q prefetch depth.
+
+Tolerances: fp16x3 carries Q/K/V/P as hi + lo planes (~2^-22 relative), so its error is the
+fp32 accumulation's: 2e-5 absolute on O (|O| <= max|V| = 1); fp16 rounds P to fp16 and
+the output to fp16: 2e-3."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+LENS = [1, 31, 32, 33, 244, 257, 288, 64, 7, 200, 511]
+
+
+def _reference(q, k, v, cu):
+    """float64 (torch's fp32 GEMM path on the device is not relied on)"""
+    q, k, v = q.double(), k.double(), v.double()
+    out = torch.empty_like(q)
+    for b in range(len(cu) - 1):
+        a, e = cu[b], cu[b + 1]
+        for h in range(12):
+            sl = slice(32 * h, 32 * h + 32)
+            s = (q[a:e, sl] @ k[a:e, sl].T) / np.sqrt(32.0)
+            out[a:e, sl] = torch.softmax(s, dim=1) @ v[a:e, sl]
+    return out
+
+
+@pytest.fixture(scope="module")
+def data():
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    cu = np.r_[0, np.cumsum(LENS)].astype(np.int32)
+    T = int(cu[-1])
+    x = torch.randn((T, 1152), generator=g, device="cuda") * 2.0
+    x[:, 768:] = torch.rand((T, 384), generator=g, device="cuda") * 2 - 1   # |V| <= 1
+    hi = x.half()
+    lo = (x - hi.float()).half()
+    return x, hi, lo, cu
+
+
+@pytest.mark.parametrize("variant", range(8))
+@pytest.mark.parametrize("split", [True, False], ids=["fp16x3", "fp16"])
+def test_attention_matches_fp32(gpu, data, variant, split):
+    from ragmi.encoders import attention
+    x, hi, lo, cu = data
+    cu_t = torch.from_numpy(cu).cuda()
+    out = attention(hi, cu_t, max(LENS), lo if split else None, variant)
+    torch.cuda.synchronize()
+    if split:
+        xs = hi.float() + lo.float()                 # the operands the kernel sees
+        got = out[0].float() + out[1].float()
+        tol = 2e-5
+    else:
+        xs = hi.float()
+        got = out.float()
+        tol = 2e-3
+    ref = _reference(xs[:, :384], xs[:, 384:768], xs[:, 768:], cu)
+    d = (got.double() - ref).abs()
+    err = d.max().item()
+    if err >= tol:
+        t, c = divmod(int(d.argmax()), 384)
+        b = int(np.searchsorted(cu, t, side="right")) - 1
+        raise AssertionError(f"variant {variant}: max |err| {err:.3g} at token {t} (sequence "
+                             f"{b}, len {LENS[b]}, query {t - cu[b]}), head {c // 32}; "
+                             f"got {got[t, c].item():.6f} ref {ref[t, c].item():.6f}")

@@ -10,8 +10,8 @@ Also the a4 shape: /embed of 64 chunks x ~200-260 tokens through the 12-layer bg
 forward (ingest.embed_chunks, ingest.py:52-66; EMBED_BATCH = 64).
 
 Oracle: oracle/bert_ref.py (numpy fp32 restatement pinned to transformers 5.15), computed in
-sub-batches of 32 sequences padded to their longest. Bounds: logits <= 1e-3 (north_star's
-rerank tolerance) and embeddings <= 5e-5 in fp16x3; fp16 fast mode 2e-2 / 2e-3.
+sub-batches of 32 sequences padded to their longest. Bounds: logits <= 1e-4 (north_star's
+rerank tolerance is 1e-3) and embeddings <= 5e-6 in fp16x3; fp16 fast mode 2e-2 / 2e-3.
 """
 import numpy as np
 import pytest
@@ -22,7 +22,10 @@ import bert_ref as R
 pytestmark = pytest.mark.gpu
 
 B, K, TOPK = 32, 15, 5
-TOL = {"fp16x3": dict(ce=1e-3, bge=5e-5), "fp16": dict(ce=2e-2, bge=2e-3)}
+# fp16x3 bounds tighter than north_star's 1e-3: measured 2.7e-5 / 3.8e-7 once hi and lo of
+# every split come from one fp32 value (bert_kernels.hip split16; 3.3e-4 before), so a
+# regression to fp16-level rounding anywhere in the forward fails here
+TOL = {"fp16x3": dict(ce=1e-4, bge=5e-6), "fp16": dict(ce=2e-2, bge=2e-3)}
 
 
 def _padded(ids, types, cu, lo, hi):

@@ -19,7 +19,8 @@ import bert_ref as R
 
 pytestmark = pytest.mark.gpu
 
-TOL = {"fp16x3": dict(bge=5e-5, cos=0.9999999, ce=1e-3),
+# fp16x3: measured 6.5e-7 (bge) / 2.6e-5 (ce) with consistent hi/lo splits (split16)
+TOL = {"fp16x3": dict(bge=5e-6, cos=0.9999999, ce=1e-4),
        "fp16": dict(bge=2e-3, cos=0.99995, ce=2e-2)}
 
 
@@ -59,7 +60,8 @@ def test_bge_golden(bge, golden, prec):
     g = golden
     out = enc.forward_padded(g["ids_q"], g["tt_q"], g["m_q"]).cpu().numpy()
     assert _report(f"[{prec}] bge vs transformers", out, g["bge_emb"]) <= TOL[prec]["bge"]
-    cos = (out * g["bge_emb"]).sum(1) / np.linalg.norm(out, axis=1)
+    o64, r64 = out.astype(np.float64), g["bge_emb"].astype(np.float64)   # fp32 cos: +-2e-7 noise
+    cos = (o64 * r64).sum(1) / np.linalg.norm(o64, axis=1) / np.linalg.norm(r64, axis=1)
     assert cos.min() >= TOL[prec]["cos"]
     np.testing.assert_allclose(np.linalg.norm(out, axis=1), 1.0, atol=1e-5)
 
