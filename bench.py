@@ -203,7 +203,7 @@ def main():
     ap.add_argument("--streams", type=int, default=0,
                     help="batches in flight (0 = by shard size: 4 below 4M rows per GPU, "
                          "else 2; 1 on a single GPU)")
-    ap.add_argument("--scan-order", choices=["auto", "serial", "free"], default="auto",
+    ap.add_argument("--scan-order", choices=["auto", "serial", "free", "stream"], default="auto",
                     help="serial: each batch's scan waits for the previous batch's scan "
                          "(rag_index_set_scan_order); free: scans on different streams overlap")
     ap.add_argument("--config", choices=["4", "2", "3", "5", "filtered"], default="4",
@@ -266,7 +266,11 @@ def main():
     n_streams = args.streams or (4 if rows_local < 4_000_000 else 2)
     serial = args.scan_order == "serial" or (args.scan_order == "auto"
                                              and rows_local >= 4_000_000)
-    idx.set_scan_order(serial)
+    if args.scan_order == "stream":
+        serial = True
+        idx.set_scan_order(2)
+    else:
+        idx.set_scan_order(serial)
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev)
                                                   for _ in range(n_streams - 1)]
     n_step = [0]
@@ -380,7 +384,8 @@ def main():
                        "corpus_rows": n_total, "dim": D, "batch": B, "k": K_TOP,
                        "rows_per_gpu": local_rows, "parallelism": f"corpus-shard{world}",
                        "batches_in_flight": n_streams,
-                       "scan_order": "serial" if serial else "free"},
+                       "scan_order": args.scan_order if args.scan_order == "stream" else
+                                     "serial" if serial else "free"},
             "recall_at_5": check and check["recall_at_5"],
             "recall_at_5_min": check and check["recall_at_5_min"],
             "exact_batches": check and check["exact_batches"],
@@ -393,7 +398,8 @@ def main():
                          "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK, 4),
                          "traffic": traffic, "traffic_source": traffic_source,
-                         "kernel": "scan_kernel<384,false>", "avg_ms": round(scan_avg_ms, 4),
+                         "kernel": "scan_kernel<384,false>",
+                         "avg_ms": round(scan_avg_ms, 4),
                          "algorithmic_bytes_per_launch": algo_bytes,
                          # whole-step view: the shard's bytes per batch over the step time
                          "step_frac": round(algo_bytes / (elapsed / args.steps) / HBM_PEAK, 4),

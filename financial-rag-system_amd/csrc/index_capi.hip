@@ -44,6 +44,9 @@ struct Workspace {
   float* eps = nullptr;         // [groups][32] per-query |MFMA - exact| score bound (qprep)
   int* fb_tier = nullptr;       // [groups][32] certifying path per query of the last pass
   unsigned long long* fb_cnt = nullptr;   // [2] tier-1 / tier-2 totals since creation
+  int* tileq = nullptr;         // [8][kTileQStride] per-XCD tile-queue heads (dynamic scan)
+  hipEvent_t ev_in = nullptr;   // scan-stream order: caller stream -> scan stream -> caller
+  hipEvent_t ev_out = nullptr;
   hipStream_t owner = nullptr;  // stream of the last pass that used this slot
   bool used = false;
   uint64_t tick = 0;            // last use (LRU rebinding)
@@ -76,7 +79,10 @@ struct rag_index {
   // scan order (rag_index_set_scan_order): when set, every scan launch waits for the
   // previous one (on whichever stream it ran), so passes on several streams overlap their
   // query prep / seeding / select with another pass's scan but never two scans
-  bool serial_scans = false;
+  // 0 free, 1 serial (event chain across the callers' streams), 2 serial on the handle's own
+  // scan stream (each pass hands its scan to it and waits for it before select)
+  int serial_scans = 0;
+  hipStream_t scan_stream = nullptr;
   hipEvent_t scan_done = nullptr;
   hipStream_t scan_last = nullptr;
   int prof = 0;                // 0 off; n > 0: time every n-th scan launch
@@ -169,9 +175,17 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
     grid = (int)std::min<int64_t>(h->max_wgs, std::max<int64_t>(1, (n_tiles + 3) / 4));
     grid = std::min(grid, kMaxLists / kWavesPerWG);
   }
-  if (h->serial_scans) {
+  const hipStream_t caller = st;
+  if (h->serial_scans == 1) {
     if (!h->scan_done) RAG_HIP(hipEventCreateWithFlags(&h->scan_done, hipEventDisableTiming));
     if (h->scan_last && h->scan_last != st) RAG_HIP(hipStreamWaitEvent(st, h->scan_done, 0));
+  } else if (h->serial_scans == 2) {
+    if (!h->scan_stream) RAG_HIP(hipStreamCreateWithFlags(&h->scan_stream, hipStreamNonBlocking));
+    if (!w.ev_in) RAG_HIP(hipEventCreateWithFlags(&w.ev_in, hipEventDisableTiming));
+    if (!w.ev_out) RAG_HIP(hipEventCreateWithFlags(&w.ev_out, hipEventDisableTiming));
+    RAG_HIP(hipEventRecord(w.ev_in, st));
+    RAG_HIP(hipStreamWaitEvent(h->scan_stream, w.ev_in, 0));
+    st = h->scan_stream;
   }
   ProfPair pp{};
   const bool timed = h->prof > 0 && (h->prof_seq++ % h->prof) == 0;
@@ -218,9 +232,13 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
     RAG_HIP(hipEventRecord(pp.b, st));
     h->prof_pairs.push_back(pp);
   }
-  if (h->serial_scans) {
+  if (h->serial_scans == 1) {
     RAG_HIP(hipEventRecord(h->scan_done, st));
     h->scan_last = st;
+  } else if (h->serial_scans == 2) {
+    RAG_HIP(hipEventRecord(w.ev_out, st));
+    RAG_HIP(hipStreamWaitEvent(caller, w.ev_out, 0));
+    st = caller;
   }
   const int n_lists = wide ? grid : grid * (kLdsQ ? kLdsWaves : kWavesPerWG);   // per group
   const ExactStats fb{w.fb_tier, w.fb_cnt};
@@ -333,14 +351,17 @@ void launch_variant(rag_index* h, Workspace& w, int grid, hipStream_t st) {
   using namespace ragmi;
   const int n_tiles = (int)((h->count + 15) / 16);
   // 0 prod (seeded) | 1 unseeded | 2 contiguous | 3 mfma-only | 4 loads-only | 5 no-nt
-  // 6 no-sb
-  constexpr int MODE = V == 3 ? 1 : (V == 4 ? 2 : 0);
+  // 6 no-sb | 9 / 10 / 11 dynamic tile queue, chunks of 2 / 1 / 4 tiles | 12 dynamic (2),
+  // loads only | 13 / 14 static production / loads only (9-14: each launch timed on its own,
+  // the queue heads zeroed between launches outside the timed window)
+  constexpr int MODE = V == 3 ? 1 : (V == 4 || V == 12 || V == 14 ? 2 : 0);
   constexpr bool STRIDED = V != 2;
   constexpr bool NT = V != 5;
   constexpr bool SB = V != 6;
-  scan_kernel<D, false, MODE, STRIDED, NT, SB><<<dim3(grid), dim3(256), 0, st>>>(
+  constexpr int DYN = V == 9 || V == 12 ? 2 : V == 10 ? 1 : V == 11 ? 4 : 0;
+  scan_kernel<D, false, MODE, STRIDED, NT, SB, DYN><<<dim3(grid), dim3(256), 0, st>>>(
       h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, n_tiles, V == 1 ? nullptr : w.seed,
-      w.part_s, w.part_i, w.heads_s, w.heads_i, w.heads_n);
+      w.part_s, w.part_i, w.heads_s, w.heads_i, w.heads_n, w.tileq);
 }
 
 template <int D>
@@ -393,13 +414,34 @@ int bench_scan(rag_index* h, const float* q, int B, int variant, int reps, doubl
       default: launch_variant<D, 6>(h, w, grid, nullptr); break;
     }
   };
-  one();  // warm
-  RAG_HIP(hipEventRecord(a, nullptr));
-  for (int r = 0; r < reps; ++r) one();
-  RAG_HIP(hipEventRecord(b, nullptr));
-  RAG_HIP(hipEventSynchronize(b));
   float ms = 0.f;
-  RAG_HIP(hipEventElapsedTime(&ms, a, b));
+  if (variant >= 9) {
+    // one launch per event pair; the tile-queue heads are zeroed before each, outside it
+    for (int r = -1; r < reps; ++r) {
+      RAG_HIP(hipMemsetAsync(w.tileq, 0, 8 * kTileQStride * 4, nullptr));
+      RAG_HIP(hipEventRecord(a, nullptr));
+      switch (variant) {
+        case 9: launch_variant<D, 9>(h, w, grid, nullptr); break;
+        case 10: launch_variant<D, 10>(h, w, grid, nullptr); break;
+        case 11: launch_variant<D, 11>(h, w, grid, nullptr); break;
+        case 12: launch_variant<D, 12>(h, w, grid, nullptr); break;
+        case 13: launch_variant<D, 0>(h, w, grid, nullptr); break;
+        default: launch_variant<D, 14>(h, w, grid, nullptr); break;
+      }
+      RAG_HIP(hipEventRecord(b, nullptr));
+      RAG_HIP(hipEventSynchronize(b));
+      float m1 = 0.f;
+      RAG_HIP(hipEventElapsedTime(&m1, a, b));
+      if (r >= 0) ms += m1;   // r = -1: warm-up
+    }
+  } else {
+    one();  // warm
+    RAG_HIP(hipEventRecord(a, nullptr));
+    for (int r = 0; r < reps; ++r) one();
+    RAG_HIP(hipEventRecord(b, nullptr));
+    RAG_HIP(hipEventSynchronize(b));
+    RAG_HIP(hipEventElapsedTime(&ms, a, b));
+  }
   (void)hipEventDestroy(a);
   (void)hipEventDestroy(b);
   if (rows64) (void)hipFree(rows64);
@@ -512,6 +554,9 @@ int rag_index_create(int dim, int64_t capacity_rows, int device, rag_index_t** o
               hipMalloc(reinterpret_cast<void**>(&w.eps), G * Q * 4) == hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&w.fb_tier), G * Q * 4) == hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&w.fb_cnt), 16) == hipSuccess &&
+              hipMalloc(reinterpret_cast<void**>(&w.tileq), 8 * ragmi::kTileQStride * 4) ==
+                  hipSuccess &&
+              hipMemset(w.tileq, 0, 8 * ragmi::kTileQStride * 4) == hipSuccess &&
               hipMemset(w.fb_cnt, 0, 16) == hipSuccess &&
               hipMemset(w.fb_tier, 0, G * Q * 4) == hipSuccess;
     if (!ok) {
@@ -543,12 +588,16 @@ int rag_index_destroy(rag_index_t* h) {
     if (w.eps) (void)hipFree(w.eps);
     if (w.fb_tier) (void)hipFree(w.fb_tier);
     if (w.fb_cnt) (void)hipFree(w.fb_cnt);
+    if (w.tileq) (void)hipFree(w.tileq);
+    if (w.ev_in) (void)hipEventDestroy(w.ev_in);
+    if (w.ev_out) (void)hipEventDestroy(w.ev_out);
   }
   for (auto& p : h->prof_pairs) {
     (void)hipEventDestroy(p.a);
     (void)hipEventDestroy(p.b);
   }
   if (h->scan_done) (void)hipEventDestroy(h->scan_done);
+  if (h->scan_stream) (void)hipStreamDestroy(h->scan_stream);
   if (h->corpus) (void)hipFree(h->corpus);
   if (h->tags) (void)hipFree(h->tags);
   if (h->stage) (void)hipFree(h->stage);
@@ -755,7 +804,7 @@ int rag_merge_topk_packed(const int32_t* in_packed, int n_lists, int B, int k, f
 int rag_bench_scan(rag_index_t* h, const float* queries_dev, int B, int variant, int reps,
                    double* avg_ms) {
   ragmi::clear_error();
-  if (!h || !queries_dev || B < 1 || reps < 1 || !avg_ms || variant < 0 || variant > 8)
+  if (!h || !queries_dev || B < 1 || reps < 1 || !avg_ms || variant < 0 || variant > 14)
     return ragmi::fail(RAG_EINVAL, "bad bench args");
   std::lock_guard<std::mutex> lk(h->mu);
   RAG_HIP(hipSetDevice(h->device));
@@ -805,7 +854,7 @@ int rag_index_set_scan_order(rag_index_t* h, int serial) {
   ragmi::clear_error();
   if (!h) return ragmi::fail(RAG_EINVAL, "index is NULL");
   std::lock_guard<std::mutex> lk(h->mu);
-  h->serial_scans = serial != 0;
+  h->serial_scans = serial < 0 || serial > 2 ? 1 : serial;
   h->scan_last = nullptr;
   return RAG_OK;
 }

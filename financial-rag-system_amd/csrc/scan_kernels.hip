@@ -23,6 +23,8 @@ constexpr int kP = 8;             // pending slots per (lane, query tile)
 constexpr int kWavesPerWG = 4;
 constexpr int kMaxLists = 2048;   // max scan waves (= per-wave lists) per pass
 constexpr int kLdsPerWave = 4096; // dwords: keep_s[32][32] keep_i[32][32] pend_s[2][8][64] pend_i[2][8][64]
+constexpr int kTileQStride = 16;  // ints between the 8 per-XCD tile-queue heads (64 B apart)
+constexpr int kDynChunk = 2;      // tiles per dequeue of the dynamic scan schedule
 
 template <int D>
 __host__ __device__ constexpr int steps() { return D / 32; }
@@ -381,13 +383,24 @@ __device__ __forceinline__ void tile_sequence(int gw, int nw, int n_tiles, int& 
 //      'nt-weights': once-read streams)
 //   SB sched_barrier after each tile's load batch, so the scheduler cannot sink the next
 //      tile's loads below the current tile's wait (which leaves one tile in flight)
+//   DYN > 0 (diagnostic, rag_bench_scan variants 9-12; round 2): dynamic tile queue instead
+//      of the static interleave — waves dequeue chunks of DYN tiles from per-XCD heads (tileq,
+//      zeroed before each launch): head x hands out chunks x, x + 8, x + 16, ... in increasing
+//      order, so every wave still visits increasing rows (the strict `> thr` tie rule). The
+//      next chunk's dequeue is issued when a chunk starts. Measured and dropped
+//      (profiles/r02_scan_dyn.jsonl): loads-only 0.142 -> 0.180 ms at 1.25M rows, 1.099 ->
+//      1.356 ms at 10M; production 15-20% slower with chunks of 2 or 4, 48% with 1. The
+//      returning atomic sits in the wave's in-order vmcnt queue, so every later tile load of
+//      the wave waits out its ~2-3 us fabric round trip: each dequeue stalls the wave's stream.
 // Query B-operands live in VGPRs (2 x D/32 half8 per lane): the D = 384 production kernel.
-template <int D, bool FILTER, int MODE = 0, bool STRIDED = true, bool NT = true, bool SB = true>
+template <int D, bool FILTER, int MODE = 0, bool STRIDED = true, bool NT = true, bool SB = true,
+          int DYN = 0>
 __global__ __launch_bounds__(256, 2) void scan_kernel(
     const half8* __restrict__ corpus, const uint32_t* __restrict__ tags,
     const uint32_t* __restrict__ filt, const half8* __restrict__ qfrag, int n_rows, int n_tiles,
     const float* __restrict__ seed_thr, float* __restrict__ part_s, int* __restrict__ part_i,
-    float* __restrict__ heads_s, int* __restrict__ heads_i, int* __restrict__ heads_n) {
+    float* __restrict__ heads_s, int* __restrict__ heads_i, int* __restrict__ heads_n,
+    int* __restrict__ tileq = nullptr) {
   constexpr int S = steps<D>();
   __shared__ int lds[kWavesPerWG * kLdsPerWave];
   const int lane = threadIdx.x & 63;
@@ -430,13 +443,67 @@ __global__ __launch_bounds__(256, 2) void scan_kernel(
     }
   };
 
-  if (n_mine > 0) {
+  // Buffer loads off a wave-uniform per-tile descriptor: the address lives in SGPRs and the
+  // per-lane part is one VGPR (lane*16), so no 64-bit address VGPRs are live across the
+  // loop (their reuse as load destinations forced a vmcnt(0) at the loop head).
+  const char* cbase = reinterpret_cast<const char*>(corpus);
+  const int voff = lane * 16;
+  auto load_t = [&](half8(&a)[S], int t_in) __attribute__((always_inline)) {
+    const int t = __builtin_amdgcn_readfirstlane(t_in);
+    const char* tp = cbase + (int64_t)t * (S * 1024);
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(tp), 0, S * 1024, 0x00020000);
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, s * 1024, NT ? 2 : 0);
+      a[s] = __builtin_bit_cast(half8, v);
+    }
+    if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
+  };
+  if constexpr (DYN > 0) {
+    const int xcd = blockIdx.x & 7;
+    int* head = tileq + kTileQStride * xcd;
+    // The head address is hidden behind an opaque zero offset: with a provably uniform address
+    // the AMDGPU atomic optimizer rewrites the atomic into a wave-reduced one whose result is
+    // consumed (readfirstlane) right after the issue, i.e. a vmcnt(0) wait on every dequeue.
+    int zoff = 0;
+    asm volatile("" : "+v"(zoff));
+    auto deq = [&]() __attribute__((always_inline)) {
+      int v = 0;
+      if (lane == 0)
+        v = __hip_atomic_fetch_add(head + zoff, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return v;   // lane 0's VGPR; read (readfirstlane) only when the chunk is needed
+    };
+    int pend = deq();
+    int cb = 0, ce = 0;          // current chunk: tiles [cb, ce) (wave-uniform)
+    // once the queue is empty every call returns -1 (at most two dequeues past the last chunk)
+    auto next_tile = [&]() __attribute__((always_inline)) {
+      if (cb >= ce) {
+        cb = (8 * __builtin_amdgcn_readfirstlane(pend) + xcd) * DYN;
+        ce = min(cb + DYN, n_tiles);
+        pend = deq();
+      }
+      return cb < ce ? cb++ : -1;
+    };
     half8 a0[S], a1[S];
-    // Buffer loads off a wave-uniform per-tile descriptor: the address lives in SGPRs and the
-    // per-lane part is one VGPR (lane*16), so no 64-bit address VGPRs are live across the
-    // loop (their reuse as load destinations forced a vmcnt(0) at the loop head).
-    const char* cbase = reinterpret_cast<const char*>(corpus);
-    const int voff = lane * 16;
+    int t_cur = next_tile();
+    if (t_cur >= 0) {
+      load_t(a0, t_cur);
+      while (true) {
+        int t_nxt = next_tile();
+        load_t(a1, t_nxt >= 0 ? t_nxt : t_cur);
+        process_v(a0, t_cur);
+        if (t_nxt < 0) break;
+        t_cur = t_nxt;
+        t_nxt = next_tile();
+        load_t(a0, t_nxt >= 0 ? t_nxt : t_cur);
+        process_v(a1, t_cur);
+        if (t_nxt < 0) break;
+        t_cur = t_nxt;
+      }
+    }
+  } else if (n_mine > 0) {
+    half8 a0[S], a1[S];
     auto load = [&](half8(&a)[S], int j) {
       const int t = __builtin_amdgcn_readfirstlane(t_first + j * t_step);
       const char* tp = cbase + (int64_t)t * (S * 1024);

@@ -202,7 +202,8 @@ class FlatIndex:
     def set_scan_order(self, serial: bool) -> None:
         """serial=True: each pass's scan waits for the previous pass's scan on any stream
         (rag_index_set_scan_order); prep / seeding / select still overlap across streams."""
-        check(self._L.rag_index_set_scan_order(self._h, int(bool(serial))))
+        mode = serial if isinstance(serial, int) and not isinstance(serial, bool) else int(bool(serial))
+        check(self._L.rag_index_set_scan_order(self._h, mode))
 
     def exactness_stats(self, n_last: int = 0):
         """(tier1 total, tier2 total, tiers of the last pass's first n_last queries): which

@@ -147,13 +147,16 @@ int rag_merge_topk_packed(const int32_t* in_packed_dev, int n_lists, int B, int 
 int rag_index_exactness_stats(rag_index_t* index, int64_t* tier1, int64_t* tier2,
                               int32_t* last_tiers, int n_last);
 
-/* Scan order across streams. serial != 0: each search pass's scan launch waits for the
+/* Scan order across streams. serial = 1: each search pass's scan launch waits for the
  * previous pass's scan, whichever stream that ran on (one HIP event per handle), so passes
  * issued on several streams overlap their query prep, seed sampling and select with another
- * pass's scan while the HBM-bound scans themselves run one at a time. serial = 0 (default):
- * passes on different streams are unordered. No reference counterpart: the reference issues
- * one HTTP search per query (main.py:232-237); this is serving-loop plumbing for
- * main2.py:281-295's batch processor with several batches in flight. */
+ * pass's scan while the HBM-bound scans themselves run one at a time (measured effective with
+ * 2 streams; with 4 the traced scans still overlap). serial = 2: every pass hands
+ * its scan to the handle's own scan stream and waits for it before select (two event hops
+ * per pass; strictly one scan at a time). serial = 0 (default): passes on different streams
+ * are unordered. No reference counterpart: the reference issues one HTTP search per query
+ * (main.py:232-237); this is serving-loop plumbing for main2.py:281-295's batch processor
+ * with several batches in flight. */
 int rag_index_set_scan_order(rag_index_t* index, int serial);
 
 /* Kernel timing hook for bench.py: average device time (ms) of `rag_index_search` scan-kernel
@@ -168,7 +171,9 @@ int rag_profile_scan_ms(rag_index_t* index, double* total_ms, int64_t* launches)
  * thresholds), 1 unseeded, 2 contiguous per-wave tile ranges, 3 MFMA without top-k,
  * 4 loads only, 5 without non-temporal loads, 6 without the load sched-barrier, 7 production
  * with every seed at +inf (top-k compares only), 8 the VALU ablation: v_dot2_f32_f16 instead
- * of MFMA over a row-group-major copy of the corpus, same top-k. dim 1024: variants 0-4 of
+ * of MFMA over a row-group-major copy of the corpus, same top-k; 9 / 10 / 11 the dynamic tile
+ * queue with chunks of 2 / 1 / 4 tiles, 12 dynamic (2) loads only, 13 / 14 static production
+ * / loads only (9-14 time every launch on its own event pair). dim 1024: variants 0-4 of
  * the wide (33-128 query) scan. */
 int rag_bench_scan(rag_index_t* index, const float* queries_dev, int B, int variant, int reps,
                    double* avg_ms);

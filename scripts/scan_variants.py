@@ -17,7 +17,12 @@ from ragmi.index import FlatIndex  # noqa: E402
 
 NAMES = {0: "prod (seeded, interleaved, nt, sched-barrier)", 1: "unseeded", 2: "contiguous",
          3: "mfma-only", 4: "loads-only", 5: "no-nt", 6: "no-sb", 7: "top-k never taken",
-         8: "VALU v_dot2_f32_f16 (no MFMA), same loads and top-k"}
+         8: "VALU v_dot2_f32_f16 (no MFMA), same loads and top-k",
+         9: "dynamic tile queue, chunks of 2 (timed per launch)",
+         10: "dynamic tile queue, chunks of 1 (timed per launch)",
+         11: "dynamic tile queue, chunks of 4 (timed per launch)",
+         12: "dynamic (2), loads only (timed per launch)",
+         13: "static prod (timed per launch)", 14: "static loads only (timed per launch)"}
 
 
 def main():

@@ -233,8 +233,9 @@ def test_one_million_rows_planted_and_exact(gpu):
 @pytest.mark.parametrize("dim,b", [(384, 32), (1024, 128)])
 def test_serial_scan_order_across_streams(gpu, dim, b):
     """rag_index_set_scan_order(1): batches issued round-robin on 3 streams without host
-    syncs, every scan chained behind the previous one by the handle's event; each batch's
-    result equals the oracle's (and the unordered mode gives the same)."""
+    syncs, every scan chained behind the previous one by the handle's event; (2): every scan
+    on the handle's own scan stream; each batch's result equals the oracle's (and the
+    unordered mode gives the same)."""
     rng = np.random.default_rng(dim + b)
     n = 20_000
     x = rng.standard_normal((n, dim)).astype(np.float32)
@@ -245,7 +246,7 @@ def test_serial_scan_order_across_streams(gpu, dim, b):
     want = [O.search(enc, q, 15) for q in qs]
     qd = [torch.from_numpy(q).to(gpu) for q in qs]
     streams = [torch.cuda.Stream(gpu) for _ in range(3)]
-    for serial in (True, False):
+    for serial in (1, 2, 0):
         idx.set_scan_order(serial)
         torch.cuda.synchronize()
         outs = []
