@@ -739,7 +739,7 @@ int rag_bert_attention(int variant, const void* qkv, const void* qkv_lo, const i
   if ((qkv_lo == nullptr) != (ctx_lo == nullptr))
     return ragmi::fail(RAG_EINVAL, "qkv_lo and ctx_lo: both (fp16x3) or neither (fp16)");
   if (variant == -1) variant = kAttnVar;
-  if (variant < 0 || variant > 7) return ragmi::fail(RAG_EINVAL, "variant: -1 or 0..7");
+  if (variant < 0 || variant > 15) return ragmi::fail(RAG_EINVAL, "variant: -1 or 0..15");
   constexpr int H = 384, HD = 32, NH = H / HD;
   const int planes = qkv_lo ? 2 : 1;
   const int kc = attn_chunk_keys<HD>(max_len, planes);
@@ -775,7 +775,15 @@ int rag_bert_attention(int variant, const void* qkv, const void* qkv_lo, const i
     case 4: return go(std::integral_constant<int, 4>{});
     case 5: return go(std::integral_constant<int, 5>{});
     case 6: return go(std::integral_constant<int, 6>{});
-    default: return go(std::integral_constant<int, 7>{});
+    case 7: return go(std::integral_constant<int, 7>{});
+    case 8: return go(std::integral_constant<int, 8>{});
+    case 9: return go(std::integral_constant<int, 9>{});
+    case 10: return go(std::integral_constant<int, 10>{});
+    case 11: return go(std::integral_constant<int, 11>{});
+    case 12: return go(std::integral_constant<int, 12>{});
+    case 13: return go(std::integral_constant<int, 13>{});
+    case 14: return go(std::integral_constant<int, 14>{});
+    default: return go(std::integral_constant<int, 15>{});
   }
 }
 

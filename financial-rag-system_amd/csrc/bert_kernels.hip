@@ -37,6 +37,23 @@ __device__ __forceinline__ half2 split16(float v) {   // {hi, lo}
   return half2{hi, (_Float16)(v - (float)hi)};
 }
 
+// The same split of two values in 3 instructions instead of 8 (round 2): the hi pair by one
+// v_cvt_pk_f16_f32, each lo by v_fma_mix{lo,hi}_f16 computing -hi * 1 + v exactly and rounding
+// once to fp16. v - hi is exact in fp32 (Sterbenz: hi is within a factor 2 of v, or 0), so
+// this is fp16(v - hi) bit for bit, as split16 computes it (which converts hi back to fp32,
+// subtracts and converts again, and converts hi twice). Inputs pinned as above.
+__device__ __forceinline__ void split16x2(float v0, float v1, half2& h, half2& l) {
+  asm("" : "+v"(v0), "+v"(v1));
+  h = half2{(_Float16)v0, (_Float16)v1};
+  const uint32_t hu = __builtin_bit_cast(uint32_t, h);
+  uint32_t lu;
+  asm("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %0, -%1, 1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+      : "=&v"(lu)
+      : "v"(hu), "v"(v0), "v"(v1));
+  l = __builtin_bit_cast(half2, lu);
+}
+
 // erf-GELU, 0.5 x (1 + erf(x / sqrt 2)), with erfc(|z|) from Abramowitz & Stegun 7.1.26
 // (|error of erf| <= 1.5e-7 absolute, i.e. at fp32 rounding level for the GELU output):
 // 1 + erf(z) = 2 - erfc(z) for z >= 0 and erfc(-z) for z < 0 (no cancellation for z << 0).
@@ -324,9 +341,15 @@ __global__ __launch_bounds__(256) void gemm_kernel(const _Float16* __restrict__ 
         } else {
           half8 h, l;
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            if constexpr (SPLIT) { const half2 s16_ = split16(v[e]); h[e] = s16_[0]; l[e] = s16_[1]; }
-            else h[e] = (_Float16)v[e];
+          for (int e = 0; e < 8; e += 2) {
+            if constexpr (SPLIT) {
+              half2 h2, l2;
+              split16x2(v[e], v[e + 1], h2, l2);
+              h[e] = h2[0]; h[e + 1] = h2[1]; l[e] = l2[0]; l[e + 1] = l2[1];
+            } else {
+              h[e] = (_Float16)v[e];
+              h[e + 1] = (_Float16)v[e + 1];
+            }
           }
           *reinterpret_cast<half8*>(static_cast<_Float16*>(Cout) + (int64_t)m * N + gn) = h;
           if constexpr (SPLIT) *reinterpret_cast<half8*>(Clo + (int64_t)m * N + gn) = l;
@@ -504,13 +527,18 @@ __device__ __forceinline__ void pipe_epi_pair(const floatx4& a0, const floatx4& 
     }
     half4 ha, hb, la, lb;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < 4; r += 2) {
       if constexpr (SPLIT) {
-        { const half2 s16_ = split16(va[r]); ha[r] = s16_[0]; la[r] = s16_[1]; }
-        { const half2 s16_ = split16(vb[r]); hb[r] = s16_[0]; lb[r] = s16_[1]; }
+        half2 h2, l2;
+        split16x2(va[r], va[r + 1], h2, l2);
+        ha[r] = h2[0]; ha[r + 1] = h2[1]; la[r] = l2[0]; la[r + 1] = l2[1];
+        split16x2(vb[r], vb[r + 1], h2, l2);
+        hb[r] = h2[0]; hb[r + 1] = h2[1]; lb[r] = l2[0]; lb[r + 1] = l2[1];
       } else {
         ha[r] = (_Float16)va[r];
+        ha[r + 1] = (_Float16)va[r + 1];
         hb[r] = (_Float16)vb[r];
+        hb[r + 1] = (_Float16)vb[r + 1];
       }
     }
     if (!NO_STORE || va[0] == 1234.5f) store_f16_pair<AUX>(ha, hb, rc, vo);
@@ -849,9 +877,12 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
                                                      sf(jp + 1), 0);
               half4 ha, hb, la, lb;
 #pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                { const half2 s16_ = split16(va[r]); ha[r] = s16_[0]; la[r] = s16_[1]; }
-                { const half2 s16_ = split16(vb[r]); hb[r] = s16_[0]; lb[r] = s16_[1]; }
+              for (int r = 0; r < 4; r += 2) {
+                half2 h2, l2;
+                split16x2(va[r], va[r + 1], h2, l2);
+                ha[r] = h2[0]; ha[r + 1] = h2[1]; la[r] = l2[0]; la[r + 1] = l2[1];
+                split16x2(vb[r], vb[r + 1], h2, l2);
+                hb[r] = h2[0]; hb[r + 1] = h2[1]; lb[r] = l2[0]; lb[r + 1] = l2[1];
               }
               const int vo = ((wr * WTM + i * 16 + (lane & 15)) * N + wc * WTN + jp * 16 + cofs) * 2;
               store_f16_pair(ha, hb, rh, vo);
@@ -872,9 +903,15 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
                                                    sf(j), 0);
             half4 h, l;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              if constexpr (SPLIT) { const half2 s16_ = split16(v[r]); h[r] = s16_[0]; l[r] = s16_[1]; }
-              else h[r] = (_Float16)v[r];
+            for (int r = 0; r < 4; r += 2) {
+              if constexpr (SPLIT) {
+                half2 h2, l2;
+                split16x2(v[r], v[r + 1], h2, l2);
+                h[r] = h2[0]; h[r + 1] = h2[1]; l[r] = l2[0]; l[r + 1] = l2[1];
+              } else {
+                h[r] = (_Float16)v[r];
+                h[r + 1] = (_Float16)v[r + 1];
+              }
             }
             const int vh = vf(i) / 2;                  // same element offsets in fp16
             __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, h), rh, vh,
@@ -1181,11 +1218,17 @@ struct AttnState {
 
 // VAR (bit mask; rag_bert_attention A/Bs them): 1 = rolling Q prefetch, 2 = fp16x3 row sums
 // by MFMA (else v_dot2), 4 = software-pipelined scores (block kb+1's K.Q^T MFMAs issued
-// before block kb's softmax, so they run in the matrix pipe under its vector work).
+// before block kb's softmax, so they run in the matrix pipe under its vector work), 8 = lean
+// block (round 2): the cross-lane max by v_permlane16/32_swap instead of two ds_bpermute
+// round trips, P and O split by split16x2 (3 instead of 8 VALU per pair), and a block's V^T
+// fragments read in one batch before its P.V MFMAs (one LDS wait instead of DT). Bitwise the
+// same results as without it.
 // Measured at the rerank shape (scripts/bench_attn.py, profiles/r02_attn_variants.jsonl):
 // fp16x3 0.270-0.283 ms over all eight, 2 the fastest; fp16 0.140 ms without 4, 0.19-0.21
 // with it (64-VGPR budget). The kernel's time is not in these (staging / latency bound).
-constexpr int kAttnVar = 2;
+// Bit 8 (profiles/r02e_lean_split.jsonl, same process): fp16x3 2 -> 10 0.281 -> 0.272 ms
+// (the default since), fp16 unchanged (0.148 / 0.149: no split there).
+constexpr int kAttnVar = 10;
 template <int H, int HD, bool SPLIT, int VAR = kAttnVar>
 __global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) void attn_kernel(
     const _Float16* __restrict__ qkv, const _Float16* __restrict__ qkv_lo,
@@ -1305,8 +1348,20 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) 
             mx = fmaxf(mx, sc[j][r]);
           }
       }
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      if constexpr ((VAR & 8) != 0) {
+        // lanes l, l^16, l^32, l^48 hold the same query's other keys
+        const uint32_t mu = __builtin_bit_cast(uint32_t, mx);
+        const auto r16 = __builtin_amdgcn_permlane16_swap(mu, mu, false, false);
+        mx = fmaxf(__builtin_bit_cast(float, (uint32_t)r16[0]),
+                   __builtin_bit_cast(float, (uint32_t)r16[1]));
+        const uint32_t mu2 = __builtin_bit_cast(uint32_t, mx);
+        const auto r32 = __builtin_amdgcn_permlane32_swap(mu2, mu2, false, false);
+        mx = fmaxf(__builtin_bit_cast(float, (uint32_t)r32[0]),
+                   __builtin_bit_cast(float, (uint32_t)r32[1]));
+      } else {
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      }
       // Deferred rescale: the running max only moves when some query's block max exceeds it
       // by more than 8 / c2 (P = 2^(s c2 - m c2) then stays <= 2^8, exact in the fp16 MFMA
       // operand and far from its range limit); otherwise the old max is kept and the
@@ -1326,14 +1381,28 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) 
       }
       const float nm = -st.m * c2;
       half8 ph, pl;
+      if constexpr (SPLIT && (VAR & 8) != 0) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float e = __builtin_amdgcn_exp2f(fmaf(sc[j][r], c2, nm));
-          if constexpr (SPLIT) { const half2 s16_ = split16(e); ph[4 * j + r] = s16_[0]; pl[4 * j + r] = s16_[1]; }
-          else ph[4 * j + r] = (_Float16)e;
-        }
+          for (int r = 0; r < 4; r += 2) {
+            const float e0 = __builtin_amdgcn_exp2f(fmaf(sc[j][r], c2, nm));
+            const float e1 = __builtin_amdgcn_exp2f(fmaf(sc[j][r + 1], c2, nm));
+            half2 h2, l2;
+            split16x2(e0, e1, h2, l2);
+            ph[4 * j + r] = h2[0]; ph[4 * j + r + 1] = h2[1];
+            pl[4 * j + r] = l2[0]; pl[4 * j + r + 1] = l2[1];
+          }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float e = __builtin_amdgcn_exp2f(fmaf(sc[j][r], c2, nm));
+            if constexpr (SPLIT) { const half2 s16_ = split16(e); ph[4 * j + r] = s16_[0]; pl[4 * j + r] = s16_[1]; }
+            else ph[4 * j + r] = (_Float16)e;
+          }
+      }
       // row sum of P exactly as the MFMA sees it (hi [+ lo]). fp16x3: the same MFMA against
       // a ones fragment (the MFMA pipe has the slack there, the vector ALU does not: 2 MFMAs
       // for 8 v_dot2, and every lane ends up with its query's whole sum); fp16: v_dot2 (the
@@ -1349,6 +1418,29 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) 
           if constexpr (SPLIT)
             st.l[0] = __builtin_amdgcn_fdot2(half2{pl[2 * e2], pl[2 * e2 + 1]}, one2, st.l[0], false);
         }
+      }
+      if constexpr ((VAR & 8) != 0) {
+        half8 vh[DT], vlo[DT];
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          const int vr = kb * HD + voff(dt);
+          vh[dt] = __builtin_shufflevector(lds_read_tr16(vls[0] + vr),
+                                           lds_read_tr16(vls[0] + vr + 16 * HD),
+                                           0, 1, 2, 3, 4, 5, 6, 7);
+          if constexpr (SPLIT)
+            vlo[dt] = __builtin_shufflevector(lds_read_tr16(vls[1] + vr),
+                                              lds_read_tr16(vls[1] + vr + 16 * HD),
+                                              0, 1, 2, 3, 4, 5, 6, 7);
+        }
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          if constexpr (SPLIT) {
+            st.o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vlo[dt], ph, st.o[dt], 0, 0, 0);
+            st.o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh[dt], pl, st.o[dt], 0, 0, 0);
+          }
+          st.o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh[dt], ph, st.o[dt], 0, 0, 0);
+        }
+        return;
       }
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
@@ -1398,11 +1490,20 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) 
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
         half4 a, al;
+        if constexpr (SPLIT && (VAR & 8) != 0) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float x = st.o[dt][r] * inv;
-          if constexpr (SPLIT) { const half2 s16_ = split16(x); a[r] = s16_[0]; al[r] = s16_[1]; }
-          else a[r] = (_Float16)x;
+          for (int r = 0; r < 4; r += 2) {
+            half2 h2, l2;
+            split16x2(st.o[dt][r] * inv, st.o[dt][r + 1] * inv, h2, l2);
+            a[r] = h2[0]; a[r + 1] = h2[1]; al[r] = l2[0]; al[r + 1] = l2[1];
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float x = st.o[dt][r] * inv;
+            if constexpr (SPLIT) { const half2 s16_ = split16(x); a[r] = s16_[0]; al[r] = s16_[1]; }
+            else a[r] = (_Float16)x;
+          }
         }
         *reinterpret_cast<half4*>(ctx + off + 16 * dt) = a;
         if constexpr (SPLIT) *reinterpret_cast<half4*>(ctx_lo + off + 16 * dt) = al;

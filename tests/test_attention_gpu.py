@@ -43,7 +43,7 @@ def data():
     return x, hi, lo, cu
 
 
-@pytest.mark.parametrize("variant", range(8))
+@pytest.mark.parametrize("variant", range(16))
 @pytest.mark.parametrize("split", [True, False], ids=["fp16x3", "fp16"])
 def test_attention_matches_fp32(gpu, data, variant, split):
     from ragmi.encoders import attention
@@ -68,3 +68,19 @@ def test_attention_matches_fp32(gpu, data, variant, split):
         raise AssertionError(f"variant {variant}: max |err| {err:.3g} at token {t} (sequence "
                              f"{b}, len {LENS[b]}, query {t - cu[b]}), head {c // 32}; "
                              f"got {got[t, c].item():.6f} ref {ref[t, c].item():.6f}")
+
+
+@pytest.mark.parametrize("variant", [0, 2, 4, 6])
+@pytest.mark.parametrize("split", [True, False], ids=["fp16x3", "fp16"])
+def test_lean_block_is_bitwise_identical(gpu, data, variant, split):
+    """VAR bit 8 (permlane max, split16x2 of P and O, batched V^T reads) changes how the same
+    arithmetic is issued, not the arithmetic: outputs equal the variant without it bit for
+    bit (split16x2's fp16(v - hi) by v_fma_mix equals split16's convert-subtract-convert)."""
+    from ragmi.encoders import attention
+    x, hi, lo, cu = data
+    cu_t = torch.from_numpy(cu).cuda()
+    a = attention(hi, cu_t, max(LENS), lo if split else None, variant)
+    b = attention(hi, cu_t, max(LENS), lo if split else None, variant | 8)
+    torch.cuda.synchronize()
+    for x1, x2 in (zip(a, b) if split else [(a, b)]):
+        assert torch.equal(x1.view(torch.int16), x2.view(torch.int16))

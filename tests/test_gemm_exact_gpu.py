@@ -66,3 +66,29 @@ def test_gemm_epilogue_bit_exact(gpu, shape, epi, split, variant):
         raise AssertionError(
             f"{int(bad.sum())} fp16 elements differ; first at rows {rows[:8].tolist()} "
             f"cols {cols[:8].tolist()} (row % 16: {(rows[:8] % 16).tolist()})")
+
+
+@pytest.mark.parametrize("shape", [(20000, 1152, 384), (3001, 384, 1536), (777, 1536, 384)],
+                         ids=lambda s: "x".join(map(str, s)))
+@pytest.mark.parametrize("variant", [1, 2, 10, 19], ids=["tile", "pipe", "small64", "ws"])
+def test_split_planes_match_fp32_epilogue(gpu, shape, variant):
+    """Random (non-dyadic) fp16x3 operands: the fp16 epilogue's planes are exactly
+    hi = fp16(v), lo = fp16(v - hi) of the fp32 value v the same kernel's fp32 epilogue stores
+    (same MFMA chains, only the epilogue differs) — checks split16x2's v_fma_mix lo plane
+    bit for bit where v - hi needs every fp16 rounding case."""
+    from ragmi.encoders import linear
+    M, N, K = shape
+    g = torch.Generator(device="cuda")
+    g.manual_seed(M + 3 * N + K)
+    a32 = torch.randn((M, K), generator=g, device="cuda")
+    w32 = torch.randn((N, K), generator=g, device="cuda") * 0.05
+    bias = torch.randn((N,), generator=g, device="cuda") * 0.1
+    a, w = a32.half(), w32.half()
+    al, wl = (a32 - a.float()).half(), (w32 - w.float()).half()
+    v = linear(a, w, bias, 2, al, wl, variant)
+    hi, lo = linear(a, w, bias, 0, al, wl, variant)
+    torch.cuda.synchronize()
+    hi_ref = v.half()
+    lo_ref = (v - hi_ref.float()).half()
+    assert torch.equal(hi.view(torch.int16), hi_ref.view(torch.int16))
+    assert torch.equal(lo.view(torch.int16), lo_ref.view(torch.int16))
