@@ -346,7 +346,7 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
   if (variant == RAG_GEMM_WS || variant == RAG_GEMM_WS_MFMA_ONLY ||
       variant == RAG_GEMM_WS_NO_STORE || variant == RAG_GEMM_WS_DMA_ONLY ||
       variant == RAG_GEMM_WS_L2_STORE || variant == RAG_GEMM_WS_NT ||
-      variant == RAG_GEMM_WS_NOROT) {
+      variant == RAG_GEMM_WS_NOROT || variant == RAG_GEMM_WS_READS_FIRST) {
     auto go = [&](auto pc) {
       constexpr int P = decltype(pc)::value;
       if (Al) launch_ws<EPI, true, PipeLarge, P>(A, Al, W, Wl, bias, M, N, K, C, Clo, st);
@@ -364,6 +364,12 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
     else if (variant == RAG_GEMM_WS_NO_STORE) go(std::integral_constant<int, 6>{});
     else if (variant == RAG_GEMM_WS_L2_STORE) go(std::integral_constant<int, 9>{});
     else if (variant == RAG_GEMM_WS_DMA_ONLY) go(std::integral_constant<int, 8>{});
+    else if (variant == RAG_GEMM_WS_READS_FIRST) {
+      constexpr int AX = EPI == kEpiF32 ? 0 : 2;
+      // the all-reads-first fragment order (PROBE 13) the WS kernel used before its interleaved one
+      if (Al) launch_ws<EPI, true, PipeLarge, 13, AX>(A, Al, W, Wl, bias, M, N, K, C, Clo, st);
+      else launch_ws<EPI, false, PipeLarge, 13, AX>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st);
+    }
     else if (variant == RAG_GEMM_WS_NOROT) {
       constexpr int AX = EPI == kEpiF32 ? 0 : 2;
       if (Al) launch_ws<EPI, true, PipeLarge, 11, AX>(A, Al, W, Wl, bias, M, N, K, C, Clo, st);
@@ -678,7 +684,8 @@ int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, co
     return ragmi::fail(RAG_EINVAL, "fp16x3 fp16-output GEMM needs C_lo");
   if ((variant == RAG_GEMM_PIPE || variant == RAG_GEMM_SMALL || variant == RAG_GEMM_WIDE ||
        variant == RAG_GEMM_SMALL_BK64 || variant == RAG_GEMM_BIG || variant == RAG_GEMM_BIG128 ||
-       variant == RAG_GEMM_WS || variant == RAG_GEMM_WS_NT || variant == RAG_GEMM_WS_NOROT) &&
+       variant == RAG_GEMM_WS || variant == RAG_GEMM_WS_NT || variant == RAG_GEMM_WS_NOROT ||
+       variant == RAG_GEMM_WS_READS_FIRST) &&
       !pipe_ok(M, N, K))
     return ragmi::fail(RAG_EINVAL, "pipe/small/wide variants need N % 128 == 0, K % 64 == 0, "
                                    "N <= 4096, M*K*2 and M*N*4 < 2^31");
@@ -692,7 +699,7 @@ int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, co
                      variant == RAG_GEMM_WIDE || variant == RAG_GEMM_SMALL_BK64 ||
                      variant == RAG_GEMM_BIG || variant == RAG_GEMM_BIG128 ||
                      variant == RAG_GEMM_WS || variant == RAG_GEMM_WS_NT ||
-                     variant == RAG_GEMM_WS_NOROT || probe;
+                     variant == RAG_GEMM_WS_NOROT || variant == RAG_GEMM_WS_READS_FIRST || probe;
   if (!known || (probe && !pipe_ok(M, N, K)))
     return ragmi::fail(RAG_EINVAL, "unknown GEMM variant, or a probe on a non-pipe shape");
   auto* a = static_cast<const _Float16*>(A);

@@ -1109,7 +1109,31 @@ __global__ __launch_bounds__(CFG::THREADS + 256, 1) void gemm_ws_kernel(
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[ks][0][j], af[ks][0][i], acc[i][j], 0, 0, 0);
       }
     };
-    {
+    if constexpr (PROBE != 13 && !P_NO_MFMA) {
+      // interleaved order: A_0, W_0..W_{FN-1}, A_1, ... read in the order the i-major MFMAs
+      // consume them, with no barrier between the reads and the MFMAs, so the first MFMA
+      // waits for 4 reads instead of 13 (all 8 waves issue their reads together after the
+      // barrier; the LDS serves them interleaved). 123 instead of 138 VGPRs; measured
+      // (profiles/r02e_gemm_ilv.jsonl, same process, PROBE 13 = the previous all-reads-first
+      // order): 117K-token layer fp16x3 1.274 -> 1.264 ms, fp16 0.586 -> 0.581, QKV -3 to -6%,
+      // the others within +-1%.
+      read_a(0);
+#pragma unroll
+      for (int j = 0; j < FN; ++j)      // W_j's planes together: MFMA (0, j) needs 2 + 2j reads
+#pragma unroll
+        for (int ks = 0; ks < KSN; ++ks)
+#pragma unroll
+          for (int p = 0; p < NPL; ++p)
+            wf[ks][p][j] = sw[p * W_H8 + swz<CPR>(wc * WTN + j * 16 + (lane & 15), ks * 4 + (lane >> 4))];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        if (i + 1 < FM) read_a(i + 1);
+#pragma unroll
+        for (int ks = 0; ks < KSN; ++ks)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) mma(ks, i, j);
+      }
+    } else {
       if constexpr (!P_NO_MFMA) {
 #pragma unroll
         for (int i = 0; i < FM; ++i) read_a(i);

@@ -95,7 +95,9 @@ int rag_build_pairs(const int32_t* q_ids, const int32_t* q_cu, int B, const int6
  * its loads and barriers / its epilogue stores / loads and stores (_MFMA_ONLY) / MFMAs and
  * stores (_DMA_ONLY). _WS: PIPE's tiles with the DMAs on 4 loader waves beside the 8 MFMA
  * waves; _WS_NT the same with non-temporal output stores; _WS_* probes as the PIPE ones, and
- * _WS_L2_STORE with every tile stored over the first row band (L2-resident writes).
+ * _WS_L2_STORE with every tile stored over the first row band (L2-resident writes);
+ * _WS_NOROT rotated-K-order-off A/B; _WS_READS_FIRST the MFMA waves' previous fragment order
+ * (all reads of a K step before its MFMAs) for A/B against the interleaved one.
  * N % 128 == 0, K % 64 == 0 (PIPE/SMALL also N <= 4096). */
 enum { RAG_EPI_F16 = 0, RAG_EPI_GELU_F16 = 1, RAG_EPI_F32 = 2 };
 enum { RAG_GEMM_AUTO = 0, RAG_GEMM_TILE = 1, RAG_GEMM_PIPE = 2, RAG_GEMM_PROBE_NO_MFMA = 3,
@@ -104,7 +106,7 @@ enum { RAG_GEMM_AUTO = 0, RAG_GEMM_TILE = 1, RAG_GEMM_PIPE = 2, RAG_GEMM_PROBE_N
        RAG_GEMM_BIG128 = 12, RAG_GEMM_PROBE_NO_STORE = 13, RAG_GEMM_PROBE_MFMA_ONLY = 14,
        RAG_GEMM_PROBE_DMA_ONLY = 15, RAG_GEMM_WS = 19, RAG_GEMM_WS_MFMA_ONLY = 20,
        RAG_GEMM_WS_NO_STORE = 21, RAG_GEMM_WS_DMA_ONLY = 22, RAG_GEMM_WS_L2_STORE = 23,
-       RAG_GEMM_WS_NT = 24, RAG_GEMM_WS_NOROT = 26 };
+       RAG_GEMM_WS_NT = 24, RAG_GEMM_WS_NOROT = 26, RAG_GEMM_WS_READS_FIRST = 27 };
 int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, const void* W,
                   const void* W_lo, const float* bias, int M, int N, int K, void* C,
                   void* C_lo, void* stream);
