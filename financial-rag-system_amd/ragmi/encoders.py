@@ -260,14 +260,45 @@ class BertEncoder:
 
 # ------------------------------------------------------------------ tokenisation
 class WordPiece:
-    """BERT uncased WordPiece from a local vocab.txt ([CLS] a [SEP] (b [SEP]); truncation
-    'longest_first' to max_length; token types 0/1)."""
+    """BERT WordPiece from a local vocab.txt ([CLS] a [SEP] (b [SEP]); truncation
+    'longest_first' to max_length; token types 0/1) — what sentence-transformers' tokenizer
+    does for both reference models (transformers BertTokenizer: BertNormalizer(clean_text,
+    handle_chinese_chars, strip_accents, lowercase) + BertPreTokenizer + WordPiece('##',
+    100-char words)). The normaliser flags come from the checkpoint's tokenizer_config.json
+    (`from_model_dir`; bge-small-en-v1.5 and ms-marco-MiniLM-L-6-v2: do_lower_case true,
+    strip_accents unset = follow lowercasing, tokenize_chinese_chars true). Parity: tests/
+    test_tokenizer_cpu.py, against transformers.BertTokenizer and a pure-Python restatement
+    (oracle/wordpiece_ref.py)."""
 
-    def __init__(self, vocab_file: str, max_length: int = 512, lowercase: bool = True):
+    def __init__(self, vocab_file: str, max_length: int = 512, lowercase: bool = True,
+                 strip_accents: bool | None = None, tokenize_chinese_chars: bool = True):
         from tokenizers import BertWordPieceTokenizer
-        self.tok = BertWordPieceTokenizer(vocab_file, lowercase=lowercase)
+        self.tok = BertWordPieceTokenizer(vocab_file, lowercase=lowercase,
+                                          strip_accents=strip_accents,
+                                          handle_chinese_chars=tokenize_chinese_chars,
+                                          clean_text=True, wordpieces_prefix="##")
         self.tok.enable_truncation(max_length=max_length, strategy="longest_first")
         self.max_length = max_length
+
+    @classmethod
+    def from_model_dir(cls, model_dir: str, max_length: int | None = None) -> "WordPiece":
+        """vocab.txt + tokenizer_config.json (+ sentence_bert_config.json's max_seq_length)
+        of a local checkpoint; max_length: explicit > sentence_bert_config > model_max_length
+        > 512."""
+        def _json(name):
+            f = os.path.join(model_dir, name)
+            if not os.path.exists(f):
+                return {}
+            with open(f) as fh:
+                return json.load(fh)
+        tc, sb = _json("tokenizer_config.json"), _json("sentence_bert_config.json")
+        if max_length is None:
+            max_length = sb.get("max_seq_length") or tc.get("model_max_length") or 512
+            max_length = min(int(max_length), 512)
+        return cls(os.path.join(model_dir, "vocab.txt"), int(max_length),
+                   lowercase=bool(tc.get("do_lower_case", True)),
+                   strip_accents=tc.get("strip_accents"),
+                   tokenize_chinese_chars=bool(tc.get("tokenize_chinese_chars", True)))
 
     def encode_packed(self, texts, pairs=None):
         encs = (self.tok.encode_batch(list(texts)) if pairs is None else
@@ -292,14 +323,16 @@ class SentenceTransformer:
     """`SentenceTransformer(model_dir).encode(...)` for bge-small-en-v1.5 (CLS + L2 norm)."""
 
     def __init__(self, model_dir: str | None = None, device=None, *, cfg=None, weights=None,
-                 vocab_file=None, max_seq_length: int = 512, precision: str = "fp16x3"):
+                 vocab_file=None, max_seq_length: int | None = None, precision: str = "fp16x3"):
         if model_dir is not None:
             cfg, weights, vocab_file = _load_dir(model_dir)
         if cfg is None or weights is None:
             raise ValueError("need a local model_dir or cfg + weights (no hub access)")
         self.encoder = BertEncoder(cfg, weights, HEAD_CLS_L2, device, precision)
-        self.tokenizer = WordPiece(vocab_file, max_seq_length) if vocab_file else None
-        self.max_seq_length = max_seq_length
+        self.tokenizer = (WordPiece.from_model_dir(model_dir, max_seq_length) if model_dir
+                          else WordPiece(vocab_file, max_seq_length or 512) if vocab_file
+                          else None)
+        self.max_seq_length = self.tokenizer.max_length if self.tokenizer else max_seq_length
 
     def encode(self, sentences, batch_size: int = 32, convert_to_numpy: bool = True,
                show_progress_bar=None, **kwargs):
@@ -328,13 +361,14 @@ class CrossEncoder:
     (identity activation, num_labels = 1)."""
 
     def __init__(self, model_dir: str | None = None, device=None, *, cfg=None, weights=None,
-                 vocab_file=None, max_length: int = 512, precision: str = "fp16x3"):
+                 vocab_file=None, max_length: int | None = None, precision: str = "fp16x3"):
         if model_dir is not None:
             cfg, weights, vocab_file = _load_dir(model_dir)
         if cfg is None or weights is None:
             raise ValueError("need a local model_dir or cfg + weights (no hub access)")
         self.encoder = BertEncoder(cfg, weights, HEAD_POOLER_CLS, device, precision)
-        self.tokenizer = WordPiece(vocab_file, max_length) if vocab_file else None
+        self.tokenizer = (WordPiece.from_model_dir(model_dir, max_length) if model_dir
+                          else WordPiece(vocab_file, max_length or 512) if vocab_file else None)
 
     def predict(self, sentences, batch_size: int = 32, convert_to_numpy: bool = True, **kwargs):
         pairs = [list(p) for p in sentences]
