@@ -163,7 +163,7 @@ def verify_exact(idx, q, gpu_s, gpu_ids, lo, rank, world, dev):
     Returns (per-query recall@5, per-query exact-match flags) on rank 0, else None."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_scan as O
-    enc = idx.export_rows()
+    enc = idx.export_rows32() if idx.storage == "fp32" else idx.export_rows()
     qn = O.normalize(q)
     own = (gpu_ids >= lo) & (gpu_ids < lo + enc.shape[0])
     e_gpu = O.rescore(enc, qn, np.where(own, gpu_ids - lo, -1))
@@ -206,6 +206,10 @@ def main():
     ap.add_argument("--scan-order", choices=["auto", "serial", "free", "stream"], default="auto",
                     help="serial: each batch's scan waits for the previous batch's scan "
                          "(rag_index_set_scan_order); free: scans on different streams overlap")
+    ap.add_argument("--storage", choices=["fp16", "fp32"], default="fp16",
+                    help="vector storage (rag_index_create_ex): fp16 (the metric's fp16 corpus) "
+                         "or fp32 (Qdrant's default Float32 datatype: exact scores on the fp32 "
+                         "rows, the scan on their fp16 copy)")
     ap.add_argument("--config", choices=["4", "2", "3", "5", "filtered"], default="4",
                     help="4 (default): the headline 10M x 384 line (BASELINE configs[3] at N "
                          "GPUs); 2 / 3: encode + search (+ rerank) pipeline over 1M x 384; "
@@ -237,7 +241,7 @@ def main():
     from ragmi.dist import ShardedIndex
 
     n_total = args.rows
-    sh = ShardedIndex(n_total, dim=D, device=dev)
+    sh = ShardedIndex(n_total, dim=D, device=dev, storage=args.storage)
     idx, lo, hi = sh.local, sh.lo, sh.hi
     build_shard(idx, lo, hi, n_total, dev)
     nb = args.warmup + args.steps
@@ -383,7 +387,7 @@ def main():
                                    (" + RCCL all-gather merge" if world > 1 else ""),
                        "corpus_rows": n_total, "dim": D, "batch": B, "k": K_TOP,
                        "rows_per_gpu": local_rows, "parallelism": f"corpus-shard{world}",
-                       "batches_in_flight": n_streams,
+                       "batches_in_flight": n_streams, "storage": args.storage,
                        "scan_order": args.scan_order if args.scan_order == "stream" else
                                      "serial" if serial else "free"},
             "recall_at_5": check and check["recall_at_5"],

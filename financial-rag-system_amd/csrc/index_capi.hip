@@ -5,6 +5,7 @@
 // on the host; every entry point either enqueues on the caller's stream or (for *_host)
 // stages through device memory and synchronises.
 #include <hip/hip_runtime.h>
+#include <cmath>
 #include <cstdlib>
 
 #include <algorithm>
@@ -65,6 +66,11 @@ struct rag_index {
   int64_t count = 0;
   half8* corpus = nullptr;
   uint32_t* tags = nullptr;
+  // storage (rag_index_create_ex): RAG_STORE_FP16 keeps only the scan's fp16 tile16 rows;
+  // RAG_STORE_FP32 also the normalised fp32 rows (row-major [cap][dim]), which the exact
+  // rescoring reads — Qdrant's default Float32 datatype
+  int storage = RAG_STORE_FP16;
+  float* rows32 = nullptr;
   int max_wgs = 0;        // scan workgroups at full occupancy
   int groups = 1;         // query groups of 32 per search pass
   std::mutex mu;
@@ -120,8 +126,16 @@ int ensure_stage(rag_index* h, size_t bytes) {
 template <int D>
 void launch_upsert(rag_index* h, const float* v, const int64_t* rows, const uint32_t* tags,
                    int64_t n, hipStream_t st) {
-  ragmi::upsert_kernel<D><<<dim3((unsigned)n), dim3(64), 0, st>>>(v, rows, tags, h->corpus,
-                                                                  h->tags, n, h->cap_rows);
+  ragmi::upsert_kernel<D><<<dim3((unsigned)n), dim3(64), 0, st>>>(
+      v, rows, tags, h->corpus, h->tags, n, h->cap_rows, h->rows32);
+}
+
+// qprep's extra error-bound term for fp32 storage (scan_kernels.hip qprep_kernel): the exact
+// score reads the fp32 row c32, the scan its fp16 rounding c: |sum (c - c32) qn| <=
+// ||c - c32|| ||qn|| <= (2^-11 ||c32|| + 2^-25 sqrt(D)) (1 + 2^-20), ||c32|| <= 1 + 2^-20
+double store_eps(const rag_index* h) {
+  if (h->storage != RAG_STORE_FP32) return 0.0;
+  return (0x1p-11 * (1.0 + 0x1p-20) + 0x1p-25 * std::sqrt((double)h->dim)) * (1.0 + 0x1p-20);
 }
 
 // sample + thresh: seed thresholds for the scan (see sample_kernel). ~0.8% of the shard's
@@ -156,7 +170,7 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
   // Bq <= 32 * h->groups queries: `groups` query groups of 32 (one for D <= 384)
   const int groups = (Bq + kQ - 1) / kQ;
   qprep_kernel<D><<<dim3(groups * kQ), dim3(64), 0, st>>>(q, Bq, filt, w.qn, w.qfrag, w.filt,
-                                                          w.eps);
+                                                          w.eps, store_eps(h));
   if (filt)
     launch_seed<D, true>(h, w, groups, st);
   else
@@ -248,7 +262,7 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
   select_kernel<D, F><<<dim3(Bq), dim3(256), 0, st>>>(                                         \
       w.part_s, w.part_i, w.heads_s, w.heads_i, w.heads_n, n_lists, h->corpus, h->tags,      \
       w.filt, w.qfrag, (int)h->count, w.qn, k, w.eps, w.seed, fb, id_offset, out_s, out_i,   \
-      out_packed)
+      out_packed, h->rows32)
   if (filt)
     RAG_SELECT(true);
   else
@@ -263,6 +277,13 @@ void launch_import(rag_index* h, const half8* in, int64_t row0, int64_t n, hipSt
   const int64_t total = n * (D / 8);
   ragmi::import_kernel<D><<<dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st>>>(
       in, row0, n, h->corpus);
+}
+
+template <int D>
+void launch_import32(rag_index* h, const float* in, int64_t row0, int64_t n, hipStream_t st) {
+  const int64_t total = n * (D / 8);
+  ragmi::import32_kernel<D><<<dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st>>>(
+      in, row0, n, h->corpus, h->rows32);
 }
 
 template <int D>
@@ -370,7 +391,7 @@ int bench_scan(rag_index* h, const float* q, int B, int variant, int reps, doubl
   Workspace& w = h->ws[0];
   RAG_HIP(hipDeviceSynchronize());
   qprep_kernel<D><<<dim3(kQ), dim3(64), 0, nullptr>>>(q, std::min(B, kQ), nullptr, w.qn,
-                                                      w.qfrag, w.filt, w.eps);
+                                                      w.qfrag, w.filt, w.eps, store_eps(h));
   launch_seed<D, false>(h, w, 1, nullptr);
   // variant 7: the production kernel with every seed threshold at +inf, i.e. the top-k's
   // per-tile compares and branches with no candidate ever taken (its fixed cost)
@@ -461,7 +482,7 @@ int bench_wide(rag_index* h, const float* q, int B, int mode, int reps, double* 
   if (groups < 2) return ragmi::fail(RAG_EINVAL, "wide scan variants need 33..128 queries");
   RAG_HIP(hipDeviceSynchronize());
   qprep_kernel<D><<<dim3(groups * kQ), dim3(64), 0, nullptr>>>(
-      q, std::min(B, groups * kQ), nullptr, w.qn, w.qfrag, w.filt, w.eps);
+      q, std::min(B, groups * kQ), nullptr, w.qn, w.qfrag, w.filt, w.eps, store_eps(h));
   launch_seed<D, false>(h, w, groups, nullptr);
   const int64_t n_tiles = (h->count + 15) / 16;
   const int grid = (int)std::min<int64_t>(h->max_wgs / 2, std::max<int64_t>(1, n_tiles));
@@ -504,10 +525,17 @@ const char* rag_last_error(void) { return ragmi::last_error().c_str(); }
 const char* rag_version(void) { return "ragmi 0.1.0 (gfx950)"; }
 
 int rag_index_create(int dim, int64_t capacity_rows, int device, rag_index_t** out) {
+  return rag_index_create_ex(dim, capacity_rows, device, RAG_STORE_FP16, out);
+}
+
+int rag_index_create_ex(int dim, int64_t capacity_rows, int device, int storage,
+                        rag_index_t** out) {
   ragmi::clear_error();
   if (!out) return ragmi::fail(RAG_EINVAL, "out is NULL");
   *out = nullptr;
   if (dim != 384 && dim != 1024) return ragmi::fail(RAG_EINVAL, "dim must be 384 or 1024");
+  if (storage != RAG_STORE_FP16 && storage != RAG_STORE_FP32)
+    return ragmi::fail(RAG_EINVAL, "storage must be RAG_STORE_FP16 or RAG_STORE_FP32");
   if (capacity_rows < 0 || capacity_rows > (int64_t(1) << 31) - 16)
     return ragmi::fail(RAG_ERANGE, "capacity_rows out of range [0, 2^31-16]");
   RAG_HIP(hipSetDevice(device));
@@ -515,10 +543,19 @@ int rag_index_create(int dim, int64_t capacity_rows, int device, rag_index_t** o
   h->dim = dim;
   h->device = device;
   h->cap_rows = round16(std::max<int64_t>(capacity_rows, 16));
+  h->storage = storage;
   int rc = alloc_corpus(h, h->cap_rows, &h->corpus, &h->tags);
   if (rc) {
     delete h;
     return rc;
+  }
+  if (storage == RAG_STORE_FP32) {
+    const size_t b32 = (size_t)h->cap_rows * dim * 4;
+    if (hipMalloc(reinterpret_cast<void**>(&h->rows32), b32) != hipSuccess ||
+        hipMemset(h->rows32, 0, b32) != hipSuccess) {
+      rag_index_destroy(h);
+      return ragmi::fail(RAG_ENOMEM, "hipMalloc(rows32) failed");
+    }
   }
   int n_cu = 0;
   if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) !=
@@ -600,6 +637,7 @@ int rag_index_destroy(rag_index_t* h) {
   if (h->scan_stream) (void)hipStreamDestroy(h->scan_stream);
   if (h->corpus) (void)hipFree(h->corpus);
   if (h->tags) (void)hipFree(h->tags);
+  if (h->rows32) (void)hipFree(h->rows32);
   if (h->stage) (void)hipFree(h->stage);
   delete h;
   return RAG_OK;
@@ -618,13 +656,27 @@ int rag_index_reserve(rag_index_t* h, int64_t capacity_rows) {
   uint32_t* nt = nullptr;
   int rc = alloc_corpus(h, cap, &nc, &nt);
   if (rc) return rc;
+  float* n32 = nullptr;
+  if (h->rows32) {
+    const size_t b32 = (size_t)cap * h->dim * 4;
+    if (hipMalloc(reinterpret_cast<void**>(&n32), b32) != hipSuccess) {
+      (void)hipFree(nc);
+      (void)hipFree(nt);
+      return ragmi::fail(RAG_ENOMEM, "hipMalloc(rows32) failed");
+    }
+    RAG_HIP(hipMemset(n32, 0, b32));
+  }
   RAG_HIP(hipDeviceSynchronize());
   RAG_HIP(hipMemcpy(nc, h->corpus, (size_t)h->cap_rows * h->dim * 2, hipMemcpyDeviceToDevice));
   RAG_HIP(hipMemcpy(nt, h->tags, (size_t)h->cap_rows * 4, hipMemcpyDeviceToDevice));
+  if (n32)
+    RAG_HIP(hipMemcpy(n32, h->rows32, (size_t)h->cap_rows * h->dim * 4, hipMemcpyDeviceToDevice));
   (void)hipFree(h->corpus);
   (void)hipFree(h->tags);
+  if (h->rows32) (void)hipFree(h->rows32);
   h->corpus = nc;
   h->tags = nt;
+  h->rows32 = n32;
   h->cap_rows = cap;
   return RAG_OK;
 }
@@ -744,6 +796,8 @@ int rag_index_import_rows(rag_index_t* h, int64_t row0, int64_t n, const uint16_
   ragmi::clear_error();
   if (!h || (n > 0 && !rows) || row0 < 0 || n < 0 || row0 + n > h->cap_rows)
     return ragmi::fail(RAG_EINVAL, "bad import range (reserve capacity first)");
+  if (h->rows32)
+    return ragmi::fail(RAG_EINVAL, "fp32-storage index: load its fp32 rows (rag_index_import_rows32)");
   if (new_count < 0 || new_count > h->cap_rows)
     return ragmi::fail(RAG_ERANGE, "new_count exceeds capacity");
   std::lock_guard<std::mutex> lk(h->mu);
@@ -755,6 +809,49 @@ int rag_index_import_rows(rag_index_t* h, int64_t row0, int64_t n, const uint16_
     RAG_HIP(hipDeviceSynchronize());
     RAG_HIP(hipMemcpy(h->stage, rows, bytes, hipMemcpyHostToDevice));
     RAG_DISPATCH_DIM(h->dim, launch_import, h, static_cast<const half8*>(h->stage), row0, n,
+                     nullptr);
+    RAG_HIP(hipGetLastError());
+    if (tags)
+      RAG_HIP(hipMemcpy(h->tags + row0, tags, (size_t)n * 4, hipMemcpyHostToDevice));
+    RAG_HIP(hipDeviceSynchronize());
+  }
+  h->count = new_count;
+  return RAG_OK;
+}
+
+int rag_index_storage(const rag_index_t* h) { return h ? h->storage : -1; }
+
+int rag_index_export_rows32(rag_index_t* h, int64_t row0, int64_t n, float* out) {
+  ragmi::clear_error();
+  if (!h || !out || row0 < 0 || n < 0 || row0 + n > h->cap_rows)
+    return ragmi::fail(RAG_EINVAL, "bad export range");
+  if (!h->rows32) return ragmi::fail(RAG_EINVAL, "index has fp16 storage (no fp32 rows)");
+  if (n == 0) return RAG_OK;
+  std::lock_guard<std::mutex> lk(h->mu);
+  RAG_HIP(hipSetDevice(h->device));
+  RAG_HIP(hipDeviceSynchronize());
+  RAG_HIP(hipMemcpy(out, h->rows32 + row0 * h->dim, (size_t)n * h->dim * 4,
+                    hipMemcpyDeviceToHost));
+  return RAG_OK;
+}
+
+int rag_index_import_rows32(rag_index_t* h, int64_t row0, int64_t n, const float* rows,
+                            const uint32_t* tags, int64_t new_count) {
+  ragmi::clear_error();
+  if (!h || (n > 0 && !rows) || row0 < 0 || n < 0 || row0 + n > h->cap_rows)
+    return ragmi::fail(RAG_EINVAL, "bad import range (reserve capacity first)");
+  if (!h->rows32) return ragmi::fail(RAG_EINVAL, "index has fp16 storage (no fp32 rows)");
+  if (new_count < 0 || new_count > h->cap_rows)
+    return ragmi::fail(RAG_ERANGE, "new_count exceeds capacity");
+  std::lock_guard<std::mutex> lk(h->mu);
+  RAG_HIP(hipSetDevice(h->device));
+  if (n > 0) {
+    const size_t bytes = (size_t)n * h->dim * 4;
+    int rc = ensure_stage(h, bytes);
+    if (rc) return rc;
+    RAG_HIP(hipDeviceSynchronize());
+    RAG_HIP(hipMemcpy(h->stage, rows, bytes, hipMemcpyHostToDevice));
+    RAG_DISPATCH_DIM(h->dim, launch_import32, h, static_cast<const float*>(h->stage), row0, n,
                      nullptr);
     RAG_HIP(hipGetLastError());
     if (tags)

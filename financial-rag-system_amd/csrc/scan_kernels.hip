@@ -38,7 +38,8 @@ __global__ __launch_bounds__(64) void upsert_kernel(const float* __restrict__ ve
                                                     const uint32_t* __restrict__ tags_in,
                                                     half8* __restrict__ corpus,
                                                     uint32_t* __restrict__ tags, int64_t n,
-                                                    int64_t cap_rows) {
+                                                    int64_t cap_rows,
+                                                    float* __restrict__ rows32 = nullptr) {
   const int64_t i = blockIdx.x;
   if (i >= n) return;
   const int lane = threadIdx.x;
@@ -50,10 +51,19 @@ __global__ __launch_bounds__(64) void upsert_kernel(const float* __restrict__ ve
   const int r = (int)(row & 15);
   for (int c = lane; c < D / 8; c += 64) {
     half8 h;
+    float y[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) h[j] = f32_to_f16(canon_scale(x[8 * c + j], norm));
+    for (int j = 0; j < 8; ++j) {
+      y[j] = canon_scale(x[8 * c + j], norm);
+      h[j] = f32_to_f16(y[j]);
+    }
     const int s = c >> 2, hh = c & 3;
     corpus[t * (steps<D>() * 64) + s * 64 + hh * 16 + r] = h;
+    if (rows32) {   // fp32 storage: the normalised fp32 row itself (exact rescoring operand)
+      float4* o = reinterpret_cast<float4*>(rows32 + row * D + 8 * c);
+      o[0] = float4{y[0], y[1], y[2], y[3]};
+      o[1] = float4{y[4], y[5], y[6], y[7]};
+    }
   }
   if (lane == 0) tags[row] = tags_in ? tags_in[i] : 0u;
 }
@@ -73,6 +83,10 @@ __global__ __launch_bounds__(64) void upsert_kernel(const float* __restrict__ ve
 //            + D 2^-23 ||c|| ||h||          (<= D roundings of the fp32 accumulator, each
 //                                            <= 1 ulp: holds for any internal MFMA order)
 //            + 2^-23                        (e's own fp32 rounding)
+//            [+ store_eps]                  (fp32 storage: the exact score reads the fp32 row
+//                                            c32 while the scan reads c = fp16(c32):
+//                                            |sum (c - c32) qn| <= ||c - c32|| ||qn|| <=
+//                                            2^-11 ||c32|| + 2^-25 sqrt(D), times ||qn||)
 // inflated by 2^-10 relative + 2^-22 absolute so the fp32 comparisons that use it in select
 // stay conservative.
 // ----------------------------------------------------------------------------------------
@@ -84,7 +98,8 @@ __global__ __launch_bounds__(64) void qprep_kernel(const float* __restrict__ q, 
                                                    float* __restrict__ qn,
                                                    half8* __restrict__ qfrag,
                                                    uint32_t* __restrict__ filt,
-                                                   float* __restrict__ eps) {
+                                                   float* __restrict__ eps,
+                                                   double store_eps = 0.0) {
   const int b = blockIdx.x;
   const int lane = threadIdx.x;
   const bool live = b < B;
@@ -117,7 +132,8 @@ __global__ __launch_bounds__(64) void qprep_kernel(const float* __restrict__ q, 
     hh2 += __shfl_xor(hh2, d, 64);
   }
   if (lane == 0) {
-    double e = kRowNorm * sqrt(dq2) + (double)D * 0x1p-23 * kRowNorm * sqrt(hh2) + 0x1p-23;
+    double e = kRowNorm * sqrt(dq2) + (double)D * 0x1p-23 * kRowNorm * sqrt(hh2) + 0x1p-23 +
+               store_eps;
     e = e * (1.0 + 0x1p-10) + 0x1p-22;
     eps[b] = live ? (float)(e * (1.0 + 0x1p-20)) : 0.0f;   // rounded up past fp32's RNE
   }
@@ -1573,17 +1589,30 @@ __device__ __forceinline__ void exact_scores_pairs(const half8* __restrict__ cor
                                                    const int (&rows)[NC],
                                                    const int (&qoff)[NC],
                                                    const float* __restrict__ qn, int lane,
-                                                   float (&out)[NC]) {
+                                                   float (&out)[NC],
+                                                   const float* __restrict__ rows32) {
   constexpr int S = steps<D>();
   double acc[NC];
 #pragma unroll
   for (int i = 0; i < NC; ++i) acc[i] = 0.0;
   for (int c = lane; c < D / 8; c += 64) {
-    half8 h[NC];
+    // stored row elements as fp32: fp16 storage widens the tile16 halves (exact), fp32
+    // storage reads the fp32 row (rows32 != nullptr, wave-uniform)
+    float h[NC][8];
 #pragma unroll
     for (int i = 0; i < NC; ++i) {
       const int row = rows[i] < 0 ? 0 : rows[i];
-      h[i] = corpus[(int64_t)(row >> 4) * (S * 64) + (c >> 2) * 64 + (c & 3) * 16 + (row & 15)];
+      if (rows32) {
+        const float4* p = reinterpret_cast<const float4*>(rows32 + (int64_t)row * D + 8 * c);
+        const float4 u = p[0], v = p[1];
+        h[i][0] = u.x; h[i][1] = u.y; h[i][2] = u.z; h[i][3] = u.w;
+        h[i][4] = v.x; h[i][5] = v.y; h[i][6] = v.z; h[i][7] = v.w;
+      } else {
+        const half8 x =
+            corpus[(int64_t)(row >> 4) * (S * 64) + (c >> 2) * 64 + (c & 3) * 16 + (row & 15)];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) h[i][j] = (float)x[j];
+      }
     }
 #pragma unroll
     for (int i = 0; i < NC; ++i) {
@@ -1617,11 +1646,12 @@ template <int D, int NC>
 __device__ __forceinline__ void exact_scores_wave(const half8* __restrict__ corpus,
                                                   const int (&rows)[NC],
                                                   const float* __restrict__ qq, int lane,
-                                                  float (&out)[NC]) {
+                                                  float (&out)[NC],
+                                                  const float* __restrict__ rows32) {
   int qoff[NC];
 #pragma unroll
   for (int i = 0; i < NC; ++i) qoff[i] = 0;
-  exact_scores_pairs<D, NC>(corpus, rows, qoff, qq, lane, out);
+  exact_scores_pairs<D, NC>(corpus, rows, qoff, qq, lane, out, rows32);
 }
 
 // ----------------------------------------------------------------------------------------
@@ -1680,7 +1710,8 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
                                                      ExactStats fb, int64_t id_offset,
                                                      float* __restrict__ out_s,
                                                      int64_t* __restrict__ out_i,
-                                                     int32_t* __restrict__ out_packed) {
+                                                     int32_t* __restrict__ out_packed,
+                                                     const float* __restrict__ rows32) {
   __shared__ float w_s[4][32];
   __shared__ int64_t w_i[4][32];
   __shared__ int sel[32];
@@ -1902,7 +1933,7 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
       const int c = wid * 8 + j;
       rows[j] = c_s[0][c] != kNegInf ? c_i[0][c] : -1;
     }
-    exact_scores_wave<D, 8>(corpus, rows, qq, lane, es);
+    exact_scores_wave<D, 8>(corpus, rows, qq, lane, es, rows32);
     if (lane == 0) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -2014,7 +2045,7 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
           if (m) m &= m - 1;
           rows[j] = ln >= 0 ? t * kTileRows + ln : -1;
         }
-        exact_scores_wave<D, 8>(corpus, rows, qq, lane, es);
+        exact_scores_wave<D, 8>(corpus, rows, qq, lane, es, rows32);
         float ns = kNegInf;
         int ni = kIdNone32;
 #pragma unroll
@@ -2062,7 +2093,7 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
         const int r = __shfl(id, min(c0 + j, 63), 64);
         rows[j] = c0 + j < m ? r : -1;
       }
-      exact_scores_wave<D, 8>(corpus, rows, qq, lane, es);
+      exact_scores_wave<D, 8>(corpus, rows, qq, lane, es, rows32);
       float ns = kNegInf;
       int ni = kIdNone32;
 #pragma unroll
@@ -2179,6 +2210,27 @@ __global__ void import_kernel(const half8* __restrict__ in, int64_t row0, int64_
   const int c = (int)(idx % (D / 8));
   const int64_t row = row0 + i;
   corpus[(row >> 4) * (steps<D>() * 64) + (c >> 2) * 64 + (c & 3) * 16 + (row & 15)] = in[idx];
+}
+
+// import, fp32 storage: row-major fp32 rows (already normalised) -> rows32 unchanged and the
+// scan's fp16 tile16 copy by the same RNE conversion as upsert (f32_to_f16), so a reloaded
+// index is bit-identical to the one that was saved
+template <int D>
+__global__ void import32_kernel(const float* __restrict__ in, int64_t row0, int64_t n,
+                                half8* __restrict__ corpus, float* __restrict__ rows32) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n * (D / 8)) return;
+  const int64_t i = idx / (D / 8);
+  const int c = (int)(idx % (D / 8));
+  const int64_t row = row0 + i;
+  const float* src = in + i * D + 8 * c;
+  half8 h;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    rows32[row * D + 8 * c + j] = src[j];
+    h[j] = f32_to_f16(src[j]);
+  }
+  corpus[(row >> 4) * (steps<D>() * 64) + (c >> 2) * 64 + (c & 3) * 16 + (row & 15)] = h;
 }
 
 }  // namespace ragmi

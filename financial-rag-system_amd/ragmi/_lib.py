@@ -44,6 +44,12 @@ INDEX_API = {
     "rag_version": (ctypes.c_char_p, []),
     "rag_index_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, ctypes.c_int,
                                         ctypes.POINTER(c_vp)]),
+    "rag_index_create_ex": (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, ctypes.c_int,
+                                           ctypes.c_int, ctypes.POINTER(c_vp)]),
+    "rag_index_storage": (ctypes.c_int, [c_vp]),
+    "rag_index_export_rows32": (ctypes.c_int, [c_vp, ctypes.c_int64, ctypes.c_int64, c_f32p]),
+    "rag_index_import_rows32": (ctypes.c_int, [c_vp, ctypes.c_int64, ctypes.c_int64, c_f32p,
+                                               c_u32p, ctypes.c_int64]),
     "rag_index_destroy": (ctypes.c_int, [c_vp]),
     "rag_index_reserve": (ctypes.c_int, [c_vp, ctypes.c_int64]),
     "rag_index_capacity": (ctypes.c_int64, [c_vp]),

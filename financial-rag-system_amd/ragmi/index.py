@@ -19,6 +19,7 @@ from ._lib import check
 
 MAX_K = 32          # RAG_MAX_K in include/ragmi.h
 QUERY_TILE = 32     # RAG_QUERY_TILE
+STORAGE = {"fp16": 0, "fp32": 1}   # RAG_STORE_FP16 / RAG_STORE_FP32
 
 
 def _stream_ptr(device: torch.device) -> int:
@@ -35,9 +36,11 @@ def _as_dev(x, dtype, device) -> torch.Tensor:
 
 
 class FlatIndex:
-    """In-HBM fp16 flat index with exact (score desc, row asc) top-k search."""
+    """In-HBM flat index with exact (score desc, row asc) top-k search. storage "fp16": the
+    fp16 rows only (what the scan streams); "fp32": the normalised fp32 rows too, which the
+    exact scores read (Qdrant's default Float32 vectors; rag_index_create_ex)."""
 
-    def __init__(self, dim: int = 384, capacity: int = 0, device=None):
+    def __init__(self, dim: int = 384, capacity: int = 0, device=None, storage: str = "fp16"):
         _lib.require_gpu()
         self._L = _lib.load()
         if device is None:
@@ -48,9 +51,12 @@ class FlatIndex:
         self.device = torch.device("cuda", device.index if device.index is not None
                                    else torch.cuda.current_device())
         self.dim = int(dim)
+        if storage not in STORAGE:
+            raise ValueError(f"storage must be one of {sorted(STORAGE)}")
+        self.storage = storage
         h = ctypes.c_void_p()
-        check(self._L.rag_index_create(self.dim, int(capacity), self.device.index,
-                                       ctypes.byref(h)))
+        check(self._L.rag_index_create_ex(self.dim, int(capacity), self.device.index,
+                                          STORAGE[storage], ctypes.byref(h)))
         self._h = h
 
     # ---------------------------------------------------------------- lifetime
@@ -188,6 +194,36 @@ class FlatIndex:
         torch.cuda.current_stream(self.device).synchronize()
         check(self._L.rag_index_import_rows(
             self._h, int(row0), int(n), a.ctypes.data_as(_lib.c_u16p),
+            t.ctypes.data_as(_lib.c_u32p) if t is not None else None, int(new_count)))
+
+    def export_rows32(self, row0: int = 0, n: int | None = None) -> np.ndarray:
+        """fp32 storage: the stored normalised fp32 rows [n, dim]."""
+        if n is None:
+            n = self.count - row0
+        out = np.empty((n, self.dim), dtype=np.float32)
+        torch.cuda.current_stream(self.device).synchronize()
+        check(self._L.rag_index_export_rows32(self._h, int(row0), int(n),
+                                              out.ctypes.data_as(_lib.c_f32p)))
+        return out
+
+    def import_rows32(self, rows_f32, row0: int = 0, tags=None,
+                      new_count: int | None = None) -> None:
+        """fp32 storage: write saved fp32 rows [n, dim] back unchanged (their fp16 scan copy
+        is re-derived by the same rounding as upsert)."""
+        a = np.ascontiguousarray(rows_f32, dtype=np.float32)
+        if a.ndim != 2 or a.shape[1] != self.dim:
+            raise ValueError(f"rows must be float32 [n, {self.dim}]")
+        n = a.shape[0]
+        t = None
+        if tags is not None:
+            t = np.ascontiguousarray(tags, dtype=np.uint32)
+            if t.shape != (n,):
+                raise ValueError("tags must be [n]")
+        if new_count is None:
+            new_count = max(self.count, row0 + n)
+        torch.cuda.current_stream(self.device).synchronize()
+        check(self._L.rag_index_import_rows32(
+            self._h, int(row0), int(n), a.ctypes.data_as(_lib.c_f32p),
             t.ctypes.data_as(_lib.c_u32p) if t is not None else None, int(new_count)))
 
     def export_tags(self, row0: int = 0, n: int | None = None) -> np.ndarray:

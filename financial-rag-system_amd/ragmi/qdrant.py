@@ -205,15 +205,28 @@ class Coalescer:
         return req.result
 
 
+def _storage_of(vectors_config) -> str:
+    """VectorParams.datatype -> FlatIndex storage. Qdrant stores Float32 unless told otherwise
+    (the reference never sets a datatype, database.py:124-130, ingest.py:89-95), so the
+    default is fp32 storage: exact scores on the fp32 rows, the scan on their fp16 copy."""
+    dt = getattr(vectors_config, "datatype", None)
+    dt = getattr(dt, "value", dt)
+    if dt is None or str(dt).lower() == "float32":
+        return "fp32"
+    if str(dt).lower() == "float16":
+        return "fp16"
+    raise NotImplementedError(f"vector datatype {dt!r} (float32 and float16 are supported)")
+
+
 class Collection:
     """One COSINE collection: FlatIndex in HBM + host-side id/payload maps."""
 
     def __init__(self, name: str, dim: int, device, tag_fields=DEFAULT_TAG_FIELDS,
-                 capacity: int = 1024):
+                 capacity: int = 1024, storage: str = "fp32"):
         self.name = name
         self.dim = dim
         self.tags = PayloadTags(tag_fields)
-        self.index = FlatIndex(dim=dim, capacity=capacity, device=device)
+        self.index = FlatIndex(dim=dim, capacity=capacity, device=device, storage=storage)
         self.id_to_row: dict[Any, int] = {}
         self.row_ids: list[Any] = []
         self.payloads: list[dict | None] = []
@@ -293,7 +306,8 @@ class Collection:
         payload = self.payloads[row] if with_payload else None
         vec = None
         if with_vectors:
-            vec = self.index.export_rows(row, 1)[0].view(np.float16).astype(np.float32).tolist()
+            vec = (self.index.export_rows32(row, 1)[0] if self.index.storage == "fp32" else
+                   self.index.export_rows(row, 1)[0].view(np.float16).astype(np.float32)).tolist()
         return models.ScoredPoint(id=self.row_ids[row], version=self.versions[row],
                                   score=score, payload=payload, vector=vec)
 
@@ -353,11 +367,12 @@ class QdrantClient:
                           capacity: int = 1024, **kwargs) -> bool:
         if vectors_config.distance != models.Distance.COSINE:
             raise NotImplementedError("only Distance.COSINE collections (database.py:126)")
+        storage = _storage_of(vectors_config)
         with self._lock:
             if collection_name in self._collections:
                 raise ValueError(f"collection {collection_name!r} already exists")
             col = Collection(collection_name, int(vectors_config.size), self.device,
-                             tuple(payload_tag_fields), capacity)
+                             tuple(payload_tag_fields), capacity, storage)
             col.coalescer.window = self.coalesce_window_s
             self._collections[collection_name] = col
         return True

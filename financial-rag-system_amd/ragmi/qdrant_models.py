@@ -23,11 +23,19 @@ class Distance(str, enum.Enum):
     MANHATTAN = "Manhattan"
 
 
+class Datatype(str, enum.Enum):
+    FLOAT32 = "float32"
+    FLOAT16 = "float16"
+    UINT8 = "uint8"
+
+
 @dataclass
 class VectorParams:
     size: int
     distance: Distance = Distance.COSINE
     on_disk: Optional[bool] = None
+    # None = Qdrant's default, Float32 (the reference sets none: database.py:124-130,
+    # ingest.py:89-95) -> fp32 storage; FLOAT16 -> fp16 storage (ragmi FlatIndex storage)
     datatype: Optional[str] = None
 
 

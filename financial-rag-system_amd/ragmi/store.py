@@ -4,8 +4,11 @@ at start-up).
 
 A shard directory holds exactly what the GPU index stores, so loading is a byte copy:
 
-  meta.json          {"format": "ragmi-shard", "version": 1, "dim": D, "count": N}
+  meta.json          {"format": "ragmi-shard", "version": 1, "dim": D, "count": N,
+                      "storage": "fp16" | "fp32"}  (no "storage": fp16)
   vectors.f16.npy    [N, D] float16 — the stored (normalised, fp16-rounded) rows, row-major
+  vectors.f32.npy    [N, D] float32 — instead, for fp32 storage: the normalised fp32 rows
+                     (their fp16 scan copy is re-derived on load by the same rounding)
   tags.u32.npy       [N] uint32     — per-row payload tags (PayloadTags codes)
 
 A collection directory adds the host-side state of `qdrant.Collection`:
@@ -38,30 +41,45 @@ def _write_json(path, obj):
     os.replace(tmp, path)
 
 
+def _vec_file(storage: str) -> tuple[str, type]:
+    return ("vectors.f32.npy", np.float32) if storage == "fp32" else ("vectors.f16.npy", np.float16)
+
+
+def _export(index, r0: int, m: int) -> np.ndarray:
+    return (index.export_rows32(r0, m) if getattr(index, "storage", "fp16") == "fp32"
+            else index.export_rows(r0, m).view(np.float16))
+
+
 def save_index(index, path: str, chunk_rows: int = CHUNK_ROWS) -> None:
     """Write FlatIndex `index` (rows [0, count)) to shard directory `path`."""
     os.makedirs(path, exist_ok=True)
     n, d = index.count, index.dim
+    storage = getattr(index, "storage", "fp16")
+    vname, vdt = _vec_file(storage)
     # meta.json marks a complete save: drop it before the arrays are rewritten in place, so a
     # crash mid-save leaves an incomplete directory (load refuses it), never a stale meta.json
     # over partially written rows
     meta = os.path.join(path, "meta.json")
     if os.path.exists(meta):
         os.remove(meta)
-    vec = np.lib.format.open_memmap(os.path.join(path, "vectors.f16.npy"), mode="w+",
-                                    dtype=np.float16, shape=(n, d))
+    for old in ("vectors.f16.npy", "vectors.f32.npy"):   # a re-save may change storage
+        if old != vname and os.path.exists(os.path.join(path, old)):
+            os.remove(os.path.join(path, old))
+    vec = np.lib.format.open_memmap(os.path.join(path, vname), mode="w+", dtype=vdt,
+                                    shape=(n, d))
     tags = np.lib.format.open_memmap(os.path.join(path, "tags.u32.npy"), mode="w+",
                                      dtype=np.uint32, shape=(n,))
     for r0 in range(0, n, chunk_rows):
         m = min(chunk_rows, n - r0)
-        vec[r0:r0 + m] = index.export_rows(r0, m).view(np.float16)
+        vec[r0:r0 + m] = _export(index, r0, m)
         tags[r0:r0 + m] = index.export_tags(r0, m)
     vec.flush()
     tags.flush()
     del vec, tags
     # meta last: a directory without meta.json is an incomplete save
     _write_json(os.path.join(path, "meta.json"),
-                {"format": FORMAT, "version": VERSION, "dim": d, "count": n})
+                {"format": FORMAT, "version": VERSION, "dim": d, "count": n,
+                 "storage": storage})
 
 
 def read_meta(path: str) -> dict:
@@ -79,7 +97,12 @@ def load_into(index, path: str, row0: int = 0, chunk_rows: int = CHUNK_ROWS,
     meta = read_meta(path)
     if meta["dim"] != index.dim:
         raise ValueError(f"shard dim {meta['dim']} != index dim {index.dim}")
-    vec = np.load(os.path.join(path, "vectors.f16.npy"), mmap_mode="r")
+    saved = meta.get("storage", "fp16")
+    into = getattr(index, "storage", "fp16")
+    if saved == "fp16" and into == "fp32":
+        raise ValueError(f"{path}: fp16 shard cannot fill an fp32-storage index (the fp32 "
+                         "rows were not saved)")
+    vec = np.load(os.path.join(path, _vec_file(saved)[0]), mmap_mode="r")
     tags = np.load(os.path.join(path, "tags.u32.npy"), mmap_mode="r")
     if vec.shape != (meta["count"], meta["dim"]) or tags.shape != (meta["count"],):
         raise ValueError(f"{path}: array shapes disagree with meta.json")
@@ -91,9 +114,13 @@ def load_into(index, path: str, row0: int = 0, chunk_rows: int = CHUNK_ROWS,
         index.reserve(row0 + n)
     for c0 in range(0, n, chunk_rows):
         m = min(chunk_rows, n - c0)
-        index.import_rows(np.asarray(vec[a + c0:a + c0 + m]), row0 + c0,
-                          np.asarray(tags[a + c0:a + c0 + m]),
-                          new_count=max(index.count, row0 + c0 + m))
+        v = np.asarray(vec[a + c0:a + c0 + m])
+        t = np.asarray(tags[a + c0:a + c0 + m])
+        nc = max(index.count, row0 + c0 + m)
+        if into == "fp32":
+            index.import_rows32(v, row0 + c0, t, new_count=nc)
+        else:   # an fp32 shard into an fp16 index: upsert's RNE rounding of the fp32 rows
+            index.import_rows(v.astype(np.float16), row0 + c0, t, new_count=nc)
     return n
 
 
@@ -102,7 +129,7 @@ def load_index(path: str, device=None, capacity: int | None = None):
     from .index import FlatIndex
     meta = read_meta(path)
     idx = FlatIndex(dim=meta["dim"], capacity=max(capacity or 0, meta["count"], 16),
-                    device=device)
+                    device=device, storage=meta.get("storage", "fp16"))
     try:
         load_into(idx, path)
     except BaseException:
@@ -119,12 +146,14 @@ def save_sharded(sharded, path: str, chunk_rows: int = CHUNK_ROWS) -> None:
     import torch.distributed as dist
     n, d = sharded.n_total, sharded.local.dim
     multi = sharded.world > 1
-    vp, tp = os.path.join(path, "vectors.f16.npy"), os.path.join(path, "tags.u32.npy")
+    storage = getattr(sharded.local, "storage", "fp16")
+    vname, vdt = _vec_file(storage)
+    vp, tp = os.path.join(path, vname), os.path.join(path, "tags.u32.npy")
     if sharded.rank == 0:
         os.makedirs(path, exist_ok=True)
         if os.path.exists(os.path.join(path, "meta.json")):
             os.remove(os.path.join(path, "meta.json"))
-        np.lib.format.open_memmap(vp, mode="w+", dtype=np.float16, shape=(n, d)).flush()
+        np.lib.format.open_memmap(vp, mode="w+", dtype=vdt, shape=(n, d)).flush()
         np.lib.format.open_memmap(tp, mode="w+", dtype=np.uint32, shape=(n,)).flush()
     if multi:
         dist.barrier(group=sharded.group)
@@ -134,7 +163,7 @@ def save_sharded(sharded, path: str, chunk_rows: int = CHUNK_ROWS) -> None:
     for c0 in range(0, have, chunk_rows):
         m = min(chunk_rows, have - c0)
         g = sharded.lo + c0
-        vec[g:g + m] = sharded.local.export_rows(c0, m).view(np.float16)
+        vec[g:g + m] = _export(sharded.local, c0, m)
         tags[g:g + m] = sharded.local.export_tags(c0, m)
     vec.flush()
     tags.flush()
@@ -143,7 +172,8 @@ def save_sharded(sharded, path: str, chunk_rows: int = CHUNK_ROWS) -> None:
         dist.barrier(group=sharded.group)
     if sharded.rank == 0:
         _write_json(os.path.join(path, "meta.json"),
-                    {"format": FORMAT, "version": VERSION, "dim": d, "count": n})
+                    {"format": FORMAT, "version": VERSION, "dim": d, "count": n,
+                     "storage": storage})
     if multi:
         dist.barrier(group=sharded.group)
 
@@ -170,6 +200,7 @@ def save_collection(col, path: str) -> None:
         os.replace(tmp, os.path.join(path, "points.jsonl"))
         _write_json(os.path.join(path, "collection.json"), {
             "name": col.name, "dim": col.dim, "distance": "Cosine", "op": col.op,
+            "storage": col.index.storage,
             "tag_fields": list(col.tags.fields),
             "codebooks": [[[v, c] for v, c in t.items()] for t in col.tags.codes]})
 
@@ -181,7 +212,8 @@ def load_collection(path: str, device=None):
         cj = json.load(f)
     meta = read_meta(os.path.join(path, "shard"))
     col = Collection(cj["name"], int(cj["dim"]), device, tuple(cj["tag_fields"]),
-                     capacity=max(meta["count"], 1024))
+                     capacity=max(meta["count"], 1024),
+                     storage=cj.get("storage", meta.get("storage", "fp16")))
     for f_i, book in enumerate(cj["codebooks"]):
         col.tags.codes[f_i] = {v: int(c) for v, c in book}
     with open(os.path.join(path, "points.jsonl")) as f:

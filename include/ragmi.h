@@ -78,6 +78,20 @@ const char* rag_version(void);
  * Replaces QdrantClient.create_collection(vectors_config=VectorParams(size, COSINE)),
  * ingest.py:86-96. */
 int rag_index_create(int dim, int64_t capacity_rows, int device, rag_index_t** out);
+
+/* Vector storage of an index. RAG_STORE_FP16: the normalised rows rounded to fp16 (RNE) —
+ * the scan's operand, 2 B per element; scores are exact on the fp16 rows. RAG_STORE_FP32
+ * (Qdrant's default Float32 datatype: VectorParams without `datatype`, database.py:124-130,
+ * ingest.py:89-95): the normalised fp32 rows are kept as well (4 B more per element) and the
+ * exact scores read them — score(row) = fp32(sum_k fp64(y_k) fp64(q_k)) over the fp32 row y,
+ * ranking identical to an fp32 store — while the scan still streams the fp16 copy (the
+ * certified select's error bound grows by ||fp16(y) - y|| <= 2^-11 ||y||). */
+enum { RAG_STORE_FP16 = 0, RAG_STORE_FP32 = 1 };
+/* rag_index_create with an explicit storage (rag_index_create = RAG_STORE_FP16). */
+int rag_index_create_ex(int dim, int64_t capacity_rows, int device, int storage,
+                        rag_index_t** out);
+/* RAG_STORE_FP16 / RAG_STORE_FP32 of an index (-1 for NULL). */
+int rag_index_storage(const rag_index_t* index);
 int rag_index_destroy(rag_index_t* index);
 
 /* Grow capacity (keeps contents). */
@@ -125,6 +139,12 @@ int rag_index_export_rows(rag_index_t* index, int64_t row0, int64_t n, uint16_t*
  * likewise; `new_count` = valid rows afterwards. Synchronous. */
 int rag_index_import_rows(rag_index_t* index, int64_t row0, int64_t n, const uint16_t* rows_host,
                           const uint32_t* tags_host, int64_t new_count);
+/* fp32 storage: copy the stored fp32 rows [row0, row0+n) out ([n][dim] float, host), and
+ * load saved fp32 rows back (their fp16 scan copy is re-derived by the same RNE rounding, so
+ * a reloaded index is bit-identical). rag_index_import_rows is refused on fp32 storage. */
+int rag_index_export_rows32(rag_index_t* index, int64_t row0, int64_t n, float* out_host);
+int rag_index_import_rows32(rag_index_t* index, int64_t row0, int64_t n, const float* rows_host,
+                            const uint32_t* tags_host, int64_t new_count);
 /* Copy stored tags of rows [row0, row0+n) to host. */
 int rag_index_export_tags(rag_index_t* index, int64_t row0, int64_t n, uint32_t* out_host);
 

@@ -49,6 +49,12 @@ def lib():
                                  f32p, i64p]
         L.orc_rescore.argtypes = [u16p, ctypes.c_int, f32p, ctypes.c_int, i64p, ctypes.c_int,
                                   f32p]
+        L.orc_encode_rows32.argtypes = [f32p, ctypes.c_int64, ctypes.c_int, f32p]
+        L.orc_search32.argtypes = [f32p, u32p, ctypes.c_int64, ctypes.c_int, f32p, ctypes.c_int,
+                                   ctypes.c_int, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32,
+                                   f32p, i64p]
+        L.orc_rescore32.argtypes = [f32p, ctypes.c_int, f32p, ctypes.c_int, i64p, ctypes.c_int,
+                                    f32p]
         L.orc_f32_to_f16.restype = ctypes.c_uint16
         L.orc_f32_to_f16.argtypes = [ctypes.c_float]
         _lib = L
@@ -68,6 +74,21 @@ def encode_rows(x: np.ndarray) -> np.ndarray:
     return out
 
 
+def encode_rows32(x: np.ndarray) -> np.ndarray:
+    """fp32 storage: the canonical normalised fp32 rows [n, D] (Qdrant's Float32 vectors)."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    n, d = x.shape
+    out = np.empty((n, d), dtype=np.float32)
+    lib().orc_encode_rows32(_p(x, ctypes.c_float), n, d, _p(out, ctypes.c_float))
+    return out
+
+
+def _rows_f32(corpus: np.ndarray, r0: int, n: int) -> np.ndarray:
+    """Rows [r0, r0+n) of a stored corpus as fp32: fp16 bits (uint16) or fp32 storage."""
+    c = corpus[r0:r0 + n]
+    return c.view(np.float16).astype(np.float32) if c.dtype == np.uint16 else c
+
+
 def normalize(x: np.ndarray) -> np.ndarray:
     """Canonical fp32 normalisation of each row of x [n, D]."""
     x = np.ascontiguousarray(x, dtype=np.float32)
@@ -80,7 +101,10 @@ def normalize(x: np.ndarray) -> np.ndarray:
 
 def search(corpus16: np.ndarray, queries: np.ndarray, k: int, tags: np.ndarray | None = None,
            mask: int = 0, value: int = 0, use_filter: bool = False):
-    """Exact top-k by (score desc, row asc). corpus16: uint16 fp16 bits [N, D]."""
+    """Exact top-k by (score desc, row asc). corpus16: uint16 fp16 bits [N, D] (fp16 storage)
+    or float32 [N, D] (fp32 storage, encode_rows32)."""
+    if corpus16.dtype == np.float32:
+        return _search32(corpus16, queries, k, tags, mask, value, use_filter)
     corpus16 = np.ascontiguousarray(corpus16, dtype=np.uint16)
     queries = np.ascontiguousarray(queries, dtype=np.float32)
     n, d = corpus16.shape
@@ -96,7 +120,32 @@ def search(corpus16: np.ndarray, queries: np.ndarray, k: int, tags: np.ndarray |
     return out_s, out_i
 
 
+def _search32(corpus32, queries, k, tags, mask, value, use_filter):
+    corpus32 = np.ascontiguousarray(corpus32, dtype=np.float32)
+    queries = np.ascontiguousarray(queries, dtype=np.float32)
+    n, d = corpus32.shape
+    b = queries.shape[0]
+    if tags is None:
+        tags = np.zeros(max(n, 1), dtype=np.uint32)
+    tags = np.ascontiguousarray(tags, dtype=np.uint32)
+    out_s = np.empty((b, k), dtype=np.float32)
+    out_i = np.empty((b, k), dtype=np.int64)
+    lib().orc_search32(_p(corpus32, ctypes.c_float), _p(tags, ctypes.c_uint32), n, d,
+                       _p(queries, ctypes.c_float), b, k, int(use_filter), mask, value,
+                       _p(out_s, ctypes.c_float), _p(out_i, ctypes.c_int64))
+    return out_s, out_i
+
+
 def rescore(corpus16: np.ndarray, qn: np.ndarray, cand: np.ndarray) -> np.ndarray:
+    if corpus16.dtype == np.float32:
+        c32 = np.ascontiguousarray(corpus16)
+        qn = np.ascontiguousarray(qn, dtype=np.float32)
+        cand = np.ascontiguousarray(cand, dtype=np.int64)
+        b, m = cand.shape
+        sc = np.empty((b, m), dtype=np.float32)
+        lib().orc_rescore32(_p(c32, ctypes.c_float), c32.shape[1], _p(qn, ctypes.c_float), b,
+                            _p(cand, ctypes.c_int64), m, _p(sc, ctypes.c_float))
+        return sc
     corpus16 = np.ascontiguousarray(corpus16, dtype=np.uint16)
     qn = np.ascontiguousarray(qn, dtype=np.float32)
     cand = np.ascontiguousarray(cand, dtype=np.int64)
@@ -108,7 +157,7 @@ def rescore(corpus16: np.ndarray, qn: np.ndarray, cand: np.ndarray) -> np.ndarra
 
 
 def _blas_scores(corpus16, qn, r0, chunk, tags, mask, value, use_filter):
-    c = corpus16[r0:r0 + chunk].view(np.float16).astype(np.float32)
+    c = _rows_f32(corpus16, r0, chunk)
     s = qn @ c.T  # [b, chunk]
     if use_filter:
         t = tags[r0:r0 + chunk]
@@ -195,7 +244,7 @@ def candidates_above(corpus16: np.ndarray, qn: np.ndarray, floor: np.ndarray,
     thr = (np.asarray(floor, np.float32) - blas_delta(d))[:, None]
     hits = [[] for _ in range(b)]
     for r0 in range(0, n, chunk):
-        c = corpus16[r0:r0 + chunk].view(np.float16).astype(np.float32)
+        c = _rows_f32(corpus16, r0, chunk)
         s = qn @ c.T
         qq, rr = np.nonzero(s >= thr)
         for q in np.unique(qq):

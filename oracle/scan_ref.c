@@ -22,8 +22,10 @@
  *             fp64 fma in order; xor-butterfly d = 32..1 (v[i] += v[i^d]); take v[0].
  *   norm    : sqrt(sumsq) (fp64, correctly rounded)
  *   y_k     : fp32(fp64(x_k) / norm), 0 if norm == 0
- *   stored  : fp16_rne(y_k)
- *   score   : fp32( canonical fp64 sum of fp64(c16_k) * fp64(qn_k) ): 64 lane partials
+ *   stored  : fp16_rne(y_k)            (fp16 storage; fp32 storage keeps y_k itself:
+ *                                        Qdrant's default Float32 vectors, database.py:124-130)
+ *   score   : fp32( canonical fp64 sum of fp64(c_k) * fp64(qn_k) ), c = the stored row (fp16
+ *             or fp32): 64 lane partials
  *             (chunks of 8, fp64 fma in order) + xor-butterfly, exactly as for sumsq
  *   order   : score desc, row asc; rows with (tag & mask) != value are excluded when filtering.
  */
@@ -122,16 +124,23 @@ ORC_API void orc_encode_rows(const float* x, int64_t n, int D, uint16_t* out16) 
   free(y);
 }
 
+/* fp32 storage: the canonical normalised fp32 rows [n][D]. */
+ORC_API void orc_encode_rows32(const float* x, int64_t n, int D, float* out32) {
+  for (int64_t i = 0; i < n; ++i) orc_normalize(x + i * D, D, out32 + i * D, NULL);
+}
+
 /* Canonical exact score: 64 lane partials (lane l: chunks c = l, l+64, ... of 8 elements,
  * fp64 fma in order), xor-butterfly d = 32..1, v[0] rounded to fp32 — the order of the HIP
- * select kernel's exact_score_wave. */
-ORC_API float orc_exact_score(const uint16_t* c16, const float* qn, int D) {
+ * select kernel's exact_score_wave. Row = fp16 bits (c16) or, when c16 is NULL, fp32 (c32). */
+static float exact_score_any(const uint16_t* c16, const float* c32, const float* qn, int D) {
   double v[64];
   for (int l = 0; l < 64; ++l) {
     double acc = 0.0;
     for (int c = l; c < D / 8; c += 64)
-      for (int j = 0; j < 8; ++j)
-        acc = fma((double)orc_f16_to_f32(c16[8 * c + j]), (double)qn[8 * c + j], acc);
+      for (int j = 0; j < 8; ++j) {
+        const double r = c16 ? (double)orc_f16_to_f32(c16[8 * c + j]) : (double)c32[8 * c + j];
+        acc = fma(r, (double)qn[8 * c + j], acc);
+      }
     v[l] = acc;
   }
   for (int d = 32; d > 0; d >>= 1) {
@@ -142,15 +151,25 @@ ORC_API float orc_exact_score(const uint16_t* c16, const float* qn, int D) {
   return (float)v[0];
 }
 
+ORC_API float orc_exact_score(const uint16_t* c16, const float* qn, int D) {
+  return exact_score_any(c16, NULL, qn, D);
+}
+
+ORC_API float orc_exact_score32(const float* c32, const float* qn, int D) {
+  return exact_score_any(NULL, c32, qn, D);
+}
+
 static int better(float as, int64_t ai, float bs, int64_t bi) {
   return (as > bs) || (as == bs && ai < bi);
 }
 
-/* Exact top-k over a row-major fp16 corpus. queries [B][D] fp32 (raw, normalised here).
- * out_s [B][k], out_i [B][k] (-1 / -inf when fewer than k rows qualify). */
-ORC_API void orc_search(const uint16_t* corpus16, const uint32_t* tags, int64_t n_rows, int D,
-                        const float* queries, int B, int k, int use_filter, uint32_t mask,
-                        uint32_t value, float* out_s, int64_t* out_i) {
+/* Exact top-k over a row-major fp16 (corpus16) or, when corpus16 is NULL, fp32 (corpus32)
+ * corpus. queries [B][D] fp32 (raw, normalised here). out_s [B][k], out_i [B][k] (-1 / -inf
+ * when fewer than k rows qualify). */
+static void search_any(const uint16_t* corpus16, const float* corpus32, const uint32_t* tags,
+                       int64_t n_rows, int D, const float* queries, int B, int k,
+                       int use_filter, uint32_t mask, uint32_t value, float* out_s,
+                       int64_t* out_i) {
   float* qn = (float*)malloc(sizeof(float) * (size_t)D);
   float* bs = (float*)malloc(sizeof(float) * (size_t)k);
   int64_t* bi = (int64_t*)malloc(sizeof(int64_t) * (size_t)k);
@@ -162,7 +181,8 @@ ORC_API void orc_search(const uint16_t* corpus16, const uint32_t* tags, int64_t 
     }
     for (int64_t r = 0; r < n_rows; ++r) {
       if (use_filter && (tags[r] & mask) != value) continue;
-      const float s = orc_exact_score(corpus16 + r * D, qn, D);
+      const float s = exact_score_any(corpus16 ? corpus16 + r * D : NULL,
+                                      corpus16 ? NULL : corpus32 + r * D, qn, D);
       if (bi[k - 1] >= 0 && !better(s, r, bs[k - 1], bi[k - 1])) continue;
       int p = k - 1;
       while (p > 0 && (bi[p - 1] < 0 || better(s, r, bs[p - 1], bi[p - 1]))) {
@@ -183,14 +203,41 @@ ORC_API void orc_search(const uint16_t* corpus16, const uint32_t* tags, int64_t 
   free(bi);
 }
 
+ORC_API void orc_search(const uint16_t* corpus16, const uint32_t* tags, int64_t n_rows, int D,
+                        const float* queries, int B, int k, int use_filter, uint32_t mask,
+                        uint32_t value, float* out_s, int64_t* out_i) {
+  search_any(corpus16, NULL, tags, n_rows, D, queries, B, k, use_filter, mask, value, out_s,
+             out_i);
+}
+
+ORC_API void orc_search32(const float* corpus32, const uint32_t* tags, int64_t n_rows, int D,
+                          const float* queries, int B, int k, int use_filter, uint32_t mask,
+                          uint32_t value, float* out_s, int64_t* out_i) {
+  search_any(NULL, corpus32, tags, n_rows, D, queries, B, k, use_filter, mask, value, out_s,
+             out_i);
+}
+
 /* Exact rescoring of given candidate rows (used by the fast numpy oracle):
- * cand [B][m] row ids (-1 = none) -> sc [B][m]. qn is already normalised [B][D]. */
-ORC_API void orc_rescore(const uint16_t* corpus16, int D, const float* qn, int B,
-                         const int64_t* cand, int m, float* sc) {
+ * cand [B][m] row ids (-1 = none) -> sc [B][m]. qn is already normalised [B][D].
+ * corpus16 NULL: fp32 rows corpus32. */
+static void rescore_any(const uint16_t* corpus16, const float* corpus32, int D, const float* qn,
+                        int B, const int64_t* cand, int m, float* sc) {
   for (int b = 0; b < B; ++b)
     for (int j = 0; j < m; ++j) {
       const int64_t r = cand[(int64_t)b * m + j];
       sc[(int64_t)b * m + j] =
-          r < 0 ? -INFINITY : orc_exact_score(corpus16 + r * D, qn + (int64_t)b * D, D);
+          r < 0 ? -INFINITY
+                : exact_score_any(corpus16 ? corpus16 + r * D : NULL,
+                                  corpus16 ? NULL : corpus32 + r * D, qn + (int64_t)b * D, D);
     }
+}
+
+ORC_API void orc_rescore(const uint16_t* corpus16, int D, const float* qn, int B,
+                         const int64_t* cand, int m, float* sc) {
+  rescore_any(corpus16, NULL, D, qn, B, cand, m, sc);
+}
+
+ORC_API void orc_rescore32(const float* corpus32, int D, const float* qn, int B,
+                           const int64_t* cand, int m, float* sc) {
+  rescore_any(NULL, corpus32, D, qn, B, cand, m, sc);
 }

@@ -81,7 +81,10 @@ def test_end_to_end_retrieval_and_rerank(rag):
     assert q.count(rag.COLLECTION_NAME).count == n
 
     col = q._col(rag.COLLECTION_NAME)
-    enc16, tags = col.index.export_rows(), col.index.export_tags()
+    # the collection stores fp32 rows (Qdrant's default Float32 datatype; ensure_collection
+    # sets none, ingest.py:89-95): the oracle searches the stored fp32 rows
+    assert col.index.storage == "fp32"
+    enc16, tags = col.index.export_rows32(), col.index.export_tags()
     query = "what was apple iphone revenue growth in fiscal quarter"
     vec = rag.embed_query(query)
     assert len(vec) == 384 and abs(np.linalg.norm(vec) - 1) < 1e-5

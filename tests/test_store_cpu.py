@@ -75,7 +75,8 @@ def test_save_load_roundtrip_chunked(tmp_path):
     src = _filled(1000, 384, 0)
     store.save_index(src, str(tmp_path / "s"), chunk_rows=97)
     meta = json.loads((tmp_path / "s" / "meta.json").read_text())
-    assert meta == {"format": "ragmi-shard", "version": 1, "dim": 384, "count": 1000}
+    assert meta == {"format": "ragmi-shard", "version": 1, "dim": 384, "count": 1000,
+                    "storage": "fp16"}
     v = np.load(tmp_path / "s" / "vectors.f16.npy")
     assert v.dtype == np.float16 and v.shape == (1000, 384)
     dst = HostIndex(384)
@@ -184,3 +185,59 @@ def test_save_drops_stale_meta_before_rewriting(tmp_path):
     assert not os.path.exists(os.path.join(d, "meta.json"))
     with pytest.raises(FileNotFoundError):
         store.read_meta(d)
+
+
+class HostIndex32(HostIndex):
+    """fp32-storage stand-in: fp32 rows kept, the fp16 copy derived by RNE rounding."""
+    storage = "fp32"
+
+    def __init__(self, dim, capacity=16):
+        super().__init__(dim, capacity)
+        self.rows32 = np.zeros((capacity, dim), np.float32)
+
+    def reserve(self, cap):
+        old = self.capacity
+        super().reserve(cap)
+        if self.rows32.shape[0] < self.capacity:
+            r = np.zeros((self.capacity, self.dim), np.float32)
+            r[:old] = self.rows32[:old]
+            self.rows32 = r
+
+    def export_rows32(self, row0=0, n=None):
+        n = self.count - row0 if n is None else n
+        return self.rows32[row0:row0 + n].copy()
+
+    def import_rows32(self, a, row0=0, tags=None, new_count=None):
+        a = np.asarray(a, np.float32)
+        self.rows32[row0:row0 + len(a)] = a
+        self.import_rows(a.astype(np.float16), row0, tags, new_count)
+
+
+def test_fp32_storage_roundtrip_and_downcast(tmp_path):
+    """fp32 storage saves vectors.f32.npy (meta storage fp32) and reloads bit for bit; the
+    same shard loads into an fp16 index as the RNE rounding of its rows; an fp16 shard is
+    refused by an fp32 index (its fp32 rows were never saved)."""
+    _paths()
+    from ragmi import store
+    rng = np.random.default_rng(4)
+    n, d = 700, 384
+    src = HostIndex32(d, 1024)
+    v = rng.standard_normal((n, d)).astype(np.float32)
+    v /= np.linalg.norm(v, axis=1, keepdims=True)
+    src.import_rows32(v, 0, rng.integers(0, 9, n).astype(np.uint32), new_count=n)
+    p = str(tmp_path / "s32")
+    store.save_index(src, p, chunk_rows=256)
+    assert store.read_meta(p)["storage"] == "fp32"
+    assert os.path.exists(os.path.join(p, "vectors.f32.npy"))
+    assert not os.path.exists(os.path.join(p, "vectors.f16.npy"))
+    dst = HostIndex32(d)
+    assert store.load_into(dst, p, chunk_rows=300) == n
+    assert np.array_equal(dst.rows32[:n], v) and np.array_equal(dst.rows[:n], src.rows[:n])
+    assert np.array_equal(dst.tags[:n], src.tags[:n])
+    d16 = HostIndex(d)
+    store.load_into(d16, p)
+    assert np.array_equal(d16.rows[:n], v.astype(np.float16).view(np.uint16))
+    p16 = str(tmp_path / "s16")
+    store.save_index(d16, p16)
+    with pytest.raises(ValueError, match="fp16 shard"):
+        store.load_into(HostIndex32(d), p16)
