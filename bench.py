@@ -163,7 +163,7 @@ def verify_exact(idx, q, gpu_s, gpu_ids, lo, rank, world, dev):
     Returns (per-query recall@5, per-query exact-match flags) on rank 0, else None."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_scan as O
-    enc = idx.export_rows32() if idx.storage == "fp32" else idx.export_rows()
+    enc = idx.export_rows32() if getattr(idx, "storage", "fp16") == "fp32" else idx.export_rows()
     qn = O.normalize(q)
     own = (gpu_ids >= lo) & (gpu_ids < lo + enc.shape[0])
     e_gpu = O.rescore(enc, qn, np.where(own, gpu_ids - lo, -1))
