@@ -1243,7 +1243,8 @@ struct AttnState {
 // VAR (bit mask; rag_bert_attention A/Bs them): 1 = rolling Q prefetch, 2 = fp16x3 row sums
 // by MFMA (else v_dot2), 4 = software-pipelined scores (block kb+1's K.Q^T MFMAs issued
 // before block kb's softmax, so they run in the matrix pipe under its vector work), 8 = lean
-// block (round 2): the cross-lane max by v_permlane16/32_swap instead of two ds_bpermute
+// block (round 2): the block max by IEEE maximum (fmax_nc: no canonicalising v_max per MFMA
+// result), the cross-lane max by v_permlane16/32_swap instead of two ds_bpermute
 // round trips, P and O split by split16x2 (3 instead of 8 VALU per pair), and a block's V^T
 // fragments read in one batch before its P.V MFMAs (one LDS wait instead of DT). Bitwise the
 // same results as without it.
@@ -1360,8 +1361,12 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) 
       // folded into one FMA: p = 2^(s*c - m*c), c = scale*log2(e) > 0 (max commutes).
       float mx;
       if (k0 + kb + 32 <= len) {
-        mx = fmaxf(fmaxf(fmaxf(sc[0][0], sc[0][1]), fmaxf(sc[0][2], sc[0][3])),
-                   fmaxf(fmaxf(sc[1][0], sc[1][1]), fmaxf(sc[1][2], sc[1][3])));
+        if constexpr ((VAR & 8) != 0)   // IEEE maximum: no per-input canonicalisation
+          mx = fmax_nc(fmax_nc(fmax_nc(sc[0][0], sc[0][1]), fmax_nc(sc[0][2], sc[0][3])),
+                       fmax_nc(fmax_nc(sc[1][0], sc[1][1]), fmax_nc(sc[1][2], sc[1][3])));
+        else
+          mx = fmaxf(fmaxf(fmaxf(sc[0][0], sc[0][1]), fmaxf(sc[0][2], sc[0][3])),
+                     fmaxf(fmaxf(sc[1][0], sc[1][1]), fmaxf(sc[1][2], sc[1][3])));
       } else {
         mx = kNegInf;
 #pragma unroll
@@ -1369,19 +1374,19 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) 
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             if (k0 + kb + 16 * j + 4 * g + r >= len) sc[j][r] = kNegInf;
-            mx = fmaxf(mx, sc[j][r]);
+            mx = (VAR & 8) != 0 ? fmax_nc(mx, sc[j][r]) : fmaxf(mx, sc[j][r]);
           }
       }
       if constexpr ((VAR & 8) != 0) {
         // lanes l, l^16, l^32, l^48 hold the same query's other keys
         const uint32_t mu = __builtin_bit_cast(uint32_t, mx);
         const auto r16 = __builtin_amdgcn_permlane16_swap(mu, mu, false, false);
-        mx = fmaxf(__builtin_bit_cast(float, (uint32_t)r16[0]),
-                   __builtin_bit_cast(float, (uint32_t)r16[1]));
+        mx = fmax_nc(__builtin_bit_cast(float, (uint32_t)r16[0]),
+                     __builtin_bit_cast(float, (uint32_t)r16[1]));
         const uint32_t mu2 = __builtin_bit_cast(uint32_t, mx);
         const auto r32 = __builtin_amdgcn_permlane32_swap(mu2, mu2, false, false);
-        mx = fmaxf(__builtin_bit_cast(float, (uint32_t)r32[0]),
-                   __builtin_bit_cast(float, (uint32_t)r32[1]));
+        mx = fmax_nc(__builtin_bit_cast(float, (uint32_t)r32[0]),
+                     __builtin_bit_cast(float, (uint32_t)r32[1]));
       } else {
         mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
         mx = fmaxf(mx, __shfl_xor(mx, 32, 64));

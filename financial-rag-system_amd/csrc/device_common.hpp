@@ -186,6 +186,14 @@ __device__ __forceinline__ double canon_sumsq(const float* __restrict__ x, int l
 // fp32 -> fp16 RNE of an fp32 value. The empty asm makes `y` opaque: without it LLVM folds
 // (half)(float)(double) into one direct f64->f16 rounding, which differs from the canonical
 // double rounding (fp64 -> fp32 -> fp16) in ~1/8192 of the elements.
+// max of values that are never NaN (MFMA scores, exp2 outputs, -inf masks): IEEE-754
+// `maximum` lowers to v_maximum(3)_f32 on gfx950, where fmaxf's maxnum first canonicalises
+// every input that is not provably canonical (one v_max_f32 x, x per MFMA result: 11 VALU
+// for an 8-value max instead of 5). Equal to fmaxf for every non-NaN input.
+__device__ __forceinline__ float fmax_nc(float a, float b) {
+  return __builtin_elementwise_maximum(a, b);
+}
+
 __device__ __forceinline__ _Float16 f32_to_f16(float y) {
   asm volatile("" : "+v"(y));
   return (_Float16)y;

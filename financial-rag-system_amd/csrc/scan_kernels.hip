@@ -284,8 +284,8 @@ __device__ __forceinline__ void topk_tile(ScanTopK& st, const floatx4& acc0, con
     v0[r] = ok0 ? acc0[r] : kNegInf;
     v1[r] = ok1 ? acc1[r] : kNegInf;
   }
-  const float m0 = fmaxf(fmaxf(v0[0], v0[1]), fmaxf(v0[2], v0[3]));
-  const float m1 = fmaxf(fmaxf(v1[0], v1[1]), fmaxf(v1[2], v1[3]));
+  const float m0 = fmax_nc(fmax_nc(v0[0], v0[1]), fmax_nc(v0[2], v0[3]));
+  const float m1 = fmax_nc(fmax_nc(v1[0], v1[1]), fmax_nc(v1[2], v1[3]));
   if (__ballot((m0 > st.thr0) || (m1 > st.thr1))) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -688,8 +688,8 @@ __device__ __forceinline__ void rtopk_tile(RegTopK& st, const floatx4& acc0, con
     v0[r] = ok0 ? acc0[r] : kNegInf;
     v1[r] = ok1 ? acc1[r] : kNegInf;
   }
-  const float m0 = fmaxf(fmaxf(v0[0], v0[1]), fmaxf(v0[2], v0[3]));
-  const float m1 = fmaxf(fmaxf(v1[0], v1[1]), fmaxf(v1[2], v1[3]));
+  const float m0 = fmax_nc(fmax_nc(v0[0], v0[1]), fmax_nc(v0[2], v0[3]));
+  const float m1 = fmax_nc(fmax_nc(v1[0], v1[1]), fmax_nc(v1[2], v1[3]));
   if (__ballot((m0 > st.thr0) || (m1 > st.thr1))) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -992,7 +992,7 @@ __device__ __forceinline__ void wtopk_tile(WideTopK& st, const floatx4& acc, int
   float v[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) v[r] = (rbase + r) < n_rows ? acc[r] : kNegInf;
-  const float m = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+  const float m = fmax_nc(fmax_nc(v[0], v[1]), fmax_nc(v[2], v[3]));
   if (__ballot(m > st.thr)) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -1196,7 +1196,7 @@ __global__ __launch_bounds__(64 * kWideWaves, 1) void scan_wide_kernel(
       if constexpr (MODE == 0 || MODE == 3) {
         wtopk_tile(st, acc, b + j * nb, n_rows, lane);
       } else {
-        st.thr = fmaxf(st.thr, fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3])));
+        st.thr = fmax_nc(st.thr, fmax_nc(fmax_nc(acc[0], acc[1]), fmax_nc(acc[2], acc[3])));
       }
     }
   }
@@ -1362,8 +1362,8 @@ __device__ __forceinline__ void sample_epilogue(const floatx4 (&sc)[2][2], int t
         ok0 = ok0 && ((tr & fm0) == fv0);
         ok1 = ok1 && ((tr & fm1) == fv1);
       }
-      m0 = ok0 ? fmaxf(m0, acc0[r]) : m0;
-      m1 = ok1 ? fmaxf(m1, acc1[r]) : m1;
+      m0 = ok0 ? fmax_nc(m0, acc0[r]) : m0;
+      m1 = ok1 ? fmax_nc(m1, acc1[r]) : m1;
     }
     // lanes l, l^16, l^32, l^48 hold the same queries
     m0 = fmaxf(m0, __shfl_xor(m0, 16, 64));
