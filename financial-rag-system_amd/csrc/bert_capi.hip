@@ -346,11 +346,14 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
   if (variant == RAG_GEMM_WS || variant == RAG_GEMM_WS_MFMA_ONLY ||
       variant == RAG_GEMM_WS_NO_STORE || variant == RAG_GEMM_WS_DMA_ONLY ||
       variant == RAG_GEMM_WS_L2_STORE || variant == RAG_GEMM_WS_NT ||
-      variant == RAG_GEMM_WS_NOROT || variant == RAG_GEMM_WS_READS_FIRST) {
+      variant == RAG_GEMM_WS_NOROT || variant == RAG_GEMM_WS_READS_FIRST ||
+      variant == RAG_GEMM_WS_PROBE_NO_A_READS || variant == RAG_GEMM_WS_PROBE_NO_W_READS) {
+    // probes keep production's store policy (nt for fp16 outputs) since round 2's r02h runs
     auto go = [&](auto pc) {
       constexpr int P = decltype(pc)::value;
-      if (Al) launch_ws<EPI, true, PipeLarge, P>(A, Al, W, Wl, bias, M, N, K, C, Clo, st);
-      else launch_ws<EPI, false, PipeLarge, P>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st);
+      constexpr int AX = EPI == kEpiF32 ? 0 : 2;
+      if (Al) launch_ws<EPI, true, PipeLarge, P, AX>(A, Al, W, Wl, bias, M, N, K, C, Clo, st);
+      else launch_ws<EPI, false, PipeLarge, P, AX>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st);
     };
     if (variant == RAG_GEMM_WS) {
       // non-temporal stores for the fp16 outputs (QKV / FFN1: 117K x 1152 fp16x3 0.354 ->
@@ -364,6 +367,8 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
     else if (variant == RAG_GEMM_WS_NO_STORE) go(std::integral_constant<int, 6>{});
     else if (variant == RAG_GEMM_WS_L2_STORE) go(std::integral_constant<int, 9>{});
     else if (variant == RAG_GEMM_WS_DMA_ONLY) go(std::integral_constant<int, 8>{});
+    else if (variant == RAG_GEMM_WS_PROBE_NO_A_READS) go(std::integral_constant<int, 14>{});
+    else if (variant == RAG_GEMM_WS_PROBE_NO_W_READS) go(std::integral_constant<int, 15>{});
     else if (variant == RAG_GEMM_WS_READS_FIRST) {
       constexpr int AX = EPI == kEpiF32 ? 0 : 2;
       // the all-reads-first fragment order (PROBE 13) the WS kernel used before its interleaved one
@@ -693,7 +698,9 @@ int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, co
                      variant == RAG_GEMM_PROBE_NO_SYNC || variant == RAG_GEMM_PROBE_NO_STORE ||
                      variant == RAG_GEMM_PROBE_MFMA_ONLY || variant == RAG_GEMM_PROBE_DMA_ONLY ||
                      variant == RAG_GEMM_WS_MFMA_ONLY || variant == RAG_GEMM_WS_NO_STORE ||
-                     variant == RAG_GEMM_WS_DMA_ONLY || variant == RAG_GEMM_WS_L2_STORE;
+                     variant == RAG_GEMM_WS_DMA_ONLY || variant == RAG_GEMM_WS_L2_STORE ||
+                     variant == RAG_GEMM_WS_PROBE_NO_A_READS ||
+                     variant == RAG_GEMM_WS_PROBE_NO_W_READS;
   const bool known = variant == RAG_GEMM_AUTO || variant == RAG_GEMM_TILE ||
                      variant == RAG_GEMM_PIPE || variant == RAG_GEMM_SMALL ||
                      variant == RAG_GEMM_WIDE || variant == RAG_GEMM_SMALL_BK64 ||

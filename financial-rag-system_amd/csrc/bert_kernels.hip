@@ -1077,13 +1077,18 @@ __global__ __launch_bounds__(CFG::THREADS + 256, 1) void gemm_ws_kernel(
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
   int kt_c = 0, it_c = 0, slot_c = 0;
+  // (declared outside the step loop only so the PROBE 14 / 15 timing probes can keep stale
+  // fragments: every production step overwrites them all before use)
+  half8 af[KSN][NPL][FM], wf[KSN][NPL][FN];
   for (int g = 0; g < steps; ++g) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // done reading stage g-1
     __builtin_amdgcn_s_barrier();                        // stage g landed
     asm volatile("" ::: "memory");
     const half8* sa = lds + slot_c * STAGE_H8;
     const half8* sw = sa + NPL * A_H8;
-    half8 af[KSN][NPL][FM], wf[KSN][NPL][FN];
+    // timing probes (results meaningless): 14 = A fragments read from LDS only at the first
+    // step (the DMA still streams A), 15 = the same for W
+    const bool rd_a = PROBE != 14 || g == 0, rd_w = PROBE != 15 || g == 0;
     auto read_a = [&](int i) __attribute__((always_inline)) {
 #pragma unroll
       for (int ks = 0; ks < KSN; ++ks)
@@ -1117,17 +1122,18 @@ __global__ __launch_bounds__(CFG::THREADS + 256, 1) void gemm_ws_kernel(
       // (profiles/r02e_gemm_ilv.jsonl, same process, PROBE 13 = the previous all-reads-first
       // order): 117K-token layer fp16x3 1.274 -> 1.264 ms, fp16 0.586 -> 0.581, QKV -3 to -6%,
       // the others within +-1%.
-      read_a(0);
+      if (rd_a) read_a(0);
+      if (rd_w)
 #pragma unroll
-      for (int j = 0; j < FN; ++j)      // W_j's planes together: MFMA (0, j) needs 2 + 2j reads
+        for (int j = 0; j < FN; ++j)    // W_j's planes together: MFMA (0, j) needs 2 + 2j reads
 #pragma unroll
-        for (int ks = 0; ks < KSN; ++ks)
+          for (int ks = 0; ks < KSN; ++ks)
 #pragma unroll
-          for (int p = 0; p < NPL; ++p)
-            wf[ks][p][j] = sw[p * W_H8 + swz<CPR>(wc * WTN + j * 16 + (lane & 15), ks * 4 + (lane >> 4))];
+            for (int p = 0; p < NPL; ++p)
+              wf[ks][p][j] = sw[p * W_H8 + swz<CPR>(wc * WTN + j * 16 + (lane & 15), ks * 4 + (lane >> 4))];
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
-        if (i + 1 < FM) read_a(i + 1);
+        if (i + 1 < FM && rd_a) read_a(i + 1);
 #pragma unroll
         for (int ks = 0; ks < KSN; ++ks)
 #pragma unroll

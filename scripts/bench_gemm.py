@@ -24,7 +24,8 @@ VNAME = {0: "auto", 1: "tile", 2: "pipe", 3: "probe_no_mfma", 4: "probe_no_dma",
          13: "probe_no_store", 14: "probe_mfma_only", 15: "probe_dma_only",
          19: "ws", 20: "ws_mfma_only",
          21: "ws_no_store", 22: "ws_dma_only", 23: "ws_l2_store", 24: "ws_nt", 26: "ws_norot",
-         27: "ws_readsfirst"}
+         27: "ws_readsfirst",
+         28: "ws_probe_no_a_reads", 29: "ws_probe_no_w_reads"}
 LAYERS = {
     "small": [("qkv", 1152, 384, EPI_F16), ("o", 384, 384, EPI_F32),
               ("ffn1", 1536, 384, EPI_GELU_F16), ("ffn2", 384, 1536, EPI_F32)],
