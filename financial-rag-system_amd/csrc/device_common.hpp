@@ -135,6 +135,41 @@ __device__ __forceinline__ void bitonic_sort64(float& s, IdT& id, int lane) {
   bitonic_sort_from<2>(s, id, lane);
 }
 
+// Four independent 16-lane bitonic sorts (lanes 16b .. 16b+15 each end best-first): 10
+// compare-exchange stages against the 32-lane sort's 15.
+template <int K, typename IdT>
+__device__ __forceinline__ void bitonic_sort16_from(float& s, IdT& id, int lane) {
+  if constexpr (K <= 16) {
+    if constexpr (K == 16)
+      bitonic_steps<64, 8>(s, id, lane);    // final pass: every 16-lane block best-first
+    else
+      bitonic_steps<K, K / 2>(s, id, lane);
+    bitonic_sort16_from<K * 2>(s, id, lane);
+  }
+}
+
+template <typename IdT>
+__device__ __forceinline__ void bitonic_sort16x4(float& s, IdT& id, int lane) {
+  bitonic_sort16_from<2>(s, id, lane);
+}
+
+// Eight independent 8-lane bitonic sorts (6 stages).
+template <int K, typename IdT>
+__device__ __forceinline__ void bitonic_sort8_from(float& s, IdT& id, int lane) {
+  if constexpr (K <= 8) {
+    if constexpr (K == 8)
+      bitonic_steps<64, 4>(s, id, lane);
+    else
+      bitonic_steps<K, K / 2>(s, id, lane);
+    bitonic_sort8_from<K * 2>(s, id, lane);
+  }
+}
+
+template <typename IdT>
+__device__ __forceinline__ void bitonic_sort8x8(float& s, IdT& id, int lane) {
+  bitonic_sort8_from<2>(s, id, lane);
+}
+
 template <int K, typename IdT>
 __device__ __forceinline__ void bitonic_sort32_from(float& s, IdT& id, int lane) {
   if constexpr (K <= 32) {
@@ -183,9 +218,6 @@ __device__ __forceinline__ double canon_sumsq(const float* __restrict__ x, int l
   return __shfl(acc, 0, 64);
 }
 
-// fp32 -> fp16 RNE of an fp32 value. The empty asm makes `y` opaque: without it LLVM folds
-// (half)(float)(double) into one direct f64->f16 rounding, which differs from the canonical
-// double rounding (fp64 -> fp32 -> fp16) in ~1/8192 of the elements.
 // max of values that are never NaN (MFMA scores, exp2 outputs, -inf masks): IEEE-754
 // `maximum` lowers to v_maximum(3)_f32 on gfx950, where fmaxf's maxnum first canonicalises
 // every input that is not provably canonical (one v_max_f32 x, x per MFMA result: 11 VALU
@@ -194,6 +226,9 @@ __device__ __forceinline__ float fmax_nc(float a, float b) {
   return __builtin_elementwise_maximum(a, b);
 }
 
+// fp32 -> fp16 RNE of an fp32 value. The empty asm makes `y` opaque: without it LLVM folds
+// (half)(float)(double) into one direct f64->f16 rounding, which differs from the canonical
+// double rounding (fp64 -> fp32 -> fp16) in ~1/8192 of the elements.
 __device__ __forceinline__ _Float16 f32_to_f16(float y) {
   asm volatile("" : "+v"(y));
   return (_Float16)y;

@@ -374,8 +374,10 @@ void launch_variant(rag_index* h, Workspace& w, int grid, hipStream_t st) {
   // 0 prod (seeded) | 1 unseeded | 2 contiguous | 3 mfma-only | 4 loads-only | 5 no-nt
   // 6 no-sb | 9 / 10 / 11 dynamic tile queue, chunks of 2 / 1 / 4 tiles | 12 dynamic (2),
   // loads only | 13 / 14 static production / loads only (9-14: each launch timed on its own,
-  // the queue heads zeroed between launches outside the timed window)
-  constexpr int MODE = V == 3 ? 1 : (V == 4 || V == 12 || V == 14 ? 2 : 0);
+  // the queue heads zeroed between launches outside the timed window) | 15 production without
+  // the end-of-scan sort of pending-only queries (results invalid) | 16 production with the
+  // round-1 end-of-scan sort (two pending-only queries per 32-lane pass)
+  constexpr int MODE = V == 3 ? 1 : V == 4 || V == 12 || V == 14 ? 2 : V == 15 ? 3 : V == 16 ? 4 : 0;
   constexpr bool STRIDED = V != 2;
   constexpr bool NT = V != 5;
   constexpr bool SB = V != 6;
@@ -432,11 +434,13 @@ int bench_scan(rag_index* h, const float* q, int B, int variant, int reps, doubl
       case 4: launch_variant<D, 4>(h, w, grid, nullptr); break;
       case 5: launch_variant<D, 5>(h, w, grid, nullptr); break;
       case 7: launch_variant<D, 0>(h, w, grid, nullptr); break;
+      case 15: launch_variant<D, 15>(h, w, grid, nullptr); break;
+      case 16: launch_variant<D, 16>(h, w, grid, nullptr); break;
       default: launch_variant<D, 6>(h, w, grid, nullptr); break;
     }
   };
   float ms = 0.f;
-  if (variant >= 9) {
+  if (variant >= 9 && variant <= 14) {
     // one launch per event pair; the tile-queue heads are zeroed before each, outside it
     for (int r = -1; r < reps; ++r) {
       RAG_HIP(hipMemsetAsync(w.tileq, 0, 8 * kTileQStride * 4, nullptr));
@@ -901,7 +905,7 @@ int rag_merge_topk_packed(const int32_t* in_packed, int n_lists, int B, int k, f
 int rag_bench_scan(rag_index_t* h, const float* queries_dev, int B, int variant, int reps,
                    double* avg_ms) {
   ragmi::clear_error();
-  if (!h || !queries_dev || B < 1 || reps < 1 || !avg_ms || variant < 0 || variant > 14)
+  if (!h || !queries_dev || B < 1 || reps < 1 || !avg_ms || variant < 0 || variant > 16)
     return ragmi::fail(RAG_EINVAL, "bad bench args");
   std::lock_guard<std::mutex> lk(h->mu);
   RAG_HIP(hipSetDevice(h->device));

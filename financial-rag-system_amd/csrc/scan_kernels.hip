@@ -310,6 +310,12 @@ __device__ __forceinline__ void topk_tile(ScanTopK& st, const floatx4& acc0, con
 
 // End of scan: flush what is pending and write this wave's sorted list (finite entries), its
 // head and its length per query.
+// SORT: 2 = pending-only queries sorted eight per pass in 8-lane blocks when each of their
+// lanes holds <= 2 entries, else four per pass in 16-lane blocks (production: after a tile's
+// flush check no lane holds more than kP - 4 = 4 pending entries of a query, so slots 4..7 are
+// empty and a query has at most 16 entries), 1 = two per pass in 32-lane blocks (the round-1
+// path, A/B), 0 = not sorted (timing probe, results invalid)
+template <int SORT = 2>
 __device__ __forceinline__ void topk_finish(ScanTopK& st, int lane, int gw, int nw,
                                             float* __restrict__ part_s, int* __restrict__ part_i,
                                             float* __restrict__ heads_s,
@@ -333,7 +339,68 @@ __device__ __forceinline__ void topk_finish(ScanTopK& st, int lane, int gw, int 
       full &= full - 1;
       flush_query(w, q, lane, st.thr0, st.cnt0, st.thr1, st.cnt1);
     }
-    while (only) {
+    if (SORT == 0) only = 0;
+    if (SORT == 2) {
+      // queries whose four lanes hold <= 2 pending entries each (<= 8 in all): eight per pass
+      // in 8-lane blocks, slots 0..1 of lanes c + 16 g (the common case: ~2 entries per query
+      // and wave at the 8-GPU shard size); the rest take the 16-lane pass below
+      const uint64_t g0 = __ballot(st.cnt0 > 2), g1 = __ballot(st.cnt1 > 2);
+      const uint32_t big = (uint32_t)((g0 | (g0 >> 16) | (g0 >> 32) | (g0 >> 48)) & 0xffffu) |
+                           ((uint32_t)((g1 | (g1 >> 16) | (g1 >> 32) | (g1 >> 48)) & 0xffffu) << 16);
+      uint32_t small = only & ~big;
+      only &= big;
+      while (small) {
+        int qv[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          qv[t] = small ? __builtin_ctz(small) : -1;
+          if (small) small &= small - 1;
+        }
+        const int sub = lane >> 3, j = lane & 7;
+        int q = qv[0];
+#pragma unroll
+        for (int t = 1; t < 8; ++t) q = sub == t ? qv[t] : q;
+        float s = kNegInf;
+        int id = kIdNone32;
+        if (q >= 0) {
+          const int pidx = (((q >> 4) * kP + (j & 1)) * 64) + (q & 15) + 16 * (j >> 1);
+          s = w.pend_s[pidx];
+          id = w.pend_i[pidx];
+        }
+        lds_fence();
+        bitonic_sort8x8(s, id, lane);
+        if (q >= 0) {
+          w.keep_s[q * kKS + j] = s;
+          w.keep_i[q * kKS + j] = id;
+        }
+        lds_fence();
+      }
+    }
+    while (SORT == 2 && only) {
+      int qv[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        qv[t] = only ? __builtin_ctz(only) : -1;
+        if (only) only &= only - 1;
+      }
+      const int sub = lane >> 4, j = lane & 15;
+      const int q = sub == 0 ? qv[0] : sub == 1 ? qv[1] : sub == 2 ? qv[2] : qv[3];
+      float s = kNegInf;
+      int id = kIdNone32;
+      if (q >= 0) {
+        const int pidx = (((q >> 4) * kP + (j & 3)) * 64) + (q & 15) + 16 * (j >> 2);
+        s = w.pend_s[pidx];
+        id = w.pend_i[pidx];
+      }
+      lds_fence();
+      bitonic_sort16x4(s, id, lane);
+      if (q >= 0) {
+        w.keep_s[q * kKS + j] = s;
+        w.keep_i[q * kKS + j] = id;
+      }
+      lds_fence();
+    }
+    while (SORT == 1 && only) {
       const int qa = __builtin_ctz(only);
       only &= only - 1;
       const int qb = only ? __builtin_ctz(only) : -1;
@@ -393,7 +460,9 @@ __device__ __forceinline__ void tile_sequence(int gw, int nw, int n_tiles, int& 
 }
 
 // Variant knobs (A/B'd by rag_bench_scan; the production instance is scan_kernel<D, F>):
-//   MODE 0 full scan + top-k; 1 MFMA only (running max, no top-k); 2 loads only
+//   MODE 0 full scan + top-k; 1 MFMA only (running max, no top-k); 2 loads only; 3 full scan
+//        without the end-of-scan sort of pending-only queries (timing probe, results invalid);
+//        4 full scan with the round-1 end-of-scan sort (two queries per 32-lane pass, A/B)
 //   STRIDED tile order gw, gw+nw, ... (the chip sweeps one window) vs contiguous ranges
 //   NT non-temporal corpus loads (the corpus is read once per search; MI355X_MICROARCH
 //      'nt-weights': once-read streams)
@@ -451,7 +520,7 @@ __global__ __launch_bounds__(256, 2) void scan_kernel(
         acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[s], q0[s], acc0, 0, 0, 0);
         acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[s], q1[s], acc1, 0, 0, 0);
       }
-      if constexpr (MODE == 0)
+      if constexpr (MODE == 0 || MODE >= 3)
         topk_tile<FILTER>(st, acc0, acc1, t, n_rows, tags, lane);
       else
         vmax = fmaxf(vmax, fmaxf(fmaxf(fmaxf(acc0[0], acc0[1]), fmaxf(acc0[2], acc0[3])),
@@ -543,11 +612,12 @@ __global__ __launch_bounds__(256, 2) void scan_kernel(
       if (++j >= n_mine) break;
     }
   }
-  if constexpr (MODE != 0) {
+  if constexpr (MODE == 1 || MODE == 2) {
     if (vmax == 12345.0f) part_s[gw] = vmax;   // never true in practice; defeats DCE
     return;
   }
-  topk_finish(st, lane, gw, nw, part_s, part_i, heads_s, heads_i, heads_n);
+  topk_finish<MODE == 3 ? 0 : MODE == 4 ? 1 : 2>(st, lane, gw, nw, part_s, part_i, heads_s,
+                                                 heads_i, heads_n);
 }
 
 // ---- register-pending top-k (LDS-query scan): the pending candidates of a lane live in

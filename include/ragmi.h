@@ -193,7 +193,9 @@ int rag_profile_scan_ms(rag_index_t* index, double* total_ms, int64_t* launches)
  * with every seed at +inf (top-k compares only), 8 the VALU ablation: v_dot2_f32_f16 instead
  * of MFMA over a row-group-major copy of the corpus, same top-k; 9 / 10 / 11 the dynamic tile
  * queue with chunks of 2 / 1 / 4 tiles, 12 dynamic (2) loads only, 13 / 14 static production
- * / loads only (9-14 time every launch on its own event pair). dim 1024: variants 0-4 of
+ * / loads only (9-14 time every launch on its own event pair), 15 production without the
+ * end-of-scan sort of pending-only queries (timing probe), 16 production with the round-1
+ * end-of-scan sort (A/B). dim 1024: variants 0-4 of
  * the wide (33-128 query) scan. */
 int rag_bench_scan(rag_index_t* index, const float* queries_dev, int B, int variant, int reps,
                    double* avg_ms);

@@ -22,7 +22,9 @@ NAMES = {0: "prod (seeded, interleaved, nt, sched-barrier)", 1: "unseeded", 2: "
          10: "dynamic tile queue, chunks of 1 (timed per launch)",
          11: "dynamic tile queue, chunks of 4 (timed per launch)",
          12: "dynamic (2), loads only (timed per launch)",
-         13: "static prod (timed per launch)", 14: "static loads only (timed per launch)"}
+         13: "static prod (timed per launch)", 14: "static loads only (timed per launch)",
+         15: "prod without the end-of-scan pending sort (probe)",
+         16: "prod with the round-1 pending sort (32 lanes x 2 queries)"}
 
 
 def main():
