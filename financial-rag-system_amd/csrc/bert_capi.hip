@@ -22,6 +22,12 @@ struct Layer {
   _Float16 *wqkv_l = nullptr, *wo_l = nullptr, *w1_l = nullptr, *w2_l = nullptr;  // fp16x3
   float *bqkv = nullptr, *bo = nullptr, *g1 = nullptr, *be1 = nullptr, *bi1 = nullptr,
         *bi2 = nullptr, *g2 = nullptr, *be2 = nullptr;
+  // deferred LayerNorm (fp16x3, hidden 384; DlArgs in bert_kernels.hip): the consumers of a
+  // pending LN with its gamma folded into the weights — QKV (the previous layer's output LN;
+  // layers >= 1) and FFN1 (this layer's attention-output LN) — and per output column c1 (the
+  // folded planes' row sums) and c2 (bias + W beta)
+  _Float16 *wqkv_f = nullptr, *wqkv_fl = nullptr, *w1_f = nullptr, *w1_fl = nullptr;
+  float *qkv_c1 = nullptr, *qkv_c2 = nullptr, *w1_c1 = nullptr, *w1_c2 = nullptr;
 };
 
 __global__ void f32_to_f16_kernel(const float* __restrict__ in, _Float16* __restrict__ out,
@@ -33,6 +39,17 @@ __global__ void f32_to_f16_kernel(const float* __restrict__ in, _Float16* __rest
     out[i] = h;
     if (out_lo) out_lo[i] = l;
   }
+}
+
+// c1[n] = sum_k (hi + lo)[n][k] in fp64 (the folded weights exactly as the GEMM sees them)
+__global__ void fold_c1_kernel(const _Float16* __restrict__ hi, const _Float16* __restrict__ lo,
+                               int N, int K, float* __restrict__ c1) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  double s = 0.0;
+  for (int k = 0; k < K; ++k)
+    s += (double)(float)hi[(int64_t)n * K + k] + (double)(float)lo[(int64_t)n * K + k];
+  c1[n] = (float)s;
 }
 
 }  // namespace
@@ -53,11 +70,14 @@ struct EncWorkspace {
   float *xc = nullptr, *yc = nullptr;
   _Float16 *xch = nullptr, *xcl = nullptr, *cc = nullptr, *ccl = nullptr, *ffc = nullptr,
            *ffcl = nullptr;
+  // deferred LayerNorm: row statistics of z after the attention block (sa) / the FFN (sb)
+  float *sa = nullptr, *sb = nullptr;
 
   void release() {
     for (void* p : {(void*)x, (void*)y, (void*)xh, (void*)qkv, (void*)ctx, (void*)ff, (void*)xl,
                     (void*)qkv_l, (void*)ctx_l, (void*)ff_l, (void*)xc, (void*)yc, (void*)xch,
-                    (void*)xcl, (void*)cc, (void*)ccl, (void*)ffc, (void*)ffcl})
+                    (void*)xcl, (void*)cc, (void*)ccl, (void*)ffc, (void*)ffcl, (void*)sa,
+                    (void*)sb})
       if (p) (void)hipFree(p);
     *this = EncWorkspace{};
   }
@@ -76,6 +96,8 @@ struct rag_encoder {
   uint64_t uses = 0;
   // residual + LayerNorm fused into the output projections: -1 auto, 0 off, 1 on
   int fuse_ln = -1;
+  // deferred LayerNorm on the token rows (fp16x3, hidden 384): -1 auto, 0 off, 1 on
+  int defer_ln = -1;
   // host-entry staging
   void* stage = nullptr;
   size_t stage_bytes = 0;
@@ -126,13 +148,41 @@ int up_f16(rag_encoder* e, _Float16** dst, _Float16** dst_lo,
   return RAG_OK;
 }
 
+// deferred LayerNorm's folded consumer weights (see Layer): W' = W diag(gamma) (fp32 products,
+// then fp16x3 planes), c1 = the planes' row sums (fold_c1_kernel), c2 = b + W beta (fp64).
+// parts: (W [rows][K], b [rows]) blocks laid end to end (Q | K | V for the fused QKV)
+int fold_ln(rag_encoder* e, std::initializer_list<std::pair<const float*, const float*>> parts,
+            size_t rows, size_t K, const float* gam, const float* bet, _Float16** wf,
+            _Float16** wfl, float** c1, float** c2) {
+  const size_t N = parts.size() * rows;
+  std::vector<float> wv(N * K), b2(N);
+  size_t n = 0;
+  for (auto& p : parts)
+    for (size_t r = 0; r < rows; ++r, ++n) {
+      double acc = p.second[r];
+      for (size_t k = 0; k < K; ++k) {
+        wv[n * K + k] = p.first[r * K + k] * gam[k];
+        acc += (double)p.first[r * K + k] * (double)bet[k];
+      }
+      b2[n] = (float)acc;
+    }
+  int rc = up_f16(e, wf, wfl, {{wv.data(), N * K}});
+  if (!rc) rc = up_f32(e, c2, b2.data(), N);
+  if (!rc) rc = dalloc(e, c1, N);
+  if (rc) return rc;
+  fold_c1_kernel<<<dim3((unsigned)((N + 255) / 256)), dim3(256)>>>(*wf, *wfl, (int)N, (int)K, *c1);
+  RAG_HIP(hipDeviceSynchronize());
+  return RAG_OK;
+}
+
 int ensure_ws(const rag_bert_config& cfg, EncWorkspace* w, int64_t T) {
   if (T <= w->cap_t) return RAG_OK;
   const int64_t cap = std::max<int64_t>(T, std::max<int64_t>(2 * w->cap_t, 1024));
   for (void* p : {(void*)w->x, (void*)w->y, (void*)w->xh, (void*)w->qkv, (void*)w->ctx,
-                  (void*)w->ff, (void*)w->xl, (void*)w->qkv_l, (void*)w->ctx_l, (void*)w->ff_l})
+                  (void*)w->ff, (void*)w->xl, (void*)w->qkv_l, (void*)w->ctx_l, (void*)w->ff_l,
+                  (void*)w->sa, (void*)w->sb})
     if (p) (void)hipFree(p);
-  w->x = w->y = nullptr;
+  w->x = w->y = w->sa = w->sb = nullptr;
   w->xh = w->qkv = w->ctx = w->ff = nullptr;
   w->xl = w->qkv_l = w->ctx_l = w->ff_l = nullptr;
   w->cap_t = 0;
@@ -142,6 +192,10 @@ int ensure_ws(const rag_bert_config& cfg, EncWorkspace* w, int64_t T) {
     RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->qkv_l), cap * 3 * H * 2));
     RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->ctx_l), cap * H * 2));
     RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->ff_l), cap * FF * 2));
+    if (H == kDlH) {
+      RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->sa), cap * kDlParts * 8));
+      RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->sb), cap * kDlParts * 8));
+    }
   }
   RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->x), cap * H * 4));
   RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->y), cap * H * 4));
@@ -225,11 +279,29 @@ void launch_pipe(const _Float16* A, const _Float16* Al, const _Float16* W, const
 
 template <int EPI, bool SPLIT, typename CFG, int PROBE = 0, int AUX = 0>
 void launch_ws(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float16* Wl,
-               const float* bias, int M, int N, int K, void* C, _Float16* Clo, hipStream_t st) {
+               const float* bias, int M, int N, int K, void* C, _Float16* Clo, hipStream_t st,
+               const DlArgs& dl = DlArgs{}) {
   const int tiles = (N / CFG::BN) * ((M + CFG::BM - 1) / CFG::BM);
   const dim3 grid((unsigned)std::min(cu_count(), (tiles + 7) / 8 * 8));
   gemm_ws_kernel<EPI, SPLIT, CFG, PROBE, AUX><<<grid, dim3(CFG::THREADS + 256), 0, st>>>(
-      A, Al, W, Wl, bias, M, N, K, C, Clo);
+      A, Al, W, Wl, bias, M, N, K, C, Clo, dl);
+}
+
+// shapes the deferred-LayerNorm WS GEMMs take: Ln* (K = 384 input rows; c1 | c2 staged in the
+// 4096-float bias area) and ResLn (N = 384 output rows; bias | gamma | beta)
+bool dl_gemm_ok(int epi, int M, int N, int K) {
+  if (!pipe_ok(M, N, K)) return false;
+  if (epi == kEpiResLn) return N == kDlH;
+  return K == kDlH && 2 * N <= kPipeBiasMax;
+}
+
+// deferred-LayerNorm mode of the forward: -1 auto, 0 off, 1 on (where the shapes allow)
+int defer_ln_default() {
+  static int v = [] {
+    const char* s = std::getenv("RAGMI_DEFER_LN");
+    return s ? std::atoi(s) : -1;
+  }();
+  return v;
 }
 
 // the fused output projection + residual + LayerNorm (kEpiAddLn on PipeRow tiles)
@@ -456,7 +528,19 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
     const char* v = std::getenv("RAGMI_RESIDUAL_F32");      // diagnostic: keep the fp32 copy
     return !(v && std::atoi(v) == 1);
   }();
-  const bool xf = xf_on && w->xl && !fuse_for(T);
+  // deferred LayerNorm (DlArgs): auto once every token-row GEMM is a WS one (AUTO's choice:
+  // the 384-wide projections' 256 x 128 tiles reach half the CUs, ~11K tokens)
+  const bool dl = [&] {
+    if (e->defer_ln == 0 || H != kDlH || !w->xl || !w->sa || !e->layers[0].w1_f) return false;
+    if (!dl_gemm_ok(kEpiLnF16, T, 3 * H, H) || !dl_gemm_ok(kEpiLnGeluF16, T, FF, H) ||
+        !dl_gemm_ok(kEpiResLn, T, H, H) || !dl_gemm_ok(kEpiResLn, T, H, FF))
+      return false;
+    if (e->defer_ln > 0) return true;
+    const int tiles384 = (H / PBN) * ((T + PBM - 1) / PBM);
+    return gemm_variant_default() == RAG_GEMM_AUTO && 2 * tiles384 >= cu_count() &&
+           (H / 64) * ((T + 63) / 64) > 2 * cu_count();
+  }();
+  const bool xf = dl || (xf_on && w->xl && !fuse_for(T));
   embed_ln_kernel<H><<<dim3((max_len + 3) / 4, B), dim3(256), 0, st>>>(
       ids, types, cu, e->wemb, e->pemb, e->temb, e->eg, e->eb, c.layer_norm_eps, c.vocab,
       c.type_vocab, c.max_position, xf ? nullptr : w->x, w->xh, w->xl);
@@ -471,7 +555,18 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
   for (int l = 0; l < nl; ++l) {
     const Layer& L = e->layers[l];
     const bool last = l == nl - 1;                  // CLS rows only after the attention
-    gemm<kEpiF16>(w->xh, w->xl, L.wqkv, L.wqkv_l, L.bqkv, T, 3 * H, H, w->qkv, w->qkv_l, st);
+    const Layer* P = l > 0 ? &e->layers[l - 1] : nullptr;
+    if (dl && P) {
+      // LN2 of layer l-1 pending on z: folded into QKV (kEpiLnF16)
+      DlArgs a;
+      a.st_in = w->sb;
+      a.c1 = L.qkv_c1;
+      a.eps = c.layer_norm_eps;
+      launch_ws<kEpiLnF16, true, PipeLarge, 0, 2>(w->xh, w->xl, L.wqkv_f, L.wqkv_fl, L.qkv_c2, T,
+                                                  3 * H, H, w->qkv, w->qkv_l, st, a);
+    } else {
+      gemm<kEpiF16>(w->xh, w->xl, L.wqkv, L.wqkv_l, L.bqkv, T, 3 * H, H, w->qkv, w->qkv_l, st);
+    }
     const int max_qb = last ? 1 : 1 << 20;
     if (w->xl)
       attn_kernel<H, HD, true><<<agrid, dim3(kAttnThreads<true>), alds, st>>>(
@@ -479,6 +574,33 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
     else
       attn_kernel<H, HD, false><<<agrid, dim3(kAttnThreads<false>), alds, st>>>(
           w->qkv, nullptr, cu, max_len, kc, scale, w->ctx, nullptr, max_qb);
+    if (dl && !last) {
+      // z1 = LN2_{l-1}(z) + O-proj (stats -> sa); FFN1 with LN1 folded; z2 = LN1(z1) + FFN2
+      // (stats -> sb); z lives in xh + xl throughout (updated in place)
+      DlArgs o;
+      o.st_in = P ? w->sb : nullptr;
+      o.gamma = P ? P->g2 : nullptr;
+      o.beta = P ? P->be2 : nullptr;
+      o.st_out = w->sa;
+      o.eps = c.layer_norm_eps;
+      launch_ws<kEpiResLn, true, PipeLarge>(w->ctx, w->ctx_l, L.wo, L.wo_l, L.bo, T, H, H, w->xh,
+                                            w->xl, st, o);
+      DlArgs f;
+      f.st_in = w->sa;
+      f.c1 = L.w1_c1;
+      f.eps = c.layer_norm_eps;
+      launch_ws<kEpiLnGeluF16, true, PipeLarge, 0, 2>(w->xh, w->xl, L.w1_f, L.w1_fl, L.w1_c2, T,
+                                                      FF, H, w->ff, w->ff_l, st, f);
+      DlArgs r;
+      r.st_in = w->sa;
+      r.gamma = L.g1;
+      r.beta = L.be1;
+      r.st_out = w->sb;
+      r.eps = c.layer_norm_eps;
+      launch_ws<kEpiResLn, true, PipeLarge>(w->ff, w->ff_l, L.w2, L.w2_l, L.bi2, T, H, FF, w->xh,
+                                            w->xl, st, r);
+      continue;
+    }
     // rows the rest of the layer runs on: all T tokens, or the B gathered CLS rows
     int R = T;
     float *x = xf ? nullptr : w->x, *y = w->y;
@@ -486,9 +608,12 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
              *ffl = w->ff_l;
     bool row_xf = xf;
     if (last) {
-      gather_cls_kernel<H><<<dim3(B), dim3(64), 0, st>>>(x, w->xh, w->xl, w->ctx, w->ctx_l, cu,
-                                                        w->xc, w->cc,
-                                                        w->xl ? w->ccl : nullptr);
+      // (deferred LayerNorm: x_cls = LN2_{l-1}(z) of the CLS rows)
+      const bool dlp = dl && P;
+      gather_cls_kernel<H><<<dim3(B), dim3(64), 0, st>>>(
+          x, w->xh, w->xl, w->ctx, w->ctx_l, cu, w->xc, w->cc, w->xl ? w->ccl : nullptr,
+          dlp ? w->sb : nullptr, dlp ? P->g2 : nullptr, dlp ? P->be2 : nullptr,
+          c.layer_norm_eps);
       row_xf = false;                                 // the B CLS rows keep an fp32 copy
       R = B;
       x = w->xc;
@@ -603,6 +728,7 @@ int rag_encoder_create(const rag_bert_config* cfg, const float* const* w, int n_
   e->cfg = *cfg;
   e->device = device;
   e->fuse_ln = fuse_ln_default();
+  e->defer_ln = defer_ln_default();
   int rc = RAG_OK;
   auto chk = [&](int r) {
     if (r && !rc) rc = r;
@@ -637,6 +763,15 @@ int rag_encoder_create(const rag_bert_config* cfg, const float* const* w, int n_
     chk(up_f32(e, &L.bi2, p[13], Hs));
     chk(up_f32(e, &L.g2, p[14], Hs));
     chk(up_f32(e, &L.be2, p[15], Hs));
+    if (sp && H == kDlH && 2 * FF <= kPipeBiasMax && !rc) {
+      if (l > 0) {
+        const float* const* pp = p - 16;               // the previous layer's output LN
+        chk(fold_ln(e, {{p[0], p[1]}, {p[2], p[3]}, {p[4], p[5]}}, H, H, pp[14], pp[15],
+                    &L.wqkv_f, &L.wqkv_fl, &L.qkv_c1, &L.qkv_c2));
+      }
+      chk(fold_ln(e, {{p[10], p[11]}}, FF, H, p[8], p[9], &L.w1_f, &L.w1_fl, &L.w1_c1,
+                  &L.w1_c2));
+    }
   }
   if (cfg->head == RAG_HEAD_POOLER_CLS && !rc) {
     const float* const* p = w + 5 + 16 * cfg->layers;
@@ -840,6 +975,51 @@ int rag_encoder_set_fusion(rag_encoder_t* e, int mode) {
   if (!e || mode < -1 || mode > 1) return ragmi::fail(RAG_EINVAL, "mode: -1 auto, 0 off, 1 on");
   std::lock_guard<std::mutex> lk(e->mu);
   e->fuse_ln = mode;
+  return RAG_OK;
+}
+
+int rag_encoder_set_defer_ln(rag_encoder_t* e, int mode) {
+  ragmi::clear_error();
+  if (!e || mode < -1 || mode > 1) return ragmi::fail(RAG_EINVAL, "mode: -1 auto, 0 off, 1 on");
+  std::lock_guard<std::mutex> lk(e->mu);
+  e->defer_ln = mode;
+  return RAG_OK;
+}
+
+int rag_bert_gemm_dl(int epilogue, const void* A, const void* A_lo, const void* W,
+                     const void* W_lo, const float* bias, const float* c1, const float* st_in,
+                     const float* gamma, const float* beta, float eps, int M, int N, int K,
+                     void* C, void* C_lo, float* st_out, void* stream) {
+  ragmi::clear_error();
+  if (!A || !A_lo || !W || !W_lo || !bias || !C || !C_lo)
+    return ragmi::fail(RAG_EINVAL, "NULL argument");
+  if (epilogue != RAG_EPI_LN_F16 && epilogue != RAG_EPI_LN_GELU_F16 &&
+      epilogue != RAG_EPI_RES_LN)
+    return ragmi::fail(RAG_EINVAL, "epilogue: RAG_EPI_LN_F16, RAG_EPI_LN_GELU_F16 or RAG_EPI_RES_LN");
+  if (M < 1 || !dl_gemm_ok(epilogue, M, N, K))
+    return ragmi::fail(RAG_EINVAL, "Ln*: K == 384, N % 128 == 0, N <= 2048; ResLn: N == 384");
+  if (epilogue == RAG_EPI_RES_LN ? (!st_out || (st_in && (!gamma || !beta))) : (!c1 || !st_in))
+    return ragmi::fail(RAG_EINVAL, "Ln*: c1 and st_in; ResLn: st_out (+ gamma, beta with st_in)");
+  DlArgs d;
+  d.st_in = st_in;
+  d.st_out = st_out;
+  d.gamma = gamma;
+  d.beta = beta;
+  d.c1 = c1;
+  d.eps = eps;
+  auto* a = static_cast<const _Float16*>(A);
+  auto* al = static_cast<const _Float16*>(A_lo);
+  auto* w = static_cast<const _Float16*>(W);
+  auto* wl = static_cast<const _Float16*>(W_lo);
+  auto* cl = static_cast<_Float16*>(C_lo);
+  const auto st = static_cast<hipStream_t>(stream);
+  if (epilogue == RAG_EPI_LN_F16)
+    launch_ws<kEpiLnF16, true, PipeLarge, 0, 2>(a, al, w, wl, bias, M, N, K, C, cl, st, d);
+  else if (epilogue == RAG_EPI_LN_GELU_F16)
+    launch_ws<kEpiLnGeluF16, true, PipeLarge, 0, 2>(a, al, w, wl, bias, M, N, K, C, cl, st, d);
+  else
+    launch_ws<kEpiResLn, true, PipeLarge>(a, al, w, wl, bias, M, N, K, C, cl, st, d);
+  RAG_HIP(hipGetLastError());
   return RAG_OK;
 }
 

@@ -561,6 +561,210 @@ __device__ __forceinline__ void pipe_plain_epilogue(const floatx4 (&acc)[CFG::FM
                                                    rl, N, n0, wr, wc, lane);
 }
 
+// ----------------------------------------------------------------------------------------
+// Deferred LayerNorm (fp16x3, hidden 384, the WS GEMMs of large token batches). Between the
+// sublayers the token rows' residual stream is kept un-normalised: z = x + sublayer output, as
+// fp16 hi + lo planes, plus per row kDlParts partial statistics (mean, centred sum of squares)
+// of its 64-column blocks, written by the producing GEMM's epilogue (kEpiResLn). LN(z) is never
+// materialised for the token rows:
+//  * the consuming GEMMs (QKV, FFN1: kEpiLnF16 / kEpiLnGeluF16) multiply z by W' = W diag(gamma)
+//    and correct each row in the epilogue: LN(z) W^T + b = rs (z W'^T - mu c1) + c2, with
+//    c1[n] = sum_k W'[n][k] (of the fp16x3 planes) and c2 = b + W beta, folded at encoder
+//    creation;
+//  * the next residual add (kEpiResLn) recomputes LN(z) per element from the planes and the row
+//    statistics: x = (z - mu) rs gamma + beta (fp32), then z' = x + (A W^T + b).
+// Per element of a 384-wide projection this replaces the fp32 y write, add_ln's reads of y and
+// x and its write of x (16 B) with the residual read and the z write (8 B), and drops the
+// add_ln launches.
+// ----------------------------------------------------------------------------------------
+enum EpiDl { kEpiLnF16 = 4, kEpiLnGeluF16 = 5, kEpiResLn = 6 };
+constexpr int kDlH = 384, kDlParts = kDlH / 64;
+struct DlArgs {
+  const float* st_in = nullptr;    // [M][kDlParts] x {mean, M2}: stats of the A rows (Ln*) or of
+                                   // the residual rows (ResLn; null = already normalised)
+  float* st_out = nullptr;         // ResLn: stats of the rows written
+  const float* gamma = nullptr;    // ResLn: the LayerNorm pending on the residual rows
+  const float* beta = nullptr;
+  const float* c1 = nullptr;       // Ln*: [N] column sums of W' (the bias argument is c2)
+  float eps = 0.f;
+};
+
+// hi + lo fp16 planes (4 values each, as loaded) -> fp32 by v_fma_mix_f32 (hi * 1 + lo in one
+// instruction; exact, as (float)hi + (float)lo). The inputs come from memory loads, never
+// straight from an MFMA (no inline-asm hazard; see split16x2).
+__device__ __forceinline__ floatx4 mix_f16x4(u32x2 h, u32x2 l) {
+  floatx4 z;
+#pragma unroll
+  for (int d = 0; d < 2; ++d) {
+    float lo, hi;
+    asm("v_fma_mix_f32 %0, %1, 1.0, %2 op_sel_hi:[1,0,1]" : "=v"(lo) : "v"(h[d]), "v"(l[d]));
+    asm("v_fma_mix_f32 %0, %1, 1.0, %2 op_sel:[1,0,1] op_sel_hi:[1,0,1]"
+        : "=v"(hi) : "v"(h[d]), "v"(l[d]));
+    z[2 * d] = lo;
+    z[2 * d + 1] = hi;
+  }
+  return z;
+}
+
+// combine a row's kDlParts block statistics (s0..s2 = {mean_0, M2_0, mean_1, M2_1}, ...;
+// Chan et al.'s pairwise update over equal 64-element blocks) into its mean and 1/sqrt(var+eps)
+__device__ __forceinline__ void dl_row_stats(const floatx4& s0, const floatx4& s1,
+                                             const floatx4& s2, float eps, float& mu, float& rs) {
+  const float m[kDlParts] = {s0[0], s0[2], s1[0], s1[2], s2[0], s2[2]};
+  float q = (s0[1] + s0[3]) + (s1[1] + s1[3]) + (s2[1] + s2[3]);
+  mu = ((m[0] + m[1]) + (m[2] + m[3]) + (m[4] + m[5])) * (1.0f / kDlParts);
+#pragma unroll
+  for (int j = 0; j < kDlParts; ++j) {
+    const float d = m[j] - mu;
+    q += 64.f * d * d;
+  }
+  rs = rsqrtf(q * (1.0f / kDlH) + eps);
+}
+
+// A row's statistics as the epilogue holds them: the 4 lanes of row ml (g = lane >> 4) load
+// floats 4g..4g+3 of its 12 (g < 3: blocks 2g, 2g+1; g = 3 nothing new) a whole tile before
+// the epilogue needs them (4 VGPRs per row group; all 12 per lane would not
+// fit beside the fragments), and the epilogue combines them across the lanes.
+template <int FM>
+__device__ __forceinline__ void dl_prefetch_stats(floatx4 (&dls)[FM], __amdgpu_buffer_rsrc_t rsi,
+                                                  int wr, int lane) {
+  const int g = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int ml = wr * 16 * FM + i * 16 + (lane & 15);
+    // (lane group 3 re-reads group 2's floats; dl_lane_stats ignores them)
+    dls[i] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
+                                             rsi, (ml * kDlParts * 2 + 4 * min(g, 2)) * 4, 0, 0));
+  }
+}
+
+// mean and 1/sqrt(var + eps) of the row from the lane-split statistics (dl_row_stats' Chan
+// combination, reduced over lanes l, l^16, l^32, l^48)
+__device__ __forceinline__ void dl_lane_stats(const floatx4& v, int g, float eps, float& mu,
+                                              float& rs) {
+  float sm = g < 3 ? v[0] + v[2] : 0.f;
+  sm += __shfl_xor(sm, 16, 64);
+  sm += __shfl_xor(sm, 32, 64);
+  mu = sm * (1.0f / kDlParts);
+  float q = 0.f;
+  if (g < 3) {
+    const float d0 = v[0] - mu, d2 = v[2] - mu;
+    q = (v[1] + v[3]) + 64.f * (d0 * d0 + d2 * d2);
+  }
+  q += __shfl_xor(q, 16, 64);
+  q += __shfl_xor(q, 32, 64);
+  rs = rsqrtf(q * (1.0f / kDlH) + eps);
+}
+
+// the deferred-LayerNorm epilogues of one wave's FM x FN fragments (its 64 columns are one
+// stats block): fp16 hi + lo planes out through paired 16-B stores (store_f16_pair), ResLn also
+// the block's {mean, M2} per row. lds_f: bias | c1 (Ln*) or bias | gamma | beta (ResLn).
+// dls: the rows' prefetched statistics (dl_prefetch_stats); rs_out: the output stats panel
+// from the tile's row m0.
+template <int EPI, typename CFG, int AUX>
+__device__ __forceinline__ void ws_dl_epilogue(floatx4 (&acc)[CFG::FM][CFG::FN],
+                                               const float* lds_f, __amdgpu_buffer_rsrc_t rc,
+                                               __amdgpu_buffer_rsrc_t rl,
+                                               const floatx4 (&dls)[CFG::FM],
+                                               __amdgpu_buffer_rsrc_t rs_out, bool has_stats,
+                                               int N, int n0, int wr, int wc, int lane,
+                                               float eps) {
+  constexpr int FM = CFG::FM, FN = CFG::FN, WTM = 16 * FM, WTN = 16 * FN;
+  static_assert(WTN == 64 && FN % 2 == 0, "a wave's columns are one stats block");
+  const int g = lane >> 4;
+  const int cofs = 8 * ((g & 1) * 2 + (g >> 1));
+  const float* bias_l = lds_f;
+  const float* c1_l = lds_f + N;                          // Ln*
+  const float *gam_l = lds_f + N, *bet_l = lds_f + 2 * N;  // ResLn
+  // ResLn: residual z of row group i + 1 loaded before group i is computed (read before this
+  // wave overwrites it; all four groups at once would spill)
+  u32x2 zh[2][FN], zl[2][FN];
+  auto load_res = [&](int i) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int vo = ((wr * WTM + i * 16 + (lane & 15)) * N + n0 + wc * WTN + j * 16 + 4 * g) * 2;
+      zh[i & 1][j] = __builtin_amdgcn_raw_buffer_load_b64(rc, vo, 0, 0);
+      zl[i & 1][j] = __builtin_amdgcn_raw_buffer_load_b64(rl, vo, 0, 0);
+    }
+  };
+  if constexpr (EPI == kEpiResLn) load_res(0);
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    if constexpr (EPI == kEpiResLn)
+      if (i + 1 < FM) load_res(i + 1);
+    const int ml = wr * WTM + i * 16 + (lane & 15);
+    float mu = 0.f, rs = 1.f;
+    if (EPI != kEpiResLn || has_stats) dl_lane_stats(dls[i], g, eps, mu, rs);
+    if constexpr (EPI == kEpiResLn) {
+      // residual x = LN(z) = z rs gamma + (beta - mu rs gamma) from the planes; 4-wide vector
+      // arithmetic throughout (gfx950 packed fp32: v_pk_fma / v_pk_add / v_pk_mul)
+      const floatx4 a4 = {rs, rs, rs, rs}, b4 = {-mu * rs, -mu * rs, -mu * rs, -mu * rs};
+      floatx4 s4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int nl = n0 + wc * WTN + j * 16 + 4 * g;
+        const floatx4 z = mix_f16x4(zh[i & 1][j], zl[i & 1][j]);
+        const floatx4 b = *reinterpret_cast<const floatx4*>(bias_l + nl);
+        floatx4 xr = z;
+        if (has_stats)
+          xr = __builtin_elementwise_fma(__builtin_elementwise_fma(z, a4, b4),
+                                         *reinterpret_cast<const floatx4*>(gam_l + nl),
+                                         *reinterpret_cast<const floatx4*>(bet_l + nl));
+        acc[i][j] = (acc[i][j] + b) + xr;
+        s4 += acc[i][j];
+      }
+      // the row's 64 columns sit in lanes l, l^16, l^32, l^48
+      float s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      const float mw = s * (1.0f / 64);
+      const floatx4 m4 = {mw, mw, mw, mw};
+      floatx4 q4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const floatx4 d = acc[i][j] - m4;
+        q4 = __builtin_elementwise_fma(d, d, q4);
+      }
+      float q = (q4[0] + q4[1]) + (q4[2] + q4[3]);
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      if (g == 0) {
+        const u32x2 d = {__builtin_bit_cast(uint32_t, mw), __builtin_bit_cast(uint32_t, q)};
+        __builtin_amdgcn_raw_buffer_store_b64(d, rs_out,
+                                              (ml * kDlParts + (n0 + wc * WTN) / 64) * 8, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int nl = n0 + wc * WTN + j * 16 + 4 * g;
+        const floatx4 c1 = *reinterpret_cast<const floatx4*>(c1_l + nl);
+        const floatx4 c2 = *reinterpret_cast<const floatx4*>(bias_l + nl);
+        const floatx4 nm4 = {-mu, -mu, -mu, -mu}, rs4 = {rs, rs, rs, rs};
+        acc[i][j] = __builtin_elementwise_fma(rs4, __builtin_elementwise_fma(nm4, c1, acc[i][j]), c2);
+        if constexpr (EPI == kEpiLnGeluF16) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][j][r] = gelu_erf(acc[i][j][r]);
+        }
+      }
+    }
+#pragma unroll
+    for (int jp = 0; jp < FN; jp += 2) {
+      const int vo = (ml * N + n0 + wc * WTN + jp * 16 + cofs) * 2;
+      half4 ha, hb, la, lb;
+#pragma unroll
+      for (int r = 0; r < 4; r += 2) {
+        half2 h2, l2;
+        split16x2(acc[i][jp][r], acc[i][jp][r + 1], h2, l2);
+        ha[r] = h2[0]; ha[r + 1] = h2[1]; la[r] = l2[0]; la[r + 1] = l2[1];
+        split16x2(acc[i][jp + 1][r], acc[i][jp + 1][r + 1], h2, l2);
+        hb[r] = h2[0]; hb[r + 1] = h2[1]; lb[r] = l2[0]; lb[r + 1] = l2[1];
+      }
+      store_f16_pair<AUX>(ha, hb, rc, vo);
+      store_f16_pair<AUX>(la, lb, rl, vo);
+    }
+  }
+}
+
 // kEpiAddLn operands besides the GEMM's (Cout = the fp32 residual rows x, read and
 // overwritten; Clo = the lo plane of the fp16x3 copy)
 struct LnArgs {
@@ -953,8 +1157,10 @@ __global__ __launch_bounds__(CFG::THREADS + 256, 1) void gemm_ws_kernel(
     const _Float16* __restrict__ A, const _Float16* __restrict__ Al,
     const _Float16* __restrict__ W, const _Float16* __restrict__ Wl,
     const float* __restrict__ bias, int M, int N, int K, void* __restrict__ Cout,
-    _Float16* __restrict__ Clo) {
+    _Float16* __restrict__ Clo, DlArgs dl) {
   static_assert(EPI != kEpiAddLn && CFG::PRELOAD, "plain epilogues, large tiles");
+  constexpr bool DL = EPI == kEpiLnF16 || EPI == kEpiLnGeluF16 || EPI == kEpiResLn;
+  static_assert(!DL || SPLIT, "deferred LayerNorm: fp16x3 only");
   constexpr int BM = CFG::BM, BN = CFG::BN, NS = CFG::NS, TH = CFG::THREADS;
   constexpr int LTH = 256;                         // loader threads (4 waves)
   constexpr int FM = CFG::FM, FN = CFG::FN, WTM = 16 * FM, WTN = 16 * FN;
@@ -1001,8 +1207,16 @@ __global__ __launch_bounds__(CFG::THREADS + 256, 1) void gemm_ws_kernel(
     nt = t % nN;
   };
 
-  for (int i = tid * 4; i < N; i += (TH + LTH) * 4)
+  for (int i = tid * 4; i < N; i += (TH + LTH) * 4) {
     *reinterpret_cast<floatx4*>(bias_l + i) = *reinterpret_cast<const floatx4*>(bias + i);
+    if constexpr (EPI == kEpiLnF16 || EPI == kEpiLnGeluF16)
+      *reinterpret_cast<floatx4*>(bias_l + N + i) = *reinterpret_cast<const floatx4*>(dl.c1 + i);
+    if constexpr (EPI == kEpiResLn)
+      if (dl.st_in) {
+        *reinterpret_cast<floatx4*>(bias_l + N + i) = *reinterpret_cast<const floatx4*>(dl.gamma + i);
+        *reinterpret_cast<floatx4*>(bias_l + 2 * N + i) = *reinterpret_cast<const floatx4*>(dl.beta + i);
+      }
+  }
   __syncthreads();
 
   if (wid >= TH / 64) {
@@ -1080,6 +1294,22 @@ __global__ __launch_bounds__(CFG::THREADS + 256, 1) void gemm_ws_kernel(
   // (declared outside the step loop only so the PROBE 14 / 15 timing probes can keep stale
   // fragments: every production step overwrites them all before use)
   half8 af[KSN][NPL][FM], wf[KSN][NPL][FN];
+  // deferred LN: the current tile's row statistics, loaded right after the previous tile's
+  // epilogue (a whole tile before they are used; loaded at the tile's first K step instead, the
+  // compiler's waitcnt model put a vmcnt(0) there — a wait for the previous tile's stores)
+  floatx4 dls[FM];
+  auto prefetch = [&](int it) __attribute__((always_inline)) {
+    if constexpr (DL) {
+      if (dl.st_in && it < n_mine) {
+        int m0, nt;
+        tile_mn(it, m0, nt);
+        const __amdgpu_buffer_rsrc_t rsi =
+            panel(dl.st_in + (int64_t)m0 * kDlParts * 2, (int64_t)(M - m0) * kDlParts * 8);
+        dl_prefetch_stats<FM>(dls, rsi, wr, lane);
+      }
+    }
+  };
+  prefetch(0);
   for (int g = 0; g < steps; ++g) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // done reading stage g-1
     __builtin_amdgcn_s_barrier();                        // stage g landed
@@ -1166,12 +1396,20 @@ __global__ __launch_bounds__(CFG::THREADS + 256, 1) void gemm_ws_kernel(
       __amdgpu_buffer_rsrc_t rl = rc;
       if constexpr (SPLIT && EPI != kEpiF32)
         rl = panel(Clo + (int64_t)m0 * N, (int64_t)(M - m0) * N * 2);
-      pipe_plain_epilogue<EPI, SPLIT, CFG, P_NO_STORE, AUX>(acc, bias_l, rc, rl, N, n0, wr, wc,
-                                                            lane);
+      if constexpr (DL) {
+        const int64_t sb = (int64_t)(M - m0) * kDlParts * 8;
+        const __amdgpu_buffer_rsrc_t rso = panel(dl.st_out + (int64_t)m0 * kDlParts * 2, dl.st_out ? sb : 0);
+        ws_dl_epilogue<EPI, CFG, AUX>(acc, bias_l, rc, rl, dls, rso, dl.st_in != nullptr, N, n0,
+                                      wr, wc, lane, dl.eps);
+      } else {
+        pipe_plain_epilogue<EPI, SPLIT, CFG, P_NO_STORE, AUX>(acc, bias_l, rc, rl, N, n0, wr, wc,
+                                                              lane);
+      }
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+      prefetch(it_c);
     }
   }
 }
@@ -1603,21 +1841,32 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) 
 // the last layer computes Q|K|V for every token (K, V are needed), attention for the first
 // query block of each sequence, and everything after it — O-proj, residual + LN, FFN,
 // residual + LN — on the B gathered CLS rows instead of all T tokens.
-// gather: x_cls[b] = x[cu[b]], ctx_cls[b] = ctx[cu[b]] (+ lo plane); one wave per sequence
+// gather: x_cls[b] = x[cu[b]], ctx_cls[b] = ctx[cu[b]] (+ lo plane); one wave per sequence.
+// Deferred LayerNorm (st non-null, H = kDlH): the token rows hold z = xh + xl and its block
+// statistics, and x_cls = LN(z) with (gamma, beta) = (g, bt).
 // ----------------------------------------------------------------------------------------
 template <int H>
 __global__ __launch_bounds__(64) void gather_cls_kernel(
     const float* __restrict__ x, const _Float16* __restrict__ xh,
     const _Float16* __restrict__ xl, const _Float16* __restrict__ ctx,
     const _Float16* __restrict__ ctx_lo, const int* __restrict__ cu, float* __restrict__ x_cls,
-    _Float16* __restrict__ ctx_cls, _Float16* __restrict__ ctx_cls_lo) {
+    _Float16* __restrict__ ctx_cls, _Float16* __restrict__ ctx_cls_lo,
+    const float* __restrict__ st = nullptr, const float* __restrict__ g = nullptr,
+    const float* __restrict__ bt = nullptr, float eps = 0.f) {
   const int b = blockIdx.x, lane = threadIdx.x;
   const int64_t r = cu[b];
+  float mu = 0.f, rs = 1.f;
+  if (H == kDlH && st) {
+    const floatx4* sr = reinterpret_cast<const floatx4*>(st + r * kDlParts * 2);
+    dl_row_stats(sr[0], sr[1], sr[2], eps, mu, rs);
+  }
 #pragma unroll
   for (int j = 0; j < H / 64; ++j) {
     const int c = lane + 64 * j;
-    // (x null: the residual stream is xh + xl, add_ln_kernel<XF>)
-    x_cls[(int64_t)b * H + c] = x ? x[r * H + c] : (float)xh[r * H + c] + (float)xl[r * H + c];
+    // (x null: the residual stream is xh + xl, add_ln_kernel<XF> / deferred LayerNorm)
+    float v = x ? x[r * H + c] : (float)xh[r * H + c] + (float)xl[r * H + c];
+    if (st) v = (v - mu) * rs * g[c] + bt[c];
+    x_cls[(int64_t)b * H + c] = v;
     ctx_cls[(int64_t)b * H + c] = ctx[r * H + c];
     if (ctx_lo) ctx_cls_lo[(int64_t)b * H + c] = ctx_lo[r * H + c];
   }

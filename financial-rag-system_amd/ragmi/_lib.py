@@ -110,6 +110,10 @@ BERT_API = {
                                             ctypes.c_float, ctypes.c_int, ctypes.c_int,
                                             ctypes.c_int, c_vp, c_vp, c_vp, c_vp]),
     "rag_encoder_set_fusion": (ctypes.c_int, [c_vp, ctypes.c_int]),
+    "rag_encoder_set_defer_ln": (ctypes.c_int, [c_vp, ctypes.c_int]),
+    "rag_bert_gemm_dl": (ctypes.c_int, [ctypes.c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                        c_vp, c_vp, ctypes.c_float, ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_int, c_vp, c_vp, c_vp, c_vp]),
     "rag_bert_gemm_add_ln_probe": (ctypes.c_int, [ctypes.c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
                                                   c_vp, c_vp, ctypes.c_float, ctypes.c_int,
                                                   ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_vp,

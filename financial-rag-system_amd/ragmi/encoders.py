@@ -150,6 +150,34 @@ def linear_add_ln(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, gamma: t
     return (x, xh, xl) if split else (x, xh)
 
 
+EPI_LN_F16, EPI_LN_GELU_F16, EPI_RES_LN = 4, 5, 6   # deferred-LayerNorm epilogues
+
+
+def linear_dl(epilogue: int, a: torch.Tensor, a_lo: torch.Tensor, w: torch.Tensor,
+              w_lo: torch.Tensor, bias: torch.Tensor, c: torch.Tensor, c_lo: torch.Tensor,
+              c1: torch.Tensor | None = None, st_in: torch.Tensor | None = None,
+              gamma: torch.Tensor | None = None, beta: torch.Tensor | None = None,
+              eps: float = 1e-12, st_out: torch.Tensor | None = None) -> None:
+    """The deferred-LayerNorm GEMM epilogues (ragmi_bert.h rag_bert_gemm_dl; fp16x3 operand
+    planes): EPI_LN_F16 / EPI_LN_GELU_F16 write [gelu](rstd (a.w^T - mean c1) + bias) to the
+    planes c / c_lo; EPI_RES_LN reads the residual z from c / c_lo, applies the pending LN
+    (st_in, gamma, beta; st_in None: z is already normalised), adds a.w^T + bias and writes the
+    sum back with its block statistics to st_out ([M, 6, 2] fp32)."""
+    M, K = a.shape
+    N = w.shape[0]
+    for t in (a, a_lo, w, w_lo, c, c_lo):
+        if t.dtype != torch.float16 or not t.is_cuda or not t.is_contiguous():
+            raise ValueError("a, a_lo, w, w_lo, c, c_lo: contiguous fp16 cuda")
+    if c.shape != (M, N) or c_lo.shape != (M, N):
+        raise ValueError("c, c_lo must be [M, N]")
+    ptr = lambda t: None if t is None else t.data_ptr()   # noqa: E731
+    check(_lib.load().rag_bert_gemm_dl(
+        int(epilogue), a.data_ptr(), a_lo.data_ptr(), w.data_ptr(), w_lo.data_ptr(),
+        bias.data_ptr(), ptr(c1), ptr(st_in), ptr(gamma), ptr(beta), float(eps), M, N, K,
+        c.data_ptr(), c_lo.data_ptr(), ptr(st_out),
+        torch.cuda.current_stream(a.device).cuda_stream))
+
+
 # ------------------------------------------------------------------ device encoder
 class BertEncoder:
     """One encoder instance in HBM (fp16 GEMM weights, fp32 norms/embeddings)."""
@@ -182,6 +210,11 @@ class BertEncoder:
     def set_fusion(self, mode: int) -> None:
         """Residual + LayerNorm fused into the output projections: -1 auto, 0 off, 1 on."""
         check(self._L.rag_encoder_set_fusion(self._h, int(mode)))
+
+    def set_defer_ln(self, mode: int) -> None:
+        """Deferred LayerNorm on the token rows (fp16x3, hidden 384; ragmi_bert.h
+        rag_encoder_set_defer_ln): -1 auto, 0 off, 1 on where the model allows."""
+        check(self._L.rag_encoder_set_defer_ln(self._h, int(mode)))
 
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:

@@ -100,6 +100,8 @@ int rag_build_pairs(const int32_t* q_ids, const int32_t* q_cu, int B, const int6
  * (all reads of a K step before its MFMAs) for A/B against the interleaved one.
  * N % 128 == 0, K % 64 == 0 (PIPE/SMALL also N <= 4096). */
 enum { RAG_EPI_F16 = 0, RAG_EPI_GELU_F16 = 1, RAG_EPI_F32 = 2 };
+/* deferred-LayerNorm epilogues (rag_bert_gemm_dl) */
+enum { RAG_EPI_LN_F16 = 4, RAG_EPI_LN_GELU_F16 = 5, RAG_EPI_RES_LN = 6 };
 enum { RAG_GEMM_AUTO = 0, RAG_GEMM_TILE = 1, RAG_GEMM_PIPE = 2, RAG_GEMM_PROBE_NO_MFMA = 3,
        RAG_GEMM_PROBE_NO_DMA = 4, RAG_GEMM_SMALL = 5, RAG_GEMM_WIDE = 8,
        RAG_GEMM_PROBE_NO_SYNC = 9, RAG_GEMM_SMALL_BK64 = 10, RAG_GEMM_BIG = 11,
@@ -142,6 +144,31 @@ int rag_bert_gemm_add_ln_probe(int probe, const void* A, const void* A_lo, const
 /* forward's use of rag_bert_gemm_add_ln: -1 auto (default; env RAGMI_FUSE_LN overrides at
  * create), 0 never (separate GEMM + add-LayerNorm kernels), 1 always where the shape allows */
 int rag_encoder_set_fusion(rag_encoder_t* e, int mode);
+
+/* Deferred LayerNorm (fp16x3, hidden 384): the token rows' residual stream is kept
+ * un-normalised between sublayers — z = x + sublayer output as fp16 hi + lo planes, plus per row
+ * six {mean, centred sum of squares} statistics of its 64-column blocks — and LN(z) is applied
+ * inside the GEMMs: a consumer (QKV, FFN1) multiplies z by W' = W diag(gamma) and corrects each
+ * row in its epilogue, LN(z) W^T + b = rstd (z W'^T - mean c1) + c2 (c1 = row sums of W',
+ * c2 = b + W beta, folded at rag_encoder_create), and the next residual add recomputes
+ * LN(z) = (z - mean) rstd gamma + beta per element (modeling_bert.py BertSelfOutput /
+ * BertOutput: LayerNorm(dense(h) + x), restated). Replaces the separate add-LayerNorm passes
+ * on large token batches. Forward use: -1 auto (default, env RAGMI_DEFER_LN overrides at
+ * create: once every token-row GEMM is the WS kernel, ~11K tokens), 0 never, 1 always where
+ * the model allows (fp16x3, hidden 384). */
+int rag_encoder_set_defer_ln(rag_encoder_t* e, int mode);
+
+/* the deferred-LayerNorm GEMM epilogues alone (parity tests), on the WS kernel (fp16x3: A_lo,
+ * W_lo, C_lo required): st_in / st_out are [M][6][2] floats ({mean, M2} of columns 64j..64j+63).
+ *  RAG_EPI_LN_F16 / RAG_EPI_LN_GELU_F16 (K == 384, N % 128 == 0, N <= 2048): per row r with
+ *    (mean, rstd) from st_in, C = [gelu](rstd (A W^T - mean c1) + bias) as hi + lo planes;
+ *  RAG_EPI_RES_LN (N == 384): z = (A W^T + bias) + x, x = (C - mean) rstd gamma + beta from
+ *    the planes C / C_lo read in place (st_in NULL: x = C as is), written back to C / C_lo
+ *    with its block statistics to st_out. */
+int rag_bert_gemm_dl(int epilogue, const void* A, const void* A_lo, const void* W,
+                     const void* W_lo, const float* bias, const float* c1, const float* st_in,
+                     const float* gamma, const float* beta, float eps, int M, int N, int K,
+                     void* C, void* C_lo, float* st_out, void* stream);
 
 #ifdef __cplusplus
 }

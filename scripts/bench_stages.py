@@ -112,22 +112,30 @@ def main():
             w = R.make_weights(cfg, 1)
             enc = BertEncoder(cfg, w, head, dev, prec)
             ids, tt, cu = batch(rng, B, lo, hi, pair)
-            ms = run(enc, ids, tt, cu, reps)
-            T = int(cu[-1])
-            S = float(np.mean(np.diff(cu)))
-            fl = T * flops_per_token(cfg, S)
-            mult = 3 if prec == "fp16x3" else 1
-            line = {"stage": name, "precision": prec, "sequences": B, "tokens": T,
-                    "ms": round(ms, 4), "tokens_per_s": round(T / ms * 1e3, 1),
-                    "algo_TFLOPs": round(fl / ms / 1e9, 1),
-                    "mfma_pipe_frac_of_2.5PF": round(fl * mult / (ms * 1e-3) / PEAK_F16, 4)}
-            if do_cpu and prec == "fp16":
-                cms, thr = cpu_torch_baseline(cfg, w, ids, tt, cu, head,
-                                              budget=float(os.environ.get("CPU_BUDGET", "5")))
-                line["cpu_torch_fp32_ms"] = round(cms, 1)
-                line["cpu_threads"] = thr
-            print(json.dumps(line), flush=True)
+            # DEFERS=-1,0: the deferred LayerNorm (rag_encoder_set_defer_ln) auto, then off
+            for defer in [int(v) for v in os.environ.get("DEFERS", "-1").split(",")]:
+                enc.set_defer_ln(defer)
+                stage_line(enc, name, prec, cfg, head, w, ids, tt, cu, B, reps, do_cpu, defer)
             enc.close()
+
+
+def stage_line(enc, name, prec, cfg, head, w, ids, tt, cu, B, reps, do_cpu, defer):
+    ms = run(enc, ids, tt, cu, reps)
+    T = int(cu[-1])
+    S = float(np.mean(np.diff(cu)))
+    fl = T * flops_per_token(cfg, S)
+    mult = 3 if prec == "fp16x3" else 1
+    line = {"stage": name, "precision": prec, "sequences": B, "tokens": T,
+            "ms": round(ms, 4), "tokens_per_s": round(T / ms * 1e3, 1),
+            "algo_TFLOPs": round(fl / ms / 1e9, 1),
+            "mfma_pipe_frac_of_2.5PF": round(fl * mult / (ms * 1e-3) / PEAK_F16, 4),
+            "defer_ln": defer}
+    if do_cpu and prec == "fp16":
+        cms, thr = cpu_torch_baseline(cfg, w, ids, tt, cu, head,
+                                      budget=float(os.environ.get("CPU_BUDGET", "5")))
+        line["cpu_torch_fp32_ms"] = round(cms, 1)
+        line["cpu_threads"] = thr
+    print(json.dumps(line), flush=True)
 
 
 if __name__ == "__main__":

@@ -2,8 +2,8 @@
 micro-batch — 32 x 15 = 480 (query, chunk) pairs of ~220-290 tokens, ~117K packed tokens —
 through the production path the pipeline bench measures: pairs assembled on the GPU from
 cached chunk tokens (rag_build_pairs), ONE packed MiniLM-L6 forward (AUTO GEMM selection:
-the persistent PIPE / WIDE kernels at this token count; fused residual + LayerNorm in fp16,
-forced on once in fp16x3), top-5 per query. Reference: rerank_documents, main.py:241-247
+the WS kernels at this token count; fp16x3: deferred LayerNorm (AUTO), the two-kernel
+projections and the fused residual + LayerNorm each once; fp16: fused add-LN), top-5 per query. Reference: rerank_documents, main.py:241-247
 (main2.py:242 per request); CrossEncoder.predict -> BertForSequenceClassification.
 
 Also the a4 shape: /embed of 64 chunks x ~200-260 tokens through the 12-layer bge-small
@@ -87,13 +87,16 @@ def test_rerank_480_pairs_vs_oracle(gpu, batch, ce_ref, prec):
     w, ref = ce_ref
     ids, types, cu, mx = batch
     enc = BertEncoder(R.MINILM_CE, w, HEAD_POOLER_CLS, gpu, prec)
-    modes = [-1, 1] if prec == "fp16x3" else [-1]        # AUTO; fused add-LN forced on
+    # (fusion, deferred LN): AUTO (fp16x3: deferred LayerNorm at this size); the two-kernel
+    # projections; fused add-LN forced on
+    modes = [(-1, -1), (-1, 0), (1, 0)] if prec == "fp16x3" else [(-1, -1)]
     try:
-        for fusion in modes:
+        for fusion, defer in modes:
             enc.set_fusion(fusion)
+            enc.set_defer_ln(defer)
             out = enc.forward_device(ids, types, cu, mx).cpu().numpy()
             d = np.abs(out - ref)
-            print(f"[{prec} fusion={fusion}] 480 pairs: max|d|={d.max():.3e} "
+            print(f"[{prec} fusion={fusion} defer={defer}] 480 pairs: max|d|={d.max():.3e} "
                   f"mean|d|={d.mean():.3e}")
             assert d.max() <= TOL[prec]["ce"]
             # per-query top-5 exactly as main.py:246, wherever the oracle's top-6 scores are
@@ -110,6 +113,7 @@ def test_rerank_480_pairs_vs_oracle(gpu, batch, ce_ref, prec):
             assert checked >= B // 4, checked
     finally:
         enc.set_fusion(-1)
+        enc.set_defer_ln(-1)
         enc.close()
 
 
@@ -125,9 +129,11 @@ def test_embed_chunks_64x256_vs_oracle(gpu, prec):
     types = np.zeros(len(ids), np.int32)
     w = R.make_weights(R.BGE_SMALL, 1)
     enc = BertEncoder(R.BGE_SMALL, w, HEAD_CLS_L2, gpu, prec)
-    out = enc.forward_packed(ids.astype(np.int32), types, cu).cpu().numpy()
     ref = _oracle(R.bge_embed, w, R.BGE_SMALL, ids, types, cu)
-    d = np.abs(out - ref)
-    print(f"[{prec}] embed 64 chunks: max|d|={d.max():.3e}")
-    assert d.max() <= TOL[prec]["bge"]
+    for defer in ([-1, 0] if prec == "fp16x3" else [-1]):   # AUTO: deferred LN at 14.8K tokens
+        enc.set_defer_ln(defer)
+        out = enc.forward_packed(ids.astype(np.int32), types, cu).cpu().numpy()
+        d = np.abs(out - ref)
+        print(f"[{prec} defer={defer}] embed 64 chunks: max|d|={d.max():.3e}")
+        assert d.max() <= TOL[prec]["bge"]
     enc.close()
