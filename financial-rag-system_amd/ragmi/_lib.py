@@ -15,7 +15,11 @@ import threading
 
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
-from ._build import LIB_PATH
+from ._build import LIB_PATH as _BUILT_LIB
+
+# RAGMI_LIB_AB: diagnostic A/B timing of two builds of the same tree (scripts/gpu_ab.sh); the
+# default is the in-tree build
+LIB_PATH = os.environ.get("RAGMI_LIB_AB") or _BUILT_LIB
 
 _lock = threading.Lock()
 _lib = None
