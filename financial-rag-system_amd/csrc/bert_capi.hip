@@ -888,7 +888,8 @@ int rag_bert_attention(int variant, const void* qkv, const void* qkv_lo, const i
   if ((qkv_lo == nullptr) != (ctx_lo == nullptr))
     return ragmi::fail(RAG_EINVAL, "qkv_lo and ctx_lo: both (fp16x3) or neither (fp16)");
   if (variant == -1) variant = kAttnVar;
-  if (variant < 0 || variant > 15) return ragmi::fail(RAG_EINVAL, "variant: -1 or 0..15");
+  if ((variant < 0 || variant > 15) && variant != 18 && variant != 26)
+    return ragmi::fail(RAG_EINVAL, "variant: -1, 0..15, 18 or 26");
   constexpr int H = 384, HD = 32, NH = H / HD;
   const int planes = qkv_lo ? 2 : 1;
   const int kc = attn_chunk_keys<HD>(max_len, planes);
@@ -932,6 +933,8 @@ int rag_bert_attention(int variant, const void* qkv, const void* qkv_lo, const i
     case 12: return go(std::integral_constant<int, 12>{});
     case 13: return go(std::integral_constant<int, 13>{});
     case 14: return go(std::integral_constant<int, 14>{});
+    case 18: return go(std::integral_constant<int, 18>{});   // 16 = paired query blocks
+    case 26: return go(std::integral_constant<int, 26>{});
     default: return go(std::integral_constant<int, 15>{});
   }
 }

@@ -1515,6 +1515,9 @@ struct AttnState {
 // with it (64-VGPR budget). The kernel's time is not in these (staging / latency bound).
 // Bit 8 (profiles/r02e_lean_split.jsonl, same process): fp16x3 2 -> 10 0.281 -> 0.272 ms
 // (the default since), fp16 unchanged (0.148 / 0.149: no split there).
+// Bit 16 (two query blocks per wave side by side, bitwise the same; 114 VGPRs, no spill,
+// same 4 waves per SIMD) measured slower at the rerank shape (profiles/r02q_attn_pairs.jsonl,
+// same process, 7 rounds): 10 -> 26 0.254 -> 0.282 ms, 2 -> 18 0.268 -> 0.303: a diagnostic.
 constexpr int kAttnVar = 10;
 template <int H, int HD, bool SPLIT, int VAR = kAttnVar>
 __global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) void attn_kernel(
@@ -1803,7 +1806,37 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) 
   };
 
   const int nqb = min((len + 15) >> 4, max_qb);     // max_qb = 1: the CLS query block only
-  if (nch == 1) {
+  if ((VAR & 16) != 0 && nch == 1) {
+    // paired query blocks: a wave carries blocks qb and qb + NW through the key blocks side
+    // by side (two independent score -> softmax -> P.V chains for the scheduler to interleave;
+    // a rerank sequence of 200-288 tokens has 13-18 blocks, i.e. about one pair per wave of
+    // the 8). A wave left with one block runs it twice and stores it once. Per block the
+    // arithmetic is the single-block path's, so the outputs are bitwise the same.
+    for (int qb = wid; qb < nqb; qb += 2 * NW) {
+      const bool two = qb + NW < nqb;
+      const int qb2 = two ? qb + NW : qb;
+      St s0, s1;
+      init(s0, qb);
+      init(s1, qb2);
+      if (qb == wid) {                  // first round: the Q loads ride under the staging
+        stage(0, sp);
+        __syncthreads();
+      }
+      for (int kb = 0; kb < sp; kb += 32) {
+        floatx4 sc0[2], sc1[2];
+        qk(s0, kb, sc0);
+        qk(s1, kb, sc1);
+        softmax_pv(s0, 0, kb, sc0);
+        softmax_pv(s1, 0, kb, sc1);
+      }
+      finish(s0, qb);
+      if (two) finish(s1, qb2);
+    }
+    if (wid >= nqb) {                   // a wave without a block still joins the staging
+      stage(0, sp);
+      __syncthreads();
+    }
+  } else if (nch == 1) {
     // rolling Q prefetch: a wave's first QPF query blocks are loaded before the K/V staging
     // (their latency hides behind it), and each later one while the block QPF ahead computes
     // (fp16 at head_dim 32 runs 8 waves per SIMD in 64 VGPRs: one block ahead fits)

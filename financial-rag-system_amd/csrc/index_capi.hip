@@ -979,4 +979,31 @@ int rag_profile_scan_ms(rag_index_t* h, double* total_ms, int64_t* launches) {
   return RAG_OK;
 }
 
+int rag_profile_scan_intervals(rag_index_t* h, double* start_ms, double* end_ms, int64_t cap,
+                               int64_t* launches) {
+  ragmi::clear_error();
+  if (!h || !launches || cap < 0 || (cap > 0 && (!start_ms || !end_ms)))
+    return ragmi::fail(RAG_EINVAL, "bad args");
+  std::lock_guard<std::mutex> lk(h->mu);
+  const int64_t n = (int64_t)h->prof_pairs.size();
+  for (int64_t i = 0; i < n; ++i) RAG_HIP(hipEventSynchronize(h->prof_pairs[(size_t)i].b));
+  // every interval relative to the first recorded launch's start event (events of different
+  // streams on one device share the device clock; an earlier launch reads negative)
+  for (int64_t i = 0; i < n && i < cap; ++i) {
+    const ProfPair& p = h->prof_pairs[(size_t)i];
+    float a = 0.f, b = 0.f;
+    RAG_HIP(hipEventElapsedTime(&a, h->prof_pairs[0].a, p.a));
+    RAG_HIP(hipEventElapsedTime(&b, h->prof_pairs[0].a, p.b));
+    start_ms[i] = a;
+    end_ms[i] = b;
+  }
+  for (auto& p : h->prof_pairs) {
+    (void)hipEventDestroy(p.a);
+    (void)hipEventDestroy(p.b);
+  }
+  h->prof_pairs.clear();
+  *launches = n;
+  return RAG_OK;
+}
+
 }  // extern "C"

@@ -83,6 +83,9 @@ INDEX_API = {
     "rag_index_exactness_stats": (ctypes.c_int, [c_vp, c_i64p, c_i64p, c_i32p, ctypes.c_int]),
     "rag_profile_enable": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "rag_profile_scan_ms": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_double), c_i64p]),
+    "rag_profile_scan_intervals": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_double),
+                                                  ctypes.POINTER(ctypes.c_double),
+                                                  ctypes.c_int64, c_i64p]),
 }
 
 class RagBertConfig(ctypes.Structure):

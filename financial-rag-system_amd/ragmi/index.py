@@ -273,6 +273,36 @@ class FlatIndex:
         check(self._L.rag_profile_scan_ms(self._h, ctypes.byref(tot), ctypes.byref(n)))
         return float(tot.value), int(n.value)
 
+    def profile_scan_intervals(self, cap: int = 1 << 16) -> tuple[np.ndarray, np.ndarray]:
+        """(start_ms, end_ms) of every recorded scan launch, relative to the first one's start
+        (rag_profile_scan_intervals); clears the record."""
+        a = np.zeros(cap, np.float64)
+        b = np.zeros(cap, np.float64)
+        n = ctypes.c_int64()
+        dp = ctypes.POINTER(ctypes.c_double)
+        check(self._L.rag_profile_scan_intervals(self._h, a.ctypes.data_as(dp),
+                                                 b.ctypes.data_as(dp), cap, ctypes.byref(n)))
+        m = min(int(n.value), cap)
+        return a[:m], b[:m]
+
+
+def busy_union_ms(start_ms, end_ms) -> float:
+    """Length of the union of [start, end) intervals: the time at least one of the launches
+    was running (overlapping launches counted once)."""
+    order = np.argsort(start_ms, kind="stable")
+    busy, cur_a, cur_b = 0.0, None, None
+    for i in order:
+        a, b = float(start_ms[i]), float(end_ms[i])
+        if cur_b is None or a > cur_b:
+            if cur_b is not None:
+                busy += cur_b - cur_a
+            cur_a, cur_b = a, b
+        else:
+            cur_b = max(cur_b, b)
+    if cur_b is not None:
+        busy += cur_b - cur_a
+    return busy
+
 
 def merge_topk(scores: torch.Tensor, ids: torch.Tensor, k: int):
     """Merge per-shard exact lists [n_lists, B, k] -> global [B, k] on the GPU."""

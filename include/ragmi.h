@@ -185,6 +185,13 @@ int rag_index_set_scan_order(rag_index_t* index, int serial);
  * time, so bench.py samples instead of timing every pass). */
 int rag_profile_enable(rag_index_t* index, int enable);
 int rag_profile_scan_ms(rag_index_t* index, double* total_ms, int64_t* launches);
+/* The same event pairs as intervals: start_ms[i] / end_ms[i] of the i-th recorded launch,
+ * relative to the first recorded launch's start (cap entries at most; *launches = how many
+ * were recorded), then clears them like rag_profile_scan_ms. With several batches in flight
+ * the launches of different streams overlap in time; bench.py takes the union of these
+ * intervals as the time the scan kernel occupied the device. */
+int rag_profile_scan_intervals(rag_index_t* index, double* start_ms, double* end_ms, int64_t cap,
+                               int64_t* launches);
 
 /* Diagnostic: average device ms of `reps` launches of scan variant `variant` on the current
  * corpus with the first min(B,32) queries (dim 384 only). Variants: 0 production (seeded

@@ -127,9 +127,10 @@ int rag_bert_gemm_add_ln(const void* A, const void* A_lo, const void* W, const v
 /* Encoder attention alone, hidden 384 / head_dim 32 (bge-small, MiniLM-L6): ctx[T][384] =
  * per (sequence, head) softmax(Q K^T / sqrt(32)) V over the packed rows of qkv[T][1152]
  * (Q | K | V), cu[B+1] row offsets, max_len >= every sequence length (<= 512). qkv_lo /
- * ctx_lo: the fp16x3 lo planes (both or neither). variant: the kernel's VAR bit mask, 0..7
- * (1 rolling Q prefetch, 2 fp16x3 row sums by MFMA, 4 software-pipelined scores), or -1 for
- * the one the forward runs. For A/B timing and parity tests. */
+ * ctx_lo: the fp16x3 lo planes (both or neither). variant: the kernel's VAR bit mask, 0..15
+ * (1 rolling Q prefetch, 2 fp16x3 row sums by MFMA, 4 software-pipelined scores, 8 lean
+ * block), 18 or 26 (16 = two query blocks per wave side by side), or -1 for the one the
+ * forward runs. For A/B timing and parity tests. */
 int rag_bert_attention(int variant, const void* qkv, const void* qkv_lo, const int32_t* cu,
                        int B, int max_len, void* ctx, void* ctx_lo, void* stream);
 

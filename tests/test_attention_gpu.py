@@ -43,7 +43,7 @@ def data():
     return x, hi, lo, cu
 
 
-@pytest.mark.parametrize("variant", range(16))
+@pytest.mark.parametrize("variant", list(range(16)) + [18, 26])
 @pytest.mark.parametrize("split", [True, False], ids=["fp16x3", "fp16"])
 def test_attention_matches_fp32(gpu, data, variant, split):
     from ragmi.encoders import attention
@@ -81,6 +81,22 @@ def test_lean_block_is_bitwise_identical(gpu, data, variant, split):
     cu_t = torch.from_numpy(cu).cuda()
     a = attention(hi, cu_t, max(LENS), lo if split else None, variant)
     b = attention(hi, cu_t, max(LENS), lo if split else None, variant | 8)
+    torch.cuda.synchronize()
+    for x1, x2 in (zip(a, b) if split else [(a, b)]):
+        assert torch.equal(x1.view(torch.int16), x2.view(torch.int16))
+
+
+@pytest.mark.parametrize("variant", [2, 10])
+@pytest.mark.parametrize("split", [True, False], ids=["fp16x3", "fp16"])
+def test_paired_blocks_are_bitwise_identical(gpu, data, variant, split):
+    """VAR bit 16 (two query blocks per wave side by side) only reorders whole blocks: outputs
+    equal the variant without it bit for bit, including waves left with one block and
+    sequences shorter than one block per wave."""
+    from ragmi.encoders import attention
+    x, hi, lo, cu = data
+    cu_t = torch.from_numpy(cu).cuda()
+    a = attention(hi, cu_t, max(LENS), lo if split else None, variant)
+    b = attention(hi, cu_t, max(LENS), lo if split else None, variant | 16)
     torch.cuda.synchronize()
     for x1, x2 in (zip(a, b) if split else [(a, b)]):
         assert torch.equal(x1.view(torch.int16), x2.view(torch.int16))

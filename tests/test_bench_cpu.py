@@ -145,3 +145,16 @@ def test_verify_exact_two_shards(monkeypatch):
     monkeypatch.setattr(bench.dist, "all_gather_object", merged)
     r5, ok = bench.verify_exact(_Shard(shards[0][1]), q, s, i, 0, 0, 2, torch.device("cpu"))
     assert ok.all() and (r5 == 1.0).all()
+
+
+def test_busy_union_counts_overlap_once():
+    """bench.py's device time for overlapped scan launches: the union of their intervals."""
+    import numpy as np
+    from ragmi.index import busy_union_ms
+    assert busy_union_ms(np.array([]), np.array([])) == 0.0
+    # disjoint: the plain sum of durations (== the average launch duration x launches)
+    assert busy_union_ms(np.array([0.0, 2.0, 5.0]), np.array([1.0, 3.0, 6.5])) == 3.5
+    # nested / overlapping / unsorted, negative starts (launches recorded before the first)
+    a = np.array([4.0, 0.0, 0.5, -1.0, 10.0])
+    b = np.array([6.0, 2.0, 1.0, 0.25, 10.5])
+    assert busy_union_ms(a, b) == (2.0 - (-1.0)) + 2.0 + 0.5
