@@ -419,7 +419,8 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
       variant == RAG_GEMM_WS_NO_STORE || variant == RAG_GEMM_WS_DMA_ONLY ||
       variant == RAG_GEMM_WS_L2_STORE || variant == RAG_GEMM_WS_NT ||
       variant == RAG_GEMM_WS_NOROT || variant == RAG_GEMM_WS_READS_FIRST ||
-      variant == RAG_GEMM_WS_PROBE_NO_A_READS || variant == RAG_GEMM_WS_PROBE_NO_W_READS) {
+      variant == RAG_GEMM_WS_PROBE_NO_A_READS || variant == RAG_GEMM_WS_PROBE_NO_W_READS ||
+      variant == RAG_GEMM_WS_PRIO_LOAD || variant == RAG_GEMM_WS_PRIO_MFMA) {
     // probes keep production's store policy (nt for fp16 outputs) since round 2's r02h runs
     auto go = [&](auto pc) {
       constexpr int P = decltype(pc)::value;
@@ -441,6 +442,8 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
     else if (variant == RAG_GEMM_WS_DMA_ONLY) go(std::integral_constant<int, 8>{});
     else if (variant == RAG_GEMM_WS_PROBE_NO_A_READS) go(std::integral_constant<int, 14>{});
     else if (variant == RAG_GEMM_WS_PROBE_NO_W_READS) go(std::integral_constant<int, 15>{});
+    else if (variant == RAG_GEMM_WS_PRIO_LOAD) go(std::integral_constant<int, 16>{});
+    else if (variant == RAG_GEMM_WS_PRIO_MFMA) go(std::integral_constant<int, 17>{});
     else if (variant == RAG_GEMM_WS_READS_FIRST) {
       constexpr int AX = EPI == kEpiF32 ? 0 : 2;
       // the all-reads-first fragment order (PROBE 13) the WS kernel used before its interleaved one
@@ -825,7 +828,8 @@ int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, co
   if ((variant == RAG_GEMM_PIPE || variant == RAG_GEMM_SMALL || variant == RAG_GEMM_WIDE ||
        variant == RAG_GEMM_SMALL_BK64 || variant == RAG_GEMM_BIG || variant == RAG_GEMM_BIG128 ||
        variant == RAG_GEMM_WS || variant == RAG_GEMM_WS_NT || variant == RAG_GEMM_WS_NOROT ||
-       variant == RAG_GEMM_WS_READS_FIRST) &&
+       variant == RAG_GEMM_WS_READS_FIRST || variant == RAG_GEMM_WS_PRIO_LOAD ||
+       variant == RAG_GEMM_WS_PRIO_MFMA) &&
       !pipe_ok(M, N, K))
     return ragmi::fail(RAG_EINVAL, "pipe/small/wide variants need N % 128 == 0, K % 64 == 0, "
                                    "N <= 4096, M*K*2 and M*N*4 < 2^31");
@@ -841,7 +845,8 @@ int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, co
                      variant == RAG_GEMM_WIDE || variant == RAG_GEMM_SMALL_BK64 ||
                      variant == RAG_GEMM_BIG || variant == RAG_GEMM_BIG128 ||
                      variant == RAG_GEMM_WS || variant == RAG_GEMM_WS_NT ||
-                     variant == RAG_GEMM_WS_NOROT || variant == RAG_GEMM_WS_READS_FIRST || probe;
+                     variant == RAG_GEMM_WS_NOROT || variant == RAG_GEMM_WS_READS_FIRST ||
+                     variant == RAG_GEMM_WS_PRIO_LOAD || variant == RAG_GEMM_WS_PRIO_MFMA || probe;
   if (!known || (probe && !pipe_ok(M, N, K)))
     return ragmi::fail(RAG_EINVAL, "unknown GEMM variant, or a probe on a non-pipe shape");
   auto* a = static_cast<const _Float16*>(A);

@@ -1239,6 +1239,7 @@ __global__ __launch_bounds__(CFG::THREADS + 256, 1) void gemm_ws_kernel(
 
   if (wid >= TH / 64) {
     // ---- loader waves: stage g+NS-1 issued after the barrier of step g ----
+    if constexpr (PROBE == 16) __builtin_amdgcn_s_setprio(3);   // A/B: loaders first in issue
     const int lw = wid - TH / 64;
     uint32_t voA[LA], voW[LW];
 #pragma unroll
@@ -1302,6 +1303,7 @@ __global__ __launch_bounds__(CFG::THREADS + 256, 1) void gemm_ws_kernel(
   }
 
   // ---- MFMA waves ----
+  if constexpr (PROBE == 17) __builtin_amdgcn_s_setprio(2);   // A/B: MFMA waves first in issue
   const int wr = wid / CFG::WAVES_N, wc = wid % CFG::WAVES_N;
   floatx4 acc[FM][FN];
 #pragma unroll
