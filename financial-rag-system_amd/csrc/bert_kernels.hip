@@ -1170,6 +1170,17 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
 // landed, the MFMA waves once they are done reading stage g-1 (whose slot the loaders refill
 // right after it). 12 waves: 3 per SIMD, <= 168 VGPRs each (the MFMA path needs ~145).
 // ----------------------------------------------------------------------------------------
+// PROBE 18 (the WS kernel's FULL / FREE ring): wait until an LDS counter reaches `target`
+// (bounded: a wrong count ends the wait after ~1.7 ms instead of hanging the wave)
+__device__ __forceinline__ void lds_spin_ge(uint32_t* p, uint32_t target) {
+  for (int n = 0; n < (1 << 16); ++n) {
+    const uint32_t v = __builtin_amdgcn_readfirstlane(
+        __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+    if (v >= target) return;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
 template <int EPI, bool SPLIT, typename CFG, int PROBE = 0, int AUX = 0>
 __global__ __launch_bounds__(CFG::THREADS + 256, 1) void gemm_ws_kernel(
     const _Float16* __restrict__ A, const _Float16* __restrict__ Al,
@@ -1196,6 +1207,11 @@ __global__ __launch_bounds__(CFG::THREADS + 256, 1) void gemm_ws_kernel(
   static_assert((NS - 2) * L <= 63, "vmcnt range");
   __shared__ half8 lds[NS * STAGE_H8 + kPipeBiasMax / 4];
   float* bias_l = reinterpret_cast<float*>(lds + NS * STAGE_H8);
+  // PROBE 18: FULL[s] (loader waves' landed stages) and FREE[s] (MFMA waves' released
+  // stages) counters of ring slot s, in the last 16 floats of the bias area (the launcher
+  // keeps 3N of the staged vectors below them)
+  uint32_t* ring_cnt = reinterpret_cast<uint32_t*>(bias_l + kPipeBiasMax - 16);
+  constexpr bool FLAGS = PROBE == 18;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1235,6 +1251,8 @@ __global__ __launch_bounds__(CFG::THREADS + 256, 1) void gemm_ws_kernel(
         *reinterpret_cast<floatx4*>(bias_l + 2 * N + i) = *reinterpret_cast<const floatx4*>(dl.beta + i);
       }
   }
+  if constexpr (FLAGS)
+    if (tid < 16) ring_cnt[tid] = 0u;
   __syncthreads();
 
   if (wid >= TH / 64) {
@@ -1295,7 +1313,16 @@ __global__ __launch_bounds__(CFG::THREADS + 256, 1) void gemm_ws_kernel(
     for (int p = 0; p < NS - 1; ++p) issue_next();
     for (int g = 0; g < steps; ++g) {
       wait_ring<L, 0, NS - 2>(min(NS - 2, steps - 1 - g), false);   // stage g landed
-      __builtin_amdgcn_s_barrier();
+      if constexpr (FLAGS) {
+        // publish stage g, then take slot (g-1) % NS once all 8 MFMA waves released stage g-1
+        if (lane == 0)
+          __hip_atomic_fetch_add(&ring_cnt[g % NS], 1u, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (g >= 1 && g + NS - 1 < steps)
+          lds_spin_ge(&ring_cnt[8 + (g - 1) % NS], (uint32_t)(TH / 64) * ((g - 1) / NS + 1));
+      } else {
+        __builtin_amdgcn_s_barrier();
+      }
       asm volatile("" ::: "memory");
       issue_next();                     // stage g+NS-1 -> slot (g-1) % NS
     }
@@ -1332,7 +1359,16 @@ __global__ __launch_bounds__(CFG::THREADS + 256, 1) void gemm_ws_kernel(
   prefetch(0);
   for (int g = 0; g < steps; ++g) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // done reading stage g-1
-    __builtin_amdgcn_s_barrier();                        // stage g landed
+    if constexpr (FLAGS) {
+      // release stage g-1, wait for the 4 loader waves' stage g (no workgroup barrier: the
+      // MFMA waves drift up to the ring's depth apart)
+      if (g >= 1 && lane == 0)
+        __hip_atomic_fetch_add(&ring_cnt[8 + (g - 1) % NS], 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+      lds_spin_ge(&ring_cnt[g % NS], (uint32_t)(LTH / 64) * (g / NS + 1));
+    } else {
+      __builtin_amdgcn_s_barrier();                      // stage g landed
+    }
     asm volatile("" ::: "memory");
     const half8* sa = lds + slot_c * STAGE_H8;
     const half8* sw = sa + NPL * A_H8;

@@ -429,6 +429,7 @@ def _cpu_search_baseline(sample16, q, n_total, k, budget_s, tags=None, filt=None
 
 def run_search(args, mode):
     from ragmi.dist import ShardedIndex
+    from ragmi.index import busy_union_ms
     world, rank = _world()
     dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
     torch.cuda.set_device(dev)
@@ -475,15 +476,22 @@ def run_search(args, mode):
     for i in range(args.warmup):
         step(i)
     _sync(dev)
-    idx.profile(4)
+    # free scan order (several streams' scans overlap): every launch timed, the scan kernel's
+    # device time per launch is the union of the launches' event intervals / launches
+    # (bench.py); serial order: every 4th launch (timing every one cost 3-4% of
+    # the filtered / config-5 throughput, profiles/r02q_lines_every_launch.jsonl), where the
+    # union of the sampled launches is their summed duration
+    idx.profile(1 if n_streams > 1 and not serial else 4)
     t0 = time.perf_counter()
     outs = [step(args.warmup + k) for k in range(args.steps)]
     _sync(dev)
     elapsed = time.perf_counter() - t0
     idx.profile(0)
-    scan_ms, launches = idx.profile_scan_ms()
-    scan_avg = scan_ms / max(launches, 1)
-    elapsed, scan_avg = _max_over_ranks([elapsed, scan_avg], dev)
+    iv_a, iv_b = idx.profile_scan_intervals()
+    launches = len(iv_a)
+    scan_avg = float((iv_b - iv_a).sum()) / max(launches, 1)
+    busy = busy_union_ms(iv_a, iv_b) / max(launches, 1)
+    elapsed, scan_avg, busy = _max_over_ranks([elapsed, scan_avg, busy], dev)
     extra = {}
     if not args.no_recall and world == 1:
         # the first timed planted batch and the first timed pure-random one (every 4th)
@@ -531,7 +539,7 @@ def run_search(args, mode):
     if rank == 0:
         per_row = D * 2 + (4 if mode == "filtered" else 0)
         algo = (hi - lo) * per_row
-        ach = algo / (scan_avg * 1e-3)
+        ach = algo / (busy * 1e-3)
         kern = ("scan_wide_kernel<1024,0,true>" if mode == "5" else
                 "scan_kernel<384,true>")
         metric = ("queries/sec + recall@5, batch=128 over 50Mx1024 corpus (config 5)"
@@ -551,7 +559,13 @@ def run_search(args, mode):
              "scan_order": "serial" if serial else "free"},
             roofline={"bound": "hbm", "achieved": round(ach / 1e9, 1), "peak": HBM_PEAK / 1e9,
                       "unit": "GB/s", "frac": round(ach / HBM_PEAK, 4), "traffic": None,
-                      "kernel": kern, "avg_ms": round(scan_avg, 4),
+                      "kernel": kern,
+                      "time_basis": ("union of the scan launches' HIP-event intervals over "
+                                     "the timed region / launches" if n_streams > 1 and
+                                     not serial else "average scan launch duration (HIP "
+                                     "events, every 4th launch)"),
+                      "busy_ms_per_launch": round(busy, 4), "avg_ms": round(scan_avg, 4),
+                      "frac_of_avg_launch": round(algo / (scan_avg * 1e-3) / HBM_PEAK, 4),
                       "algorithmic_bytes_per_launch": algo,
                       "bytes_per_row": per_row,
                       "step_frac": round(algo / (elapsed / args.steps) / HBM_PEAK, 4)},

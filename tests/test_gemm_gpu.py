@@ -154,3 +154,23 @@ def test_gemm_add_ln_rejects_bad_shapes(gpu):
     x = torch.zeros((16, 768), dtype=torch.float32, device="cuda")
     with pytest.raises(RagmiError):
         linear_add_ln(a, w, v, v, v, 1e-12, x)
+
+
+@pytest.mark.parametrize("shape", [(70001, 1536, 384), (117000, 384, 1536), (33000, 1152, 384)],
+                         ids=lambda s: "x".join(map(str, s)))
+@pytest.mark.parametrize("epi", [0, 1, 2], ids=["f16", "gelu", "f32"])
+@pytest.mark.parametrize("split", [False, True], ids=["fp16", "fp16x3"])
+def test_ws_flag_ring_bitwise(gpu, shape, epi, split):
+    """RAG_GEMM_WS_FLAGS (the WS kernel's ring handed over by FULL / FREE counters in LDS
+    instead of one workgroup barrier per K step) changes only the synchronisation: every
+    output equals the barrier ring's bit for bit (many tiles per workgroup, partial last
+    row panel)."""
+    from ragmi.encoders import linear
+    M, N, K = shape
+    a, al, w, wl, bias, _, _ = _operands(M, N, K, split, seed=M + N)
+    r0 = linear(a, w, bias, epi, al, wl, 19)
+    r1 = linear(a, w, bias, epi, al, wl, 32)
+    torch.cuda.synchronize()
+    for x0, x1 in (zip(r0, r1) if isinstance(r0, tuple) else [(r0, r1)]):
+        assert torch.equal(x0.view(torch.int16) if x0.dtype == torch.float16 else x0.view(torch.int32),
+                           x1.view(torch.int16) if x1.dtype == torch.float16 else x1.view(torch.int32))
