@@ -421,7 +421,7 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
       variant == RAG_GEMM_WS_NOROT || variant == RAG_GEMM_WS_READS_FIRST ||
       variant == RAG_GEMM_WS_PROBE_NO_A_READS || variant == RAG_GEMM_WS_PROBE_NO_W_READS ||
       variant == RAG_GEMM_WS_PRIO_LOAD || variant == RAG_GEMM_WS_PRIO_MFMA ||
-      variant == RAG_GEMM_WS_FLAGS) {
+      variant == RAG_GEMM_WS_FLAGS || variant == RAG_GEMM_WS_NOHALF) {
     // probes keep production's store policy (nt for fp16 outputs) since round 2's r02h runs
     auto go = [&](auto pc) {
       constexpr int P = decltype(pc)::value;
@@ -445,6 +445,7 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
     else if (variant == RAG_GEMM_WS_PROBE_NO_W_READS) go(std::integral_constant<int, 15>{});
     else if (variant == RAG_GEMM_WS_PRIO_LOAD) go(std::integral_constant<int, 16>{});
     else if (variant == RAG_GEMM_WS_PRIO_MFMA) go(std::integral_constant<int, 17>{});
+    else if (variant == RAG_GEMM_WS_NOHALF) go(std::integral_constant<int, 19>{});
     else if (variant == RAG_GEMM_WS_FLAGS) {
       // the ring counters sit in the last 16 floats of the staged-vector area
       if (N <= kPipeBiasMax - 16) go(std::integral_constant<int, 18>{});
@@ -835,7 +836,8 @@ int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, co
        variant == RAG_GEMM_SMALL_BK64 || variant == RAG_GEMM_BIG || variant == RAG_GEMM_BIG128 ||
        variant == RAG_GEMM_WS || variant == RAG_GEMM_WS_NT || variant == RAG_GEMM_WS_NOROT ||
        variant == RAG_GEMM_WS_READS_FIRST || variant == RAG_GEMM_WS_PRIO_LOAD ||
-       variant == RAG_GEMM_WS_PRIO_MFMA || variant == RAG_GEMM_WS_FLAGS) &&
+       variant == RAG_GEMM_WS_PRIO_MFMA || variant == RAG_GEMM_WS_FLAGS ||
+       variant == RAG_GEMM_WS_NOHALF) &&
       !pipe_ok(M, N, K))
     return ragmi::fail(RAG_EINVAL, "pipe/small/wide variants need N % 128 == 0, K % 64 == 0, "
                                    "N <= 4096, M*K*2 and M*N*4 < 2^31");
@@ -853,7 +855,7 @@ int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, co
                      variant == RAG_GEMM_WS || variant == RAG_GEMM_WS_NT ||
                      variant == RAG_GEMM_WS_NOROT || variant == RAG_GEMM_WS_READS_FIRST ||
                      variant == RAG_GEMM_WS_PRIO_LOAD || variant == RAG_GEMM_WS_PRIO_MFMA ||
-                     variant == RAG_GEMM_WS_FLAGS || probe;
+                     variant == RAG_GEMM_WS_FLAGS || variant == RAG_GEMM_WS_NOHALF || probe;
   if (!known || (probe && !pipe_ok(M, N, K)))
     return ragmi::fail(RAG_EINVAL, "unknown GEMM variant, or a probe on a non-pipe shape");
   auto* a = static_cast<const _Float16*>(A);

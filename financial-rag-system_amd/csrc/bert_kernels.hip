@@ -1233,12 +1233,30 @@ __global__ __launch_bounds__(CFG::THREADS + 256, 1) void gemm_ws_kernel(
   const bool aligned = nM >= 64;
   const int t_x = aligned ? (nM > xcd ? (nM - xcd + 7) >> 3 : 0) * nN : nM * nN;
   const int l0 = aligned ? lx : xcd * per_xcd + lx, stride = aligned ? per_xcd : G;
-  const int n_mine = l0 < t_x ? (t_x - l0 + stride - 1) / stride : 0;
+  // Split last round (aligned mode): when the XCD's last round of tiles would leave more
+  // than half of its workgroups idle (r_x <= stride / 2 tiles), each of those r_x tiles runs
+  // as two 128-row halves on two workgroups, so the round ends after a half tile instead of a
+  // full one. A half tile keeps the 256-row ring image (rows past its 128 read as zeros
+  // through the A panel's extent, so no bytes move for them); the MFMA waves of the upper
+  // rows skip their MFMAs and stores. PROBE 19 = without (A/B).
+  const int r_x = aligned ? t_x % stride : 0;
+  const bool halves = PROBE != 19 && aligned && r_x > 0 && 2 * r_x <= stride;
+  const int n_full = halves ? t_x / stride : l0 < t_x ? (t_x - l0 + stride - 1) / stride : 0;
+  const int n_mine = n_full + (halves && lx < 2 * r_x ? 1 : 0);
   const int steps = n_mine * nk;
-  auto tile_mn = [&](int it, int& m0, int& nt) __attribute__((always_inline)) {
-    const int t = it * stride + l0;
-    m0 = (aligned ? xcd + 8 * (t / nN) : t / nN) * BM;
-    nt = t % nN;
+  // tile `it`: rows [m0, m_end) (m_end <= M) and n-tile nt
+  auto tile_mn = [&](int it, int& m0, int& nt, int& m_end) __attribute__((always_inline)) {
+    if (it < n_full) {
+      const int t = it * stride + l0;
+      m0 = (aligned ? xcd + 8 * (t / nN) : t / nN) * BM;
+      nt = t % nN;
+      m_end = min(M, m0 + BM);
+    } else {                                  // the half tile of the split last round
+      const int t = n_full * stride + (lx >> 1);
+      m0 = (xcd + 8 * (t / nN)) * BM + (lx & 1) * (BM / 2);
+      nt = t % nN;
+      m_end = min(M, m0 + BM / 2);
+    }
   };
 
   for (int i = tid * 4; i < N; i += (TH + LTH) * 4) {
@@ -1279,11 +1297,11 @@ __global__ __launch_bounds__(CFG::THREADS + 256, 1) void gemm_ws_kernel(
         return;
       }
       if (kt_i == 0) {
-        int m0, nt;
-        tile_mn(it_i, m0, nt);
+        int m0, nt, m_end;
+        tile_mn(it_i, m0, nt, m_end);
         const int n0 = nt * BN;
         kr_i = aligned || PROBE == 11 ? 0 : nt % nk;   // rotated K order unless aligned
-        const int64_t abytes = (int64_t)(M - m0) * K * 2, wbytes = (int64_t)BN * K * 2;
+        const int64_t abytes = (int64_t)(m_end - m0) * K * 2, wbytes = (int64_t)BN * K * 2;
         rA0 = panel(A + (int64_t)m0 * K, abytes);
         rW0 = panel(W + (int64_t)n0 * K, wbytes);
         if constexpr (SPLIT) {
@@ -1348,10 +1366,10 @@ __global__ __launch_bounds__(CFG::THREADS + 256, 1) void gemm_ws_kernel(
   auto prefetch = [&](int it) __attribute__((always_inline)) {
     if constexpr (DL) {
       if (dl.st_in && it < n_mine) {
-        int m0, nt;
-        tile_mn(it, m0, nt);
+        int m0, nt, m_end;
+        tile_mn(it, m0, nt, m_end);
         const __amdgpu_buffer_rsrc_t rsi =
-            panel(dl.st_in + (int64_t)m0 * kDlParts * 2, (int64_t)(M - m0) * kDlParts * 8);
+            panel(dl.st_in + (int64_t)m0 * kDlParts * 2, (int64_t)(m_end - m0) * kDlParts * 8);
         dl_prefetch_stats<FM>(dls, rsi, wr, lane);
       }
     }
@@ -1400,60 +1418,67 @@ __global__ __launch_bounds__(CFG::THREADS + 256, 1) void gemm_ws_kernel(
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[ks][0][j], af[ks][0][i], acc[i][j], 0, 0, 0);
       }
     };
-    if constexpr (PROBE != 13 && !P_NO_MFMA) {
-      // interleaved order: A_0, W_0..W_{FN-1}, A_1, ... read in the order the i-major MFMAs
-      // consume them, with no barrier between the reads and the MFMAs, so the first MFMA
-      // waits for 4 reads instead of 13 (all 8 waves issue their reads together after the
-      // barrier; the LDS serves them interleaved). 123 instead of 138 VGPRs; measured
-      // (profiles/r02e_gemm_ilv.jsonl, same process, PROBE 13 = the previous all-reads-first
-      // order): 117K-token layer fp16x3 1.274 -> 1.264 ms, fp16 0.586 -> 0.581, QKV -3 to -6%,
-      // the others within +-1%.
-      if (rd_a) read_a(0);
-      if (rd_w)
-#pragma unroll
-        for (int j = 0; j < FN; ++j)    // W_j's planes together: MFMA (0, j) needs 2 + 2j reads
-#pragma unroll
+    // the upper-row MFMA waves of a half tile (split last round) have no rows: no reads,
+    // MFMAs or stores (they still keep the ring's barriers)
+    const bool idle = halves && it_c == n_full && wr >= CFG::WAVES_M / 2;
+    if (!idle) {
+      if constexpr (PROBE != 13 && !P_NO_MFMA) {
+        // interleaved order: A_0, W_0..W_{FN-1}, A_1, ... read in the order the i-major MFMAs
+        // consume them, with no barrier between the reads and the MFMAs, so the first MFMA
+        // waits for 4 reads instead of 13 (all 8 waves issue their reads together after the
+        // barrier; the LDS serves them interleaved). 123 instead of 138 VGPRs; measured
+        // (profiles/r02e_gemm_ilv.jsonl, same process, PROBE 13 = the previous all-reads-first
+        // order): 117K-token layer fp16x3 1.274 -> 1.264 ms, fp16 0.586 -> 0.581, QKV -3 to -6%,
+        // the others within +-1%.
+        if (rd_a) read_a(0);
+        if (rd_w)
+  #pragma unroll
+          for (int j = 0; j < FN; ++j)    // W_j's planes together: MFMA (0, j) needs 2 + 2j reads
+  #pragma unroll
+            for (int ks = 0; ks < KSN; ++ks)
+  #pragma unroll
+              for (int p = 0; p < NPL; ++p)
+                wf[ks][p][j] = sw[p * W_H8 + swz<CPR>(wc * WTN + j * 16 + (lane & 15), ks * 4 + (lane >> 4))];
+  #pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          if (i + 1 < FM && rd_a) read_a(i + 1);
+  #pragma unroll
           for (int ks = 0; ks < KSN; ++ks)
-#pragma unroll
-            for (int p = 0; p < NPL; ++p)
-              wf[ks][p][j] = sw[p * W_H8 + swz<CPR>(wc * WTN + j * 16 + (lane & 15), ks * 4 + (lane >> 4))];
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        if (i + 1 < FM && rd_a) read_a(i + 1);
-#pragma unroll
+  #pragma unroll
+            for (int j = 0; j < FN; ++j) mma(ks, i, j);
+        }
+      } else {
+        if constexpr (!P_NO_MFMA) {
+  #pragma unroll
+          for (int i = 0; i < FM; ++i) read_a(i);
+          read_w();
+          __builtin_amdgcn_sched_barrier(0);
+        }
+  #pragma unroll
         for (int ks = 0; ks < KSN; ++ks)
-#pragma unroll
-          for (int j = 0; j < FN; ++j) mma(ks, i, j);
+  #pragma unroll
+          for (int i = 0; i < FM; ++i)
+  #pragma unroll
+            for (int j = 0; j < FN; ++j) mma(ks, i, j);
       }
-    } else {
-      if constexpr (!P_NO_MFMA) {
-#pragma unroll
-        for (int i = 0; i < FM; ++i) read_a(i);
-        read_w();
-        __builtin_amdgcn_sched_barrier(0);
-      }
-#pragma unroll
-      for (int ks = 0; ks < KSN; ++ks)
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j) mma(ks, i, j);
     }
     if (++slot_c == NS) slot_c = 0;
     if (++kt_c == nk) {               // tile done (stores never waited on)
       kt_c = 0;
-      int m0, nt;
-      tile_mn(it_c, m0, nt);
+      int m0, nt, m_end;
+      tile_mn(it_c, m0, nt, m_end);
       ++it_c;
       if (PROBE == 9) m0 = 0;   // every tile stored over the first row band: L2-resident writes
       const int n0 = nt * BN;
-      const __amdgpu_buffer_rsrc_t rc =
-          panel(static_cast<char*>(Cout) + (int64_t)m0 * N * OUT_B, (int64_t)(M - m0) * N * OUT_B);
+      const __amdgpu_buffer_rsrc_t rc = panel(static_cast<char*>(Cout) + (int64_t)m0 * N * OUT_B,
+                                              (int64_t)(m_end - m0) * N * OUT_B);
       __amdgpu_buffer_rsrc_t rl = rc;
       if constexpr (SPLIT && EPI != kEpiF32)
-        rl = panel(Clo + (int64_t)m0 * N, (int64_t)(M - m0) * N * 2);
-      if constexpr (DL) {
-        const int64_t sb = (int64_t)(M - m0) * kDlParts * 8;
+        rl = panel(Clo + (int64_t)m0 * N, (int64_t)(m_end - m0) * N * 2);
+      if (idle) {
+        // no rows of this wave in the half tile
+      } else if constexpr (DL) {
+        const int64_t sb = (int64_t)(m_end - m0) * kDlParts * 8;
         const __amdgpu_buffer_rsrc_t rso = panel(dl.st_out + (int64_t)m0 * kDlParts * 2, dl.st_out ? sb : 0);
         ws_dl_epilogue<EPI, CFG, AUX>(acc, bias_l, rc, rl, dls, rso, dl.st_in != nullptr, N, n0,
                                       wr, wc, lane, dl.eps);

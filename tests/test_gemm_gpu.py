@@ -174,3 +174,23 @@ def test_ws_flag_ring_bitwise(gpu, shape, epi, split):
     for x0, x1 in (zip(r0, r1) if isinstance(r0, tuple) else [(r0, r1)]):
         assert torch.equal(x0.view(torch.int16) if x0.dtype == torch.float16 else x0.view(torch.int32),
                            x1.view(torch.int16) if x1.dtype == torch.float16 else x1.view(torch.int32))
+
+
+@pytest.mark.parametrize("shape", [(117000, 384, 1536), (117000, 1152, 384), (70001, 1536, 384),
+                                   (20000, 384, 384)], ids=lambda s: "x".join(map(str, s)))
+@pytest.mark.parametrize("epi", [0, 2], ids=["f16", "f32"])
+@pytest.mark.parametrize("split", [False, True], ids=["fp16", "fp16x3"])
+def test_ws_split_last_round_bitwise(gpu, shape, epi, split):
+    """The WS kernel's split last round (the XCD's last r <= 16 tiles run as 128-row halves on
+    two workgroups each) computes every output row with the same per-tile arithmetic: equal
+    bit for bit to the kernel without it (RAG_GEMM_WS_NOHALF), rows of the half tiles and the
+    partial last panel included."""
+    from ragmi.encoders import linear
+    M, N, K = shape
+    a, al, w, wl, bias, _, _ = _operands(M, N, K, split, seed=M + 3 * N)
+    r0 = linear(a, w, bias, epi, al, wl, 33)
+    r1 = linear(a, w, bias, epi, al, wl, 19)
+    torch.cuda.synchronize()
+    for x0, x1 in (zip(r0, r1) if isinstance(r0, tuple) else [(r0, r1)]):
+        v = torch.int16 if x0.dtype == torch.float16 else torch.int32
+        assert torch.equal(x0.view(v), x1.view(v))
