@@ -682,6 +682,27 @@ __device__ __forceinline__ void dl_lane_stats(const floatx4& v, int g, float eps
 // the block's {mean, M2} per row. lds_f: bias | c1 (Ln*) or bias | gamma | beta (ResLn).
 // dls: the rows' prefetched statistics (dl_prefetch_stats); rs_out: the output stats panel
 // from the tile's row m0.
+// fragments (i, jp), (i, jp + 1) of a deferred-LN epilogue -> fp16 hi / lo planes (16-B
+// paired stores, store_f16_pair)
+template <int AUX, int FM, int FN>
+__device__ __forceinline__ void dl_store_pair(const floatx4 (&acc)[FM][FN], int i, int jp, int ml,
+                                              int N, int n0, int wc, int cofs,
+                                              __amdgpu_buffer_rsrc_t rc,
+                                              __amdgpu_buffer_rsrc_t rl) {
+  const int vo = (ml * N + n0 + wc * (16 * FN) + jp * 16 + cofs) * 2;
+  half4 ha, hb, la, lb;
+#pragma unroll
+  for (int r = 0; r < 4; r += 2) {
+    half2 h2, l2;
+    split16x2(acc[i][jp][r], acc[i][jp][r + 1], h2, l2);
+    ha[r] = h2[0]; ha[r + 1] = h2[1]; la[r] = l2[0]; la[r + 1] = l2[1];
+    split16x2(acc[i][jp + 1][r], acc[i][jp + 1][r + 1], h2, l2);
+    hb[r] = h2[0]; hb[r + 1] = h2[1]; lb[r] = l2[0]; lb[r + 1] = l2[1];
+  }
+  store_f16_pair<AUX>(ha, hb, rc, vo);
+  store_f16_pair<AUX>(la, lb, rl, vo);
+}
+
 template <int EPI, typename CFG, int AUX>
 __device__ __forceinline__ void ws_dl_epilogue(floatx4 (&acc)[CFG::FM][CFG::FN],
                                                const float* lds_f, __amdgpu_buffer_rsrc_t rc,
@@ -765,21 +786,23 @@ __device__ __forceinline__ void ws_dl_epilogue(floatx4 (&acc)[CFG::FM][CFG::FN],
         if constexpr (EPI == kEpiLnGeluF16) acc[i][j] = gelu_erf4(acc[i][j]);
       }
     }
+    if constexpr (EPI == kEpiResLn) {   // z planes (default policy): row group by row group
 #pragma unroll
-    for (int jp = 0; jp < FN; jp += 2) {
-      const int vo = (ml * N + n0 + wc * WTN + jp * 16 + cofs) * 2;
-      half4 ha, hb, la, lb;
-#pragma unroll
-      for (int r = 0; r < 4; r += 2) {
-        half2 h2, l2;
-        split16x2(acc[i][jp][r], acc[i][jp][r + 1], h2, l2);
-        ha[r] = h2[0]; ha[r + 1] = h2[1]; la[r] = l2[0]; la[r + 1] = l2[1];
-        split16x2(acc[i][jp + 1][r], acc[i][jp + 1][r + 1], h2, l2);
-        hb[r] = h2[0]; hb[r + 1] = h2[1]; lb[r] = l2[0]; lb[r + 1] = l2[1];
-      }
-      store_f16_pair<AUX>(ha, hb, rc, vo);
-      store_f16_pair<AUX>(la, lb, rl, vo);
+      for (int jp = 0; jp < FN; jp += 2) dl_store_pair<AUX>(acc, i, jp, ml, N, n0, wc, cofs, rc, rl);
     }
+  }
+  // QKV / FFN1 outputs (non-temporal): column pair outer, row group inner — the plain
+  // epilogue's order. Stored row group by row group like the z planes, these nt streams
+  // measured 1.37 / 1.42x their bytes in WRITE_SIZE inside the forward, 1.12 / 1.10x in this
+  // order (and FETCH 1.25 -> 1.22 / 1.55 -> 1.43x); the z planes go the other way (1.00 ->
+  // 1.14 / 1.20x), so they keep theirs (profiles/r02t_fwd_pmc.jsonl,
+  // r02u_fwd_pmc_storeorder_all.jsonl)
+  if constexpr (EPI != kEpiResLn) {
+#pragma unroll
+    for (int jp = 0; jp < FN; jp += 2)
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+        dl_store_pair<AUX>(acc, i, jp, wr * WTM + i * 16 + (lane & 15), N, n0, wc, cofs, rc, rl);
   }
 }
 
