@@ -9,12 +9,19 @@ The corpus is fixed at 10M rows and sharded over the N ranks (strong scaling), c
 row ranges, identical data for every N (1M-row chunks, each from its own seed).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-       N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+       N > 1 either under a launcher that sets WORLD_SIZE / RANK / LOCAL_RANK
+       (python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...), or
+       plain `python bench.py --gpus N`: the process then starts N rank processes itself
+       (launch_ranks) before anything touches the GPU, and exits with their status.
+       WORLD_SIZE set but != N is an error (exit 2): the line's n_gpus is what ran.
 Rank 0 prints ONE JSON line.
 """
 import argparse
 import json
 import os
+import signal
+import socket
+import subprocess
 import sys
 import time
 
@@ -113,6 +120,29 @@ def cpu_baseline(corpus16_sample: np.ndarray, q: np.ndarray, n_total: int, budge
                       f"scaled linearly to {n_total} rows"}
 
 
+def scan_traffic(rows_per_gpu: int, storage: str = "fp16", path: str | None = None):
+    """HBM bytes per scan launch from the committed rocprofv3 --pmc FETCH_SIZE passes
+    (profiles/scan_pmc.json, written by scripts/profile.sh; x2 gfx950 correction), keyed by
+    the rows one launch scans: a rank's shard of R rows runs the same launch as a 1-GPU run
+    of `bench.py --rows R`. Returns (bytes, source) or (None, None) when no pass matches."""
+    path = path or os.path.join(ROOT, "profiles", "scan_pmc.json")
+    try:
+        with open(path) as f:
+            p = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    table = dict(p.get("by_rows_per_gpu", {}))
+    if "hbm_bytes_per_launch" in p:                 # the headline pass (10M rows per GPU)
+        table.setdefault(str(p.get("rows_per_gpu", 10_000_000)), p)
+    e = table.get(str(int(rows_per_gpu)))
+    if storage != "fp16" or not e or e.get("hbm_bytes_per_launch") is None:
+        return None, None
+    return e["hbm_bytes_per_launch"], (
+        "not measured in this run: rocprofv3 --pmc FETCH_SIZE pass (x2 gfx950 correction) "
+        f"of a scan launch over {int(rows_per_gpu)} rows, " + str(e.get("source")) + ", " +
+        str(e.get("commit", "")))
+
+
 def recall_fp32(q, gpu_ids, lo, hi, n_total, rank, world, dev, qchunk=512):
     """recall@5 against the UNROUNDED corpus ("also report recall vs the unrounded
     fp32 corpus") for every query of q [n, D]: each rank regenerates its rows in fp32, scores
@@ -191,6 +221,75 @@ def verify_exact(idx, q, gpu_s, gpu_ids, lo, rank, world, dev):
     return r5, ok
 
 
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv: list[str], cmd: list[str] | None = None,
+                 env: dict | None = None, poll_s: float = 0.05) -> int:
+    """Start `n` rank processes of this script (or of `cmd`) on this node with the env
+    contract of torch.distributed.run — RANK = LOCAL_RANK = r, WORLD_SIZE = LOCAL_WORLD_SIZE
+    = n, MASTER_ADDR 127.0.0.1, a free MASTER_PORT — and wait for them. The parent never
+    initialises the GPU (it only imports torch) and never execs: children are plain
+    subprocesses. If a rank fails, the others are terminated and its exit status returned
+    (a signal death -s as 128 + s); 0 when every rank exits 0."""
+    base = dict(os.environ if env is None else env)
+    base.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE=str(n),
+                LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", GROUP_WORLD_SIZE="1",
+                HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = cmd or [sys.executable, os.path.abspath(__file__)] + list(argv)
+    procs = [subprocess.Popen(cmd, env=dict(base, RANK=str(r), LOCAL_RANK=str(r),
+                                            ROLE_RANK=str(r)))
+             for r in range(n)]
+
+    def stop(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+    old = signal.signal(signal.SIGTERM, lambda *a: (stop(), sys.exit(143)))
+    rc = 0
+    try:
+        live = set(range(n))
+        while live:
+            for r in sorted(live):
+                c = procs[r].poll()
+                if c is None:
+                    continue
+                live.discard(r)
+                if c != 0 and rc == 0:
+                    rc = c if c > 0 else 128 - c
+                    stop()
+            if live:
+                time.sleep(poll_s)
+    finally:
+        stop()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        signal.signal(signal.SIGTERM, old)
+    return rc
+
+
+def check_world(gpus: int, environ=None) -> int:
+    """World size the run will have: WORLD_SIZE when a launcher set it (it must equal --gpus),
+    else --gpus (launch_ranks starts the ranks when > 1). Raises SystemExit(2) on mismatch."""
+    environ = os.environ if environ is None else environ
+    if gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if "WORLD_SIZE" in environ:
+        w = int(environ["WORLD_SIZE"])
+        if w != gpus:
+            print(f"bench.py: WORLD_SIZE={w} from the launcher but --gpus {gpus}; refusing "
+                  "to report a line whose n_gpus differs from the request", file=sys.stderr)
+            raise SystemExit(2)
+        return w
+    return gpus
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -221,6 +320,11 @@ def main():
     ap.add_argument("--precision", choices=["fp16x3", "fp16"], default="fp16x3",
                     help="encoder precision for --config 2/3 (fp16x3 = the 1e-3 contract)")
     args = ap.parse_args()
+    world = check_world(args.gpus)
+    if world > 1 and "WORLD_SIZE" not in os.environ:
+        # plain `python bench.py --gpus N`: one rank process per GPU, started before this
+        # process touches the GPU; rank 0 prints the line
+        sys.exit(launch_ranks(world, sys.argv[1:]))
     if args.config != "4":
         sys.path.insert(0, os.path.join(ROOT, "scripts"))
         import bench_modes
@@ -228,11 +332,11 @@ def main():
             args.rows = 0            # each mode's own default size
         return bench_modes.run(args)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
     torch.cuda.set_device(dev)
+    backend, ranks_seen = None, 1
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         backend = os.environ.get("RAGMI_DIST_BACKEND", "nccl")   # nccl = RCCL over xGMI
@@ -240,6 +344,10 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
+        backend = dist.get_backend()
+        ranks_seen = dist.get_world_size()
+        if ranks_seen != world:
+            raise SystemExit(f"bench.py: process group has {ranks_seen} ranks, expected {world}")
 
     from ragmi.dist import ShardedIndex
     from ragmi.index import busy_union_ms
@@ -362,9 +470,13 @@ def main():
                      "recall_at_5_vs_fp32_corpus_min": round(float(f32_b.min()), 6)}
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and not args.no_cpu:
+        # at every N (north_star: the CPU path "in the same run"), rank 0, after the timed
+        # region: the whole-corpus CPU rate, from a sample of rank 0's shard
         sample = idx.export_rows(0, min(CHUNK, hi - lo))
         cpu = cpu_baseline(sample, qs[args.warmup].cpu().numpy(), n_total, args.cpu_budget)
+    if world > 1:
+        dist.barrier()
 
     if rank == 0:
         local_rows = hi - lo
@@ -374,23 +486,15 @@ def main():
         # (the union of the launches' HIP-event intervals over the timed region, / launches);
         # without overlap this IS the average launch duration (avg_ms)
         achieved = algo_bytes / (busy_ms * 1e-3)
-        traffic, traffic_source = None, None
-        pmc = os.path.join(ROOT, "profiles", "scan_pmc.json")
-        if os.path.exists(pmc) and world == 1 and n_total == 10_000_000:
-            try:
-                p = json.load(open(pmc))
-                traffic = p.get("hbm_bytes_per_launch")
-                traffic_source = ("not measured in this run: rocprofv3 --pmc FETCH_SIZE pass "
-                                  "of this bench command (x2 gfx950 correction), " +
-                                  str(p.get("source")) + ", " + str(p.get("commit", "")))
-            except Exception:
-                traffic = None
+        traffic, traffic_source = scan_traffic(local_rows, args.storage)
         qps = B * args.steps / elapsed
         line = {
             "metric": "queries/sec + recall@5, batch=32 over 10Mx384 corpus",
             "value": round(qps, 2),
             "unit": "queries/s",
             "n_gpus": world,
+            "backend": backend,            # torch.distributed backend ("nccl" = RCCL); None at N=1
+            "ranks_seen": ranks_seen,      # dist.get_world_size() of the process group
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -16,6 +17,9 @@
 namespace {
 
 using namespace ragmi::bert;
+
+// largest static fp16 range bound accepted (fp16 max 65504; see range_bounds)
+constexpr double kF16Safe = 60000.0;
 
 struct Layer {
   _Float16 *wqkv = nullptr, *wo = nullptr, *w1 = nullptr, *w2 = nullptr;
@@ -98,6 +102,10 @@ struct rag_encoder {
   int fuse_ln = -1;
   // deferred LayerNorm on the token rows (fp16x3, hidden 384): -1 auto, 0 off, 1 on
   int defer_ln = -1;
+  // static fp16 range analysis of the weights (range_bounds): the largest |value| any fp16
+  // (hi) plane of the forward can hold, for any input — without / with the deferred LayerNorm
+  // (whose z planes hold the un-normalised residual sums)
+  double bound_plain = 0.0, bound_defer = 0.0;
   // host-entry staging
   void* stage = nullptr;
   size_t stage_bytes = 0;
@@ -541,7 +549,9 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
   // deferred LayerNorm (DlArgs): auto once every token-row GEMM is a WS one (AUTO's choice:
   // the 384-wide projections' 256 x 128 tiles reach half the CUs, ~11K tokens)
   const bool dl = [&] {
-    if (e->defer_ln == 0 || H != kDlH || !w->xl || !w->sa || !e->layers[0].w1_f) return false;
+    if (e->defer_ln == 0 || H != kDlH || !w->xl || !w->sa || !e->layers[0].w1_f ||
+        e->bound_defer > kF16Safe)
+      return false;
     if (!dl_gemm_ok(kEpiLnF16, T, 3 * H, H) || !dl_gemm_ok(kEpiLnGeluF16, T, FF, H) ||
         !dl_gemm_ok(kEpiResLn, T, H, H) || !dl_gemm_ok(kEpiResLn, T, H, FF))
       return false;
@@ -671,6 +681,69 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
   return RAG_OK;
 }
 
+// fp16 range guard. Every activation the forward stores as an fp16 plane is bounded, for ANY
+// input, by the weights alone (interval arithmetic, modeling_bert.py's layer, restated):
+//   LayerNorm output  |y_i| <= |gamma_i| sqrt(H - 1) + |beta_i|   (a standardised entry of H
+//                     values is at most sqrt(H - 1) in magnitude; eps only shrinks it)
+//   Linear output     |(W x + b)_j| <= sum_i |W_ji| bound(x_i) + |b_j|
+//   attention context a convex combination of V rows: <= bound(V) per dimension
+//   erf-GELU          |gelu(y)| <= max(|y|, 0.17)
+// The plain forward stores LN outputs (xh/xl), Q|K|V, the attention context and the FFN
+// intermediate in fp16 planes; the O-proj / FFN2 outputs and every pre-LN residual sum stay
+// fp32. The deferred-LayerNorm forward (DlArgs) stores the pre-LN sums z = x + sublayer
+// output as planes too. fp16 overflows above 65504; kF16Safe leaves margin for the fp32
+// rounding of the bounded quantities themselves. So:
+//   bound_plain > kF16Safe -> rag_encoder_create refuses the weights (RAG_ERANGE);
+//   bound_defer > kF16Safe -> the deferred LayerNorm is never used (auto skips it, forcing it
+//                             on fails).
+// Real BERT checkpoints are far inside: the stress profile of ragmi.synth (outlier
+// dimensions with gammas up to 20, |hidden| ~ 100-400) gives 790 / 15.6K.
+void range_bounds(const rag_bert_config& c, const float* const* w, double* plain,
+                  double* defer) {
+  const int H = c.hidden, FF = c.intermediate;
+  const double s = std::sqrt((double)(H - 1));
+  auto ln = [&](const float* g, const float* b, std::vector<double>& out) {
+    out.resize(H);
+    for (int i = 0; i < H; ++i) out[i] = std::fabs((double)g[i]) * s + std::fabs((double)b[i]);
+  };
+  auto lin = [&](const float* W, const float* b, int N, int K, const std::vector<double>& x,
+                 std::vector<double>& out) {
+    out.resize(N);
+    for (int n = 0; n < N; ++n) {
+      double a = std::fabs((double)b[n]);
+      const float* r = W + (size_t)n * K;
+      for (int k = 0; k < K; ++k) a += std::fabs((double)r[k]) * x[k];
+      out[n] = a;
+    }
+  };
+  auto mx = [](const std::vector<double>& v) {
+    double m = 0.0;
+    for (double x : v) m = std::max(m, x);
+    return m;
+  };
+  std::vector<double> g, q, k, v, a, g1, f, o, g2;
+  ln(w[3], w[4], g);
+  double bp = mx(g), bd = 0.0;
+  for (int l = 0; l < c.layers; ++l) {
+    const float* const* p = w + 5 + 16 * l;
+    lin(p[0], p[1], H, H, g, q);
+    lin(p[2], p[3], H, H, g, k);
+    lin(p[4], p[5], H, H, g, v);                       // context <= V per dimension
+    lin(p[6], p[7], H, H, v, a);                       // O-proj (fp32)
+    for (int i = 0; i < H; ++i) bd = std::max(bd, g[i] + a[i]);          // z1
+    ln(p[8], p[9], g1);
+    lin(p[10], p[11], FF, H, g1, f);
+    for (double& x : f) x = std::max(x, 0.17);         // erf-GELU
+    lin(p[12], p[13], H, FF, f, o);                    // FFN2 (fp32)
+    for (int i = 0; i < H; ++i) bd = std::max(bd, g1[i] + o[i]);         // z2
+    ln(p[14], p[15], g2);
+    bp = std::max({bp, mx(q), mx(k), mx(v), mx(g1), mx(f), mx(g2)});
+    g.swap(g2);
+  }
+  *plain = bp;
+  *defer = std::max(bp, bd);
+}
+
 // Built (hidden, head_dim) shapes: 384/32 (bge-small, MiniLM-L6), 768/64 (bge-base),
 // 1024/64 (bge-large, SURVEY config 5).
 bool shape_supported(int hidden, int heads) {
@@ -726,6 +799,13 @@ int rag_encoder_create(const rag_bert_config* cfg, const float* const* w, int n_
     return ragmi::fail(RAG_EINVAL, "wrong number of weight tensors");
   for (int i = 0; i < n_weights; ++i)
     if (!w[i]) return ragmi::fail(RAG_EINVAL, "NULL weight tensor");
+  double b_plain = 0.0, b_defer = 0.0;
+  range_bounds(*cfg, w, &b_plain, &b_defer);
+  if (!(b_plain <= kF16Safe))
+    return ragmi::fail(RAG_ERANGE,
+                       "weights can drive an fp16 activation plane past 65504 (static bound " +
+                           std::to_string(b_plain) +
+                           "; see rag_encoder_range_bounds): refusing rather than returning inf");
   RAG_HIP(hipSetDevice(device));
   // attention stages K/V in dynamic LDS (up to 160 KB)
   {
@@ -739,6 +819,8 @@ int rag_encoder_create(const rag_bert_config* cfg, const float* const* w, int n_
   e->device = device;
   e->fuse_ln = fuse_ln_default();
   e->defer_ln = defer_ln_default();
+  e->bound_plain = b_plain;
+  e->bound_defer = b_defer;
   int rc = RAG_OK;
   auto chk = [&](int r) {
     if (r && !rc) rc = r;
@@ -998,8 +1080,34 @@ int rag_encoder_set_fusion(rag_encoder_t* e, int mode) {
 int rag_encoder_set_defer_ln(rag_encoder_t* e, int mode) {
   ragmi::clear_error();
   if (!e || mode < -1 || mode > 1) return ragmi::fail(RAG_EINVAL, "mode: -1 auto, 0 off, 1 on");
+  if (mode == 1 && !(e->bound_defer <= kF16Safe))
+    return ragmi::fail(RAG_ERANGE, "deferred LayerNorm refused: these weights can drive its "
+                                   "un-normalised residual planes past fp16 range (static "
+                                   "bound " + std::to_string(e->bound_defer) + ")");
   std::lock_guard<std::mutex> lk(e->mu);
   e->defer_ln = mode;
+  return RAG_OK;
+}
+
+int rag_encoder_range_bounds(const rag_encoder_t* e, double* plain, double* deferred) {
+  ragmi::clear_error();
+  if (!e) return ragmi::fail(RAG_EINVAL, "encoder is NULL");
+  if (plain) *plain = e->bound_plain;
+  if (deferred) *deferred = e->bound_defer;
+  return RAG_OK;
+}
+
+int rag_encoder_weight_bounds(const rag_bert_config* cfg, const float* const* weights,
+                              int n_weights, double* plain, double* deferred) {
+  ragmi::clear_error();
+  if (!cfg || !weights || n_weights != rag_encoder_num_weights(cfg))
+    return ragmi::fail(RAG_EINVAL, "bad config / weights");
+  for (int i = 0; i < n_weights; ++i)
+    if (!weights[i]) return ragmi::fail(RAG_EINVAL, "NULL weight tensor");
+  double p = 0.0, d = 0.0;
+  range_bounds(*cfg, weights, &p, &d);
+  if (plain) *plain = p;
+  if (deferred) *deferred = d;
   return RAG_OK;
 }
 

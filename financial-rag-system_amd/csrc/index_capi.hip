@@ -658,14 +658,22 @@ int rag_index_reserve(rag_index_t* h, int64_t capacity_rows) {
   RAG_HIP(hipSetDevice(h->device));
   half8* nc = nullptr;
   uint32_t* nt = nullptr;
+  float* n32 = nullptr;
+  // the new buffers are freed on every error return below; released once the handle owns them
+  struct Guard {
+    half8** c; uint32_t** t; float** f;
+    ~Guard() {
+      if (*c) (void)hipFree(*c);
+      if (*t) (void)hipFree(*t);
+      if (*f) (void)hipFree(*f);
+    }
+  } guard{&nc, &nt, &n32};
   int rc = alloc_corpus(h, cap, &nc, &nt);
   if (rc) return rc;
-  float* n32 = nullptr;
   if (h->rows32) {
     const size_t b32 = (size_t)cap * h->dim * 4;
     if (hipMalloc(reinterpret_cast<void**>(&n32), b32) != hipSuccess) {
-      (void)hipFree(nc);
-      (void)hipFree(nt);
+      n32 = nullptr;
       return ragmi::fail(RAG_ENOMEM, "hipMalloc(rows32) failed");
     }
     RAG_HIP(hipMemset(n32, 0, b32));
@@ -682,6 +690,9 @@ int rag_index_reserve(rag_index_t* h, int64_t capacity_rows) {
   h->tags = nt;
   h->rows32 = n32;
   h->cap_rows = cap;
+  nc = nullptr;                                  // owned by the handle now
+  nt = nullptr;
+  n32 = nullptr;
   return RAG_OK;
 }
 

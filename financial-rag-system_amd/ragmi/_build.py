@@ -35,15 +35,18 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not needs_build():
         return LIB_PATH
     srcs = [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
-    objs = []
-    for src in srcs:
+    objs, procs = [], []
+    for src in srcs:                     # translation units compile in parallel
         obj = os.path.join(CSRC, os.path.basename(src) + ".o")
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
                "-fno-strict-aliasing", "-Wall", "-Wno-unused-function", "-c", src, "-o", obj]
         if verbose:
             print(" ".join(cmd))
-        subprocess.check_call(cmd)
+        procs.append((subprocess.Popen(cmd), cmd))
         objs.append(obj)
+    failed = [cmd for p, cmd in procs if p.wait() != 0]
+    if failed:
+        raise subprocess.CalledProcessError(1, failed[0])
     tmp = LIB_PATH + ".tmp"
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
     if verbose:

@@ -118,6 +118,12 @@ BERT_API = {
                                             ctypes.c_int, c_vp, c_vp, c_vp, c_vp]),
     "rag_encoder_set_fusion": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "rag_encoder_set_defer_ln": (ctypes.c_int, [c_vp, ctypes.c_int]),
+    "rag_encoder_range_bounds": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_double),
+                                                ctypes.POINTER(ctypes.c_double)]),
+    "rag_encoder_weight_bounds": (ctypes.c_int, [ctypes.POINTER(RagBertConfig),
+                                                 ctypes.POINTER(ctypes.POINTER(ctypes.c_float)),
+                                                 ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                                 ctypes.POINTER(ctypes.c_double)]),
     "rag_bert_gemm_dl": (ctypes.c_int, [ctypes.c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                         c_vp, c_vp, ctypes.c_float, ctypes.c_int, ctypes.c_int,
                                         ctypes.c_int, c_vp, c_vp, c_vp, c_vp]),

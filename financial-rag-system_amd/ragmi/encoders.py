@@ -14,6 +14,7 @@ access, and no CPU forward to fall back to.
 from __future__ import annotations
 
 import ctypes
+import itertools
 import json
 import os
 
@@ -65,10 +66,100 @@ def load_safetensors(path: str) -> dict:
 
 
 def config_from_hf(cfg: dict) -> dict:
-    return dict(vocab=cfg["vocab_size"], hidden=cfg["hidden_size"],
-                layers=cfg["num_hidden_layers"], heads=cfg["num_attention_heads"],
-                inter=cfg["intermediate_size"], max_pos=cfg["max_position_embeddings"],
-                type_vocab=cfg.get("type_vocab_size", 2), eps=cfg.get("layer_norm_eps", 1e-12))
+    """HF BertConfig dict -> encoder shape. Refuses what the kernels do not implement (they
+    hard-code erf-GELU, absolute positions and post-LN BERT, modeling_bert.py:96-107,325-351)
+    instead of running a different function silently."""
+    act = cfg.get("hidden_act", "gelu")
+    if act != "gelu":
+        raise NotImplementedError(f"hidden_act {act!r}: only erf-GELU ('gelu') is implemented")
+    pos = cfg.get("position_embedding_type", "absolute")
+    if pos != "absolute":
+        raise NotImplementedError(f"position_embedding_type {pos!r}: only 'absolute'")
+    mt = cfg.get("model_type", "bert")
+    if mt != "bert":
+        raise NotImplementedError(f"model_type {mt!r}: only 'bert'")
+    out = dict(vocab=cfg["vocab_size"], hidden=cfg["hidden_size"],
+               layers=cfg["num_hidden_layers"], heads=cfg["num_attention_heads"],
+               inter=cfg["intermediate_size"], max_pos=cfg["max_position_embeddings"],
+               type_vocab=cfg.get("type_vocab_size", 2), eps=cfg.get("layer_norm_eps", 1e-12))
+    out["num_labels"] = hf_num_labels(cfg)
+    return out
+
+
+def hf_num_labels(cfg: dict) -> int:
+    """PretrainedConfig.num_labels: len(id2label) when present, else num_labels, else 2 (the
+    transformers default)."""
+    if cfg.get("id2label"):
+        return len(cfg["id2label"])
+    return int(cfg.get("num_labels", 2))
+
+
+# sentence-transformers' activation names (CrossEncoder: config.json
+# "sentence_transformers": {"activation_fn": ...} (v4+) or "sbert_ce_default_activation_function"
+# (v2/v3)) -> the activations this head implements
+_ACTIVATIONS = {
+    "torch.nn.modules.linear.Identity": "identity", "torch.nn.Identity": "identity",
+    "torch.nn.modules.activation.Sigmoid": "sigmoid", "torch.nn.Sigmoid": "sigmoid",
+}
+
+
+def ce_activation(hf_cfg: dict | None, override=None) -> str:
+    """The activation sentence-transformers' CrossEncoder applies to the logits in predict()
+    (reference main.py:245 returns these scores to users as sources[].score):
+      1. an explicit override (CrossEncoder(..., activation_fn=...));
+      2. config.json "sentence_transformers"."activation_fn" (sentence-transformers >= 4);
+      3. config.json "sbert_ce_default_activation_function" (2.x / 3.x; the
+         ms-marco-MiniLM-L-6-v2 checkpoint sets torch.nn.modules.linear.Identity);
+      4. otherwise Sigmoid when num_labels == 1 (Identity for more labels, which this head
+         does not implement).
+    Returns "identity" or "sigmoid"; anything else raises NotImplementedError."""
+    hf_cfg = hf_cfg or {}
+    name = override
+    if name is None:
+        name = (hf_cfg.get("sentence_transformers") or {}).get("activation_fn")
+    if name is None:
+        name = hf_cfg.get("sbert_ce_default_activation_function")
+    if name is None:
+        return "sigmoid" if hf_num_labels(hf_cfg) == 1 else "identity"
+    if isinstance(name, torch.nn.Module):
+        name = type(name).__module__ + "." + type(name).__name__
+    if name in ("identity", "sigmoid"):
+        return name
+    if name not in _ACTIVATIONS:
+        raise NotImplementedError(f"cross-encoder activation {name!r}: only Identity and "
+                                  "Sigmoid are implemented")
+    return _ACTIVATIONS[name]
+
+
+_POOL_MODES = ("pooling_mode_cls_token", "pooling_mode_mean_tokens", "pooling_mode_max_tokens",
+               "pooling_mode_mean_sqrt_len_tokens", "pooling_mode_weightedmean_tokens",
+               "pooling_mode_lasttoken")
+
+
+def st_head_from_dir(model_dir: str) -> int:
+    """The sentence-transformers module stack of a local checkpoint (modules.json +
+    <pooling>/config.json) -> the encoder head. Implemented: Transformer -> Pooling(cls) ->
+    Normalize (bge-small-en-v1.5's stack: HEAD_CLS_L2). Everything else raises — including a
+    directory without modules.json, for which sentence-transformers would build MEAN pooling
+    (a different embedding), so it must not silently get the CLS head."""
+    mj = os.path.join(model_dir, "modules.json")
+    if not os.path.exists(mj):
+        raise NotImplementedError(
+            f"{model_dir}: no modules.json (sentence-transformers would use mean pooling; "
+            "only Transformer -> Pooling(cls) -> Normalize is implemented)")
+    with open(mj) as f:
+        mods = json.load(f)
+    types = [m.get("type", "").rsplit(".", 1)[-1] for m in mods]
+    if types != ["Transformer", "Pooling", "Normalize"]:
+        raise NotImplementedError(f"{model_dir}: module stack {types}; only "
+                                  "[Transformer, Pooling, Normalize] is implemented")
+    with open(os.path.join(model_dir, mods[1].get("path", ""), "config.json")) as f:
+        pc = json.load(f)
+    on = [m for m in _POOL_MODES if pc.get(m)]
+    if on != ["pooling_mode_cls_token"]:
+        raise NotImplementedError(f"{model_dir}: pooling {on or 'none'}; only CLS pooling is "
+                                  "implemented")
+    return HEAD_CLS_L2
 
 
 # ------------------------------------------------------------------ one encoder GEMM
@@ -178,6 +269,32 @@ def linear_dl(epilogue: int, a: torch.Tensor, a_lo: torch.Tensor, w: torch.Tenso
         torch.cuda.current_stream(a.device).cuda_stream))
 
 
+def _weight_ptrs(cfg: dict, weights: dict, head: int, precision: str):
+    c = _lib.RagBertConfig(cfg["vocab"], cfg["hidden"], cfg["layers"], cfg["heads"],
+                           cfg["inter"], cfg["max_pos"], cfg["type_vocab"], cfg["eps"], head,
+                           PRECISIONS[precision])
+    names = weight_order(cfg["layers"], head)
+    if _lib.load().rag_encoder_num_weights(ctypes.byref(c)) != len(names):
+        raise RuntimeError("weight order / ABI mismatch")
+    arrs = [np.ascontiguousarray(_lookup(weights, n), dtype=np.float32) for n in names]
+    ptrs = (ctypes.POINTER(ctypes.c_float) * len(arrs))(
+        *[a.ctypes.data_as(ctypes.POINTER(ctypes.c_float)) for a in arrs])
+    return c, arrs, ptrs
+
+
+def weight_bounds(cfg: dict, weights: dict, head: int = None) -> tuple[float, float]:
+    """Static fp16 range bounds of a model's weights (rag_encoder_weight_bounds, host only):
+    (plain, deferred) = the largest |value| any fp16 activation plane of the forward can hold
+    for any input, without / with the deferred LayerNorm. create refuses plain > 60000; the
+    deferred LayerNorm is not used above 60000."""
+    head = HEAD_CLS_L2 if head is None else head
+    c, arrs, ptrs = _weight_ptrs(cfg, weights, head, "fp16x3")
+    p, d = ctypes.c_double(), ctypes.c_double()
+    check(_lib.load().rag_encoder_weight_bounds(ctypes.byref(c), ptrs, len(arrs),
+                                                ctypes.byref(p), ctypes.byref(d)))
+    return p.value, d.value
+
+
 # ------------------------------------------------------------------ device encoder
 class BertEncoder:
     """One encoder instance in HBM (fp16 GEMM weights, fp32 norms/embeddings)."""
@@ -192,15 +309,7 @@ class BertEncoder:
             self.device = torch.device("cuda", torch.cuda.current_device())
         self.cfg, self.head = dict(cfg), head
         self.precision = precision
-        c = _lib.RagBertConfig(cfg["vocab"], cfg["hidden"], cfg["layers"], cfg["heads"],
-                               cfg["inter"], cfg["max_pos"], cfg["type_vocab"], cfg["eps"], head,
-                               PRECISIONS[precision])
-        names = weight_order(cfg["layers"], head)
-        if self._L.rag_encoder_num_weights(ctypes.byref(c)) != len(names):
-            raise RuntimeError("weight order / ABI mismatch")
-        arrs = [np.ascontiguousarray(_lookup(weights, n), dtype=np.float32) for n in names]
-        ptrs = (ctypes.POINTER(ctypes.c_float) * len(arrs))(
-            *[a.ctypes.data_as(ctypes.POINTER(ctypes.c_float)) for a in arrs])
+        c, arrs, ptrs = _weight_ptrs(cfg, weights, head, precision)
         h = ctypes.c_void_p()
         check(self._L.rag_encoder_create(ctypes.byref(c), ptrs, len(arrs), self.device.index,
                                          ctypes.byref(h)))
@@ -215,6 +324,12 @@ class BertEncoder:
         """Deferred LayerNorm on the token rows (fp16x3, hidden 384; ragmi_bert.h
         rag_encoder_set_defer_ln): -1 auto, 0 off, 1 on where the model allows."""
         check(self._L.rag_encoder_set_defer_ln(self._h, int(mode)))
+
+    def range_bounds(self) -> tuple[float, float]:
+        """(plain, deferred) static fp16 range bounds of this model (rag_encoder_range_bounds)."""
+        p, d = ctypes.c_double(), ctypes.c_double()
+        check(self._L.rag_encoder_range_bounds(self._h, ctypes.byref(p), ctypes.byref(d)))
+        return p.value, d.value
 
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:
@@ -334,11 +449,25 @@ class WordPiece:
                    tokenize_chinese_chars=bool(tc.get("tokenize_chinese_chars", True)))
 
     def encode_packed(self, texts, pairs=None):
-        encs = (self.tok.encode_batch(list(texts)) if pairs is None else
-                self.tok.encode_batch(list(zip(texts, pairs))))
-        ids = np.concatenate([np.asarray(e.ids, np.int32) for e in encs])
-        types = np.concatenate([np.asarray(e.type_ids, np.int32) for e in encs])
-        cu = np.concatenate([[0], np.cumsum([len(e.ids) for e in encs])]).astype(np.int32)
+        """Packed WordPiece ids / token types (int32 [T]) and cu_seqlens (int32 [B+1]) of a
+        batch of texts (or (text, pair) pairs). Uses the Rust tokenizer's offset-free batch
+        encoder (`encode_batch_fast`: same ids and type ids, no character offsets, ~5x less
+        host time per batch) and packs with one fromiter per array."""
+        inp = list(texts) if pairs is None else list(zip(texts, pairs))
+        raw = getattr(self.tok, "_tokenizer", None)
+        encs = (raw.encode_batch_fast(inp) if raw is not None and
+                hasattr(raw, "encode_batch_fast") else self.tok.encode_batch(inp))
+        id_lists = [e.ids for e in encs]
+        lens = np.fromiter((len(x) for x in id_lists), np.int32, len(id_lists))
+        T = int(lens.sum())
+        ids = np.fromiter(itertools.chain.from_iterable(id_lists), np.int32, T)
+        if pairs is None:
+            types = np.zeros(T, np.int32)
+        else:
+            types = np.fromiter(itertools.chain.from_iterable(e.type_ids for e in encs),
+                                np.int32, T)
+        cu = np.zeros(len(id_lists) + 1, np.int32)
+        np.cumsum(lens, out=cu[1:])
         return ids, types, cu
 
 
@@ -348,7 +477,7 @@ def _load_dir(model_dir: str):
     st = os.path.join(model_dir, "model.safetensors")
     if not os.path.exists(st):
         raise FileNotFoundError(f"{st}: only safetensors checkpoints are loaded")
-    return config_from_hf(hf), load_safetensors(st), os.path.join(model_dir, "vocab.txt")
+    return config_from_hf(hf), load_safetensors(st), os.path.join(model_dir, "vocab.txt"), hf
 
 
 # ------------------------------------------------------------------ reference-shaped APIs
@@ -358,7 +487,8 @@ class SentenceTransformer:
     def __init__(self, model_dir: str | None = None, device=None, *, cfg=None, weights=None,
                  vocab_file=None, max_seq_length: int | None = None, precision: str = "fp16x3"):
         if model_dir is not None:
-            cfg, weights, vocab_file = _load_dir(model_dir)
+            st_head_from_dir(model_dir)            # refuses any head but CLS + Normalize
+            cfg, weights, vocab_file, _ = _load_dir(model_dir)
         if cfg is None or weights is None:
             raise ValueError("need a local model_dir or cfg + weights (no hub access)")
         self.encoder = BertEncoder(cfg, weights, HEAD_CLS_L2, device, precision)
@@ -390,20 +520,41 @@ class SentenceTransformer:
 
 
 class CrossEncoder:
-    """`CrossEncoder(model_dir).predict([[q, t], ...])` for ms-marco-MiniLM-L-6-v2: raw logits
-    (identity activation, num_labels = 1)."""
+    """`CrossEncoder(model_dir).predict([[q, t], ...])` for ms-marco-MiniLM-L-6-v2
+    (BertForSequenceClassification, num_labels = 1). The activation applied to the logits is
+    sentence-transformers' (`ce_activation`): the checkpoint's configured one — Identity for
+    ms-marco-MiniLM-L-6-v2, i.e. raw logits, which frontend.py:112-117 then squashes itself —
+    or Sigmoid when num_labels == 1 and the config names none. `activation_fn` overrides it
+    (sentence-transformers' CrossEncoder(default_activation_function=...) /
+    (activation_fn=...)); predict(activation_fct=...) overrides it per call."""
 
     def __init__(self, model_dir: str | None = None, device=None, *, cfg=None, weights=None,
-                 vocab_file=None, max_length: int | None = None, precision: str = "fp16x3"):
+                 vocab_file=None, max_length: int | None = None, precision: str = "fp16x3",
+                 activation_fn=None, default_activation_function=None):
+        hf = None
         if model_dir is not None:
-            cfg, weights, vocab_file = _load_dir(model_dir)
+            cfg, weights, vocab_file, hf = _load_dir(model_dir)
         if cfg is None or weights is None:
             raise ValueError("need a local model_dir or cfg + weights (no hub access)")
+        nl = hf_num_labels(hf) if hf is not None else int(cfg.get("num_labels", 1))
+        if nl != 1:
+            raise NotImplementedError(f"num_labels {nl}: only the 1-logit head is implemented")
+        self.activation = ce_activation(
+            hf if hf is not None else {"num_labels": 1, **{k: cfg[k] for k in (
+                "sbert_ce_default_activation_function", "sentence_transformers") if k in cfg}},
+            activation_fn if activation_fn is not None else default_activation_function)
         self.encoder = BertEncoder(cfg, weights, HEAD_POOLER_CLS, device, precision)
         self.tokenizer = (WordPiece.from_model_dir(model_dir, max_length) if model_dir
                           else WordPiece(vocab_file, max_length or 512) if vocab_file else None)
 
-    def predict(self, sentences, batch_size: int = 32, convert_to_numpy: bool = True, **kwargs):
+    def _activate(self, logits: torch.Tensor, activation_fct=None) -> torch.Tensor:
+        if activation_fct is not None and not isinstance(activation_fct, (str, torch.nn.Module)):
+            return activation_fct(logits)              # a caller's own callable
+        act = self.activation if activation_fct is None else ce_activation(None, activation_fct)
+        return torch.sigmoid(logits) if act == "sigmoid" else logits
+
+    def predict(self, sentences, batch_size: int = 32, convert_to_numpy: bool = True,
+                activation_fct=None, **kwargs):
         pairs = [list(p) for p in sentences]
         if not pairs:
             return np.zeros((0,), np.float32)
@@ -415,8 +566,9 @@ class CrossEncoder:
             ids, types, cu = self.tokenizer.encode_packed([p[0] for p in chunk],
                                                           [p[1] for p in chunk])
             outs.append(self.encoder.forward_packed(ids, types, cu))
-        s = torch.cat(outs)
+        s = self._activate(torch.cat(outs), activation_fct)
         return s.cpu().numpy() if convert_to_numpy else s
 
-    def predict_ids(self, ids, types, cu) -> np.ndarray:
-        return self.encoder.forward_packed(ids, types, cu).cpu().numpy()
+    def predict_ids(self, ids, types, cu, activation_fct=None) -> np.ndarray:
+        return self._activate(self.encoder.forward_packed(ids, types, cu),
+                              activation_fct).cpu().numpy()

@@ -244,7 +244,11 @@ class FlatIndex:
     def exactness_stats(self, n_last: int = 0):
         """(tier1 total, tier2 total, tiers of the last pass's first n_last queries): which
         path certified each top-k (0 error-bound check, 1 list re-scoring, 2 second pass);
-        rag_index_exactness_stats. Synchronises the device."""
+        rag_index_exactness_stats. The totals count every query since creation; the per-query
+        tiers cover only the most recent PASS (<= 32 queries, <= 128 on the D = 1024 wide
+        scan) of this handle on any stream — not the whole last search when it had more
+        queries, and not a search of this thread when other threads search concurrently.
+        Synchronises the device."""
         t1 = ctypes.c_int64()
         t2 = ctypes.c_int64()
         last = np.empty((max(n_last, 0),), dtype=np.int32)

@@ -171,35 +171,46 @@ class Coalescer:
                 if req.exc is not None:
                     raise req.exc
                 return req.result
-        if self.window > 0:
-            t_end = time.perf_counter() + self.window
-            while time.perf_counter() < t_end:
-                with self.lock:
-                    if len(self.pending) >= self.max_batch:
-                        break
-                time.sleep(min(5e-5, self.window / 4))
-        with self.lock:
-            batch = self.pending[:self.max_batch]
-            del self.pending[:self.max_batch]
-            self.batches += 1
+        batch: list[_Req] = []
+        fatal = None
         try:
+            if self.window > 0:
+                t_end = time.perf_counter() + self.window
+                while time.perf_counter() < t_end:
+                    with self.lock:
+                        if len(self.pending) >= self.max_batch:
+                            break
+                    time.sleep(min(5e-5, self.window / 4))
+            with self.lock:
+                batch = self.pending[:self.max_batch]
+                del self.pending[:self.max_batch]
+                self.batches += 1
             hits = self.col.search(np.stack([r.q for r in batch]),
                                    max(r.limit for r in batch), [r.filt for r in batch])
             for r, h in zip(batch, hits):
                 r.result = h[:r.limit]
-        except Exception as e:                     # every rider sees the failure
+        except BaseException as e:                 # every rider sees the failure
             for r in batch:
                 r.exc = e
-        with self.lock:
-            if self.pending:                       # hand leadership to the oldest waiter
-                nxt = self.pending[0]
-                nxt.lead = True
-                nxt.wake.set()
-            else:
-                self.leader_active = False
-        for r in batch:
-            if r is not req:
-                r.wake.set()
+            if not isinstance(e, Exception):       # KeyboardInterrupt, SystemExit: re-raise
+                fatal = e                          # after the hand-off below
+        finally:
+            # whatever was raised: hand leadership on and wake every rider, so no caller of
+            # this collection can block forever behind a leader that is gone
+            with self.lock:
+                if req in self.pending:            # interrupted before taking the batch
+                    self.pending.remove(req)
+                if self.pending:                   # hand leadership to the oldest waiter
+                    nxt = self.pending[0]
+                    nxt.lead = True
+                    nxt.wake.set()
+                else:
+                    self.leader_active = False
+            for r in batch:
+                if r is not req:
+                    r.wake.set()
+        if fatal is not None:
+            raise fatal
         if req.exc is not None:
             raise req.exc
         return req.result

@@ -90,10 +90,33 @@ def read_meta(path: str) -> dict:
     return meta
 
 
+# Row-norm bounds the exact top-k certificate assumes (scan_kernels.hip kRowNorm, index_capi.hip
+# store_eps): a stored fp16 row is the RNE rounding of a unit vector, ||c|| - 1 within
+# 2^-11 + sqrt(D) 2^-25 (<= 1e-3 for D <= 1024); a stored fp32 row is fp32(x / ||x||),
+# ||y|| - 1 within 2^-20. Zero rows (never-filled slots, zero vectors) are allowed.
+NORM_TOL = {"fp16": 1e-3, "fp32": 2.0 ** -20}
+
+
+def check_row_norms(v: np.ndarray, storage: str, first_row: int = 0) -> None:
+    """Refuse rows a ragmi index could not have stored: the scan's per-query error bound (and
+    with it the certified exact top-k) holds only for normalised rows, so a hand-built or
+    corrupted shard must not load silently."""
+    if v.size == 0:
+        return
+    x = np.asarray(v, dtype=np.float64 if storage == "fp32" else np.float32)
+    nrm = np.sqrt(np.einsum("ij,ij->i", x, x, dtype=np.float64))
+    bad = ~((nrm == 0.0) | (np.abs(nrm - 1.0) <= NORM_TOL[storage]))
+    if bad.any():
+        r = int(np.argmax(bad))
+        raise ValueError(f"shard row {first_row + r} has norm {nrm[r]!r}: not a normalised "
+                         f"{storage} row (shards must come from save_index / save_sharded)")
+
+
 def load_into(index, path: str, row0: int = 0, chunk_rows: int = CHUNK_ROWS,
-              rows: tuple[int, int] | None = None) -> int:
+              rows: tuple[int, int] | None = None, check_norms: bool = True) -> int:
     """Copy a saved shard (or its row range `rows` = (start, stop)) into `index` at row0.
-    Returns the number of rows loaded. The index must have capacity for them."""
+    Returns the number of rows loaded. The index must have capacity for them. Every row's
+    norm is checked first (check_row_norms) unless check_norms=False."""
     meta = read_meta(path)
     if meta["dim"] != index.dim:
         raise ValueError(f"shard dim {meta['dim']} != index dim {index.dim}")
@@ -116,6 +139,8 @@ def load_into(index, path: str, row0: int = 0, chunk_rows: int = CHUNK_ROWS,
         m = min(chunk_rows, n - c0)
         v = np.asarray(vec[a + c0:a + c0 + m])
         t = np.asarray(tags[a + c0:a + c0 + m])
+        if check_norms:
+            check_row_norms(v, saved, a + c0)
         nc = max(index.count, row0 + c0 + m)
         if into == "fp32":
             index.import_rows32(v, row0 + c0, t, new_count=nc)

@@ -162,8 +162,11 @@ int rag_merge_topk_packed(const int32_t* in_packed_dev, int n_lists, int B, int 
  * was created, whose top-k was certified by the list re-scoring fallback / needed the second
  * pass over the shard (all other queries passed the error-bound check directly).
  * last_tiers (host, may be NULL when n_last == 0) receives, for the first n_last queries of
- * the most recent search pass, 0 / 1 / 2 = the path that certified them (-1 past the pass's
- * query count). Synchronises the device. */
+ * the most recent search PASS, 0 / 1 / 2 = the path that certified them (-1 past the pass's
+ * query count). Scope: a pass is one scan of <= 32 queries (<= 128 on the D = 1024 wide
+ * scan); a search of more queries runs several passes and only its last one is reported, and
+ * the state is per handle, so searches issued concurrently on several streams overwrite each
+ * other's record (the tier1 / tier2 totals are exact in every case). Synchronises the device. */
 int rag_index_exactness_stats(rag_index_t* index, int64_t* tier1, int64_t* tier2,
                               int32_t* last_tiers, int n_last);
 

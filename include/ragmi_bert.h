@@ -161,6 +161,20 @@ int rag_encoder_set_fusion(rag_encoder_t* e, int mode);
  * the model allows (fp16x3, hidden 384). */
 int rag_encoder_set_defer_ln(rag_encoder_t* e, int mode);
 
+/* fp16 range guard (no reference counterpart: the reference's torch forward is fp32). Every
+ * activation the forward keeps as an fp16 plane is bounded by the weights alone, for any input
+ * (interval arithmetic over the layer: |LN_i| <= |gamma_i| sqrt(H-1) + |beta_i|,
+ * |W x + b|_j <= sum |W_ji| bound(x_i) + |b_j|, context <= bound(V), |gelu(y)| <= |y|).
+ * plain: the largest such bound over the LN outputs, Q|K|V, attention context and FFN
+ * intermediate; deferred: also over the un-normalised residual sums z the deferred
+ * LayerNorm stores as planes. rag_encoder_create fails with RAG_ERANGE when plain > 60000
+ * (fp16 max 65504), and the deferred LayerNorm is never used when deferred > 60000
+ * (rag_encoder_set_defer_ln(1) then fails with RAG_ERANGE): no forward can return inf from an
+ * fp16 overflow. rag_encoder_weight_bounds computes the same from host weights (no device). */
+int rag_encoder_range_bounds(const rag_encoder_t* e, double* plain, double* deferred);
+int rag_encoder_weight_bounds(const rag_bert_config* cfg, const float* const* weights,
+                              int n_weights, double* plain, double* deferred);
+
 /* the deferred-LayerNorm GEMM epilogues alone (parity tests), on the WS kernel (fp16x3: A_lo,
  * W_lo, C_lo required): st_in / st_out are [M][6][2] floats ({mean, M2} of columns 64j..64j+63).
  *  RAG_EPI_LN_F16 / RAG_EPI_LN_GELU_F16 (K == 384, N % 128 == 0, N <= 2048): per row r with

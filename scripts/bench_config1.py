@@ -39,16 +39,8 @@ N_QUERIES = int(os.environ.get("N_QUERIES", 200))
 
 
 def write_model(d, cfg, w, vocab):
-    from safetensors.numpy import save_file
-    os.makedirs(d)
-    save_file(w, os.path.join(d, "model.safetensors"))
-    with open(os.path.join(d, "config.json"), "w") as f:
-        json.dump({"vocab_size": cfg["vocab"], "hidden_size": 384,
-                   "num_hidden_layers": cfg["layers"], "num_attention_heads": 12,
-                   "intermediate_size": 1536, "max_position_embeddings": 512,
-                   "type_vocab_size": 2, "layer_norm_eps": 1e-12}, f)
-    with open(os.path.join(d, "vocab.txt"), "w") as f:
-        f.write("\n".join(vocab) + "\n")
+    from ragmi.synth import write_checkpoint
+    write_checkpoint(d, cfg, w, vocab, "bge")
 
 
 def hf_bge(cfg, w):

@@ -48,6 +48,17 @@ def _max_over_ranks(vals, dev):
     return [float(v) for v in t]
 
 
+def _init_dist(dev):
+    """One process per GPU; backend from RAGMI_DIST_BACKEND (default nccl = RCCL over xGMI)."""
+    if _world()[0] > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        backend = os.environ.get("RAGMI_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+
+
 def _sync(dev):
     torch.cuda.synchronize(dev)
     if _world()[0] > 1:
@@ -98,7 +109,9 @@ def _line(metric, value, unit, args, elapsed, world, dtype, data, config, **extr
          "steps": args.steps, "warmup": args.warmup,
          "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
          "scaling": "strong" if config.get("corpus_rows") else "weak", "vs_baseline": None,
-         "dtype": dtype, "data": data, "config": config}
+         "dtype": dtype, "data": data, "config": config,
+         "backend": dist.get_backend() if dist.is_initialized() else None,
+         "ranks_seen": dist.get_world_size() if dist.is_initialized() else 1}
     d.update(extra)
     return d
 
@@ -203,10 +216,9 @@ def run_pipeline(args, cfg_id):
     from ragmi.index import FlatIndex
     from ragmi.pairs import build_pairs_gpu
     world, rank = _world()
-    dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+    dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1))
     torch.cuda.set_device(dev)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    _init_dist(dev)
     n, D, prec = args.rows or 1_000_000, 384, args.precision
     idx = FlatIndex(dim=D, capacity=n, device=dev)
     build_shard(idx, 0, n, n, D, 1000, dev)
@@ -215,13 +227,28 @@ def run_pipeline(args, cfg_id):
     c_toks = torch.randint(1000, 30000, (n, 260), generator=g, device=dev,
                            dtype=torch.int32).to(torch.int16)
     c_lens = torch.randint(180, 261, (n,), generator=g, device=dev, dtype=torch.int32)
+    # stage 1 starts from STRINGS (main2.py:170-171 encode(list[str]) tokenises every call):
+    # seeded question-like texts over a synthetic 30522-entry WordPiece vocab, tokenised by
+    # the product tokenizer (ragmi.encoders.WordPiece) inside the timed region on a host
+    # worker thread pipelined ahead of the GPU; the same batches pre-tokenised are timed
+    # after it as the id-input comparison
+    import tempfile
+    from concurrent.futures import ThreadPoolExecutor
+
+    from ragmi.encoders import WordPiece
+    vocab = R.make_vocab(30522, seed=5)
+    vdir = tempfile.mkdtemp(prefix="ragmi_vocab_")
+    with open(os.path.join(vdir, "vocab.txt"), "w") as f:
+        f.write("\n".join(vocab) + "\n")
+    tok = WordPiece(os.path.join(vdir, "vocab.txt"), 512)
     rng = np.random.default_rng(3 + rank)
-    batches = []
-    for _ in range(args.warmup + args.steps):
-        lens = rng.integers(16, 33, B)
-        ids = np.concatenate([np.r_[101, rng.integers(1000, 30000, L - 2), 102] for L in lens])
-        batches.append((ids.astype(np.int32), np.zeros(len(ids), np.int32),
-                        np.r_[0, np.cumsum(lens)].astype(np.int32)))
+    texts = [R.query_texts(rng, vocab, B) for _ in range(args.warmup + args.steps)]
+    batches = [tok.encode_packed(t) for t in texts]
+    t_tok = time.perf_counter()
+    for t in texts[:20]:
+        tok.encode_packed(t)
+    tok_ms = (time.perf_counter() - t_tok) / min(20, len(texts)) * 1e3
+    q_lens = np.concatenate([np.diff(b[2]) for b in batches])
     bge_w, ce_w = R.make_weights(R.BGE_SMALL, 1), R.make_weights(R.MINILM_CE, 2)
     bge = BertEncoder(R.BGE_SMALL, bge_w, HEAD_CLS_L2, dev, prec)
     ce = BertEncoder(R.MINILM_CE, ce_w, HEAD_POOLER_CLS, dev, prec)
@@ -230,8 +257,8 @@ def run_pipeline(args, cfg_id):
     ev_every = 4                        # CE forward events on every 4th batch (sampled)
     evs, flops = [], []
 
-    def step(i, timed):
-        ids, tt, cu = batches[i]
+    def step(i, timed, toks=None):
+        ids, tt, cu = toks if toks is not None else batches[i]
         st = streams[i % S]
         with torch.cuda.stream(st):
             q = bge.forward_packed(ids, tt, cu)
@@ -256,11 +283,32 @@ def run_pipeline(args, cfg_id):
     for i in range(args.warmup):
         step(i, False)
     _sync(dev)
+    # timed region: strings in, top-5 (config 3) / top-15 (config 2) out; tokenisation of
+    # batch i+depth runs on the worker while the GPU works on batch i
+    depth = S + 1
+    pool = ThreadPoolExecutor(max_workers=1)
     t0 = time.perf_counter()
-    outs = [step(args.warmup + k, True) for k in range(args.steps)]
+    futs = {k: pool.submit(tok.encode_packed, texts[args.warmup + k])
+            for k in range(min(depth, args.steps))}
+    outs = []
+    for k in range(args.steps):
+        toks = futs.pop(k).result()
+        if k + depth < args.steps:
+            futs[k + depth] = pool.submit(tok.encode_packed, texts[args.warmup + k + depth])
+        outs.append(step(args.warmup + k, True, toks))
     _sync(dev)
     elapsed = time.perf_counter() - t0
+    pool.shutdown()
     ce_ms = float(np.mean([a.elapsed_time(b) for a, b in evs])) if evs else None
+    # the same batches from pre-tokenised ids (the round-2 line's input), for the delta
+    n_ev = len(evs)
+    _sync(dev)
+    t1 = time.perf_counter()
+    for k in range(args.steps):
+        step(args.warmup + k, False)
+    _sync(dev)
+    elapsed_ids = time.perf_counter() - t1
+    del evs[n_ev:]
     flops = [_ce_flops(c.cpu().numpy(), R.MINILM_CE) for c in flops]
     ce_alone = None
     if cfg_id == 3:
@@ -277,7 +325,7 @@ def run_pipeline(args, cfg_id):
         b.record()
         torch.cuda.synchronize(dev)
         ce_alone = a.elapsed_time(b) / 5
-    elapsed, = _max_over_ranks([elapsed], dev)
+    elapsed, elapsed_ids = _max_over_ranks([elapsed, elapsed_ids], dev)
 
     # parity legs (after the timed region): search top-15 of the first timed batch certified
     # against the oracle; CE logits of its first query's 15 pairs vs bert_ref
@@ -316,7 +364,7 @@ def run_pipeline(args, cfg_id):
             extra["rerank_max_abs_diff_vs_oracle"] = float(
                 np.abs(logits[0].cpu().numpy() - ref).max())
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and not args.no_cpu:
         ids, tt, cu = batches[args.warmup]
         pb = None
         if cfg_id == 3:
@@ -350,15 +398,20 @@ def run_pipeline(args, cfg_id):
             (" + MiniLM-L6 rerank of 32x15 pairs -> top-5" if cfg_id == 3 else "") +
             f" (config {cfg_id})", qps, "queries/s", args, elapsed, world, prec,
             "synthetic (torch randn corpus seeded 1000+c; seeded synthetic weights of the "
-            "bge-small / MiniLM-L6 architectures; random token ids: queries 16-32, chunks "
-            "180-260 tokens)",
-            {"workload": f"config {cfg_id}: 32 queries -> bge-small ({prec}) -> top-15 of "
-                         f"{n}x384" + (" -> CE rerank 480 pairs -> top-5" if cfg_id == 3
-                                       else ""),
+            "bge-small / MiniLM-L6 architectures; seeded question-like query strings over a "
+            "synthetic 30522-entry WordPiece vocab, ~21 tokens; chunk token ids 180-260)",
+            {"workload": f"config {cfg_id}: 32 query STRINGS -> WordPiece tokenisation (host "
+                         f"worker thread, pipelined) -> bge-small ({prec}) -> top-15 of "
+                         f"{n}x384" + (" -> CE rerank 480 pairs (chunk tokens cached at "
+                                       "ingest) -> top-5" if cfg_id == 3 else ""),
+             "query_tokens_mean": round(float(q_lens.mean()), 1),
+             "tokenize_ms_per_batch": round(tok_ms, 3),
              "batch": B, "k": K_TOP, "rerank_top_k": TOPK if cfg_id == 3 else None,
              "precision": prec, "batches_in_flight": S,
              "parallelism": f"replicas{world}" if world > 1 else "1 GPU"},
-            roofline=roof, cpu_baseline=cpu, **extra)
+            roofline=roof, cpu_baseline=cpu,
+            id_input_qps=round(B * args.steps / elapsed_ids * world, 3),
+            text_vs_id_input=round(elapsed_ids / elapsed, 4), **extra)
         line["scaling"] = "weak"
         print(json.dumps(line), flush=True)
     idx.close()
@@ -431,11 +484,9 @@ def run_search(args, mode):
     from ragmi.dist import ShardedIndex
     from ragmi.index import busy_union_ms
     world, rank = _world()
-    dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+    dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1))
     torch.cuda.set_device(dev)
-    if world > 1:
-        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        dist.init_process_group("nccl", device_id=dev)
+    _init_dist(dev)
     if mode == "5":
         n, D, batch, seed0, qseed = args.rows or 50_000_000, 1024, 128, 5000, 7
     else:
@@ -530,7 +581,7 @@ def run_search(args, mode):
             extra["planted_found_first"] = \
                 f"{int((g_i[:, 0] == picks[args.warmup + ks[0]]).sum())}/{batch}"
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and not args.no_cpu:
         m = min(hi - lo, CHUNK if D == 384 else CHUNK // 4)
         cpu = _cpu_search_baseline(
             idx.export_rows(0, m), qs[args.warmup].cpu().numpy(), n, K_TOP, args.cpu_budget,

@@ -1,10 +1,13 @@
-"""Generate tests/golden/bert_golden.npz with the installed `transformers` (5.15.0) BERT
+"""Generate tests/golden/bert_golden.npz (and bert_golden_stress.npz) with the installed `transformers` (5.15.0) BERT
 classes — the library the reference's sentence-transformers stack runs on — built from a
 LOCAL config with the seeded synthetic weights of oracle/bert_ref.make_weights (no hub
 access; the real checkpoints are not on disk).
 
 Stored: input ids / token types / masks and, per model, the CLS-normalised bge embeddings
 [B,384] and the cross-encoder logits [B] computed by transformers in fp32 (eager attention).
+bert_golden_stress.npz: the same for the "stress" weight profile (ragmi.synth.make_weights:
+heavy-tailed matrices, outlier hidden dimensions with LayerNorm gammas 8-20 and massive
+pre-LN activations, |hidden| ~ 100-400) — full 12-layer bge-small and 6-layer MiniLM shapes.
 """
 import os
 import sys
@@ -75,7 +78,26 @@ def main():
                         bge_seed=11, ce_seed=12, ids_l=ids_l, tt_l=tt_l, m_l=m_l,
                         bgel_emb=emb_l, bgel_seed=13)
     print("bge", emb.shape, "ce", logit, "bge-large-2L", emb_l.shape)
+    main_stress()
+
+
+def main_stress():
+    torch.manual_seed(0)
+    rng = np.random.default_rng(4048)
+    ids_q, tt_q, m_q = R.random_batch(rng, 8, 32)
+    ids_p, tt_p, m_p = R.random_batch(rng, 8, 96, pair=True)
+    wb = R.make_weights(R.BGE_SMALL, seed=41, profile="stress")
+    wc = R.make_weights(R.MINILM_CE, seed=42, profile="stress")
+    emb = hf_bge(R.BGE_SMALL, wb, ids_q, tt_q, m_q)
+    logit = hf_ce(R.MINILM_CE, wc, ids_p, tt_p, m_p)
+    np.savez_compressed(os.path.join(HERE, "bert_golden_stress.npz"), ids_q=ids_q, tt_q=tt_q,
+                        m_q=m_q, ids_p=ids_p, tt_p=tt_p, m_p=m_p, bge_emb=emb,
+                        ce_logits=logit, bge_seed=41, ce_seed=42)
+    print("stress: bge", emb.shape, "ce", logit)
 
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["stress"]:
+        main_stress()
+    else:
+        main()

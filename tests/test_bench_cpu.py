@@ -158,3 +158,77 @@ def test_busy_union_counts_overlap_once():
     a = np.array([4.0, 0.0, 0.5, -1.0, 10.0])
     b = np.array([6.0, 2.0, 1.0, 0.25, 10.5])
     assert busy_union_ms(a, b) == (2.0 - (-1.0)) + 2.0 + 0.5
+
+
+# ------------------------------------------------------------------ N-rank launcher (bench.py)
+_RANK_BODY = ("import json, os, sys\n"
+              "keys = ['RANK', 'LOCAL_RANK', 'WORLD_SIZE', 'LOCAL_WORLD_SIZE', 'MASTER_ADDR',"
+              " 'MASTER_PORT', 'HSA_ENABLE_IPC_MODE_LEGACY']\n"
+              "open(os.path.join(os.environ['OUT'], os.environ['RANK']), 'w')"
+              ".write(json.dumps({k: os.environ.get(k) for k in keys}))\n")
+
+
+def test_launch_ranks_starts_n_children_with_the_env_contract(tmp_path):
+    env = dict(os.environ, OUT=str(tmp_path))
+    env.pop("WORLD_SIZE", None)
+    rc = bench.launch_ranks(4, [], cmd=[sys.executable, "-c", _RANK_BODY], env=env)
+    assert rc == 0
+    import json
+    got = {int(p.name): json.loads(p.read_text()) for p in tmp_path.iterdir()}
+    assert sorted(got) == [0, 1, 2, 3]
+    ports = {g["MASTER_PORT"] for g in got.values()}
+    assert len(ports) == 1 and int(ports.pop()) > 0
+    for r, g in got.items():
+        assert g["RANK"] == g["LOCAL_RANK"] == str(r)
+        assert g["WORLD_SIZE"] == g["LOCAL_WORLD_SIZE"] == "4"
+        assert g["MASTER_ADDR"] == "127.0.0.1"
+        assert g["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+
+
+def test_launch_ranks_failure_stops_the_others(tmp_path):
+    """rank 1 fails at once; the others would sleep for a minute: the launcher must return
+    rank 1's status and terminate them."""
+    body = ("import os, sys, time\n"
+            "if os.environ['RANK'] == '1': sys.exit(3)\n"
+            "time.sleep(60)\n")
+    import time as _t
+    t0 = _t.time()
+    rc = bench.launch_ranks(3, [], cmd=[sys.executable, "-c", body], env=dict(os.environ))
+    assert rc == 3
+    assert _t.time() - t0 < 30
+
+
+def test_check_world_mismatch_and_default():
+    assert bench.check_world(1, {}) == 1
+    assert bench.check_world(8, {}) == 8                    # launch_ranks will start 8
+    assert bench.check_world(2, {"WORLD_SIZE": "2"}) == 2   # under torch.distributed.run
+    with pytest.raises(SystemExit) as e:
+        bench.check_world(8, {"WORLD_SIZE": "1"})
+    assert e.value.code == 2
+    with pytest.raises(SystemExit):
+        bench.check_world(0, {})
+
+
+def test_bench_py_refuses_world_size_mismatch_before_gpu():
+    """`WORLD_SIZE=3 python bench.py --gpus 2` exits 2 before any GPU or data work."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2
+    assert "WORLD_SIZE=3" in r.stderr
+
+
+def test_scan_traffic_table(tmp_path):
+    import json
+    p = tmp_path / "pmc.json"
+    p.write_text(json.dumps({"hbm_bytes_per_launch": 7.7e9, "source": "a.csv", "commit": "x",
+                             "by_rows_per_gpu": {"1250000": {"hbm_bytes_per_launch": 9.7e8,
+                                                             "source": "b.csv"}}}))
+    b, src = bench.scan_traffic(10_000_000, path=str(p))
+    assert b == 7.7e9 and "a.csv" in src and "10000000 rows" in src
+    b, src = bench.scan_traffic(1_250_000, path=str(p))
+    assert b == 9.7e8 and "b.csv" in src
+    assert bench.scan_traffic(2_500_000, path=str(p)) == (None, None)
+    assert bench.scan_traffic(10_000_000, "fp32", path=str(p)) == (None, None)
+    assert bench.scan_traffic(10_000_000, path=str(tmp_path / "missing.json")) == (None, None)

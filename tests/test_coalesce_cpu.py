@@ -108,3 +108,43 @@ def test_failure_reaches_every_rider():
     [t.join() for t in th]
     assert errs == ["device error"] * 10
     assert not co.leader_active and not co.pending
+
+
+def test_base_exception_in_leader_does_not_strand_riders():
+    """A BaseException (KeyboardInterrupt here) raised by the leader's search must still hand
+    leadership on: riders of that batch see it, later callers are served normally."""
+    _paths()
+    from ragmi.qdrant import Coalescer
+    rng = np.random.default_rng(3)
+    col = FakeCollection(rng.standard_normal((500, 32)).astype(np.float32),
+                         np.ones(500, np.uint32), delay=0.01)
+    orig = col.search
+    state = {"n": 0}
+
+    def search(q, limit, filters):
+        state["n"] += 1
+        if state["n"] == 1:
+            time.sleep(0.01)
+            raise KeyboardInterrupt
+        return orig(q, limit, filters)
+    col.search = search
+    co = Coalescer(col)
+    out = {}
+
+    def worker(j):
+        try:
+            out[j] = co.search(rng.standard_normal(32).astype(np.float32), 5, (0, 0))
+        except KeyboardInterrupt:
+            out[j] = "interrupted"
+
+    th = [threading.Thread(target=worker, args=(j,)) for j in range(8)]
+    for t in th:
+        t.start()
+        time.sleep(0.001)
+    for t in th:
+        t.join(timeout=10)
+    assert not any(t.is_alive() for t in th), "a rider was stranded"
+    assert "interrupted" in out.values() and len(out) == 8
+    # the collection still serves
+    assert len(co.search(rng.standard_normal(32).astype(np.float32), 5, (0, 0))) == 5
+    assert not co.leader_active and not co.pending

@@ -172,6 +172,16 @@ def test_text_api_with_local_vocab(gpu, tmp_path):
         '"max_position_embeddings": 512, "type_vocab_size": 2, "layer_norm_eps": 1e-12}'
         % len(words))
     (d / "vocab.txt").write_text(voc.read_text())
+    # bge-small-en-v1.5's sentence-transformers stack: Transformer -> Pooling(cls) -> Normalize
+    (d / "modules.json").write_text(
+        '[{"idx": 0, "name": "0", "path": "", "type": "sentence_transformers.models.Transformer"},'
+        ' {"idx": 1, "name": "1", "path": "1_Pooling", "type": "sentence_transformers.models.Pooling"},'
+        ' {"idx": 2, "name": "2", "path": "2_Normalize", "type": "sentence_transformers.models.Normalize"}]')
+    (d / "1_Pooling").mkdir()
+    (d / "1_Pooling" / "config.json").write_text(
+        '{"word_embedding_dimension": 384, "pooling_mode_cls_token": true, '
+        '"pooling_mode_mean_tokens": false, "pooling_mode_max_tokens": false, '
+        '"pooling_mode_mean_sqrt_len_tokens": false}')
     st = SentenceTransformer(str(d), device=gpu)
     one = st.encode("What was Apple total revenue in fiscal 2023?")
     many = st.encode(["What was Apple total revenue in fiscal 2023?", "risk factors"])
@@ -181,8 +191,27 @@ def test_text_api_with_local_vocab(gpu, tmp_path):
     cw = R.make_weights(dict(R.MINILM_CE, vocab=len(words), layers=2), 8)
     ce = CrossEncoder(device=gpu, cfg=dict(R.MINILM_CE, vocab=len(words), layers=2),
                       weights=cw, vocab_file=str(voc))
-    s = ce.predict([["net income", "apple net income 2023"], ["net income", "iphone margin"]])
+    pairs = [["net income", "apple net income 2023"], ["net income", "iphone margin"]]
+    s = ce.predict(pairs)
     assert s.shape == (2,) and s.dtype == np.float32
+    # no configured activation, num_labels 1: sentence-transformers' Sigmoid default
+    raw = ce.predict(pairs, activation_fct=torch.nn.Identity())
+    np.testing.assert_allclose(s, 1.0 / (1.0 + np.exp(-raw.astype(np.float64))), rtol=1e-6)
+    # a checkpoint directory with ms-marco-MiniLM-L-6-v2's configured Identity: raw logits
+    c = tmp_path / "ce"
+    c.mkdir()
+    save_file(cw, str(c / "model.safetensors"))
+    (c / "vocab.txt").write_text(voc.read_text())
+    (c / "config.json").write_text(
+        '{"vocab_size": %d, "hidden_size": 384, "num_hidden_layers": 2, '
+        '"num_attention_heads": 12, "intermediate_size": 1536, '
+        '"max_position_embeddings": 512, "type_vocab_size": 2, "layer_norm_eps": 1e-12, '
+        '"id2label": {"0": "LABEL_0"}, "label2id": {"LABEL_0": 0}, '
+        '"sbert_ce_default_activation_function": "torch.nn.modules.linear.Identity"}'
+        % len(words))
+    ce2 = CrossEncoder(str(c), device=gpu)
+    assert ce2.activation == "identity"
+    np.testing.assert_array_equal(ce2.predict(pairs), raw)
 
 
 def test_fused_add_ln_path(bge, ce, golden, prec):

@@ -68,3 +68,17 @@ def test_live_transformers_recheck():
     ids, tt, m = R.random_batch(rng, 3, 17, pair=True)
     np.testing.assert_allclose(R.ce_logits(w, cfg, ids, tt, m), M.hf_ce(cfg, w, ids, tt, m),
                                rtol=0, atol=2e-5)
+
+
+def test_stress_oracle_matches_transformers_fixture():
+    """The stress weight profile (outlier dimensions, |hidden| ~ 100-400): oracle vs the
+    transformers 5.15 fixture (tests/golden/make_golden_bert.py main_stress)."""
+    import os
+    from conftest import GOLDEN
+    g = dict(np.load(os.path.join(GOLDEN, "bert_golden_stress.npz")))
+    wb = R.make_weights(R.BGE_SMALL, int(g["bge_seed"]), profile="stress")
+    wc = R.make_weights(R.MINILM_CE, int(g["ce_seed"]), profile="stress")
+    np.testing.assert_allclose(R.bge_embed(wb, R.BGE_SMALL, g["ids_q"], g["tt_q"], g["m_q"]),
+                               g["bge_emb"], rtol=0, atol=3e-6)
+    np.testing.assert_allclose(R.ce_logits(wc, R.MINILM_CE, g["ids_p"], g["tt_p"], g["m_p"]),
+                               g["ce_logits"], rtol=0, atol=2e-5)

@@ -20,15 +20,12 @@ WORDS = ("apple iphone revenue services margin risk supply chain china tariffs c
          "operating income net sales fiscal quarter guidance inflation currency debt").split()
 
 
-def _write_model(d, cfg, w, vocab):
-    from safetensors.numpy import save_file
-    d.mkdir()
-    save_file(w, str(d / "model.safetensors"))
-    (d / "config.json").write_text(json.dumps({
-        "vocab_size": cfg["vocab"], "hidden_size": 384, "num_hidden_layers": cfg["layers"],
-        "num_attention_heads": 12, "intermediate_size": 1536, "max_position_embeddings": 512,
-        "type_vocab_size": 2, "layer_norm_eps": 1e-12}))
-    (d / "vocab.txt").write_text("\n".join(vocab) + "\n")
+def _write_model(d, cfg, w, vocab, kind):
+    """A local checkpoint in the real models' layout (ragmi.synth.write_checkpoint: bge with its
+    Transformer -> Pooling(cls) -> Normalize stack, the cross-encoder with its configured
+    Identity activation)."""
+    from ragmi.synth import write_checkpoint
+    write_checkpoint(str(d), cfg, w, vocab, kind)
 
 
 @pytest.fixture(scope="module")
@@ -40,8 +37,8 @@ def rag(gpu, tmp_path_factory):
     cb = dict(R.BGE_SMALL, vocab=len(vocab), layers=2)
     cc = dict(R.MINILM_CE, vocab=len(vocab), layers=2)
     wb, wc = R.make_weights(cb, 21), R.make_weights(cc, 22)
-    _write_model(root / "bge", cb, wb, vocab)
-    _write_model(root / "ce", cc, wc, vocab)
+    _write_model(root / "bge", cb, wb, vocab, "bge")
+    _write_model(root / "ce", cc, wc, vocab, "ce")
     mp = pytest.MonkeyPatch()
     mp.setenv("TESTING", "False")
     mp.setenv("RAGMI_BGE_DIR", str(root / "bge"))

@@ -64,7 +64,10 @@ class HostIndex:
 def _filled(n, dim, seed):
     rng = np.random.default_rng(seed)
     h = HostIndex(dim, n)
-    h.import_rows(rng.standard_normal((n, dim)).astype(np.float16), 0,
+    x = rng.standard_normal((n, dim))
+    x /= np.linalg.norm(x, axis=1, keepdims=True)
+    x[::97] = 0.0                                    # never-filled slots are zero rows
+    h.import_rows(x.astype(np.float16), 0,
                   rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32), n)
     return h
 
@@ -241,3 +244,25 @@ def test_fp32_storage_roundtrip_and_downcast(tmp_path):
     store.save_index(d16, p16)
     with pytest.raises(ValueError, match="fp16 shard"):
         store.load_into(HostIndex32(d), p16)
+
+
+def test_unnormalised_rows_refused(tmp_path):
+    """A hand-built or corrupted shard (rows not unit-norm) would void the exact top-k
+    certificate (its error bound assumes ||c|| <= 1.001): load refuses it, naming the row."""
+    _paths()
+    from ragmi import store
+    src = _filled(300, 64, 9)
+    bad = src.rows[123].view(np.float16).astype(np.float32) * 1.01
+    src.rows[123] = bad.astype(np.float16).view(np.uint16)
+    p = str(tmp_path / "bad")
+    store.save_index(src, p)
+    with pytest.raises(ValueError, match="shard row 123"):
+        store.load_into(HostIndex(64), p, chunk_rows=100)
+    assert store.load_into(HostIndex(64), p, check_norms=False) == 300
+    rng = np.random.default_rng(1)
+    v = rng.standard_normal((50, 64)).astype(np.float32)
+    v /= np.linalg.norm(v, axis=1, keepdims=True)
+    store.check_row_norms(v, "fp32")
+    v[7] *= 1.0 + 1e-5
+    with pytest.raises(ValueError, match="shard row 107"):
+        store.check_row_norms(v, "fp32", first_row=100)
