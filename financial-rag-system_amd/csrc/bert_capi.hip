@@ -20,6 +20,10 @@ using namespace ragmi::bert;
 
 // largest static fp16 range bound accepted (fp16 max 65504; see range_bounds)
 constexpr double kF16Safe = 60000.0;
+// split-K of the small-batch fp32-output GEMMs (small_ksplit): most parts, and the workspace
+// rows up to which y keeps room for them
+constexpr int kMaxKSplit = 4;
+constexpr int64_t kSplitMaxRows = 8192;
 
 struct Layer {
   _Float16 *wqkv = nullptr, *wo = nullptr, *w1 = nullptr, *w2 = nullptr;
@@ -66,6 +70,7 @@ struct EncWorkspace {
   hipStream_t stream = nullptr;
   uint64_t last_use = 0;
   int64_t cap_t = 0;
+  int64_t y_rows = 0, yc_rows = 0;   // rows y / yc hold (room for split-K parts at small T)
   float *x = nullptr, *y = nullptr;
   _Float16 *xh = nullptr, *qkv = nullptr, *ctx = nullptr, *ff = nullptr;
   _Float16 *xl = nullptr, *qkv_l = nullptr, *ctx_l = nullptr, *ff_l = nullptr;  // fp16x3
@@ -206,7 +211,8 @@ int ensure_ws(const rag_bert_config& cfg, EncWorkspace* w, int64_t T) {
     }
   }
   RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->x), cap * H * 4));
-  RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->y), cap * H * 4));
+  w->y_rows = cap <= kSplitMaxRows ? cap * kMaxKSplit : cap;
+  RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->y), w->y_rows * H * 4));
   RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->xh), cap * H * 2));
   RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->qkv), cap * 3 * H * 2));
   RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->ctx), cap * H * 2));
@@ -278,11 +284,27 @@ bool pipe_ok(int M, int N, int K) {
 template <int EPI, bool SPLIT, typename CFG, int PROBE = 0>
 void launch_pipe(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float16* Wl,
                  const float* bias, int M, int N, int K, void* C, _Float16* Clo, hipStream_t st,
-                 int max_wg, const LnArgs& ln = LnArgs{}) {
-  const int tiles = (N / CFG::BN) * ((M + CFG::BM - 1) / CFG::BM);
+                 int max_wg, const LnArgs& ln = LnArgs{}, int ksplit = 1) {
+  const int tiles = (N / CFG::BN) * ((M + CFG::BM - 1) / CFG::BM) * ksplit;
   const dim3 grid((unsigned)std::min(max_wg, (tiles + 7) / 8 * 8));   // multiple of 8
   gemm_pipe_kernel<EPI, SPLIT, CFG, PROBE><<<grid, dim3(CFG::THREADS), 0, st>>>(
-      A, Al, W, Wl, bias, M, N, K, C, Clo, ln);
+      A, Al, W, Wl, bias, M, N, K, C, Clo, ln, ksplit);
+}
+
+// split-K of the small-batch fp32-output GEMMs (O-proj, FFN2 of query batches: 64x64 tiles,
+// one serial K loop per tile): K parts per tile, a function of K only, so a sequence's output
+// never depends on what else is in its batch (tests/test_encoders_gpu.py batch independence).
+// The parts are summed in order by add_ln_kernel. 0 = no split for this shape.
+int small_ksplit(int K, int BK) {
+  static const int force = [] {
+    const char* v = std::getenv("RAGMI_KSPLIT");            // diagnostic: 1 = off, n = force
+    return v ? std::atoi(v) : 0;
+  }();
+  const int nk = K / BK;
+  int s = force > 0 ? force : K >= 1536 ? 3 : K >= 384 ? 2 : 1;
+  s = std::min(s, kMaxKSplit);
+  while (s > 1 && nk % s) --s;
+  return s;
 }
 
 template <int EPI, bool SPLIT, typename CFG, int PROBE = 0, int AUX = 0>
@@ -355,7 +377,8 @@ int ensure_cls(const rag_bert_config& cfg, EncWorkspace* w, int64_t B) {
   w->cap_b = 0;
   const int64_t cap = std::max<int64_t>(B, 256), H = cfg.hidden, FF = cfg.intermediate;
   RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->xc), cap * H * 4));
-  RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->yc), cap * H * 4));
+  w->yc_rows = cap * kMaxKSplit;
+  RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->yc), w->yc_rows * H * 4));
   RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->xch), cap * H * 2));
   RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->cc), cap * H * 2));
   RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->ffc), cap * FF * 2));
@@ -368,10 +391,14 @@ int ensure_cls(const rag_bert_config& cfg, EncWorkspace* w, int64_t B) {
   return RAG_OK;
 }
 
+// ksplit_io: in = the split-K parts the caller's C can hold (1 = no split; kEpiF32 only),
+// out = the parts written (the caller sums them: add_ln_kernel)
 template <int EPI>
 void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float16* Wl,
           const float* bias, int M, int N, int K, void* C, _Float16* Clo, hipStream_t st,
-          int variant = RAG_GEMM_AUTO) {
+          int variant = RAG_GEMM_AUTO, int* ksplit_io = nullptr) {
+  const int ks_room = ksplit_io ? *ksplit_io : 1;
+  if (ksplit_io) *ksplit_io = 1;
   if (variant == RAG_GEMM_AUTO) variant = gemm_variant_default();
   const bool auto_pick = variant == RAG_GEMM_AUTO;
   const int pipe_tiles = (N / PBN) * ((M + PBM - 1) / PBM);
@@ -388,7 +415,27 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
               : 2 * pipe_tiles >= cu_count()     ? RAG_GEMM_WS
                                                  : RAG_GEMM_TILE;
   if (variant != RAG_GEMM_TILE && !pipe_ok(M, N, K)) variant = RAG_GEMM_TILE;
-  if (auto_pick && variant == RAG_GEMM_SMALL && Al) variant = RAG_GEMM_SMALL_BK64;
+  // knobs of the small-batch fp16x3 GEMMs (A/B): the BK-32 SMALL kernel (64 KB LDS, 2
+  // workgroups per CU, split-K) is the default since round 3 — 782-token bge-small forward
+  // 0.637 / 0.644 ms with SMALL_BK64 (160 KB, 1 per CU) vs 0.628 / 0.627, and the config-2
+  // line at 3 batches in flight 65.9K vs 71.1K qps, where a 1-per-CU GEMM keeps the other
+  // batches' kernels off its CUs (profiles/r03b_small_gemm.jsonl); RAGMI_SMALL_BK=64 restores
+  // SMALL_BK64. RAGMI_SMALL_WIDE=1 runs N >= 1024 GEMMs whose 64 x 64 tiles exceed the CUs on
+  // 64 x 128 tiles (0.620 ms alone, 0.628 with BK 32: not kept)
+  static const int small_bk = [] {
+    const char* v = std::getenv("RAGMI_SMALL_BK");
+    return v ? std::atoi(v) : 32;
+  }();
+  static const bool small_wide = [] {
+    const char* v = std::getenv("RAGMI_SMALL_WIDE");
+    return v && std::atoi(v) == 1;
+  }();
+  if (auto_pick && variant == RAG_GEMM_SMALL && Al && small_wide && N % 128 == 0 && N >= 1024 &&
+      small_tiles > cu_count()) {
+    launch_pipe<EPI, true, PipeSmallWide64>(A, Al, W, Wl, bias, M, N, K, C, Clo, st, cu_count());
+    return;
+  }
+  if (auto_pick && variant == RAG_GEMM_SMALL && Al && small_bk != 32) variant = RAG_GEMM_SMALL_BK64;
   // diagnostic probes of the PIPE kernel (parts removed; bert_kernels.hip PROBE)
   const int probe = variant == RAG_GEMM_PROBE_NO_MFMA           ? 1
                     : variant == RAG_GEMM_PROBE_NO_DMA          ? 2
@@ -494,20 +541,31 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
                                          cu_count());
     return;
   }
+  // split-K parts for the small fp32-output GEMMs (small_ksplit), where the caller has room
+  auto ks_for = [&](int BK) {
+    if constexpr (EPI != kEpiF32) return 1;
+    if (ks_room <= 1 || N > kPipeBiasMax / 2) return 1;
+    return std::min(ks_room, small_ksplit(K, BK));
+  };
   if (variant == RAG_GEMM_SMALL_BK64 && Al) {
-    launch_pipe<EPI, true, PipeSmallSplit64>(A, Al, W, Wl, bias, M, N, K, C, Clo, st, cu_count());
+    const int ks = ks_for(PipeSmallSplit64::BK);
+    launch_pipe<EPI, true, PipeSmallSplit64>(A, Al, W, Wl, bias, M, N, K, C, Clo, st, cu_count(),
+                                             LnArgs{}, ks);
+    if (ksplit_io) *ksplit_io = ks;
     return;
   }
   if (variant == RAG_GEMM_SMALL || variant == RAG_GEMM_SMALL_BK64) {
     // fp16: 80 KB LDS -> 2 workgroups per CU; fp16x3 (AUTO's choice is SMALL_BK64, above:
     // one MiniLM layer's four GEMMs at 782 / 3056 tokens 49.1 -> 46.6 / 96.3 -> 87.5 us):
     // 112 KB -> 1
-    if (Al)
+    const int ks = ks_for(Al ? kBK<true> : kBK<false>);
+    if (Al)   // 48 KB ring + 16 KB bias area: two workgroups per CU
       launch_pipe<EPI, true, PipeSmall<true>>(A, Al, W, Wl, bias, M, N, K, C, Clo, st,
-                                              cu_count());
+                                              2 * cu_count(), LnArgs{}, ks);
     else
       launch_pipe<EPI, false, PipeSmall<false>>(A, nullptr, W, nullptr, bias, M, N, K, C,
-                                                nullptr, st, 2 * cu_count());
+                                                nullptr, st, 2 * cu_count(), LnArgs{}, ks);
+    if (ksplit_io) *ksplit_io = ks;
     return;
   }
   const unsigned tiles = (unsigned)((N / BN) * ((M + BM - 1) / BM));
@@ -624,6 +682,7 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
     // rows the rest of the layer runs on: all T tokens, or the B gathered CLS rows
     int R = T;
     float *x = xf ? nullptr : w->x, *y = w->y;
+    int64_t y_rows = w->y_rows;
     _Float16 *xh = w->xh, *xl = w->xl, *ctx = w->ctx, *ctxl = w->ctx_l, *ff = w->ff,
              *ffl = w->ff_l;
     bool row_xf = xf;
@@ -638,6 +697,7 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
       R = B;
       x = w->xc;
       y = w->yc;
+      y_rows = w->yc_rows;
       xh = w->xch;
       xl = w->xl ? w->xcl : nullptr;
       ctx = w->cc;
@@ -647,28 +707,34 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
     }
     const unsigned lg = (unsigned)((R + 3) / 4);
     const bool fuse = !row_xf && fuse_for(R);
-    auto add_ln = [&](const float* gam, const float* bet) {
+    // split-K parts y can hold for R rows (the small-batch GEMMs' K split, summed by add_ln)
+    const int ks_room = (int)std::max<int64_t>(1, std::min<int64_t>(kMaxKSplit, y_rows / R));
+    auto add_ln = [&](const float* gam, const float* bet, int parts) {
+      const int64_t ps = (int64_t)R * H;
       if (row_xf)
         add_ln_kernel<H, true><<<dim3(lg), dim3(256), 0, st>>>(nullptr, y, gam, bet,
-                                                              c.layer_norm_eps, xh, xl, R);
+                                                              c.layer_norm_eps, xh, xl, R,
+                                                              parts, ps);
       else
         add_ln_kernel<H><<<dim3(lg), dim3(256), 0, st>>>(x, y, gam, bet, c.layer_norm_eps, xh,
-                                                        xl, R);
+                                                        xl, R, parts, ps);
     };
     if (fuse) {
       gemm_add_ln(ctx, ctxl, L.wo, L.wo_l, L.bo, L.g1, L.be1, c.layer_norm_eps, R, H, H, x, xh,
                   xl, st);
     } else {
-      gemm<kEpiF32>(ctx, ctxl, L.wo, L.wo_l, L.bo, R, H, H, y, nullptr, st);
-      add_ln(L.g1, L.be1);
+      int ks = ks_room;
+      gemm<kEpiF32>(ctx, ctxl, L.wo, L.wo_l, L.bo, R, H, H, y, nullptr, st, RAG_GEMM_AUTO, &ks);
+      add_ln(L.g1, L.be1, ks);
     }
     gemm<kEpiGeluF16>(xh, xl, L.w1, L.w1_l, L.bi1, R, FF, H, ff, ffl, st);
     if (fuse) {
       gemm_add_ln(ff, ffl, L.w2, L.w2_l, L.bi2, L.g2, L.be2, c.layer_norm_eps, R, H, FF, x, xh,
                   xl, st);
     } else {
-      gemm<kEpiF32>(ff, ffl, L.w2, L.w2_l, L.bi2, R, H, FF, y, nullptr, st);
-      add_ln(L.g2, L.be2);
+      int ks = ks_room;
+      gemm<kEpiF32>(ff, ffl, L.w2, L.w2_l, L.bi2, R, H, FF, y, nullptr, st, RAG_GEMM_AUTO, &ks);
+      add_ln(L.g2, L.be2, ks);
     }
   }
   // the final hidden states of the CLS tokens are rows 0 .. B-1 of w->xc (cu = null)
@@ -952,6 +1018,26 @@ int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, co
     case kEpiF32: gemm<kEpiF32>(a, al, w, wl, bias, M, N, K, C, clo, st, variant); break;
     default: return ragmi::fail(RAG_EINVAL, "unknown epilogue");
   }
+  RAG_HIP(hipGetLastError());
+  return RAG_OK;
+}
+
+int rag_bert_gemm_splitk(int variant, const void* A, const void* A_lo, const void* W,
+                         const void* W_lo, const float* bias, int M, int N, int K, float* C,
+                         int max_parts, int* parts, void* stream) {
+  ragmi::clear_error();
+  if (!A || !W || !bias || !C || !parts) return ragmi::fail(RAG_EINVAL, "NULL argument");
+  if ((A_lo == nullptr) != (W_lo == nullptr))
+    return ragmi::fail(RAG_EINVAL, "A_lo and W_lo: both (fp16x3) or neither (fp16)");
+  if (variant != RAG_GEMM_AUTO && variant != RAG_GEMM_SMALL && variant != RAG_GEMM_SMALL_BK64)
+    return ragmi::fail(RAG_EINVAL, "split-K runs on the SMALL GEMMs (AUTO, SMALL, SMALL_BK64)");
+  if (M < 1 || max_parts < 1 || N % BN != 0 || K % 64 != 0 || !pipe_ok(M, N, K))
+    return ragmi::fail(RAG_EINVAL, "bad shape");
+  int ks = std::min(max_parts, kMaxKSplit);
+  gemm<kEpiF32>(static_cast<const _Float16*>(A), static_cast<const _Float16*>(A_lo),
+                static_cast<const _Float16*>(W), static_cast<const _Float16*>(W_lo), bias, M, N,
+                K, C, nullptr, static_cast<hipStream_t>(stream), variant, &ks);
+  *parts = ks;
   RAG_HIP(hipGetLastError());
   return RAG_OK;
 }

@@ -148,13 +148,16 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(
 // (fp16(x - xh) keeps x to 2^-22 relative), so the fp32 copy is neither read nor written:
 // 12 instead of 20 bytes per element.
 // ----------------------------------------------------------------------------------------
+// y may hold `parts` split-K partial products (gemm_pipe_kernel ksplit > 1), part p at
+// y + p * pstride: they are summed in part order (deterministic) before the residual add.
 template <int H, bool XF = false>
 __global__ __launch_bounds__(256) void add_ln_kernel(float* __restrict__ x,
                                                      const float* __restrict__ y,
                                                      const float* __restrict__ g,
                                                      const float* __restrict__ bt, float eps,
                                                      _Float16* __restrict__ xh,
-                                                     _Float16* __restrict__ xl, int T) {
+                                                     _Float16* __restrict__ xl, int T,
+                                                     int parts = 1, int64_t pstride = 0) {
   const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (t >= T) return;
@@ -164,7 +167,9 @@ __global__ __launch_bounds__(256) void add_ln_kernel(float* __restrict__ x,
   for (int j = 0; j < H / 64; ++j) {
     const int c = lane + 64 * j;
     const float r = XF ? (float)xh[t * H + c] + (float)xl[t * H + c] : x[t * H + c];
-    v[j] = r + y[t * H + c];
+    float yy = y[t * H + c];
+    for (int p = 1; p < parts; ++p) yy += y[p * pstride + t * H + c];
+    v[j] = r + yy;
     s += v[j];
   }
 #pragma unroll
@@ -434,6 +439,9 @@ template <bool SPLIT> using PipeSmall = PipeCfg<64, 64, 2, 2, SPLIT ? 3 : 4>;
 // CU): half the K steps of PipeSmall<true> — a query-batch GEMM is a few dozen tiles whose
 // time is the serial K loop's per-step latency
 using PipeSmallSplit64 = PipeCfg<64, 64, 2, 2, 4, 64>;
+// 64 x 128 tiles at BK 64, 3 stages (fp16x3: 144 KB ring + the bias area = the whole 160 KB):
+// the N = 1536 FFN1 of a query batch in one round of tiles (156 at 782 tokens vs 312 64 x 64)
+using PipeSmallWide64 = PipeCfg<64, 128, 2, 2, 3, 64>;
 // wider N tiles: fewer panel bytes per FLOP (256x256: 128 FLOP/B fp16 vs 85 at 256x128) at
 // the price of a 2-stage ring (one stage in flight)
 using PipeWide256 = PipeCfg<256, 256, 4, 2, 2>;
@@ -830,7 +838,7 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
     const _Float16* __restrict__ A, const _Float16* __restrict__ Al,
     const _Float16* __restrict__ W, const _Float16* __restrict__ Wl,
     const float* __restrict__ bias, int M, int N, int K, void* __restrict__ Cout,
-    _Float16* __restrict__ Clo, LnArgs ln) {
+    _Float16* __restrict__ Clo, LnArgs ln, int ksplit = 1) {
   constexpr int BM = CFG::BM, BN = CFG::BN, NS = CFG::NS, TH = CFG::THREADS;
   constexpr int FM = CFG::FM, FN = CFG::FN, WTM = 16 * FM, WTN = 16 * FN;
   constexpr int BK = CFG::BK ? CFG::BK : kBK<SPLIT>, CPR = BK / 8;
@@ -867,13 +875,22 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wid / CFG::WAVES_N, wc = wid % CFG::WAVES_N;
   const uint32_t lbase = lds_addr_of(lds);
+  // split-K (kEpiF32 only; the launcher checks K / BK % ksplit == 0 and N <= kPipeBiasMax / 2):
+  // work unit u = (tile u % n_tiles, K part u / n_tiles) over nk = K / BK / ksplit K steps;
+  // part p writes its fp32 partial product to Cout + p M N, the bias only in part 0 (the
+  // other parts read zeros staged in the upper half of the bias area); add_ln_kernel sums
+  // the parts in order
   const int nN = N / BN, nM = (M + BM - 1) / BM, n_tiles = nM * nN;
-  const int nk = K / BK;
+  const int nk = K / BK / ksplit;
+  const int n_units = n_tiles * ksplit;
   const int G = gridDim.x, per_xcd = G >> 3;
   const int off = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
-  const int n_mine = off < n_tiles ? (n_tiles - off + G - 1) / G : 0;
+  const int n_mine = off < n_units ? (n_units - off + G - 1) / G : 0;
   const int steps = n_mine * nk;
 
+  if (ksplit > 1)
+    for (int i = tid * 4; i < N; i += TH * 4)
+      *reinterpret_cast<floatx4*>(bias_l + kPipeBiasMax / 2 + i) = floatx4{0.f, 0.f, 0.f, 0.f};
   for (int i = tid * 4; i < N; i += TH * 4) {
     *reinterpret_cast<floatx4*>(bias_l + i) = *reinterpret_cast<const floatx4*>(bias + i);
     if constexpr (EPI == kEpiAddLn) {          // N == BN here (checked by the launcher)
@@ -904,7 +921,7 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
   // that share an A panel (same XCD, same time) then touch different K slices of it at any
   // moment, so one of them takes each slice's L2 miss and the others hit, instead of all of
   // them waiting on the same HBM fetch at every step.
-  int it_i = 0, kt_i = 0, kr_i = 0, slot_i = 0;
+  int it_i = 0, kt_i = 0, kr_i = 0, slot_i = 0, kb_i = 0;
   __amdgpu_buffer_rsrc_t rA0 = panel(A, 0), rA1 = rA0, rW0 = rA0, rW1 = rA0;
   auto issue_next = [&]() {
     if (it_i >= n_mine) return;
@@ -913,7 +930,9 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
       return;
     }
     if (kt_i == 0) {
-      const int tile = it_i * G + off;
+      const int unit = it_i * G + off;
+      const int tile = unit % n_tiles;
+      kb_i = (unit / n_tiles) * nk;
       const int m0 = (tile / nN) * BM, n0 = (tile % nN) * BN;
       kr_i = (tile % nN) % nk;
       const int64_t abytes = (int64_t)(M - m0) * K * 2, wbytes = (int64_t)BN * K * 2;
@@ -925,7 +944,7 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
       }
     }
     // (wave-uniform by construction; readfirstlane keeps it an SGPR in every instance)
-    const uint32_t soff = __builtin_amdgcn_readfirstlane((uint32_t)kr_i * (BK * 2));
+    const uint32_t soff = __builtin_amdgcn_readfirstlane((uint32_t)(kb_i + kr_i) * (BK * 2));
     if (++kr_i == nk) kr_i = 0;
     const uint32_t slot = lbase + (uint32_t)slot_i * (STAGE_H8 * 16);
 #pragma unroll
@@ -1030,12 +1049,13 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
 
     if (++kt_c == nk) {               // tile done: epilogue from registers
       kt_c = 0;
-      const int tile = it_c * G + off;
+      const int unit = it_c * G + off;
+      const int tile = unit % n_tiles, kpart = unit / n_tiles;
       ++it_c;
       const int m0 = (tile / nN) * BM, n0 = (tile % nN) * BN;
       const int64_t cbytes = (int64_t)(M - m0) * N * OUT_B;
       const __amdgpu_buffer_rsrc_t rc =
-          panel(static_cast<char*>(Cout) + (int64_t)m0 * N * OUT_B, cbytes);
+          panel(static_cast<char*>(Cout) + ((int64_t)kpart * M + m0) * N * OUT_B, cbytes);
       __amdgpu_buffer_rsrc_t rl = rc;
       if constexpr (SPLIT && EPI != kEpiF32)
         rl = panel(Clo + (int64_t)m0 * N, (int64_t)(M - m0) * N * 2);
@@ -1167,7 +1187,8 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
           }
         }
       } else {
-        pipe_plain_epilogue<EPI, SPLIT, CFG, P_NO_STORE>(acc, bias_l, rc, rl, N, n0, wr, wc, lane);
+        pipe_plain_epilogue<EPI, SPLIT, CFG, P_NO_STORE>(
+            acc, kpart ? bias_l + kPipeBiasMax / 2 : bias_l, rc, rl, N, n0, wr, wc, lane);
       }
 #pragma unroll
       for (int i = 0; i < FM; ++i)

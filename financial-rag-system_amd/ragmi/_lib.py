@@ -113,6 +113,9 @@ BERT_API = {
                                        c_vp]),
     "rag_bert_gemm": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
                                      ctypes.c_int, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_vp]),
+    "rag_bert_gemm_splitk": (ctypes.c_int, [ctypes.c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                            ctypes.c_int, ctypes.c_int, ctypes.c_int, c_vp,
+                                            ctypes.c_int, ctypes.POINTER(ctypes.c_int), c_vp]),
     "rag_bert_gemm_add_ln": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                             ctypes.c_float, ctypes.c_int, ctypes.c_int,
                                             ctypes.c_int, c_vp, c_vp, c_vp, c_vp]),

@@ -116,6 +116,15 @@ int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, co
                   const void* W_lo, const float* bias, int M, int N, int K, void* C,
                   void* C_lo, void* stream);
 
+/* Diagnostic (parity tests, GEMM benchmark): the fp32-output GEMM with the split-K the forward
+ * uses for small token batches — C holds max_parts x [M][N] floats and receives `*parts`
+ * partial products (part 0 carries the bias) whose sum is A . W^T + bias; the forward sums
+ * them in order inside its residual + LayerNorm pass. variant: AUTO, SMALL or SMALL_BK64
+ * (AUTO outside the small-batch regime writes one part). */
+int rag_bert_gemm_splitk(int variant, const void* A, const void* A_lo, const void* W,
+                         const void* W_lo, const float* bias, int M, int N, int K, float* C,
+                         int max_parts, int* parts, void* stream);
+
 /* the output projection of an encoder layer with its residual + LayerNorm fused
  * (modeling_bert.py BertSelfOutput / BertOutput: LayerNorm(dense(h) + x), eval mode), in place
  * on the fp32 residual rows: x[M,N] = LN(x + A . W^T + bias) * gamma + beta, xh = fp16(x),

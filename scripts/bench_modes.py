@@ -252,7 +252,11 @@ def run_pipeline(args, cfg_id):
     bge_w, ce_w = R.make_weights(R.BGE_SMALL, 1), R.make_weights(R.MINILM_CE, 2)
     bge = BertEncoder(R.BGE_SMALL, bge_w, HEAD_CLS_L2, dev, prec)
     ce = BertEncoder(R.MINILM_CE, ce_w, HEAD_POOLER_CLS, dev, prec)
-    S = args.streams or 2
+    # 3 batches in flight: each stream takes one of the process's 4 hardware queues with the
+    # null stream on the 4th (GPU_MAX_HW_QUEUES); a 4th stream would share a queue with
+    # another and serialise behind it (config 2: 2 / 3 / 4 in flight 60.7K / 71.1K / 60.4K
+    # qps, profiles/r03b_small_gemm.jsonl)
+    S = args.streams or 3
     streams = [torch.cuda.Stream(dev) for _ in range(S)]
     ev_every = 4                        # CE forward events on every 4th batch (sampled)
     evs, flops = [], []

@@ -194,3 +194,44 @@ def test_ws_split_last_round_bitwise(gpu, shape, epi, split):
     for x0, x1 in (zip(r0, r1) if isinstance(r0, tuple) else [(r0, r1)]):
         v = torch.int16 if x0.dtype == torch.float16 else torch.int32
         assert torch.equal(x0.view(v), x1.view(v))
+
+
+@pytest.mark.parametrize("shape", [(1, 384, 384), (782, 384, 384), (782, 384, 1536),
+                                   (33, 1024, 4096), (3001, 384, 1536)],
+                         ids=lambda s: "x".join(map(str, s)))
+@pytest.mark.parametrize("split", [False, True], ids=["fp16", "fp16x3"])
+@pytest.mark.parametrize("variant", [0, 5, 10], ids=["auto", "small", "small64"])
+def test_gemm_splitk_parts_sum_to_fp64(gpu, shape, split, variant):
+    """Split-K of the small-batch fp32-output GEMMs (rag_bert_gemm_splitk: the parts the
+    forward sums in its residual + LayerNorm pass): sum of parts vs fp64 at the fp32-output
+    bound, part 0 alone carries the bias, and the part count depends on K only (batch
+    independence)."""
+    import ctypes
+
+    from ragmi import _lib
+    M, N, K = shape
+    a, al, w, wl, bias, a64, w64 = _operands(M, N, K, split, seed=3 * M + K)
+    c = torch.full((4, M, N), float("nan"), device="cuda")
+    parts = ctypes.c_int()
+    _lib.check(_lib.load().rag_bert_gemm_splitk(
+        variant, a.data_ptr(), al.data_ptr() if split else None, w.data_ptr(),
+        wl.data_ptr() if split else None, bias.data_ptr(), M, N, K, c.data_ptr(), 4,
+        ctypes.byref(parts), torch.cuda.current_stream().cuda_stream))
+    torch.cuda.synchronize()
+    p = parts.value
+    assert 1 <= p <= 4
+    tot = c[:p].double().sum(0)
+    _check(tot, _ref(a64, w64, bias, 2), 2, split)
+    if p > 1:
+        # parts 1.. are bias-free partial products (no part is left unwritten)
+        assert not bool(torch.isnan(c[:p]).any())
+    if M > 1 and variant != 0:
+        one = torch.full((4, 1, N), float("nan"), device="cuda")
+        p1 = ctypes.c_int()
+        _lib.check(_lib.load().rag_bert_gemm_splitk(
+            variant, a[:1].contiguous().data_ptr(), al[:1].contiguous().data_ptr() if split else None,
+            w.data_ptr(), wl.data_ptr() if split else None, bias.data_ptr(), 1, N, K,
+            one.data_ptr(), 4, ctypes.byref(p1), torch.cuda.current_stream().cuda_stream))
+        torch.cuda.synchronize()
+        assert p1.value == p
+        assert torch.equal(one[:p].sum(0)[0], c[:p, 0].sum(0))
