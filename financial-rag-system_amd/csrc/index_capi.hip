@@ -46,6 +46,12 @@ struct Workspace {
   int* fb_tier = nullptr;       // [groups][32] certifying path per query of the last pass
   unsigned long long* fb_cnt = nullptr;   // [2] tier-1 / tier-2 totals since creation
   int* tileq = nullptr;         // [8][kTileQStride] per-XCD tile-queue heads (dynamic scan)
+  // tier-2 hand-off select -> rescan_kernel: (L, e_k) per query, the rescan workgroups' lists
+  // [query][kRescanMaxWG][32] and per-query arrival tickets (zero between passes)
+  float* t2 = nullptr;
+  float* t2_s = nullptr;
+  int* t2_i = nullptr;
+  int* t2_tk = nullptr;
   hipEvent_t ev_in = nullptr;   // scan-stream order: caller stream -> scan stream -> caller
   hipEvent_t ev_out = nullptr;
   hipStream_t owner = nullptr;  // stream of the last pass that used this slot
@@ -140,10 +146,38 @@ double store_eps(const rag_index* h) {
 
 // sample + thresh: seed thresholds for the scan (see sample_kernel). ~0.8% of the shard's
 // tiles, spread evenly, at least 256 tiles (all of them for small shards).
+// D <= 384 (one query group): qprep fused into the sample launch (qprep_sample_kernel);
+// RAGMI_FUSED_PREP=0 (diagnostic A/B) keeps the separate qprep launch
+bool fused_prep() {
+  static const bool on = [] {
+    const char* v = std::getenv("RAGMI_FUSED_PREP");
+    return !(v && std::atoi(v) == 0);
+  }();
+  return on;
+}
+
 template <int D, bool FILTER>
-void launch_seed(rag_index* h, Workspace& w, int groups, hipStream_t st) {
+void launch_seed(rag_index* h, Workspace& w, int groups, hipStream_t st,
+                 const float* q = nullptr, int Bq = 0, const uint32_t* filt_in = nullptr) {
   using namespace ragmi;
   const int n_tiles = (int)((h->count + 15) / 16);
+  if (q) {     // fused: qprep inside the sample launch (also when there is nothing to sample)
+    if constexpr (D <= 384) {
+      static const int div_f = [] {
+        const char* v = std::getenv("RAGMI_SAMPLE_DIV");
+        return v ? std::max(1, std::atoi(v)) : 128;
+      }();
+      const int n_sample = n_tiles == 0 ? 0 : std::min({n_tiles, std::max(256, n_tiles / div_f),
+                                                        kMaxSample});
+      qprep_sample_kernel<D, FILTER><<<dim3(std::max(1, (n_sample + 7) / 8)), dim3(256), 0, st>>>(
+          q, Bq, filt_in, w.qn, w.qfrag, w.filt, w.eps, store_eps(h), h->corpus, h->tags,
+          (int)h->count, n_tiles, n_sample, w.smax);
+      if (n_sample > 0)
+        thresh_kernel<kMaxSample><<<dim3(kQ, 1), dim3(256), 0, st>>>(w.smax, n_sample, w.eps,
+                                                                    w.seed);
+    }
+    return;
+  }
   if (n_tiles == 0) return;   // the scan visits no tile; seeds are never read
   static const int div = [] {
     const char* v = std::getenv("RAGMI_SAMPLE_DIV");   // tuning knob: 1 / sampled fraction
@@ -169,12 +203,19 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
   using namespace ragmi;
   // Bq <= 32 * h->groups queries: `groups` query groups of 32 (one for D <= 384)
   const int groups = (Bq + kQ - 1) / kQ;
-  qprep_kernel<D><<<dim3(groups * kQ), dim3(64), 0, st>>>(q, Bq, filt, w.qn, w.qfrag, w.filt,
-                                                          w.eps, store_eps(h));
-  if (filt)
-    launch_seed<D, true>(h, w, groups, st);
-  else
-    launch_seed<D, false>(h, w, groups, st);
+  if (D <= 384 && groups == 1 && fused_prep()) {
+    if (filt)
+      launch_seed<D, true>(h, w, groups, st, q, Bq, filt);
+    else
+      launch_seed<D, false>(h, w, groups, st, q, Bq, nullptr);
+  } else {
+    qprep_kernel<D><<<dim3(groups * kQ), dim3(64), 0, st>>>(q, Bq, filt, w.qn, w.qfrag, w.filt,
+                                                            w.eps, store_eps(h));
+    if (filt)
+      launch_seed<D, true>(h, w, groups, st);
+    else
+      launch_seed<D, false>(h, w, groups, st);
+  }
   const int64_t n_tiles = (h->count + 15) / 16;
   // D <= 384: queries in VGPRs, 2 workgroups per CU; wider rows: queries in LDS, 1 per CU,
   // R workgroups per query group (R % 8 == 0: XCD pairing of the groups, scan_lds_kernel)
@@ -255,7 +296,7 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
     st = caller;
   }
   const int n_lists = wide ? grid : grid * (kLdsQ ? kLdsWaves : kWavesPerWG);   // per group
-  const ExactStats fb{w.fb_tier, w.fb_cnt};
+  const ExactStats fb{w.fb_tier, w.fb_cnt, w.t2};
   // select certifies every query's top-k; its fallbacks (list re-scoring, a workgroup-local
   // second pass over the shard) run inside the same launch
 #define RAG_SELECT(F)                                                                          \
@@ -268,6 +309,24 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
   else
     RAG_SELECT(false);
 #undef RAG_SELECT
+  // tier 2 of the certificate, when select marked a query (returns at once otherwise): R
+  // workgroups split the shard's tiles, ~256 tiles each, at most kRescanMaxWG (two per CU)
+  // RAGMI_RESCAN_WG (diagnostic A/B): workgroup cap of the rescan launch; 0 = not launched
+  // (tier-2 queries are then left unanswered: timing only)
+  static const int rescan_cap = [] {
+    const char* v = std::getenv("RAGMI_RESCAN_WG");
+    return v ? std::atoi(v) : ragmi::kRescanMaxWG;
+  }();
+  if (rescan_cap > 0) {
+    const int n_tiles = (int)((h->count + 15) / 16);
+    const int R = std::max(1, std::min(std::min(rescan_cap, ragmi::kRescanMaxWG), n_tiles / 256));
+#define RAG_RESCAN(F)                                                                            rescan_kernel<D, F><<<dim3(R), dim3(256), 0, st>>>(                                                w.fb_tier, w.t2, Bq, h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, w.qn, k, w.eps,       w.t2_s, w.t2_i, w.t2_tk, id_offset, out_s, out_i, out_packed, h->rows32)
+    if (filt)
+      RAG_RESCAN(true);
+    else
+      RAG_RESCAN(false);
+#undef RAG_RESCAN
+  }
   RAG_HIP(hipGetLastError());
   return RAG_OK;
 }
@@ -597,6 +656,13 @@ int rag_index_create_ex(int dim, int64_t capacity_rows, int device, int storage,
               hipMalloc(reinterpret_cast<void**>(&w.fb_cnt), 16) == hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&w.tileq), 8 * ragmi::kTileQStride * 4) ==
                   hipSuccess &&
+              hipMalloc(reinterpret_cast<void**>(&w.t2), G * Q * 2 * 4) == hipSuccess &&
+              hipMalloc(reinterpret_cast<void**>(&w.t2_s),
+                        G * Q * ragmi::kRescanMaxWG * 32 * 4) == hipSuccess &&
+              hipMalloc(reinterpret_cast<void**>(&w.t2_i),
+                        G * Q * ragmi::kRescanMaxWG * 32 * 4) == hipSuccess &&
+              hipMalloc(reinterpret_cast<void**>(&w.t2_tk), G * Q * 4) == hipSuccess &&
+              hipMemset(w.t2_tk, 0, G * Q * 4) == hipSuccess &&
               hipMemset(w.tileq, 0, 8 * ragmi::kTileQStride * 4) == hipSuccess &&
               hipMemset(w.fb_cnt, 0, 16) == hipSuccess &&
               hipMemset(w.fb_tier, 0, G * Q * 4) == hipSuccess;
@@ -630,6 +696,8 @@ int rag_index_destroy(rag_index_t* h) {
     if (w.fb_tier) (void)hipFree(w.fb_tier);
     if (w.fb_cnt) (void)hipFree(w.fb_cnt);
     if (w.tileq) (void)hipFree(w.tileq);
+    for (void* p : {(void*)w.t2, (void*)w.t2_s, (void*)w.t2_i, (void*)w.t2_tk})
+      if (p) (void)hipFree(p);
     if (w.ev_in) (void)hipEventDestroy(w.ev_in);
     if (w.ev_out) (void)hipEventDestroy(w.ev_out);
   }

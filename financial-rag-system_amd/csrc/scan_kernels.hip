@@ -92,21 +92,30 @@ __global__ __launch_bounds__(64) void upsert_kernel(const float* __restrict__ ve
 // ----------------------------------------------------------------------------------------
 constexpr double kRowNorm = 1.001;   // fp16(unit vector): ||c|| <= 1 + 2^-11 + sqrt(D) 2^-25
 
+// one query slot b by one wave. The B-fragment goes to qf (global or an LDS image of the same
+// layout); qn / filt / eps are written only when `publish` (the fused qprep_sample_kernel:
+// every workgroup builds the fragments it samples with, workgroup 0 publishes)
 template <int D>
-__global__ __launch_bounds__(64) void qprep_kernel(const float* __restrict__ q, int B,
-                                                   const uint32_t* __restrict__ filt_in,
-                                                   float* __restrict__ qn,
-                                                   half8* __restrict__ qfrag,
-                                                   uint32_t* __restrict__ filt,
-                                                   float* __restrict__ eps,
-                                                   double store_eps = 0.0) {
-  const int b = blockIdx.x;
-  const int lane = threadIdx.x;
+__device__ __forceinline__ void qprep_slot(const float* __restrict__ q, int B, int b, int lane,
+                                           const uint32_t* __restrict__ filt_in,
+                                           float* __restrict__ qn, half8* __restrict__ qf,
+                                           uint32_t* __restrict__ filt, float* __restrict__ eps,
+                                           double store_eps, bool publish,
+                                           uint32_t* __restrict__ filt_copy = nullptr,
+                                           half8* __restrict__ qf_glob = nullptr) {
   const bool live = b < B;
   if (lane == 0) {
     // per-query payload filter (mask, value); padding / unfiltered queries match every row
-    filt[2 * b] = (live && filt_in) ? filt_in[2 * b] : 0u;
-    filt[2 * b + 1] = (live && filt_in) ? filt_in[2 * b + 1] : 0u;
+    const uint32_t fm = (live && filt_in) ? filt_in[2 * b] : 0u;
+    const uint32_t fv = (live && filt_in) ? filt_in[2 * b + 1] : 0u;
+    if (publish) {
+      filt[2 * b] = fm;
+      filt[2 * b + 1] = fv;
+    }
+    if (filt_copy) {
+      filt_copy[2 * b] = fm;
+      filt_copy[2 * b + 1] = fv;
+    }
   }
   double norm = 0.0;
   if (live) norm = sqrt(canon_sumsq<D>(q + (int64_t)b * D, lane));
@@ -117,15 +126,17 @@ __global__ __launch_bounds__(64) void qprep_kernel(const float* __restrict__ q, 
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float y = live ? canon_scale(q[(int64_t)b * D + 8 * c + j], norm) : 0.0f;
-      qn[b * D + 8 * c + j] = y;
+      if (publish) qn[b * D + 8 * c + j] = y;
       h[j] = f32_to_f16(y);
       const double hd = (double)h[j], dd = hd - (double)y;
       dq2 = fma(dd, dd, dq2);
       hh2 = fma(hd, hd, hh2);
     }
     const int s = c >> 2, hh = c & 3;
-    qfrag[(qt * steps<D>() + s) * 64 + hh * 16 + c16] = h;
+    qf[(qt * steps<D>() + s) * 64 + hh * 16 + c16] = h;
+    if (qf_glob) qf_glob[(qt * steps<D>() + s) * 64 + hh * 16 + c16] = h;
   }
+  if (!publish) return;
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) {
     dq2 += __shfl_xor(dq2, d, 64);
@@ -137,6 +148,17 @@ __global__ __launch_bounds__(64) void qprep_kernel(const float* __restrict__ q, 
     e = e * (1.0 + 0x1p-10) + 0x1p-22;
     eps[b] = live ? (float)(e * (1.0 + 0x1p-20)) : 0.0f;   // rounded up past fp32's RNE
   }
+}
+
+template <int D>
+__global__ __launch_bounds__(64) void qprep_kernel(const float* __restrict__ q, int B,
+                                                   const uint32_t* __restrict__ filt_in,
+                                                   float* __restrict__ qn,
+                                                   half8* __restrict__ qfrag,
+                                                   uint32_t* __restrict__ filt,
+                                                   float* __restrict__ eps,
+                                                   double store_eps = 0.0) {
+  qprep_slot<D>(q, B, blockIdx.x, threadIdx.x, filt_in, qn, qfrag, filt, eps, store_eps, true);
 }
 
 // ----------------------------------------------------------------------------------------
@@ -1529,6 +1551,63 @@ __global__ __launch_bounds__(256) void sample_kernel(const half8* __restrict__ c
   sample_epilogue<FILTER>(sc, t0, t1, two, j0, lane, tags, filt, n_rows, n_sample, smax);
 }
 
+// qprep + sample in ONE launch (D <= 384, one query group; round 3): every workgroup builds the
+// 32 queries' B-fragments itself (qprep_slot, 8 slots per wave, into an LDS image of qfrag's
+// layout) and samples its tiles against them; workgroup 0 also publishes qn / qfrag / filt / eps
+// for the scan and select. The fragments are those qprep_kernel writes (same arithmetic), so
+// the maxima, the seeds and every result are unchanged. Why: at small shards each launch of a
+// search pass costs ~3 us of throughput (1.25M rows, 4 passes in flight: one more tiny kernel
+// per pass measured -1.8%, profiles/r03c_rescan_ab.jsonl); this removes qprep's.
+template <int D, bool FILTER>
+__global__ __launch_bounds__(256) void qprep_sample_kernel(
+    const float* __restrict__ q, int B, const uint32_t* __restrict__ filt_in,
+    float* __restrict__ qn, half8* __restrict__ qfrag, uint32_t* __restrict__ filt,
+    float* __restrict__ eps, double store_eps, const half8* __restrict__ corpus,
+    const uint32_t* __restrict__ tags, int n_rows, int n_tiles, int n_sample,
+    float* __restrict__ smax) {
+  constexpr int S = steps<D>();
+  static_assert(S <= 12, "qprep_sample_kernel: D <= 384");
+  __shared__ half8 qf_l[2 * S * 64];
+  __shared__ uint32_t filt_l[2 * kQ];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const bool publish = blockIdx.x == 0;
+  for (int b = wid; b < kQ; b += 4)
+    qprep_slot<D>(q, B, b, lane, filt_in, qn, qf_l, filt, eps, store_eps, publish, filt_l,
+                  publish ? qfrag : nullptr);
+  __syncthreads();
+  const int w = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(wid);
+  const int j0 = 2 * w;
+  if (j0 >= n_sample) return;
+  const bool two = j0 + 1 < n_sample;
+  const int t0 = (int)(((int64_t)j0 * n_tiles) / n_sample);
+  const int t1 = two ? (int)(((int64_t)(j0 + 1) * n_tiles) / n_sample) : t0;
+  const half8* p0 = corpus + (int64_t)t0 * (S * 64) + lane;
+  const half8* p1 = corpus + (int64_t)t1 * (S * 64) + lane;
+  floatx4 sc[2][2];
+  half8 a0[S], a1[S], b0[S], b1[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    a0[s] = __builtin_nontemporal_load(p0 + s * 64);
+    a1[s] = __builtin_nontemporal_load(p1 + s * 64);
+    b0[s] = qf_l[s * 64 + lane];
+    b1[s] = qf_l[(S + s) * 64 + lane];
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const half8(&a)[S] = u == 0 ? a0 : a1;
+    floatx4 acc0 = {0.f, 0.f, 0.f, 0.f};
+    floatx4 acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[s], b0[s], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[s], b1[s], acc1, 0, 0, 0);
+    }
+    sc[u][0] = acc0;
+    sc[u][1] = acc1;
+  }
+  sample_epilogue<FILTER>(sc, t0, t1, two, j0, lane, tags, filt_l, n_rows, n_sample, smax);
+}
+
 constexpr int kSampleGroups = 4;   // query groups of 32 per wide pass (index_capi kMaxGroups)
 
 // D = 1024 with several query groups: one pass over each sample tile for ALL groups (the
@@ -1732,6 +1811,7 @@ __device__ __forceinline__ void exact_scores_wave(const half8* __restrict__ corp
 struct ExactStats {
   int* tier;
   unsigned long long* cnt;
+  float* t2;        // [B][2] tier-2 hand-off: (L, e_k) of each tier-2 query (rescan_kernel)
 };
 
 // ----------------------------------------------------------------------------------------
@@ -1752,15 +1832,12 @@ struct ExactStats {
 //     tier 1 (here): if L >= the scan's seed (no such row was pruned) and no per-wave list
 //       whose tail is >= L is full (none dropped one), every row with a >= L sits in some
 //       list: rescore all of them exactly and emit their top-k.
-//     tier 2 (here too): otherwise this workgroup streams the shard once more for its query:
-//       approximate scores by v_dot2 over the query's fp16 fragment (error within eps_q,
-//       like the scan's), rows with a >= max(L, thr - eps_q) scored exactly into each wave's
-//       running exact top-32 (thr = its 32nd, starting just below e_k), merged, emitted.
-//       Only inputs with more than 32 in-band rows inside one wave's share of the tiles (or
-//       a seed above L) get here; it costs a single-CU pass over the shard, and no launch
-//       at all when unused (a separate always-launched rescan kernel cost ~5% of the
-//       small-shard throughput: its workgroups cannot start beside another stream's
-//       full-occupancy scan).
+//     tier 2 (rescan_kernel): otherwise the shard is streamed once more for this query by
+//       the rescan kernel launched after every select (its workgroups split the shard); here
+//       select only records L and e_k. Only inputs with more than 32 in-band rows inside one
+//       wave's share of the tiles (or a seed above L) get there. (Round 2 ran this pass
+//       inside select, on the query's one workgroup: a single-CU pass over the whole shard,
+//       ~0.1 s at 10M rows — unbounded by the chip's bandwidth; VERDICT/ADVICE r2.)
 // ----------------------------------------------------------------------------------------
 template <int D, bool FILTER>
 __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ part_s,
@@ -2075,68 +2152,16 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
   float rs = kNegInf;   // each wave's running exact top-32 (lanes 0..31, best first)
   int ri = kIdNone32;
   if (verdict == 2) {
-    // ---- tier 2: stream the shard (tiles t = wid, wid + 4, ...: rows increase per wave)
-    constexpr int S = steps<D>();
-    const float e = eps[bq];
-    uint32_t fm = 0, fv = 0;
-    if constexpr (FILTER) {
-      fm = filt[2 * bq];
-      fv = filt[2 * bq + 1];
-    }
-    const int hh = lane >> 4, rr = lane & 15;
-    // lane (hh, rr): dims 32 s + 8 hh .. + 7 of row 16 t + rr and of query b (qprep's
-    // B-fragment of query tile b >> 4, column b & 15)
-    const half8* qf = qfrag + grp * (2 * S * 64) + ((b >> 4) * S) * 64 + hh * 16 + (b & 15);
-    float thr = nextafterf(floor_E, kNegInf);   // every true top-k row scores >= e_k
-    const int n_tiles = (n_rows + kTileRows - 1) / kTileRows;
-    for (int t = wid; t < n_tiles; t += 4) {
-      const half8* tp = corpus + (int64_t)t * (S * 64) + hh * 16 + rr;
-      float a = 0.f;
-#pragma unroll 4
-      for (int s2 = 0; s2 < S; ++s2) {
-        const half8 x = tp[s2 * 64], y = qf[s2 * 64];
-        a = __builtin_amdgcn_fdot2(half2v{x[0], x[1]}, half2v{y[0], y[1]}, a, false);
-        a = __builtin_amdgcn_fdot2(half2v{x[2], x[3]}, half2v{y[2], y[3]}, a, false);
-        a = __builtin_amdgcn_fdot2(half2v{x[4], x[5]}, half2v{y[4], y[5]}, a, false);
-        a = __builtin_amdgcn_fdot2(half2v{x[6], x[7]}, half2v{y[6], y[7]}, a, false);
-      }
-      a += __shfl_xor(a, 16, 64);
-      a += __shfl_xor(a, 32, 64);
-      const int row = t * kTileRows + rr;
-      bool ok = lane < 16 && row < n_rows;
-      if constexpr (FILTER) ok = ok && ((tags[row < n_rows ? row : 0] & fm) == fv);
-      uint64_t m = __ballot(ok && a >= fmaxf(L, thr - e));
-      while (m) {
-        int rows[8];
-        float es[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int ln = m ? (int)__builtin_ctzll(m) : -1;
-          if (m) m &= m - 1;
-          rows[j] = ln >= 0 ? t * kTileRows + ln : -1;
-        }
-        exact_scores_wave<D, 8>(corpus, rows, qq, lane, es, rows32);
-        float ns = kNegInf;
-        int ni = kIdNone32;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          if (lane == 32 + j && rows[j] >= 0 && es[j] > thr) {
-            ns = es[j];
-            ni = rows[j];
-          }
-        }
-        if (lane >= 32) {
-          rs = ns;
-          ri = ni;
-        }
-        bitonic_sort64(rs, ri, lane);
-        thr = fmaxf(thr, __shfl(rs, 31, 64));
-      }
-    }
+    // ---- tier 2: handed to rescan_kernel (launched after every select, many workgroups):
+    // its floor L and the k-th exact score of A go to the hand-off record; nothing is emitted
+    // here (the rescan writes this query's output)
     if (tid == 0) {
       fb.tier[bq] = 2;
+      fb.t2[2 * bq] = L;
+      fb.t2[2 * bq + 1] = floor_E;
       atomicAdd(&fb.cnt[1], 1ull);
     }
+    return;
   } else {   // tier 1
   if (tid == 0) {
     fb.tier[bq] = 1;
@@ -2197,6 +2222,185 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
       bitonic_merge64(s, id, lane);
     }
     emit(s, id);
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// rescan (tier 2 of select's certificate): launched after every select with R workgroups; each
+// returns at once unless some query of the pass is marked tier 2. For such a query q,
+// workgroup r streams tiles t = 4 r + w, 4 r + w + 4 R, ... (wave w; rows increase per wave,
+// which the strict `> thr` tie rule needs), scores them approximately with v_dot2 over the
+// query's fp16 fragment (error within eps_q, the scan's bound), rescores rows with
+// a >= max(L, thr - eps_q) exactly into each wave's running exact top-32 (thr = its 32nd,
+// starting just below e_k: every true top-k row scores >= e_k), merges its 4 waves and
+// publishes its 32 best; the workgroup that arrives last (device-scope ticket) merges the R
+// lists and emits q's exact top-k. The global top-k lies in the union of the shares' top-32s
+// (k <= 32). Bounded: R workgroups over the shard instead of select's one.
+// Visibility: each workgroup's list stores, then __threadfence() (agent-scope release +
+// acquire: L2 write-back, L1 invalidate) before its ticket; the last arriver fences again
+// before it reads the other lists (MI355X_MICROARCH.md, inter-workgroup visibility).
+// Few registers and no dynamic LDS: the launch must fit beside full-occupancy scans of other
+// streams when it has nothing to do.
+// ----------------------------------------------------------------------------------------
+constexpr int kRescanMaxWG = 512;
+
+template <int D, bool FILTER>
+__global__ __launch_bounds__(256, 8) void rescan_kernel(
+    const int* __restrict__ tier, const float* __restrict__ t2, int Bq,
+    const half8* __restrict__ corpus, const uint32_t* __restrict__ tags,
+    const uint32_t* __restrict__ filt, const half8* __restrict__ qfrag, int n_rows,
+    const float* __restrict__ qn, int k, const float* __restrict__ eps,
+    float* __restrict__ lst_s, int* __restrict__ lst_i, int* __restrict__ tickets,
+    int64_t id_offset, float* __restrict__ out_s, int64_t* __restrict__ out_i,
+    int32_t* __restrict__ out_packed, const float* __restrict__ rows32) {
+  __shared__ float c_s[4][32];
+  __shared__ int c_i[4][32];
+  __shared__ int last;
+  const int R = gridDim.x, r = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  constexpr int S = steps<D>();
+  const int n_tiles = (n_rows + kTileRows - 1) / kTileRows;
+  // the pass's tier-2 queries (Bq <= 128) from two loads per lane, not one dependent load
+  // per query: the common case (none) costs one round trip
+  uint64_t todo[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int q = lane + 64 * h;
+    todo[h] = __ballot(q < Bq && tier[q < Bq ? q : 0] == 2);
+  }
+  for (int h = 0; h < 2; ++h)
+  while (todo[h]) {
+    const int bq = 64 * h + (int)__builtin_ctzll(todo[h]);
+    todo[h] &= todo[h] - 1;
+    const int grp = bq / kQ, b = bq % kQ;
+    const float L = t2[2 * bq], E = t2[2 * bq + 1];
+    const float e = eps[bq];
+    const float* qq = qn + (int64_t)bq * D;
+    uint32_t fm = 0, fv = 0;
+    if constexpr (FILTER) {
+      fm = filt[2 * bq];
+      fv = filt[2 * bq + 1];
+    }
+    const int hh = lane >> 4, rr = lane & 15;
+    // lane (hh, rr): dims 32 s + 8 hh .. + 7 of row 16 t + rr and of query b (qprep's
+    // B-fragment of query tile b >> 4, column b & 15)
+    const half8* qf = qfrag + grp * (2 * S * 64) + ((b >> 4) * S) * 64 + hh * 16 + (b & 15);
+    float thr = nextafterf(E, kNegInf);
+    float rs = kNegInf;
+    int ri = kIdNone32;
+    for (int t = 4 * r + wid; t < n_tiles; t += 4 * R) {
+      const half8* tp = corpus + (int64_t)t * (S * 64) + hh * 16 + rr;
+      float a = 0.f;
+#pragma unroll 2
+      for (int s2 = 0; s2 < S; ++s2) {
+        const half8 x = tp[s2 * 64], y = qf[s2 * 64];
+        a = __builtin_amdgcn_fdot2(half2v{x[0], x[1]}, half2v{y[0], y[1]}, a, false);
+        a = __builtin_amdgcn_fdot2(half2v{x[2], x[3]}, half2v{y[2], y[3]}, a, false);
+        a = __builtin_amdgcn_fdot2(half2v{x[4], x[5]}, half2v{y[4], y[5]}, a, false);
+        a = __builtin_amdgcn_fdot2(half2v{x[6], x[7]}, half2v{y[6], y[7]}, a, false);
+      }
+      a += __shfl_xor(a, 16, 64);
+      a += __shfl_xor(a, 32, 64);
+      const int row = t * kTileRows + rr;
+      bool ok = lane < 16 && row < n_rows;
+      if constexpr (FILTER) ok = ok && ((tags[row < n_rows ? row : 0] & fm) == fv);
+      uint64_t m = __ballot(ok && a >= fmaxf(L, thr - e));
+      while (m) {
+        int rows[2];
+        float es[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int ln = m ? (int)__builtin_ctzll(m) : -1;
+          if (m) m &= m - 1;
+          rows[j] = ln >= 0 ? t * kTileRows + ln : -1;
+        }
+        exact_scores_wave<D, 2>(corpus, rows, qq, lane, es, rows32);
+        float ns = kNegInf;
+        int ni = kIdNone32;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          if (lane == 32 + j && rows[j] >= 0 && es[j] > thr) {
+            ns = es[j];
+            ni = rows[j];
+          }
+        }
+        if (lane >= 32) {
+          rs = ns;
+          ri = ni;
+        }
+        bitonic_sort64(rs, ri, lane);
+        thr = fmaxf(thr, __shfl(rs, 31, 64));
+      }
+    }
+    // this workgroup's 32 best: merge the 4 waves' lists
+    if (lane < 32) {
+      c_s[wid][lane] = rs;
+      c_i[wid][lane] = ri;
+    }
+    __syncthreads();
+    float* ms = lst_s + ((int64_t)bq * kRescanMaxWG + r) * 32;
+    int* mi = lst_i + ((int64_t)bq * kRescanMaxWG + r) * 32;
+    if (wid == 0) {
+      float x = lane < 32 ? c_s[0][lane] : kNegInf;
+      int id = lane < 32 ? c_i[0][lane] : kIdNone32;
+      for (int v = 1; v < 4; ++v) {
+        if (lane >= 32) {
+          x = c_s[v][63 - lane];
+          id = c_i[v][63 - lane];
+        }
+        bitonic_merge64(x, id, lane);
+      }
+      if (lane < 32) {
+        ms[lane] = x;
+        mi[lane] = id;
+      }
+      __threadfence();                           // the list is visible before the ticket
+      if (lane == 0) last = atomicAdd(&tickets[bq], 1) == R - 1;
+    }
+    __syncthreads();
+    if (last) {
+      __threadfence();                           // acquire: the other workgroups' lists
+      // wave w merges lists w, w + 4, ...; wave 0 then merges the 4 results
+      float x = kNegInf;
+      int id = kIdNone32;
+      for (int w2 = wid; w2 < R; w2 += 4) {
+        const float* os = lst_s + ((int64_t)bq * kRescanMaxWG + w2) * 32;
+        const int* oi = lst_i + ((int64_t)bq * kRescanMaxWG + w2) * 32;
+        if (lane >= 32) {
+          x = os[63 - lane];
+          id = oi[63 - lane];
+        }
+        bitonic_merge64(x, id, lane);
+      }
+      if (lane < 32) {
+        c_s[wid][lane] = x;
+        c_i[wid][lane] = id;
+      }
+      __syncthreads();
+      if (wid == 0) {
+        x = lane < 32 ? c_s[0][lane] : kNegInf;
+        id = lane < 32 ? c_i[0][lane] : kIdNone32;
+        for (int v = 1; v < 4; ++v) {
+          if (lane >= 32) {
+            x = c_s[v][63 - lane];
+            id = c_i[v][63 - lane];
+          }
+          bitonic_merge64(x, id, lane);
+        }
+        if (lane < k) {
+          const bool ok = x != kNegInf;
+          if (out_packed) {
+            out_packed[((int64_t)bq * k + lane) * 2] = __float_as_int(x);
+            out_packed[((int64_t)bq * k + lane) * 2 + 1] = ok ? (int32_t)(id + id_offset) : -1;
+          } else {
+            out_s[(int64_t)bq * k + lane] = x;
+            out_i[(int64_t)bq * k + lane] = ok ? (int64_t)id + id_offset : (int64_t)-1;
+          }
+        }
+        if (lane == 0) tickets[bq] = 0;          // re-armed for the slot's next pass
+      }
+    }
+    __syncthreads();
   }
 }
 

@@ -13,7 +13,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
 # translation units of libragmi.so
-SOURCES = ["index_capi.hip", "bert_capi.hip"]
+SOURCES = ["index_capi.hip", "bert_capi.hip", "wordpiece_capi.cpp"]
 HEADERS = ["device_common.hpp", "common_host.hpp", "scan_kernels.hip", "bert_kernels.hip"]
 
 

@@ -108,6 +108,12 @@ BERT_API = {
                                            ctypes.c_int, c_vp, c_vp]),
     "rag_encoder_forward_host": (ctypes.c_int, [c_vp, c_i32p_, c_i32p_, c_i32p_, ctypes.c_int,
                                                 ctypes.c_int, c_f32p]),
+    "rag_wordpiece_create": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int64, ctypes.c_int,
+                                            ctypes.c_int, ctypes.POINTER(c_vp)]),
+    "rag_wordpiece_destroy": (ctypes.c_int, [c_vp]),
+    "rag_wordpiece_encode": (ctypes.c_int, [c_vp, ctypes.c_char_p, c_i64p, ctypes.c_char_p,
+                                            c_i64p, ctypes.c_int, c_i32p_, c_i32p_, c_i32p_,
+                                            ctypes.c_int64, ctypes.POINTER(ctypes.c_uint8)]),
     "rag_build_pairs": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, c_vp, ctypes.c_int, c_vp,
                                        ctypes.c_int, c_vp, ctypes.c_int, c_vp, c_vp, c_vp, c_vp,
                                        c_vp]),

@@ -427,6 +427,27 @@ class WordPiece:
                                           clean_text=True, wordpieces_prefix="##")
         self.tok.enable_truncation(max_length=max_length, strategy="longest_first")
         self.max_length = max_length
+        # host-native ASCII path (rag_wordpiece_*, csrc/wordpiece_capi.cpp): same ids, no GIL;
+        # texts with non-ASCII bytes go through the Rust tokenizer above
+        self._native = None
+        try:
+            with open(vocab_file, "rb") as f:
+                vb = f.read()
+            L = _lib.load()
+            h = ctypes.c_void_p()
+            check(L.rag_wordpiece_create(vb, len(vb), int(max_length), int(bool(lowercase)),
+                                         ctypes.byref(h)))
+            self._native = (L, h)
+        except _lib.RagmiUnavailable:
+            self._native = None
+
+    def __del__(self):
+        nat = getattr(self, "_native", None)
+        if nat is not None:
+            try:
+                nat[0].rag_wordpiece_destroy(nat[1])
+            except Exception:
+                pass
 
     @classmethod
     def from_model_dir(cls, model_dir: str, max_length: int | None = None) -> "WordPiece":
@@ -450,9 +471,61 @@ class WordPiece:
 
     def encode_packed(self, texts, pairs=None):
         """Packed WordPiece ids / token types (int32 [T]) and cu_seqlens (int32 [B+1]) of a
-        batch of texts (or (text, pair) pairs). Uses the Rust tokenizer's offset-free batch
-        encoder (`encode_batch_fast`: same ids and type ids, no character offsets, ~5x less
-        host time per batch) and packs with one fromiter per array."""
+        batch of texts (or (text, pair) pairs). ASCII texts: the host-native encoder
+        (rag_wordpiece_encode; releases the GIL); anything else: the Rust tokenizer, spliced
+        in place. Same ids either way (tests/test_tokenizer_cpu.py)."""
+        texts = list(texts)
+        pairs = None if pairs is None else list(pairs)
+        if self._native is not None and texts:
+            return self._encode_native(texts, pairs)
+        return self._encode_rust(texts, pairs)
+
+    def _encode_native(self, texts, pairs):
+        L, h = self._native
+        n = len(texts)
+
+        def blob(strs):
+            bs = [t.encode("utf-8") for t in strs]
+            off = np.zeros(n + 1, np.int64)
+            np.cumsum([len(b) for b in bs], out=off[1:])
+            return b"".join(bs), off
+        tb, to = blob(texts)
+        pb, po = blob(pairs) if pairs is not None else (None, None)
+        cap = n * self.max_length
+        ids = np.empty(cap, np.int32)
+        types = np.empty(cap, np.int32)
+        cu = np.empty(n + 1, np.int32)
+        fb = np.zeros(n, np.uint8)
+        check(L.rag_wordpiece_encode(
+            h, tb, to.ctypes.data_as(_lib.c_i64p), pb,
+            po.ctypes.data_as(_lib.c_i64p) if po is not None else None, n,
+            ids.ctypes.data_as(_lib.c_i32p), types.ctypes.data_as(_lib.c_i32p),
+            cu.ctypes.data_as(_lib.c_i32p), cap,
+            fb.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))))
+        if not fb.any():
+            T = int(cu[-1])
+            return ids[:T].copy(), types[:T].copy(), cu
+        # splice the Rust tokenizer's encodings of the non-ASCII entries into place
+        js = np.nonzero(fb)[0]
+        r_ids, r_types, r_cu = self._encode_rust([texts[j] for j in js],
+                                                 None if pairs is None else [pairs[j] for j in js])
+        parts_i, parts_t, lens = [], [], np.diff(cu).astype(np.int64)
+        k = 0
+        for j in range(n):
+            if fb[j]:
+                a, b = r_cu[k], r_cu[k + 1]
+                parts_i.append(r_ids[a:b])
+                parts_t.append(r_types[a:b])
+                lens[j] = b - a
+                k += 1
+            else:
+                parts_i.append(ids[cu[j]:cu[j + 1]])
+                parts_t.append(types[cu[j]:cu[j + 1]])
+        out_cu = np.zeros(n + 1, np.int32)
+        np.cumsum(lens, out=out_cu[1:])
+        return np.concatenate(parts_i), np.concatenate(parts_t), out_cu
+
+    def _encode_rust(self, texts, pairs=None):
         inp = list(texts) if pairs is None else list(zip(texts, pairs))
         raw = getattr(self.tok, "_tokenizer", None)
         encs = (raw.encode_batch_fast(inp) if raw is not None and

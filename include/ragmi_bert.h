@@ -70,6 +70,24 @@ int rag_encoder_forward(rag_encoder_t* enc, const int32_t* ids_dev, const int32_
 int rag_encoder_forward_host(rag_encoder_t* enc, const int32_t* ids, const int32_t* types,
                              const int32_t* cu_seqlens, int B, int T, float* out);
 
+/* Host-native WordPiece tokenisation of ASCII text (sentence-transformers' encode(list[str]) /
+ * CrossEncoder.predict tokenise every call: main2.py:170-171, main.py:245). Exactly the rules
+ * of the Rust tokenizers BertWordPieceTokenizer (clean_text, lowercase, punctuation split,
+ * greedy longest-match WordPiece with "##" continuations, 100-char words -> [UNK],
+ * [CLS] a [SEP] (b [SEP]) with token types 0 / 1, 'longest_first' truncation to max_length).
+ * vocab_txt: the checkpoint's vocab.txt bytes (line i = id i, trailing whitespace trimmed,
+ * later duplicates win). Texts (and optional pairs) are byte blobs with n+1 offsets; a text or
+ * pair holding any byte >= 0x80 is skipped (fallback[j] = 1, zero tokens): the caller encodes
+ * it with the Unicode-complete tokenizer. Outputs: ids / types [<= cap], cu [n+1] (packed).
+ * Host memory, synchronous, thread-safe for concurrent encodes on one handle. */
+typedef struct rag_wordpiece rag_wordpiece_t;
+int rag_wordpiece_create(const char* vocab_txt, int64_t nbytes, int max_length, int lowercase,
+                         rag_wordpiece_t** out);
+int rag_wordpiece_destroy(rag_wordpiece_t* t);
+int rag_wordpiece_encode(const rag_wordpiece_t* t, const char* texts, const int64_t* text_off,
+                         const char* pairs, const int64_t* pair_off, int n, int32_t* ids,
+                         int32_t* types, int32_t* cu, int64_t cap, uint8_t* fallback);
+
 /* Cross-encoder batch assembly on the device (the batched rerank stage without a host round
  * trip: main.py:241-247 CrossEncoder.predict([[q, t] ...]) pair encoding
  * "[CLS] q [SEP] t [SEP]", token types 0/1, chunk truncated to fit max_len). Device pointers,

@@ -145,3 +145,29 @@ def test_random_queries_need_no_fallback(gpu):
     np.testing.assert_array_equal(i, i2)
     np.testing.assert_array_equal(s, s2)
     idx.close()
+
+
+def test_second_pass_packed_output_and_shard_offset(gpu):
+    """Tier 2 writes the multi-GPU exchange form too (rag_index_search_packed: the rescan's
+    last workgroup emits (score bits, global row) pairs with the shard's id_offset)."""
+    rng = np.random.default_rng(9)
+    n, dim = 200_000, 384
+    base = rng.standard_normal((1, dim)).astype(np.float32)
+    x = rng.standard_normal((n, dim)).astype(np.float32)
+    x[1::2] = base + 1e-5 * rng.standard_normal((n // 2, dim)).astype(np.float32)
+    q = np.concatenate([base + 0.02 * rng.standard_normal((2, dim)).astype(np.float32),
+                        rng.standard_normal((1, dim)).astype(np.float32)])
+    idx = _index(gpu, x)
+    off = 5_000_000
+    p = idx.search_packed(q, 15, id_offset=off)
+    torch.cuda.synchronize()
+    _, _, tiers = idx.exactness_stats(3)
+    assert (tiers[:2] == 2).all(), tiers
+    p = p.cpu().numpy()
+    s2, i2 = O.search(idx.export_rows(), q, 15)
+    np.testing.assert_array_equal(p[..., 1], (i2 + off).astype(np.int32))
+    np.testing.assert_array_equal(p[..., 0].view(np.float32), s2)
+    # repeated passes re-arm the per-query tickets: the same answer again
+    p2 = idx.search_packed(q, 15, id_offset=off).cpu().numpy()
+    np.testing.assert_array_equal(p2, p)
+    idx.close()

@@ -146,3 +146,98 @@ def test_longest_first_rule_sweep(vocab_file):
             want, want_t = R.encode(q, vocab, pair=c, max_length=ml)
             assert ids[cu[j]:cu[j + 1]].tolist() == want, (ml, q, c)
             assert types[cu[j]:cu[j + 1]].tolist() == want_t
+
+
+def _fuzz_ascii(rng, n):
+    """Random ASCII text: vocab words, case, digits, every punctuation byte, control bytes
+    (tab / newline / return / NUL / BEL / VT / FF / DEL), runs of spaces, long words."""
+    alpha = [chr(c) for c in range(128)]
+    out = []
+    for _ in range(n):
+        parts = []
+        for _ in range(int(rng.integers(0, 30))):
+            r = rng.random()
+            if r < 0.5:
+                w = WORDS[int(rng.integers(len(WORDS)))]
+                parts.append(w.upper() if rng.random() < 0.2 else w)
+            elif r < 0.8:
+                parts.append("".join(alpha[int(c)] for c in rng.integers(0, 128, int(rng.integers(1, 8)))))
+            elif r < 0.9:
+                parts.append("z" * int(rng.integers(95, 106)))     # around the 100-char limit
+            else:
+                parts.append(WORDS[int(rng.integers(len(WORDS)))] + "ing")
+        out.append((" " if rng.random() < 0.8 else "\t").join(parts))
+    return out
+
+
+def test_native_ascii_path_matches_rust_and_oracle(vocab_file):
+    """The host-native tokenizer (rag_wordpiece_encode, csrc/wordpiece_capi.cpp) against the
+    Rust tokenizer and the pure-Python oracle on 400 fuzzed ASCII texts and 200 pairs at
+    several max_length (truncation), id for id."""
+    from ragmi.encoders import WordPiece
+    vocab = R.load_vocab(vocab_file)
+    rng = np.random.default_rng(17)
+    texts = _fuzz_ascii(rng, 400)
+    wp = WordPiece(vocab_file)
+    assert wp._native is not None, "libragmi.so (rag_wordpiece_*) must be loadable on CPU"
+    ids, types, cu = wp.encode_packed(texts)
+    r_ids, r_types, r_cu = wp._encode_rust(texts)
+    np.testing.assert_array_equal(cu, r_cu)
+    np.testing.assert_array_equal(ids, r_ids)
+    np.testing.assert_array_equal(types, r_types)
+    for j in range(0, 400, 7):
+        assert ids[cu[j]:cu[j + 1]].tolist() == R.encode(texts[j], vocab)[0]
+    for ml in (9, 17, 40, 512):
+        wpm = WordPiece(vocab_file, ml)
+        qs, cs = texts[:200], texts[200:]
+        a = wpm.encode_packed(qs, cs)
+        b = wpm._encode_rust(qs, cs)
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y)
+        for j in range(0, 200, 11):
+            want, want_t = R.encode(qs[j], vocab, pair=cs[j], max_length=ml)
+            assert a[0][a[2][j]:a[2][j + 1]].tolist() == want
+            assert a[1][a[2][j]:a[2][j + 1]].tolist() == want_t
+
+
+def test_native_path_splices_non_ascii_in_order(vocab_file):
+    """Mixed batches: non-ASCII entries go through the Rust tokenizer and land in place."""
+    from ragmi.encoders import WordPiece
+    wp = WordPiece(vocab_file)
+    texts = [TEXTS[0], TEXTS[1], TEXTS[6], TEXTS[2], "", TEXTS[9], TEXTS[3]]
+    a = wp.encode_packed(texts)
+    b = wp._encode_rust(texts)
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x, y)
+    pairs = [TEXTS[5], TEXTS[0], TEXTS[1], "", TEXTS[2], TEXTS[6], TEXTS[8]]
+    a = wp.encode_packed(texts, pairs)
+    b = wp._encode_rust(texts, pairs)
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x, y)
+
+
+def test_native_vocab_rules(tmp_path):
+    """Vocab file rules of tokenizers' WordPiece::read_file: trailing whitespace trimmed,
+    later duplicates win; missing specials are refused."""
+    import ctypes
+
+    from ragmi import _lib
+    L = _lib.load()
+    h = ctypes.c_void_p()
+    v = b"[PAD]\n[UNK]\n[CLS]\n[SEP]\nab \ncd\r\nab\n"
+    _lib.check(L.rag_wordpiece_create(v, len(v), 512, 1, ctypes.byref(h)))
+    t = b"ab cd"
+    off = np.array([0, len(t)], np.int64)
+    ids = np.zeros(16, np.int32)
+    ty = np.zeros(16, np.int32)
+    cu = np.zeros(2, np.int32)
+    fb = np.zeros(1, np.uint8)
+    _lib.check(L.rag_wordpiece_encode(h, t, off.ctypes.data_as(_lib.c_i64p), None, None, 1,
+                                      ids.ctypes.data_as(_lib.c_i32p), ty.ctypes.data_as(_lib.c_i32p),
+                                      cu.ctypes.data_as(_lib.c_i32p), 16,
+                                      fb.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))))
+    assert ids[:cu[1]].tolist() == [2, 6, 5, 3]       # "ab" -> line 6 (last wins), "cd" -> 5
+    L.rag_wordpiece_destroy(h)
+    bad = b"[PAD]\n[CLS]\n[SEP]\n"
+    with pytest.raises(_lib.RagmiError):
+        _lib.check(L.rag_wordpiece_create(bad, len(bad), 512, 1, ctypes.byref(h)))
