@@ -81,12 +81,34 @@ struct EncWorkspace {
            *ffcl = nullptr;
   // deferred LayerNorm: row statistics of z after the attention block (sa) / the FFN (sb)
   float *sa = nullptr, *sb = nullptr;
+  // hipGraph replay of small-batch forwards (forward_graph): executable graphs keyed by the
+  // padded shape (B, T, max_len), the padded inputs they read ([ids T | types T | cu B+1])
+  // and the rows they write. A graph holds this workspace's buffer addresses: any regrowth
+  // drops them (drop_graphs).
+  struct Graph {
+    int B = 0, T = 0, L = 0;
+    hipGraphExec_t exec = nullptr;
+    uint64_t last = 0;
+  };
+  std::vector<Graph> graphs;
+  int32_t* g_in = nullptr;
+  int64_t g_in_cap = 0;     // int32 elements
+  float* g_out = nullptr;
+  int64_t g_out_cap = 0;    // floats
+
+  void drop_graphs() {   // (a replay may still run on the workspace's stream: wait for it)
+    if (!graphs.empty() && stream) (void)hipStreamSynchronize(stream);
+    for (auto& g : graphs)
+      if (g.exec) (void)hipGraphExecDestroy(g.exec);
+    graphs.clear();
+  }
 
   void release() {
+    drop_graphs();
     for (void* p : {(void*)x, (void*)y, (void*)xh, (void*)qkv, (void*)ctx, (void*)ff, (void*)xl,
                     (void*)qkv_l, (void*)ctx_l, (void*)ff_l, (void*)xc, (void*)yc, (void*)xch,
                     (void*)xcl, (void*)cc, (void*)ccl, (void*)ffc, (void*)ffcl, (void*)sa,
-                    (void*)sb})
+                    (void*)sb, (void*)g_in, (void*)g_out})
       if (p) (void)hipFree(p);
     *this = EncWorkspace{};
   }
@@ -107,6 +129,11 @@ struct rag_encoder {
   int fuse_ln = -1;
   // deferred LayerNorm on the token rows (fp16x3, hidden 384): -1 auto, 0 off, 1 on
   int defer_ln = -1;
+  // hipGraph replay of small-batch forwards: -1 auto, 0 off, 1 on. A call on the null stream
+  // replays on the encoder's own stream, ordered by two events (gstream, gev_*)
+  int graphs = -1;
+  hipStream_t gstream = nullptr;
+  hipEvent_t gev_in = nullptr, gev_out = nullptr;
   // static fp16 range analysis of the weights (range_bounds): the largest |value| any fp16
   // (hi) plane of the forward can hold, for any input — without / with the deferred LayerNorm
   // (whose z planes hold the un-normalised residual sums)
@@ -190,6 +217,7 @@ int fold_ln(rag_encoder* e, std::initializer_list<std::pair<const float*, const 
 
 int ensure_ws(const rag_bert_config& cfg, EncWorkspace* w, int64_t T) {
   if (T <= w->cap_t) return RAG_OK;
+  w->drop_graphs();
   const int64_t cap = std::max<int64_t>(T, std::max<int64_t>(2 * w->cap_t, 1024));
   for (void* p : {(void*)w->x, (void*)w->y, (void*)w->xh, (void*)w->qkv, (void*)w->ctx,
                   (void*)w->ff, (void*)w->xl, (void*)w->qkv_l, (void*)w->ctx_l, (void*)w->ff_l,
@@ -369,6 +397,7 @@ int fuse_ln_default() {
 
 int ensure_cls(const rag_bert_config& cfg, EncWorkspace* w, int64_t B) {
   if (B <= w->cap_b) return RAG_OK;
+  w->drop_graphs();
   for (void* p : {(void*)w->xc, (void*)w->yc, (void*)w->xch, (void*)w->xcl, (void*)w->cc,
                   (void*)w->ccl, (void*)w->ffc, (void*)w->ffcl})
     if (p) (void)hipFree(p);
@@ -578,12 +607,33 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
 }
 
 template <int H, int HD>
+int forward_graph(rag_encoder* e, EncWorkspace* w, const int32_t* ids, const int32_t* types,
+                  const int32_t* cu, int B, int T, int max_len, float* out, hipStream_t st);
+
+// graph replay for this call? (small token batches on a non-null stream: the ~90 launches
+// of a forward cost ~260 us of host time against ~620 us of device time at 32 queries,
+// profiles/r03f_host_launch.jsonl; a replay is three host calls)
+constexpr int kGraphMaxT = 8192;
+constexpr int kGraphCache = 16;    // graphs per workspace (LRU)
+bool use_graphs(const rag_encoder* e, hipStream_t st, int T, bool null_ok = false) {
+  static const int env = [] {
+    const char* v = std::getenv("RAGMI_ENC_GRAPH");
+    return v ? std::atoi(v) : -1;
+  }();
+  const int mode = e->graphs >= 0 ? e->graphs : env;
+  if (mode == 0 || (st == nullptr && !null_ok)) return false;
+  return mode > 0 || T <= kGraphMaxT;
+}
+
+template <int H, int HD>
 int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const int32_t* cu,
-              int B, int T, int max_len, float* out, hipStream_t st) {
+              int B, int T, int max_len, float* out, hipStream_t st, bool capturing = false) {
   const rag_bert_config& c = e->cfg;
   const int NH = H / HD, FF = c.intermediate;
   EncWorkspace* w = workspace_for(e, st);
   if (!w) return ragmi::fail(RAG_EHIP, "device synchronize failed");
+  if (!capturing && use_graphs(e, st, T))
+    return forward_graph<H, HD>(e, w, ids, types, cu, B, T, max_len, out, st);
   int rc = ensure_ws(c, w, T);
   if (rc) return rc;
   rc = ensure_cls(c, w, B);
@@ -744,6 +794,90 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
     ce_head_kernel<H><<<dim3(B), dim3(256), 0, st>>>(w->xc, nullptr, e->wp, e->bp, e->wc, e->bc,
                                                      out);
   RAG_HIP(hipGetLastError());
+  return RAG_OK;
+}
+
+// padded copy of a call's inputs into the graph's staging: ids / types past T are token 0 /
+// type 0 (the pad rows [T, Tp) belong to no sequence: cu ends at T, so attention, the CLS
+// gather and every row-wise kernel leave the real rows' values as without them)
+__global__ void graph_stage_kernel(const int32_t* __restrict__ ids,
+                                   const int32_t* __restrict__ types,
+                                   const int32_t* __restrict__ cu, int B, int T, int Tp,
+                                   int32_t* __restrict__ g) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < Tp) {
+    g[i] = i < T ? ids[i] : 0;
+    g[Tp + i] = i < T ? types[i] : 0;
+  }
+  if (i <= B) g[2 * Tp + i] = cu[i];
+}
+
+// Small-batch forward by graph replay: stage the inputs (one kernel), replay the graph captured
+// for the padded shape (T up to a multiple of 64, max_len up to a multiple of 32 — the
+// attention's key chunking depends on max_len only through that rounding, attn_chunk_keys),
+// copy the B output rows out. The graph is captured on first use of its shape from the same
+// eager code path (forward_t), so it launches the same kernels with the same arguments.
+template <int H, int HD>
+int forward_graph(rag_encoder* e, EncWorkspace* w, const int32_t* ids, const int32_t* types,
+                  const int32_t* cu, int B, int T, int max_len, float* out, hipStream_t st) {
+  const rag_bert_config& c = e->cfg;
+  const int Tp = (T + 63) / 64 * 64;
+  const int Lp = std::min((max_len + 31) / 32 * 32, c.max_position);
+  const int od = c.head == RAG_HEAD_CLS_L2 ? H : 1;
+  int rc = ensure_ws(c, w, Tp);
+  if (rc) return rc;
+  rc = ensure_cls(c, w, B);
+  if (rc) return rc;
+  if (w->g_in_cap < 2 * (int64_t)Tp + B + 1 || w->g_out_cap < (int64_t)B * od) {
+    w->drop_graphs();
+    if (w->g_in) (void)hipFree(w->g_in);
+    if (w->g_out) (void)hipFree(w->g_out);
+    w->g_in = nullptr;
+    w->g_out = nullptr;
+    w->g_in_cap = w->g_out_cap = 0;
+    const int64_t ni = std::max<int64_t>(2 * (int64_t)Tp + B + 1, 2 * 4096 + 257);
+    const int64_t no = std::max<int64_t>((int64_t)B * od, 256 * (int64_t)od);
+    RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->g_in), ni * 4));
+    RAG_HIP(hipMalloc(reinterpret_cast<void**>(&w->g_out), no * 4));
+    w->g_in_cap = ni;
+    w->g_out_cap = no;
+  }
+  int32_t* g = w->g_in;
+  graph_stage_kernel<<<dim3((unsigned)((std::max(Tp, B + 1) + 255) / 256)), dim3(256), 0, st>>>(
+      ids, types, cu, B, T, Tp, g);
+  RAG_HIP(hipGetLastError());
+  EncWorkspace::Graph* hit = nullptr;
+  for (auto& gr : w->graphs)
+    if (gr.B == B && gr.T == Tp && gr.L == Lp) hit = &gr;
+  if (!hit) {
+    if ((int)w->graphs.size() >= kGraphCache) {
+      auto lru = std::min_element(w->graphs.begin(), w->graphs.end(),
+                                  [](const EncWorkspace::Graph& a, const EncWorkspace::Graph& b) {
+                                    return a.last < b.last;
+                                  });
+      RAG_HIP(hipStreamSynchronize(st));      // its last replay was on this stream
+      (void)hipGraphExecDestroy(lru->exec);
+      w->graphs.erase(lru);
+    }
+    hipGraph_t graph = nullptr;
+    RAG_HIP(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
+    rc = forward_t<H, HD>(e, g, g + Tp, g + 2 * Tp, B, Tp, Lp, w->g_out, st, true);
+    const hipError_t ec = hipStreamEndCapture(st, &graph);
+    if (rc) {
+      if (graph) (void)hipGraphDestroy(graph);
+      return rc;
+    }
+    if (ec != hipSuccess) return ragmi::fail(RAG_EHIP, "graph capture failed");
+    hipGraphExec_t exec = nullptr;
+    const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    if (ei != hipSuccess) return ragmi::fail(RAG_EHIP, "graph instantiate failed");
+    w->graphs.push_back(EncWorkspace::Graph{B, Tp, Lp, exec, 0});
+    hit = &w->graphs.back();
+  }
+  hit->last = e->uses;
+  RAG_HIP(hipGraphLaunch(hit->exec, st));
+  RAG_HIP(hipMemcpyAsync(out, w->g_out, (size_t)B * od * 4, hipMemcpyDeviceToDevice, st));
   return RAG_OK;
 }
 
@@ -954,6 +1088,9 @@ int rag_encoder_destroy(rag_encoder_t* e) {
   for (void* p : e->allocs) (void)hipFree(p);
   for (auto& w : e->ws) w.release();
   if (e->stage) (void)hipFree(e->stage);
+  if (e->gev_in) (void)hipEventDestroy(e->gev_in);
+  if (e->gev_out) (void)hipEventDestroy(e->gev_out);
+  if (e->gstream) (void)hipStreamDestroy(e->gstream);
   delete e;
   return RAG_OK;
 }
@@ -966,7 +1103,23 @@ int rag_encoder_forward(rag_encoder_t* e, const int32_t* ids, const int32_t* typ
     return ragmi::fail(RAG_EINVAL, "bad batch shape (max_len must be <= max_position)");
   std::lock_guard<std::mutex> lk(e->mu);
   RAG_HIP(hipSetDevice(e->device));
-  return forward_locked(e, ids, types, cu, B, T, max_len, out, static_cast<hipStream_t>(stream));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (st == nullptr && use_graphs(e, st, T, true)) {
+    // null stream (graphs cannot be captured on it): replay on the encoder's own stream,
+    // after everything queued on the null stream so far and before anything queued after
+    if (!e->gstream) {
+      RAG_HIP(hipStreamCreateWithFlags(&e->gstream, hipStreamNonBlocking));
+      RAG_HIP(hipEventCreateWithFlags(&e->gev_in, hipEventDisableTiming));
+      RAG_HIP(hipEventCreateWithFlags(&e->gev_out, hipEventDisableTiming));
+    }
+    RAG_HIP(hipEventRecord(e->gev_in, nullptr));
+    RAG_HIP(hipStreamWaitEvent(e->gstream, e->gev_in, 0));
+    const int rc = forward_locked(e, ids, types, cu, B, T, max_len, out, e->gstream);
+    RAG_HIP(hipEventRecord(e->gev_out, e->gstream));
+    RAG_HIP(hipStreamWaitEvent(nullptr, e->gev_out, 0));
+    return rc;
+  }
+  return forward_locked(e, ids, types, cu, B, T, max_len, out, st);
 }
 
 int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, const void* W,
@@ -1160,6 +1313,15 @@ int rag_encoder_set_fusion(rag_encoder_t* e, int mode) {
   if (!e || mode < -1 || mode > 1) return ragmi::fail(RAG_EINVAL, "mode: -1 auto, 0 off, 1 on");
   std::lock_guard<std::mutex> lk(e->mu);
   e->fuse_ln = mode;
+  for (auto& w : e->ws) w.drop_graphs();   // captured with the old mode's kernels
+  return RAG_OK;
+}
+
+int rag_encoder_set_graphs(rag_encoder_t* e, int mode) {
+  ragmi::clear_error();
+  if (!e || mode < -1 || mode > 1) return ragmi::fail(RAG_EINVAL, "mode: -1 auto, 0 off, 1 on");
+  std::lock_guard<std::mutex> lk(e->mu);
+  e->graphs = mode;
   return RAG_OK;
 }
 
@@ -1172,6 +1334,7 @@ int rag_encoder_set_defer_ln(rag_encoder_t* e, int mode) {
                                    "bound " + std::to_string(e->bound_defer) + ")");
   std::lock_guard<std::mutex> lk(e->mu);
   e->defer_ln = mode;
+  for (auto& w : e->ws) w.drop_graphs();
   return RAG_OK;
 }
 

@@ -126,6 +126,7 @@ BERT_API = {
                                             ctypes.c_float, ctypes.c_int, ctypes.c_int,
                                             ctypes.c_int, c_vp, c_vp, c_vp, c_vp]),
     "rag_encoder_set_fusion": (ctypes.c_int, [c_vp, ctypes.c_int]),
+    "rag_encoder_set_graphs": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "rag_encoder_set_defer_ln": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "rag_encoder_range_bounds": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_double),
                                                 ctypes.POINTER(ctypes.c_double)]),

@@ -320,6 +320,11 @@ class BertEncoder:
         """Residual + LayerNorm fused into the output projections: -1 auto, 0 off, 1 on."""
         check(self._L.rag_encoder_set_fusion(self._h, int(mode)))
 
+    def set_graphs(self, mode: int) -> None:
+        """hipGraph replay of small-batch forwards (rag_encoder_set_graphs): -1 auto (T <= 8192
+        tokens), 0 off, 1 on."""
+        check(self._L.rag_encoder_set_graphs(self._h, int(mode)))
+
     def set_defer_ln(self, mode: int) -> None:
         """Deferred LayerNorm on the token rows (fp16x3, hidden 384; ragmi_bert.h
         rag_encoder_set_defer_ln): -1 auto, 0 off, 1 on where the model allows."""

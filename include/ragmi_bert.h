@@ -175,6 +175,16 @@ int rag_bert_gemm_add_ln_probe(int probe, const void* A, const void* A_lo, const
  * create), 0 never (separate GEMM + add-LayerNorm kernels), 1 always where the shape allows */
 int rag_encoder_set_fusion(rag_encoder_t* e, int mode);
 
+/* hipGraph replay of small-batch forwards: -1 auto (default; env RAGMI_ENC_GRAPH=0/1
+ * overrides auto): calls with T <= 8192 tokens stage their inputs into
+ * the stream's workspace (one kernel), replay the graph captured for the padded shape (T to a
+ * multiple of 64, max_len to a multiple of 32; captured on first use from the eager path) and
+ * copy the output rows out — three host calls instead of ~90 kernel launches; 0 never; 1 for
+ * every call. A call on the null stream replays on the encoder's own stream, ordered after the
+ * null stream's earlier work and before its later work by two events. Results are those of the
+ * eager forward at the padded T. */
+int rag_encoder_set_graphs(rag_encoder_t* e, int mode);
+
 /* Deferred LayerNorm (fp16x3, hidden 384): the token rows' residual stream is kept
  * un-normalised between sublayers — z = x + sublayer output as fp16 hi + lo planes, plus per row
  * six {mean, centred sum of squares} statistics of its 64-column blocks — and LN(z) is applied
