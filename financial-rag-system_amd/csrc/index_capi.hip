@@ -203,7 +203,12 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
   using namespace ragmi;
   // Bq <= 32 * h->groups queries: `groups` query groups of 32 (one for D <= 384)
   const int groups = (Bq + kQ - 1) / kQ;
-  if (D <= 384 && groups == 1 && fused_prep()) {
+  // fused qprep + sample only in free scan order (small shards, several scans overlapping):
+  // there it is +1.1% (1.25M rows, 4 in flight, profiles/r03d_fused_prep_ab.jsonl); with the
+  // scans chained (>= 4M rows) its 256-thread workgroups of ~180 registers, which cannot share a
+  // CU with scan workgroups, landed between a scan's workgroups and stretched the scan launch
+  // (10M rows: scan 0.76 vs 0.83 of the roofline, same qps, profiles/r03i_headline_prep_ab.jsonl)
+  if (D <= 384 && groups == 1 && fused_prep() && h->serial_scans == 0) {
     if (filt)
       launch_seed<D, true>(h, w, groups, st, q, Bq, filt);
     else

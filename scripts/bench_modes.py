@@ -261,12 +261,19 @@ def run_pipeline(args, cfg_id):
     ev_every = 4                        # CE forward events on every 4th batch (sampled)
     evs, flops = [], []
 
+    # timed batches whose outputs the parity legs check after the timed region (4 spread
+    # over the run: their query embeddings, top-15 scores / rows and, config 3, CE logits)
+    check_ks = sorted({int(x) for x in np.linspace(0, args.steps - 1, min(4, args.steps))})
+    kept = {}
+
     def step(i, timed, toks=None):
         ids, tt, cu = toks if toks is not None else batches[i]
         st = streams[i % S]
         with torch.cuda.stream(st):
             q = bge.forward_packed(ids, tt, cu)
-            _, rows = idx.search(q, K_TOP)
+            sc, rows = idx.search(q, K_TOP)
+            if timed and i - args.warmup in check_ks:
+                kept[i - args.warmup] = (q, sc, rows)
             if cfg_id == 2:
                 return rows, None
             q_ids = torch.from_numpy(ids).to(dev, non_blocking=True)
@@ -359,42 +366,63 @@ def run_pipeline(args, cfg_id):
         ce_alone = a.elapsed_time(b) / 5
     elapsed, elapsed_ids = _max_over_ranks([elapsed, elapsed_ids], dev)
 
-    # parity legs (after the timed region): search top-15 of the first timed batch certified
-    # against the oracle; CE logits of its first query's 15 pairs vs bert_ref
+    # parity legs (after the timed region), on the outputs of 4 timed batches spread over the
+    # run: the top-15 of every query certified against the oracle (ids and scores bit-exact),
+    # the query embeddings vs bert_ref (the encoder bar, 5e-5), and for config 3 the CE logits
+    # of the first and last query's 15 pairs vs bert_ref (1e-3) with the top-5 they select
     import oracle_scan as O
     extra = {}
     if not args.no_recall and rank == 0:
-        ids, tt, cu = batches[args.warmup]
-        q = bge.forward_packed(ids, tt, cu)
-        s, rows = idx.search(q, K_TOP)
+        import bert_ref                        # the checker (oracle) leg only
         enc = idx.export_rows()
-        qh = q.cpu().numpy()
-        qn = O.normalize(qh)
-        g_i = rows.cpu().numpy()
-        floor = O.rescore(enc, qn, g_i).min(axis=1)
-        cand = O.candidates_above(enc, qn, floor)
-        ok = 0
-        for j, (ci, cs) in enumerate(cand):
-            o = np.lexsort((ci, -cs.astype(np.float64)))[:K_TOP]
-            ok += int(np.array_equal(ci[o], g_i[j]) and np.array_equal(cs[o], s[j].cpu().numpy()))
-        extra["search_top15_exact_queries"] = f"{ok}/{B}"
-        if cfg_id == 3:
-            pid, pty, pcu, logits = outs[0][1]
-            pcu_h = pcu.cpu().numpy()
-            hi = int(pcu_h[K_TOP])
-            sub_cu = pcu_h[:K_TOP + 1]
-            ids_h, ty_h = pid.cpu().numpy()[:hi], pty.cpu().numpy()[:hi]
-            lens = np.diff(sub_cu)
-            Smax = int(lens.max())
-            pi = np.zeros((K_TOP, Smax), np.int64)
+        ok = n_q = 0
+        emb_d = ce_d = 0.0
+        top5_ok = top5_n = 0
+        for k in check_ks:
+            q, s_k, r_k = kept[k]
+            ids, tt, cu = batches[args.warmup + k]
+            qh = q.cpu().numpy()
+            qn = O.normalize(qh)
+            g_i, g_s = r_k.cpu().numpy(), s_k.cpu().numpy()
+            floor = O.rescore(enc, qn, g_i).min(axis=1)
+            for j, (ci, cs) in enumerate(O.candidates_above(enc, qn, floor)):
+                o = np.lexsort((ci, -cs.astype(np.float64)))[:K_TOP]
+                ok += int(np.array_equal(ci[o], g_i[j]) and np.array_equal(cs[o], g_s[j]))
+                n_q += 1
+            lens = np.diff(cu)
+            pi = np.zeros((len(lens), int(lens.max())), np.int64)
             pt, pm = np.zeros_like(pi), np.zeros_like(pi)
-            for j in range(K_TOP):
-                a, b = sub_cu[j], sub_cu[j + 1]
-                pi[j, :b - a], pt[j, :b - a], pm[j, :b - a] = ids_h[a:b], ty_h[a:b], 1
-            import bert_ref                    # the checker (oracle) leg only
-            ref = bert_ref.ce_logits(ce_w, R.MINILM_CE, pi, pt, pm)
-            extra["rerank_max_abs_diff_vs_oracle"] = float(
-                np.abs(logits[0].cpu().numpy() - ref).max())
+            for j, L in enumerate(lens):
+                pi[j, :L], pt[j, :L], pm[j, :L] = ids[cu[j]:cu[j + 1]], tt[cu[j]:cu[j + 1]], 1
+            emb_d = max(emb_d, float(np.abs(qh - bert_ref.bge_embed(bge_w, R.BGE_SMALL, pi, pt,
+                                                                     pm)).max()))
+            if cfg_id == 3:
+                top, (pid, pty, pcu, logits) = outs[k]
+                pcu_h = pcu.cpu().numpy()
+                ids_h, ty_h = pid.cpu().numpy(), pty.cpu().numpy()
+                lg, tp = logits.cpu().numpy(), top.cpu().numpy()
+                for qj in (0, B - 1):
+                    sub = pcu_h[qj * K_TOP:(qj + 1) * K_TOP + 1]
+                    ln = np.diff(sub)
+                    xi = np.zeros((K_TOP, int(ln.max())), np.int64)
+                    xt, xm = np.zeros_like(xi), np.zeros_like(xi)
+                    for j in range(K_TOP):
+                        a, b = sub[j], sub[j + 1]
+                        xi[j, :b - a], xt[j, :b - a], xm[j, :b - a] = ids_h[a:b], ty_h[a:b], 1
+                    ref = bert_ref.ce_logits(ce_w, R.MINILM_CE, xi, xt, xm)
+                    ce_d = max(ce_d, float(np.abs(lg[qj] - ref).max()))
+                    srt = np.sort(ref)[::-1]
+                    if np.min(np.abs(np.diff(srt[:TOPK + 1]))) > 2e-3:   # separated scores
+                        top5_n += 1
+                        want = g_i[qj][bert_ref.rerank_order(ref, TOPK)]
+                        top5_ok += int(np.array_equal(tp[qj], want))
+        extra["checked_timed_batches"] = [int(k) for k in check_ks]
+        extra["search_top15_exact_queries"] = f"{ok}/{n_q}"
+        extra["encode_max_abs_diff_vs_oracle"] = emb_d
+        if cfg_id == 3:
+            extra["rerank_max_abs_diff_vs_oracle"] = ce_d
+            extra["rerank_checked_queries"] = 2 * len(check_ks)
+            extra["rerank_top5_order_matches"] = f"{top5_ok}/{top5_n}"
     cpu = None
     if rank == 0 and not args.no_cpu:
         ids, tt, cu = batches[args.warmup]

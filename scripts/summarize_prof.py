@@ -36,13 +36,14 @@ def main():
     scan_durs = []
     if trace:
         for r in csv.DictReader(open(trace)):
-            if "scan_kernel" in r["Kernel_Name"]:
+            if "scan_kernel" in r["Kernel_Name"] and "rescan" not in r["Kernel_Name"]:
                 scan_durs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     pmc = find(pmc_dir, "*counter_collection.csv")
     fetch = []
     if pmc:
         for r in csv.DictReader(open(pmc)):
-            if "scan_kernel" in r.get("Kernel_Name", "") and r.get("Counter_Name") == "FETCH_SIZE":
+            if ("scan_kernel" in r.get("Kernel_Name", "") and "rescan" not in r.get("Kernel_Name", "")
+                    and r.get("Counter_Name") == "FETCH_SIZE"):
                 fetch.append(float(r["Counter_Value"]))
         with open(os.path.join(out, f"{tag}_pmc_fetch_size.csv"), "w") as f:
             f.write(open(pmc).read())
