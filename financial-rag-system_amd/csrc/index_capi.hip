@@ -78,6 +78,7 @@ struct rag_index {
   int storage = RAG_STORE_FP16;
   float* rows32 = nullptr;
   int max_wgs = 0;        // scan workgroups at full occupancy
+  int scan_wgs = 0;       // D <= 384 scan grid cap: 3/4 of the CUs (launch_search_pass)
   int groups = 1;         // query groups of 32 per search pass
   std::mutex mu;
   Workspace ws[kRing];
@@ -232,7 +233,23 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
         per_group, ((n_tiles + kLdsWaves - 1) / kLdsWaves + 7) & ~int64_t(7));
     grid = std::max(8, std::min(need, kMaxLists / kLdsWaves));
   } else {
-    grid = (int)std::min<int64_t>(h->max_wgs, std::max<int64_t>(1, (n_tiles + 3) / 4));
+    // One scan workgroup on 3/4 of the CUs (h->scan_wgs), not two on every CU: measured on
+    // one MI355X (profiles/r03j_scan_wgs_*.jsonl, interleaved processes, 2 reps each) 10M rows
+    // 27.19K qps / 83.0% of the HBM roofline at 512 workgroups -> 28.67-28.82K / 86.2-86.7% at
+    // 192 (224: 86.0-86.6%, 256: 85.6-86.1%, 288: 66.2% — one CU in eight with a second
+    // workgroup makes the launch wait on them —, 160: 82.9%, 128: 72.5%); 2.5M rows 99.3K ->
+    // 103.1K; 1.25M rows with 4 in flight 189K -> 199K (union 0.71 -> 0.76). Fewer, longer
+    // wave streams keep HBM as busy as twice as many, each wave's fixed start / end-of-scan
+    // list work is paid by 768 waves instead of 2048 (select merges that many fewer lists), and
+    // the free CUs take the other streams' query prep, sampling and select beside the scan
+    // instead of behind it. RAGMI_SCAN_WGS overrides the cap (A/B).
+    static const int wg_env = [] {
+      const char* v = std::getenv("RAGMI_SCAN_WGS");
+      return v ? std::max(8, std::atoi(v)) : 0;
+    }();
+    const int wg_cap = wg_env ? wg_env : h->scan_wgs;
+    grid = (int)std::min<int64_t>(std::min(h->max_wgs, wg_cap),
+                                  std::max<int64_t>(1, (n_tiles + 3) / 4));
     grid = std::min(grid, kMaxLists / kWavesPerWG);
   }
   const hipStream_t caller = st;
@@ -464,7 +481,10 @@ int bench_scan(rag_index* h, const float* q, int B, int variant, int reps, doubl
   if (variant == 7)
     RAG_HIP(hipMemsetD32(reinterpret_cast<hipDeviceptr_t>(w.seed), 0x7f800000, kQ));
   const int64_t n_tiles = (h->count + 15) / 16;
-  int grid = (int)std::min<int64_t>(h->max_wgs, std::max<int64_t>(1, (n_tiles + 3) / 4));
+  // the production grid (launch_search_pass: 3/4 of the CUs); RAGMI_SCAN_WGS overrides
+  const char* wv = std::getenv("RAGMI_SCAN_WGS");
+  const int cap = wv ? std::max(8, std::atoi(wv)) : h->scan_wgs;
+  int grid = (int)std::min<int64_t>(std::min(h->max_wgs, cap), std::max<int64_t>(1, (n_tiles + 3) / 4));
   grid = std::min(grid, kMaxLists / kWavesPerWG);
   // variant 8: the v_dot2 VALU ablation over a row-group-major copy of the corpus
   half8* rows64 = nullptr;
@@ -631,6 +651,7 @@ int rag_index_create_ex(int dim, int64_t capacity_rows, int device, int storage,
       n_cu <= 0)
     n_cu = 256;
   h->max_wgs = n_cu * 2;  // 2 x 256-thread workgroups per CU (__launch_bounds__(256, 2))
+  h->scan_wgs = std::max(8, (n_cu * 3 / 4) & ~7);
   // wide rows (LDS-query scan) take up to 4 query groups (128 queries) per pass
   h->groups = dim > 384 ? kMaxGroups : 1;
   const size_t G = (size_t)h->groups, Q = ragmi::kQ;
