@@ -275,7 +275,15 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
   h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, (int)n_tiles, w.seed, w.part_s, w.part_i, \
       w.heads_s, w.heads_i, w.heads_n
   const bool wide = kLdsQ && groups > 1 && !filt;
-  if (wide) grid = (int)std::min<int64_t>(h->max_wgs / 2, std::max<int64_t>(1, n_tiles));
+  if (wide) {
+    // RAGMI_WIDE_WGS (A/B): workgroup cap of the wide scan (default one per CU)
+    static const int wide_env = [] {
+      const char* v = std::getenv("RAGMI_WIDE_WGS");
+      return v ? std::max(8, std::atoi(v)) : 0;
+    }();
+    const int cap = wide_env ? std::min(wide_env, h->max_wgs / 2) : h->max_wgs / 2;
+    grid = (int)std::min<int64_t>(cap, std::max<int64_t>(1, n_tiles));
+  }
   if constexpr (kLdsQ) {
     const dim3 g3(grid * groups), b3(64 * kLdsWaves);
     if (wide) {
