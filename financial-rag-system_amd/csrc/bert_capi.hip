@@ -1223,8 +1223,9 @@ int rag_bert_attention(int variant, const void* qkv, const void* qkv_lo, const i
   if ((qkv_lo == nullptr) != (ctx_lo == nullptr))
     return ragmi::fail(RAG_EINVAL, "qkv_lo and ctx_lo: both (fp16x3) or neither (fp16)");
   if (variant == -1) variant = kAttnVar;
-  if ((variant < 0 || variant > 15) && variant != 18 && variant != 26)
-    return ragmi::fail(RAG_EINVAL, "variant: -1, 0..15, 18 or 26");
+  if ((variant < 0 || variant > 15) && variant != 18 && variant != 26 && variant != 40 &&
+      variant != 42)
+    return ragmi::fail(RAG_EINVAL, "variant: -1, 0..15, 18, 26, 40 or 42");
   constexpr int H = 384, HD = 32, NH = H / HD;
   const int planes = qkv_lo ? 2 : 1;
   const int kc = attn_chunk_keys<HD>(max_len, planes);
@@ -1270,6 +1271,8 @@ int rag_bert_attention(int variant, const void* qkv, const void* qkv_lo, const i
     case 14: return go(std::integral_constant<int, 14>{});
     case 18: return go(std::integral_constant<int, 18>{});   // 16 = paired query blocks
     case 26: return go(std::integral_constant<int, 26>{});
+    case 40: return go(std::integral_constant<int, 40>{});   // 32 = peeled, prefetched blocks
+    case 42: return go(std::integral_constant<int, 42>{});
     default: return go(std::integral_constant<int, 15>{});
   }
 }

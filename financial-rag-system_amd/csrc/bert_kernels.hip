@@ -1625,7 +1625,7 @@ struct AttnState {
 // Bit 16 (two query blocks per wave side by side, bitwise the same; 114 VGPRs, no spill,
 // same 4 waves per SIMD) measured slower at the rerank shape (profiles/r02q_attn_pairs.jsonl,
 // same process, 7 rounds): 10 -> 26 0.254 -> 0.282 ms, 2 -> 18 0.268 -> 0.303: a diagnostic.
-constexpr int kAttnVar = 10;
+constexpr int kAttnVar = 42;
 template <int H, int HD, bool SPLIT, int VAR = kAttnVar>
 __global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) void attn_kernel(
     const _Float16* __restrict__ qkv, const _Float16* __restrict__ qkv_lo,
@@ -1727,12 +1727,32 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) 
         }
       }
   };
-  // softmax update and P.V for the block at LDS position kb (keys k0 + kb ..)
-  auto softmax_pv = [&](St& st, int k0, int kb, floatx4 (&sc)[2]) {
+  // softmax update and P.V for the block at LDS position kb (keys k0 + kb ..). mode (VAR bit
+  // 32's peeled loop): 0 = is the block full? checked here; 1 = known full; 2 = known partial.
+  // Bit 32 also issues the block's V^T fragment reads first, so their LDS latency runs under
+  // the max / exp / split work instead of between the P.V MFMAs.
+  auto softmax_pv_m = [&](St& st, int k0, int kb, floatx4 (&sc)[2], auto mode) {
+      constexpr int MODE = decltype(mode)::value;
+      constexpr bool VPRE = (VAR & 40) == 40;
+      half8 vh[DT], vlo[DT];
+      if constexpr (VPRE) {
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          const int vr = kb * HD + voff(dt);
+          vh[dt] = __builtin_shufflevector(lds_read_tr16(vls[0] + vr),
+                                           lds_read_tr16(vls[0] + vr + 16 * HD),
+                                           0, 1, 2, 3, 4, 5, 6, 7);
+          if constexpr (SPLIT)
+            vlo[dt] = __builtin_shufflevector(lds_read_tr16(vls[1] + vr),
+                                              lds_read_tr16(vls[1] + vr + 16 * HD),
+                                              0, 1, 2, 3, 4, 5, 6, 7);
+        }
+        __builtin_amdgcn_sched_barrier(0);   // keep the reads ahead of the softmax
+      }
       // lane: S^T[key k0 + kb + 16j + 4g + r][q]. Softmax in base 2 with the 1/sqrt(d) scale
       // folded into one FMA: p = 2^(s*c - m*c), c = scale*log2(e) > 0 (max commutes).
       float mx;
-      if (k0 + kb + 32 <= len) {
+      if (MODE == 1 || (MODE == 0 && k0 + kb + 32 <= len)) {
         if constexpr ((VAR & 8) != 0)   // IEEE maximum: no per-input canonicalisation
           mx = fmax_nc(fmax_nc(fmax_nc(sc[0][0], sc[0][1]), fmax_nc(sc[0][2], sc[0][3])),
                        fmax_nc(fmax_nc(sc[1][0], sc[1][1]), fmax_nc(sc[1][2], sc[1][3])));
@@ -1787,8 +1807,17 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) 
         for (int j = 0; j < 2; ++j)
 #pragma unroll
           for (int r = 0; r < 4; r += 2) {
-            const float e0 = __builtin_amdgcn_exp2f(fmaf(sc[j][r], c2, nm));
-            const float e1 = __builtin_amdgcn_exp2f(fmaf(sc[j][r + 1], c2, nm));
+            float e0, e1;
+            if constexpr (VPRE) {   // the two scalings as one packed fp32 FMA (v_pk_fma_f32)
+              typedef float f2 __attribute__((ext_vector_type(2)));
+              const f2 t = __builtin_elementwise_fma(f2{sc[j][r], sc[j][r + 1]}, f2{c2, c2},
+                                                     f2{nm, nm});
+              e0 = __builtin_amdgcn_exp2f(t[0]);
+              e1 = __builtin_amdgcn_exp2f(t[1]);
+            } else {
+              e0 = __builtin_amdgcn_exp2f(fmaf(sc[j][r], c2, nm));
+              e1 = __builtin_amdgcn_exp2f(fmaf(sc[j][r + 1], c2, nm));
+            }
             half2 h2, l2;
             split16x2(e0, e1, h2, l2);
             ph[4 * j + r] = h2[0]; ph[4 * j + r + 1] = h2[1];
@@ -1821,17 +1850,18 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) 
         }
       }
       if constexpr ((VAR & 8) != 0) {
-        half8 vh[DT], vlo[DT];
+        if constexpr (!VPRE) {
 #pragma unroll
-        for (int dt = 0; dt < DT; ++dt) {
-          const int vr = kb * HD + voff(dt);
-          vh[dt] = __builtin_shufflevector(lds_read_tr16(vls[0] + vr),
-                                           lds_read_tr16(vls[0] + vr + 16 * HD),
-                                           0, 1, 2, 3, 4, 5, 6, 7);
-          if constexpr (SPLIT)
-            vlo[dt] = __builtin_shufflevector(lds_read_tr16(vls[1] + vr),
-                                              lds_read_tr16(vls[1] + vr + 16 * HD),
-                                              0, 1, 2, 3, 4, 5, 6, 7);
+          for (int dt = 0; dt < DT; ++dt) {
+            const int vr = kb * HD + voff(dt);
+            vh[dt] = __builtin_shufflevector(lds_read_tr16(vls[0] + vr),
+                                             lds_read_tr16(vls[0] + vr + 16 * HD),
+                                             0, 1, 2, 3, 4, 5, 6, 7);
+            if constexpr (SPLIT)
+              vlo[dt] = __builtin_shufflevector(lds_read_tr16(vls[1] + vr),
+                                                lds_read_tr16(vls[1] + vr + 16 * HD),
+                                                0, 1, 2, 3, 4, 5, 6, 7);
+          }
         }
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) {
@@ -1859,9 +1889,58 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) 
         st.o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(v, ph, st.o[dt], 0, 0, 0);
       }
   };
+  auto softmax_pv = [&](St& st, int k0, int kb, floatx4 (&sc)[2]) {
+    softmax_pv_m(st, k0, kb, sc, std::integral_constant<int, 0>{});
+  };
+  // VAR bit 32: the K fragments of a block (read one block ahead) and their S^T MFMAs
+  auto kread = [&](int kb, half8 (&kf)[2][KS][NP]) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int krow = kb + 16 * j + ql;
+        const int kr = krow * KROW + 8 * swz_chunk<KCPR>(krow, 4 * ks + g);
+#pragma unroll
+        for (int p = 0; p < NP; ++p) kf[j][ks][p] = *reinterpret_cast<const half8*>(kls[p] + kr);
+      }
+  };
+  auto kmma = [&](const St& st, const half8 (&kf)[2][KS][NP], floatx4 (&sc)[2]) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      sc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {   // the term order of qk()
+        sc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[j][ks][0], st.qf[ks][0], sc[j], 0, 0, 0);
+        if constexpr (SPLIT) {
+          sc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[j][ks][1], st.qf[ks][0], sc[j], 0, 0, 0);
+          sc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[j][ks][0], st.qf[ks][1], sc[j], 0, 0, 0);
+        }
+      }
+    }
+  };
   // keys [k0, k0 + n) of the staged chunk (LDS positions 0 .. n-1)
   auto attend = [&](St& st, int k0, int n) {
-    if constexpr ((VAR & 4) != 0) {
+    if constexpr ((VAR & 32) != 0) {
+      // Peeled loop: the blocks wholly inside the sequence run without the key mask (no
+      // per-block branch, and no register copies between a masked and an unmasked version of
+      // the scores); the last, partial block (if any) after them. Block kb + 32's K fragments
+      // are read while block kb's softmax runs. Same arithmetic, same order: bitwise the
+      // outputs of the variant without bit 32.
+      const int nf = min(n, len - k0) & ~31;
+      half8 kf[2][KS][NP];
+      if (n > 0) kread(0, kf);
+      for (int kb = 0; kb < nf; kb += 32) {
+        floatx4 sc[2];
+        kmma(st, kf, sc);
+        if (kb + 32 < n) kread(kb + 32, kf);
+        softmax_pv_m(st, k0, kb, sc, std::integral_constant<int, 1>{});
+      }
+      if (nf < n) {
+        floatx4 sc[2];
+        kmma(st, kf, sc);
+        softmax_pv_m(st, k0, nf, sc, std::integral_constant<int, 2>{});
+      }
+    } else if constexpr ((VAR & 4) != 0) {
       floatx4 sn[2];
       qk(st, 0, sn);
       for (int kb = 0; kb < n; kb += 32) {

@@ -43,7 +43,7 @@ def data():
     return x, hi, lo, cu
 
 
-@pytest.mark.parametrize("variant", list(range(16)) + [18, 26])
+@pytest.mark.parametrize("variant", list(range(16)) + [18, 26, 40, 42])
 @pytest.mark.parametrize("split", [True, False], ids=["fp16x3", "fp16"])
 def test_attention_matches_fp32(gpu, data, variant, split):
     from ragmi.encoders import attention
@@ -97,6 +97,23 @@ def test_paired_blocks_are_bitwise_identical(gpu, data, variant, split):
     cu_t = torch.from_numpy(cu).cuda()
     a = attention(hi, cu_t, max(LENS), lo if split else None, variant)
     b = attention(hi, cu_t, max(LENS), lo if split else None, variant | 16)
+    torch.cuda.synchronize()
+    for x1, x2 in (zip(a, b) if split else [(a, b)]):
+        assert torch.equal(x1.view(torch.int16), x2.view(torch.int16))
+
+
+@pytest.mark.parametrize("variant", [8, 10])
+@pytest.mark.parametrize("split", [True, False], ids=["fp16x3", "fp16"])
+def test_peeled_prefetch_is_bitwise_identical(gpu, data, variant, split):
+    """VAR bit 32 (full key blocks without the mask, the partial tail block peeled off, the
+    next block's K and the block's V^T fragments read ahead) changes when LDS is read, not
+    what is computed: outputs equal the variant without it bit for bit — ragged lengths
+    (tail blocks of 1..31 keys), a 1-token sequence and 511 keys included."""
+    from ragmi.encoders import attention
+    x, hi, lo, cu = data
+    cu_t = torch.from_numpy(cu).cuda()
+    a = attention(hi, cu_t, max(LENS), lo if split else None, variant)
+    b = attention(hi, cu_t, max(LENS), lo if split else None, variant | 32)
     torch.cuda.synchronize()
     for x1, x2 in (zip(a, b) if split else [(a, b)]):
         assert torch.equal(x1.view(torch.int16), x2.view(torch.int16))
