@@ -341,8 +341,15 @@ void launch_ws(const _Float16* A, const _Float16* Al, const _Float16* W, const _
                const DlArgs& dl = DlArgs{}) {
   const int tiles = (N / CFG::BN) * ((M + CFG::BM - 1) / CFG::BM);
   const dim3 grid((unsigned)std::min(cu_count(), (tiles + 7) / 8 * 8));
+  // RAGMI_WS_PHASE (A/B): start delay of the odd workgroups in units of ~3.4 us (DlArgs.phase)
+  static const int phase = [] {
+    const char* v = std::getenv("RAGMI_WS_PHASE");
+    return v ? std::max(0, std::atoi(v)) : 0;
+  }();
+  DlArgs d = dl;
+  if (d.phase == 0) d.phase = phase;
   gemm_ws_kernel<EPI, SPLIT, CFG, PROBE, AUX><<<grid, dim3(CFG::THREADS + 256), 0, st>>>(
-      A, Al, W, Wl, bias, M, N, K, C, Clo, dl);
+      A, Al, W, Wl, bias, M, N, K, C, Clo, d);
 }
 
 // shapes the deferred-LayerNorm WS GEMMs take: Ln* (K = 384 input rows; c1 | c2 staged in the
@@ -1223,9 +1230,9 @@ int rag_bert_attention(int variant, const void* qkv, const void* qkv_lo, const i
   if ((qkv_lo == nullptr) != (ctx_lo == nullptr))
     return ragmi::fail(RAG_EINVAL, "qkv_lo and ctx_lo: both (fp16x3) or neither (fp16)");
   if (variant == -1) variant = kAttnVar;
-  if ((variant < 0 || variant > 15) && variant != 18 && variant != 26 && variant != 40 &&
-      variant != 42)
-    return ragmi::fail(RAG_EINVAL, "variant: -1, 0..15, 18, 26, 40 or 42");
+  if ((variant < 0 || variant > 15) && variant != 18 && variant != 26 &&
+      (variant < 40 || variant > 46 || variant % 2))
+    return ragmi::fail(RAG_EINVAL, "variant: -1, 0..15, 18, 26, 40, 42, 44 or 46");
   constexpr int H = 384, HD = 32, NH = H / HD;
   const int planes = qkv_lo ? 2 : 1;
   const int kc = attn_chunk_keys<HD>(max_len, planes);
@@ -1273,6 +1280,8 @@ int rag_bert_attention(int variant, const void* qkv, const void* qkv_lo, const i
     case 26: return go(std::integral_constant<int, 26>{});
     case 40: return go(std::integral_constant<int, 40>{});   // 32 = peeled, prefetched blocks
     case 42: return go(std::integral_constant<int, 42>{});
+    case 44: return go(std::integral_constant<int, 44>{});
+    case 46: return go(std::integral_constant<int, 46>{});
     default: return go(std::integral_constant<int, 15>{});
   }
 }

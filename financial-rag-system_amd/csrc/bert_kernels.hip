@@ -616,6 +616,7 @@ struct DlArgs {
   const float* beta = nullptr;
   const float* c1 = nullptr;       // Ln*: [N] column sums of W' (the bias argument is c2)
   float eps = 0.f;
+  int phase = 0;                   // WS kernel: start delay of the odd workgroups (see there)
 };
 
 // hi + lo fp16 planes (4 values each, as loaded) -> fp32 by v_fma_mix_f32 (hi * 1 + lo in one
@@ -1316,6 +1317,12 @@ __global__ __launch_bounds__(CFG::THREADS + 256, 1) void gemm_ws_kernel(
   if constexpr (FLAGS)
     if (tid < 16) ring_cnt[tid] = 0u;
   __syncthreads();
+  // Phase offset (dl.phase > 0, A/B): every CU runs the same tile sequence, so all of them
+  // reach their epilogues — the output store bursts — together, and the chip's MFMAs idle
+  // while HBM takes the writes. The odd workgroups start dl.phase x ~3.4 us late, which puts
+  // their store bursts between the even workgroups' ones.
+  if (dl.phase > 0 && (lx & 1))
+    for (int i = 0; i < dl.phase; ++i) __builtin_amdgcn_s_sleep(127);
 
   if (wid >= TH / 64) {
     // ---- loader waves: stage g+NS-1 issued after the barrier of step g ----
@@ -1929,6 +1936,26 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) 
       const int nf = min(n, len - k0) & ~31;
       half8 kf[2][KS][NP];
       if (n > 0) kread(0, kf);
+      if constexpr ((VAR & 4) != 0) {
+        // + bit 4: block kb + 32's S^T MFMAs issued before block kb's softmax (they run in
+        // the matrix pipe under its vector work), block kb + 64's K read behind them
+        floatx4 sn[2];
+        if (n > 0) {
+          kmma(st, kf, sn);
+          if (32 < n) kread(32, kf);
+        }
+        int kb = 0;
+        for (; kb < nf; kb += 32) {
+          floatx4 sc[2] = {sn[0], sn[1]};
+          if (kb + 32 < n) {
+            kmma(st, kf, sn);
+            if (kb + 64 < n) kread(kb + 64, kf);
+          }
+          softmax_pv_m(st, k0, kb, sc, std::integral_constant<int, 1>{});
+        }
+        if (kb < n) softmax_pv_m(st, k0, kb, sn, std::integral_constant<int, 2>{});
+        return;
+      }
       for (int kb = 0; kb < nf; kb += 32) {
         floatx4 sc[2];
         kmma(st, kf, sc);

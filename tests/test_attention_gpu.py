@@ -43,7 +43,7 @@ def data():
     return x, hi, lo, cu
 
 
-@pytest.mark.parametrize("variant", list(range(16)) + [18, 26, 40, 42])
+@pytest.mark.parametrize("variant", list(range(16)) + [18, 26, 40, 42, 44, 46])
 @pytest.mark.parametrize("split", [True, False], ids=["fp16x3", "fp16"])
 def test_attention_matches_fp32(gpu, data, variant, split):
     from ragmi.encoders import attention
@@ -102,7 +102,7 @@ def test_paired_blocks_are_bitwise_identical(gpu, data, variant, split):
         assert torch.equal(x1.view(torch.int16), x2.view(torch.int16))
 
 
-@pytest.mark.parametrize("variant", [8, 10])
+@pytest.mark.parametrize("variant", [8, 10, 12, 14])
 @pytest.mark.parametrize("split", [True, False], ids=["fp16x3", "fp16"])
 def test_peeled_prefetch_is_bitwise_identical(gpu, data, variant, split):
     """VAR bit 32 (full key blocks without the mask, the partial tail block peeled off, the
