@@ -768,6 +768,24 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
     const int ks_room = (int)std::max<int64_t>(1, std::min<int64_t>(kMaxKSplit, y_rows / R));
     auto add_ln = [&](const float* gam, const float* bet, int parts) {
       const int64_t ps = (int64_t)R * H;
+      if constexpr (H == 384) {
+        // 16-B accesses and DPP / permlane reductions (round 3; RAGMI_ADDLN_VEC=0: A/B)
+        static const bool vec = [] {
+          const char* v = std::getenv("RAGMI_ADDLN_VEC");
+          return !(v && std::atoi(v) == 0);
+        }();
+        if (vec) {
+          if (row_xf)
+            add_ln384_kernel<true><<<dim3(lg), dim3(256), 0, st>>>(nullptr, y, gam, bet,
+                                                                  c.layer_norm_eps, xh, xl, R,
+                                                                  parts, ps);
+          else
+            add_ln384_kernel<false><<<dim3(lg), dim3(256), 0, st>>>(x, y, gam, bet,
+                                                                   c.layer_norm_eps, xh, xl, R,
+                                                                   parts, ps);
+          return;
+        }
+      }
       if (row_xf)
         add_ln_kernel<H, true><<<dim3(lg), dim3(256), 0, st>>>(nullptr, y, gam, bet,
                                                               c.layer_norm_eps, xh, xl, R,

@@ -193,6 +193,110 @@ __global__ __launch_bounds__(256) void add_ln_kernel(float* __restrict__ x,
   }
 }
 
+// Sum over the 64 lanes, the same bits in every lane: DPP within each 16-lane row (xor 1,
+// xor 2, half-row mirror, row mirror — each step adds a lane's value to its partner's, and
+// fp32 addition commutes, so partners agree), then the row pairs and halves by
+// v_permlane16_swap / v_permlane32_swap. No LDS round trips (ds_bpermute: ~12 dependent ones
+// for two butterfly reductions in add_ln_kernel).
+__device__ __forceinline__ float dpp_add(float v, int ctrl_sel) {
+  int d;
+  switch (ctrl_sel) {   // dpp_ctrl must be an immediate
+    case 0: d = __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false); break;
+    case 1: d = __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false); break;
+    case 2: d = __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false); break;
+    default: d = __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false); break;
+  }
+  return v + __builtin_bit_cast(float, d);
+}
+__device__ __forceinline__ float wave_sum64(float v) {
+  v = dpp_add(v, 0);   // quad_perm [1,0,3,2]
+  v = dpp_add(v, 1);   // quad_perm [2,3,0,1]: every lane holds its quad's sum
+  v = dpp_add(v, 2);   // row_half_mirror: + the other quad of the 8
+  v = dpp_add(v, 3);   // row_mirror: + the other 8 of the row
+  const uint32_t u = __builtin_bit_cast(uint32_t, v);
+  const auto r16 = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  v = __builtin_bit_cast(float, (uint32_t)r16[0]) + __builtin_bit_cast(float, (uint32_t)r16[1]);
+  const uint32_t u2 = __builtin_bit_cast(uint32_t, v);
+  const auto r32 = __builtin_amdgcn_permlane32_swap(u2, u2, false, false);
+  return __builtin_bit_cast(float, (uint32_t)r32[0]) + __builtin_bit_cast(float, (uint32_t)r32[1]);
+}
+
+// add_ln_kernel for hidden 384 (bge-small / MiniLM; round 3): lane l < 48 owns columns
+// 8l .. 8l+7 — 16-B loads of the residual planes (or 2 x 16 B of the fp32 rows) and of each
+// split-K part, 16-B plane stores — and both reductions run on wave_sum64. The small-batch
+// forward's residual passes (2 per layer, ~87 launches per 32-query encode) were
+// latency-bound on 2-byte accesses and 12 dependent ds_bpermute round trips.
+// Same formula, parts summed in part order; the reduction order differs from add_ln_kernel's.
+template <bool XF>
+__global__ __launch_bounds__(256) void add_ln384_kernel(float* __restrict__ x,
+                                                        const float* __restrict__ y,
+                                                        const float* __restrict__ g,
+                                                        const float* __restrict__ bt, float eps,
+                                                        _Float16* __restrict__ xh,
+                                                        _Float16* __restrict__ xl, int T,
+                                                        int parts = 1, int64_t pstride = 0) {
+  constexpr int H = 384;
+  const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (t >= T) return;
+  const bool on = lane < H / 8;
+  const int64_t o = t * H + 8 * (on ? lane : 0);
+  float v[8];
+  if (on) {
+    floatx4 y0 = *reinterpret_cast<const floatx4*>(y + o);
+    floatx4 y1 = *reinterpret_cast<const floatx4*>(y + o + 4);
+#pragma unroll
+    for (int p = 1; p < 4; ++p)
+      if (p < parts) {
+        y0 += *reinterpret_cast<const floatx4*>(y + p * pstride + o);
+        y1 += *reinterpret_cast<const floatx4*>(y + p * pstride + o + 4);
+      }
+    if constexpr (XF) {
+      const half8 h = *reinterpret_cast<const half8*>(xh + o);
+      const half8 l = xl ? *reinterpret_cast<const half8*>(xl + o) : half8{};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = ((float)h[e] + (float)l[e]) + (e < 4 ? y0[e] : y1[e - 4]);
+    } else {
+      const floatx4 r0 = *reinterpret_cast<const floatx4*>(x + o);
+      const floatx4 r1 = *reinterpret_cast<const floatx4*>(x + o + 4);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = (e < 4 ? r0[e] : r1[e - 4]) + (e < 4 ? y0[e] : y1[e - 4]);
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = 0.f;
+  }
+  float s = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+  const float mu = wave_sum64(s) * (1.0f / H);
+  float q = 0.f;
+  if (on)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) q = fmaf(v[e] - mu, v[e] - mu, q);
+  const float rs = rsqrtf(wave_sum64(q) * (1.0f / H) + eps);
+  if (!on) return;
+  const floatx4 g0 = *reinterpret_cast<const floatx4*>(g + 8 * lane);
+  const floatx4 g1 = *reinterpret_cast<const floatx4*>(g + 8 * lane + 4);
+  const floatx4 b0 = *reinterpret_cast<const floatx4*>(bt + 8 * lane);
+  const floatx4 b1 = *reinterpret_cast<const floatx4*>(bt + 8 * lane + 4);
+  float out[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e)
+    out[e] = (v[e] - mu) * rs * (e < 4 ? g0[e] : g1[e - 4]) + (e < 4 ? b0[e] : b1[e - 4]);
+  if constexpr (!XF) {
+    *reinterpret_cast<floatx4*>(x + o) = floatx4{out[0], out[1], out[2], out[3]};
+    *reinterpret_cast<floatx4*>(x + o + 4) = floatx4{out[4], out[5], out[6], out[7]};
+  }
+  half8 hh, ll;
+#pragma unroll
+  for (int e = 0; e < 8; e += 2) {
+    half2 h2, l2;
+    split16x2(out[e], out[e + 1], h2, l2);
+    hh[e] = h2[0]; hh[e + 1] = h2[1]; ll[e] = l2[0]; ll[e + 1] = l2[1];
+  }
+  *reinterpret_cast<half8*>(xh + o) = hh;
+  if (xl) *reinterpret_cast<half8*>(xl + o) = ll;
+}
+
 // ----------------------------------------------------------------------------------------
 // GEMM: C[M,N] = A[M,K] . W[N,K]^T + bias[N]   (A fp16 row-major, W fp16 [N][K] = HF Linear)
 // 128x128 tile, BK = 64 (fp16) / 32 (fp16x3), 256 threads = 2x2 waves of 64x64,
