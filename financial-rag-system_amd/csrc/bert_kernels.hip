@@ -996,14 +996,42 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
   if (ksplit > 1)
     for (int i = tid * 4; i < N; i += TH * 4)
       *reinterpret_cast<floatx4*>(bias_l + kPipeBiasMax / 2 + i) = floatx4{0.f, 0.f, 0.f, 0.f};
-  for (int i = tid * 4; i < N; i += TH * 4) {
-    *reinterpret_cast<floatx4*>(bias_l + i) = *reinterpret_cast<const floatx4*>(bias + i);
-    if constexpr (EPI == kEpiAddLn) {          // N == BN here (checked by the launcher)
-      *reinterpret_cast<floatx4*>(bias_l + BN + i) = *reinterpret_cast<const floatx4*>(ln.gamma + i);
-      *reinterpret_cast<floatx4*>(bias_l + 2 * BN + i) = *reinterpret_cast<const floatx4*>(ln.beta + i);
+  // The staged vectors (bias [| gamma | beta]) are loaded into registers here and written to
+  // LDS only after the ring prologue's DMAs are issued (below), so their load latency and the
+  // first stages' run concurrently instead of back to back — a query-batch GEMM is one or two
+  // tiles per workgroup, where that serial latency was a visible part of the launch.
+  constexpr int NBV = kPipeBiasMax / (TH * 4) > 0 ? kPipeBiasMax / (TH * 4) : 1;
+  constexpr int NLN = EPI == kEpiAddLn ? (BN + TH * 4 - 1) / (TH * 4) : 0;
+  floatx4 bv[NBV], gv[NLN > 0 ? NLN : 1], ev[NLN > 0 ? NLN : 1];
+#pragma unroll
+  for (int u = 0; u < NBV; ++u) {
+    const int i = tid * 4 + u * TH * 4;
+    if (i < N) bv[u] = *reinterpret_cast<const floatx4*>(bias + i);
+  }
+#pragma unroll
+  for (int u = 0; u < NLN; ++u) {               // N == BN here (checked by the launcher)
+    const int i = tid * 4 + u * TH * 4;
+    if (i < N) {
+      gv[u] = *reinterpret_cast<const floatx4*>(ln.gamma + i);
+      ev[u] = *reinterpret_cast<const floatx4*>(ln.beta + i);
     }
   }
-  __syncthreads();
+  auto stage_vectors = [&]() {
+#pragma unroll
+    for (int u = 0; u < NBV; ++u) {
+      const int i = tid * 4 + u * TH * 4;
+      if (i < N) *reinterpret_cast<floatx4*>(bias_l + i) = bv[u];
+    }
+#pragma unroll
+    for (int u = 0; u < NLN; ++u) {
+      const int i = tid * 4 + u * TH * 4;
+      if (i < N) {
+        *reinterpret_cast<floatx4*>(bias_l + BN + i) = gv[u];
+        *reinterpret_cast<floatx4*>(bias_l + 2 * BN + i) = ev[u];
+      }
+    }
+    __syncthreads();
+  };
 
   // per-lane byte offsets inside a panel (launch constants): LDS position q of the
   // lane-linear image holds row q / CPR, 16-B chunk (q % CPR) ^ swizzle(row)
@@ -1076,6 +1104,7 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
 
 #pragma unroll
   for (int p = 0; p < NS - 1; ++p) issue_next();
+  stage_vectors();
   int kt_c = 0, it_c = 0, slot_c = 0;
   for (int g = 0; g < steps; ++g) {
     // stages issued after step g: min(NS - 2, steps - 1 - g); plus the last epilogue's
