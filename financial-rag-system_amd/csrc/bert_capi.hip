@@ -393,6 +393,15 @@ void gemm_add_ln(const _Float16* A, const _Float16* Al, const _Float16* W, const
                                            cu_count(), ln);
 }
 
+// RAGMI_ATTN_VAR (A/B): the forward's attention variant, 0 = kAttnVar (default) or 10
+int attn_var_override() {
+  static const int v = [] {
+    const char* s = std::getenv("RAGMI_ATTN_VAR");
+    return s ? std::atoi(s) : 0;
+  }();
+  return v;
+}
+
 // fusion mode of the forward: -1 auto (once the 128-row bands cover the CUs), 0 off, 1 on
 int fuse_ln_default() {
   static int v = [] {
@@ -703,7 +712,14 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
       gemm<kEpiF16>(w->xh, w->xl, L.wqkv, L.wqkv_l, L.bqkv, T, 3 * H, H, w->qkv, w->qkv_l, st);
     }
     const int max_qb = last ? 1 : 1 << 20;
-    if (w->xl)
+    if (attn_var_override() == 10) {   // RAGMI_ATTN_VAR=10: the round-2 variant (A/B)
+      if (w->xl)
+        attn_kernel<H, HD, true, 10><<<agrid, dim3(kAttnThreads<true>), alds, st>>>(
+            w->qkv, w->qkv_l, cu, max_len, kc, scale, w->ctx, w->ctx_l, max_qb);
+      else
+        attn_kernel<H, HD, false, 10><<<agrid, dim3(kAttnThreads<false>), alds, st>>>(
+            w->qkv, nullptr, cu, max_len, kc, scale, w->ctx, nullptr, max_qb);
+    } else if (w->xl)
       attn_kernel<H, HD, true><<<agrid, dim3(kAttnThreads<true>), alds, st>>>(
           w->qkv, w->qkv_l, cu, max_len, kc, scale, w->ctx, w->ctx_l, max_qb);
     else
@@ -981,6 +997,10 @@ int set_attn_lds_attr() {
   RAG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_kernel<H, HD, true>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, kAttnLdsMax));
   RAG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_kernel<H, HD, false>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kAttnLdsMax));
+  RAG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_kernel<H, HD, true, 10>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kAttnLdsMax));
+  RAG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_kernel<H, HD, false, 10>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, kAttnLdsMax));
   return RAG_OK;
 }
