@@ -98,6 +98,8 @@ struct rag_index {
   hipStream_t scan_stream = nullptr;
   hipEvent_t scan_done = nullptr;
   hipStream_t scan_last = nullptr;
+  bool scan_any = false;       // a scan has been chained since set_scan_order (scan_last may be
+                               // the null stream, whose handle is nullptr)
   int prof = 0;                // 0 off; n > 0: time every n-th scan launch
   int64_t prof_seq = 0;
   std::vector<ProfPair> prof_pairs;
@@ -247,7 +249,10 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
       const char* v = std::getenv("RAGMI_SCAN_WGS");
       return v ? std::max(8, std::atoi(v)) : 0;
     }();
-    const int wg_cap = wg_env ? wg_env : h->scan_wgs;
+    // Filtered scans (a tag load and compare per row) keep two workgroups per CU: 10M rows,
+    // per-query ticker filter, serial order: 26.8 / 27.0K qps at 512 vs 25.7 / 26.1K at 192
+    // (scan 1.170 vs 1.21-1.24 ms, profiles/r03u_filtered_wgs.jsonl)
+    const int wg_cap = wg_env ? wg_env : filt ? h->max_wgs : h->scan_wgs;
     grid = (int)std::min<int64_t>(std::min(h->max_wgs, wg_cap),
                                   std::max<int64_t>(1, (n_tiles + 3) / 4));
     grid = std::min(grid, kMaxLists / kWavesPerWG);
@@ -255,7 +260,11 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
   const hipStream_t caller = st;
   if (h->serial_scans == 1) {
     if (!h->scan_done) RAG_HIP(hipEventCreateWithFlags(&h->scan_done, hipEventDisableTiming));
-    if (h->scan_last && h->scan_last != st) RAG_HIP(hipStreamWaitEvent(st, h->scan_done, 0));
+    // (keyed on scan_any, not on scan_last being non-null: a scan on the null stream leaves
+    // scan_last == nullptr, and testing the handle let the next pass on another stream skip
+    // its wait — the filtered 10M line's scans overlapped, traced: 2.2 ms launches, 1.24 ms
+    // apart)
+    if (h->scan_any && h->scan_last != st) RAG_HIP(hipStreamWaitEvent(st, h->scan_done, 0));
   } else if (h->serial_scans == 2) {
     if (!h->scan_stream) RAG_HIP(hipStreamCreateWithFlags(&h->scan_stream, hipStreamNonBlocking));
     if (!w.ev_in) RAG_HIP(hipEventCreateWithFlags(&w.ev_in, hipEventDisableTiming));
@@ -320,6 +329,7 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
   if (h->serial_scans == 1) {
     RAG_HIP(hipEventRecord(h->scan_done, st));
     h->scan_last = st;
+    h->scan_any = true;
   } else if (h->serial_scans == 2) {
     RAG_HIP(hipEventRecord(w.ev_out, st));
     RAG_HIP(hipStreamWaitEvent(caller, w.ev_out, 0));
@@ -1070,6 +1080,7 @@ int rag_index_set_scan_order(rag_index_t* h, int serial) {
   std::lock_guard<std::mutex> lk(h->mu);
   h->serial_scans = serial < 0 || serial > 2 ? 1 : serial;
   h->scan_last = nullptr;
+  h->scan_any = false;
   return RAG_OK;
 }
 

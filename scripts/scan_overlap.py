@@ -15,8 +15,9 @@ def main():
     label = sys.argv[2] if len(sys.argv) > 2 else d
     f = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)[0]
     rows = list(csv.DictReader(open(f)))
+    # the scan launches only (not rescan_kernel, whose name contains "scan_kernel")
     sc = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows
-                if "scan_kernel" in r["Kernel_Name"])
+                if "scan_kernel" in r["Kernel_Name"] and "rescan" not in r["Kernel_Name"])
     sc = sc[len(sc) // 5:]                              # drop build / warm-up launches
     st = np.array([a for a, _ in sc], dtype=np.float64)
     en = np.array([b for _, b in sc], dtype=np.float64)
