@@ -300,8 +300,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--streams", type=int, default=0,
-                    help="batches in flight (0 = by shard size: 4 below 4M rows per GPU, "
-                         "else 2; 1 on a single GPU)")
+                    help="batches in flight (0 = by shard size: 4 below 4M rows per GPU "
+                         "(3 at N > 1 over RCCL, whose collective stream takes a hardware "
+                         "queue), else 2)")
     ap.add_argument("--scan-order", choices=["auto", "serial", "free", "stream"], default="auto",
                     help="serial: each batch's scan waits for the previous batch's scan "
                          "(rag_index_set_scan_order); free: scans on different streams overlap")
@@ -379,7 +380,14 @@ def main():
     # 26.8K); small shards keep free order, where overlapping scan ramps/tails is the gain
     # (1.25M rows, 4 in flight: 195K free vs 193K serial) — profiles/r01h_scan_order.jsonl.
     rows_local = hi - lo
-    n_streams = args.streams or (4 if rows_local < 4_000_000 else 2)
+    # Over RCCL the process group's collectives run on a stream of their own: with 4 batches
+    # in flight that is a fifth stream on the process's 4 hardware queues (GPU_MAX_HW_QUEUES),
+    # and streams sharing a queue serialise behind each other's kernels (6 or 8 streams at
+    # 1.25M rows: 149K vs 210K qps, profiles/r01f_small_shard_streams.jsonl). So small shards
+    # keep 3 in flight at N > 1 on nccl (1 GPU, no collective: 195K vs 199K qps at 3 vs 4,
+    # profiles/r03r_knob_sweep.jsonl).
+    rccl = world > 1 and backend == "nccl"
+    n_streams = args.streams or (2 if rows_local >= 4_000_000 else 3 if rccl else 4)
     serial = args.scan_order == "serial" or (args.scan_order == "auto"
                                              and rows_local >= 4_000_000)
     if args.scan_order == "stream":
