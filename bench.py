@@ -300,9 +300,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--streams", type=int, default=0,
-                    help="batches in flight (0 = by shard size: 4 below 4M rows per GPU "
-                         "(3 at N > 1 over RCCL, whose collective stream takes a hardware "
-                         "queue), else 2)")
+                    help="batches in flight (0 = by shard size: 4 below 4M rows per GPU, "
+                         "else 2)")
     ap.add_argument("--scan-order", choices=["auto", "serial", "free", "stream"], default="auto",
                     help="serial: each batch's scan waits for the previous batch's scan "
                          "(rag_index_set_scan_order); free: scans on different streams overlap")
@@ -338,13 +337,24 @@ def main():
     dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
     torch.cuda.set_device(dev)
     backend, ranks_seen = None, 1
-    if world > 1:
+    # RAGMI_DIST_REHEARSAL=1 (one GPU, diagnostic): a world-1 process group whose packed
+    # all-gather + GPU merge still run every batch (ShardedIndex force_exchange), so the RCCL
+    # stream's interplay with the batches in flight can be measured on a one-GPU box
+    rehearsal = world == 1 and os.environ.get("RAGMI_DIST_REHEARSAL") == "1"
+    if world > 1 or rehearsal:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         backend = os.environ.get("RAGMI_DIST_BACKEND", "nccl")   # nccl = RCCL over xGMI
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
+        if rehearsal:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
+        # RCCL's communicator is created lazily (no device_id: at the first collective, after
+        # the shard is built). Created eagerly here, before the corpus allocation, its buffers
+        # left the 960 MB shard with a placement that scans ~8% slower: 1.25M rows, 4 in flight,
+        # plain search 184K vs 201K qps, the same with the communicator created after the
+        # shard 201K (scripts/rccl_exchange_probe.py, profiles/r03w_rccl_probe.jsonl)
+        dist.init_process_group(backend)
         backend = dist.get_backend()
         ranks_seen = dist.get_world_size()
         if ranks_seen != world:
@@ -354,7 +364,7 @@ def main():
     from ragmi.index import busy_union_ms
 
     n_total = args.rows
-    sh = ShardedIndex(n_total, dim=D, device=dev, storage=args.storage)
+    sh = ShardedIndex(n_total, dim=D, device=dev, storage=args.storage, force_exchange=rehearsal)
     idx, lo, hi = sh.local, sh.lo, sh.hi
     build_shard(idx, lo, hi, n_total, dev)
     nb = args.warmup + args.steps
@@ -380,14 +390,7 @@ def main():
     # 26.8K); small shards keep free order, where overlapping scan ramps/tails is the gain
     # (1.25M rows, 4 in flight: 195K free vs 193K serial) — profiles/r01h_scan_order.jsonl.
     rows_local = hi - lo
-    # Over RCCL the process group's collectives run on a stream of their own: with 4 batches
-    # in flight that is a fifth stream on the process's 4 hardware queues (GPU_MAX_HW_QUEUES),
-    # and streams sharing a queue serialise behind each other's kernels (6 or 8 streams at
-    # 1.25M rows: 149K vs 210K qps, profiles/r01f_small_shard_streams.jsonl). So small shards
-    # keep 3 in flight at N > 1 on nccl (1 GPU, no collective: 195K vs 199K qps at 3 vs 4,
-    # profiles/r03r_knob_sweep.jsonl).
-    rccl = world > 1 and backend == "nccl"
-    n_streams = args.streams or (2 if rows_local >= 4_000_000 else 3 if rccl else 4)
+    n_streams = args.streams or (4 if rows_local < 4_000_000 else 2)
     serial = args.scan_order == "serial" or (args.scan_order == "auto"
                                              and rows_local >= 4_000_000)
     if args.scan_order == "stream":
@@ -514,7 +517,8 @@ def main():
                     "queries = corpus row + 0.05 N(0,1), every 4th batch pure random)",
             "config": {"workload": f"cosine top-{K_TOP} over {n_total}x{D} fp16 corpus, "
                                    f"batch={B}, {world} shard(s)" +
-                                   (" + RCCL all-gather merge" if world > 1 else ""),
+                                   (" + RCCL all-gather merge" if world > 1 else
+                                    " + world-1 exchange rehearsal" if rehearsal else ""),
                        "corpus_rows": n_total, "dim": D, "batch": B, "k": K_TOP,
                        "rows_per_gpu": local_rows, "parallelism": f"corpus-shard{world}",
                        "batches_in_flight": n_streams, "storage": args.storage,
@@ -551,7 +555,7 @@ def main():
         }
         print(json.dumps(line), flush=True)
     idx.close()
-    if world > 1:
+    if world > 1 or rehearsal:
         dist.destroy_process_group()
 
 

@@ -11,6 +11,11 @@ one id-for-id (tests/test_scan_gpu.py::test_sharded_merge_equals_unsharded).
 
 This replaces the per-request HTTP hop to the Qdrant service (reference main.py:232-237);
 the reference itself has no multi-GPU component.
+
+Allocation order matters on MI355X: build (or load) the shard BEFORE RCCL's communicator is
+created — init the process group without `device_id`, so the communicator appears at the
+first collective. Created first, its buffers left the shard with a physical placement that
+scans ~8% slower (1.25M-row shard: 184K vs 201K qps; DESIGN §6, profiles/r03w_rccl_probe.jsonl).
 """
 from __future__ import annotations
 
@@ -89,7 +94,7 @@ class ShardedIndex:
 
     def __init__(self, n_total: int, local=None, dim: int = 384, device=None, group=None,
                  merge: Callable | None = None, merge_packed: Callable | None = None,
-                 storage: str = "fp16"):
+                 storage: str = "fp16", force_exchange: bool = False):
         self.group = group
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -108,6 +113,9 @@ class ShardedIndex:
         self.packed = ((merge is None or merge_packed is not None) and
                        hasattr(local, "search_packed") and self.n_total < 2 ** 31 and
                        dist.is_initialized())
+        # force_exchange: run the packed all-gather + merge even at world 1 (bench.py's
+        # one-GPU RCCL rehearsal, RAGMI_DIST_REHEARSAL; same results as the plain search)
+        self.force_exchange = bool(force_exchange) and self.packed
 
     @property
     def rows(self) -> int:
@@ -126,7 +134,7 @@ class ShardedIndex:
             self.local.upsert(vectors[m], rows, t, new_count=cnt)
 
     def search(self, queries, k: int, filters=None):
-        if self.world > 1 and self.packed:
+        if (self.world > 1 or self.force_exchange) and self.packed:
             # one all-gather of the packed (score bits, int32 row) lists instead of two
             p = self.local.search_packed(queries, k, filters=filters, id_offset=self.lo)
             return self.merge_packed(all_gather_packed(p, self.group), k)

@@ -106,7 +106,7 @@ def main():
     torch.cuda.set_device(dev)
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        dist.init_process_group(os.environ.get("RAGMI_DIST_BACKEND", "nccl"), device_id=dev)
+        dist.init_process_group(os.environ.get("RAGMI_DIST_BACKEND", "nccl"))   # lazy comm (bench.py)
     from ragmi.dist import ShardedIndex
 
     n = args.rows

@@ -54,7 +54,7 @@ def _init_dist(dev):
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         backend = os.environ.get("RAGMI_DIST_BACKEND", "nccl")
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl")   # lazy communicator: after the shard (bench.py)
         else:
             dist.init_process_group(backend)
 
@@ -599,9 +599,7 @@ def run_search(args, mode):
             tick = tags_fn(picks[i]) if i % 4 != 3 else rng.integers(1, n_tick + 1, batch)
             f = np.stack([np.full(batch, 0xFFFF, np.uint32), tick.astype(np.uint32)], 1)
             filts.append(torch.from_numpy(f.view(np.int32)).to(dev))
-    # (3 at N > 1 over RCCL: its collective stream takes one of the 4 hardware queues; bench.py)
-    rccl = world > 1 and dist.is_initialized() and dist.get_backend() == "nccl"
-    n_streams = args.streams or (2 if hi - lo >= 4_000_000 else 3 if rccl else 4)
+    n_streams = args.streams or (4 if hi - lo < 4_000_000 else 2)
     serial = hi - lo >= 4_000_000
     idx.set_scan_order(serial)
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev)
