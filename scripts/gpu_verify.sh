@@ -11,4 +11,4 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --t
 rc=$?
 tail -3 gpurun_out/pytest_gpu.log; echo "pytest rc=$rc"
 if [ $rc -ne 0 ]; then grep -E "^(FAILED|E  )" gpurun_out/pytest_gpu.log | head -30; exit $rc; fi
-[ "${PROFILE:-1}" = "1" ] && TAG=${TAG:-r01} bash scripts/profile.sh
+if [ "${PROFILE:-1}" = "1" ]; then TAG=${TAG:-r01} bash scripts/profile.sh; fi
