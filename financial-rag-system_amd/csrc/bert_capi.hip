@@ -340,7 +340,9 @@ void launch_ws(const _Float16* A, const _Float16* Al, const _Float16* W, const _
                const float* bias, int M, int N, int K, void* C, _Float16* Clo, hipStream_t st,
                const DlArgs& dl = DlArgs{}) {
   const int tiles = (N / CFG::BN) * ((M + CFG::BM - 1) / CFG::BM);
-  const dim3 grid((unsigned)std::min(cu_count(), (tiles + 7) / 8 * 8));
+  // one workgroup per CU; the single-loader small-tile instance fits two (64 KB LDS each)
+  const int per_cu = CFG::LOADERS < 4 ? 2 : 1;
+  const dim3 grid((unsigned)std::min(per_cu * cu_count(), (tiles + 7) / 8 * 8));
   // RAGMI_WS_PHASE (A/B): start delay of the odd workgroups in units of ~3.4 us (DlArgs.phase)
   static const int phase = [] {
     const char* v = std::getenv("RAGMI_WS_PHASE");
@@ -348,7 +350,7 @@ void launch_ws(const _Float16* A, const _Float16* Al, const _Float16* W, const _
   }();
   DlArgs d = dl;
   if (d.phase == 0) d.phase = phase;
-  gemm_ws_kernel<EPI, SPLIT, CFG, PROBE, AUX><<<grid, dim3(CFG::THREADS + 256), 0, st>>>(
+  gemm_ws_kernel<EPI, SPLIT, CFG, PROBE, AUX><<<grid, dim3(CFG::THREADS + 64 * CFG::LOADERS), 0, st>>>(
       A, Al, W, Wl, bias, M, N, K, C, Clo, d);
 }
 
@@ -481,6 +483,22 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
     return;
   }
   if (auto_pick && variant == RAG_GEMM_SMALL && Al && small_bk != 32) variant = RAG_GEMM_SMALL_BK64;
+  // RAGMI_SMALL_WS=1 (A/B, off): query-batch fp16-output GEMMs (QKV, FFN1 at fp16x3) on the
+  // loader-specialised small tiles (PipeWsSmall, RAG_GEMM_WS_SMALL). Measured slower
+  // (profiles/r03zz_small_ws.jsonl, 782 tokens: QKV 9.8 vs 9.7 us, FFN1 14.3 vs 10.3,
+  // encode_q 0.726 vs 0.686 ms): moving the DMA issue off the MFMA waves does not help a
+  // GEMM of one or two tiles per workgroup
+  static const bool small_ws = [] {
+    const char* v = std::getenv("RAGMI_SMALL_WS");
+    return v && std::atoi(v) == 1;
+  }();
+  if (pipe_ok(M, N, K) &&
+      (variant == RAG_GEMM_WS_SMALL ||
+       (auto_pick && variant == RAG_GEMM_SMALL && Al && small_ws && EPI != kEpiF32))) {
+    if (Al) launch_ws<EPI, true, PipeWsSmall, 0, 0>(A, Al, W, Wl, bias, M, N, K, C, Clo, st);
+    else launch_ws<EPI, false, PipeWsSmall, 0, 0>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st);
+    return;
+  }
   // diagnostic probes of the PIPE kernel (parts removed; bert_kernels.hip PROBE)
   const int probe = variant == RAG_GEMM_PROBE_NO_MFMA           ? 1
                     : variant == RAG_GEMM_PROBE_NO_DMA          ? 2
@@ -1183,7 +1201,7 @@ int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, co
        variant == RAG_GEMM_WS || variant == RAG_GEMM_WS_NT || variant == RAG_GEMM_WS_NOROT ||
        variant == RAG_GEMM_WS_READS_FIRST || variant == RAG_GEMM_WS_PRIO_LOAD ||
        variant == RAG_GEMM_WS_PRIO_MFMA || variant == RAG_GEMM_WS_FLAGS ||
-       variant == RAG_GEMM_WS_NOHALF) &&
+       variant == RAG_GEMM_WS_NOHALF || variant == RAG_GEMM_WS_SMALL) &&
       !pipe_ok(M, N, K))
     return ragmi::fail(RAG_EINVAL, "pipe/small/wide variants need N % 128 == 0, K % 64 == 0, "
                                    "N <= 4096, M*K*2 and M*N*4 < 2^31");
@@ -1201,7 +1219,8 @@ int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, co
                      variant == RAG_GEMM_WS || variant == RAG_GEMM_WS_NT ||
                      variant == RAG_GEMM_WS_NOROT || variant == RAG_GEMM_WS_READS_FIRST ||
                      variant == RAG_GEMM_WS_PRIO_LOAD || variant == RAG_GEMM_WS_PRIO_MFMA ||
-                     variant == RAG_GEMM_WS_FLAGS || variant == RAG_GEMM_WS_NOHALF || probe;
+                     variant == RAG_GEMM_WS_FLAGS || variant == RAG_GEMM_WS_NOHALF ||
+                     variant == RAG_GEMM_WS_SMALL || probe;
   if (!known || (probe && !pipe_ok(M, N, K)))
     return ragmi::fail(RAG_EINVAL, "unknown GEMM variant, or a probe on a non-pipe shape");
   auto* a = static_cast<const _Float16*>(A);

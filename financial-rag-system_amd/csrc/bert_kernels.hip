@@ -525,10 +525,11 @@ __global__ __launch_bounds__(256) void gemm_kernel(const _Float16* __restrict__ 
 // 64x64 tiles, 4 waves of 32x32, a 4-stage ring (fp16: the whole K = 384 of a tile in
 // flight after the prologue), for query batches of a few hundred to a few thousand tokens,
 // where a GEMM is a handful of tiles per CU and latency, not MFMA rate, sets its time.
-template <int BM_, int BN_, int WAVES_M_, int WAVES_N_, int NS_, int BK_ = 0>
+template <int BM_, int BN_, int WAVES_M_, int WAVES_N_, int NS_, int BK_ = 0, int LOADERS_ = 4>
 struct PipeCfg {
   static constexpr int BM = BM_, BN = BN_, WAVES_M = WAVES_M_, WAVES_N = WAVES_N_, NS = NS_;
   static constexpr int BK = BK_;   // K step; 0 = kBK<SPLIT> (64 fp16 / 32 fp16x3)
+  static constexpr int LOADERS = LOADERS_;   // gemm_ws_kernel's loader waves
   static constexpr int THREADS = 64 * WAVES_M * WAVES_N;
   static constexpr int FM = BM / WAVES_M / 16, FN = BN / WAVES_N / 16;   // 16x16 frags/wave
   // a K step's fragments all loaded before its MFMAs (the large tiles; see the main loop)
@@ -555,6 +556,10 @@ using PipeWide256 = PipeCfg<256, 256, 4, 2, 2>;
 using PipeBig = PipeCfg<256, 256, 2, 2, 2>;
 using PipeBig128 = PipeCfg<256, 128, 2, 2, 3>;
 using PipeWide192 = PipeCfg<256, 192, 4, 2, 2>;
+// query-batch tiles on the loader-specialised kernel (round 3, RAG_GEMM_WS_SMALL; measured
+// slower than SMALL, not AUTO's pick): SMALL's 64 x 64 tiles and 3-stage BK-32 ring, the
+// DMAs moved to ONE loader wave beside the 4 MFMA waves, two workgroups per CU.
+using PipeWsSmall = PipeCfg<64, 64, 2, 2, 3, 0, 1>;
 constexpr int PBM = PipeLarge::BM, PBN = PipeLarge::BN;
 constexpr int kPipeThreads = PipeLarge::THREADS;
 constexpr int kPipeBiasMax = 4096;            // floats of bias staged in LDS (N <= 4096)
@@ -1360,16 +1365,17 @@ __device__ __forceinline__ void lds_spin_ge(uint32_t* p, uint32_t target) {
 }
 
 template <int EPI, bool SPLIT, typename CFG, int PROBE = 0, int AUX = 0>
-__global__ __launch_bounds__(CFG::THREADS + 256, 1) void gemm_ws_kernel(
+__global__ __launch_bounds__(CFG::THREADS + 64 * CFG::LOADERS, 1) void gemm_ws_kernel(
     const _Float16* __restrict__ A, const _Float16* __restrict__ Al,
     const _Float16* __restrict__ W, const _Float16* __restrict__ Wl,
     const float* __restrict__ bias, int M, int N, int K, void* __restrict__ Cout,
     _Float16* __restrict__ Clo, DlArgs dl) {
-  static_assert(EPI != kEpiAddLn && CFG::PRELOAD, "plain epilogues, large tiles");
+  static_assert(EPI != kEpiAddLn && (CFG::PRELOAD || CFG::LOADERS < 4),
+                "plain epilogues; large tiles, or the small-tile single-loader instance");
   constexpr bool DL = EPI == kEpiLnF16 || EPI == kEpiLnGeluF16 || EPI == kEpiResLn;
   static_assert(!DL || SPLIT, "deferred LayerNorm: fp16x3 only");
   constexpr int BM = CFG::BM, BN = CFG::BN, NS = CFG::NS, TH = CFG::THREADS;
-  constexpr int LTH = 256;                         // loader threads (4 waves)
+  constexpr int LTH = 64 * CFG::LOADERS;            // loader threads (4 waves; 1 for small)
   constexpr int FM = CFG::FM, FN = CFG::FN, WTM = 16 * FM, WTN = 16 * FN;
   constexpr int BK = CFG::BK ? CFG::BK : kBK<SPLIT>, CPR = BK / 8, KSN = BK / 32;
   constexpr int NPL = SPLIT ? 2 : 1;

@@ -62,7 +62,8 @@ def _check(c, ref, epi, split):
 @pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "x".join(map(str, s)))
 @pytest.mark.parametrize("epi", [0, 1, 2], ids=["f16", "gelu", "f32"])
 @pytest.mark.parametrize("split", [False, True], ids=["fp16", "fp16x3"])
-@pytest.mark.parametrize("variant", [1, 2, 5, 8, 10], ids=["tile", "pipe", "small", "wide", "small64"])
+@pytest.mark.parametrize("variant", [1, 2, 5, 8, 10, 34],
+                         ids=["tile", "pipe", "small", "wide", "small64", "ws_small"])
 def test_gemm_matches_fp64(gpu, shape, epi, split, variant):
     from ragmi.encoders import linear
     M, N, K = shape
