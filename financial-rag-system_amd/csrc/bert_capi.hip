@@ -23,6 +23,7 @@ constexpr double kF16Safe = 60000.0;
 // split-K of the small-batch fp32-output GEMMs (small_ksplit): most parts, and the workspace
 // rows up to which y keeps room for them
 constexpr int kMaxKSplit = 4;
+static_assert(kMaxKSplit <= 4, "add_ln384_kernel sums at most 4 split-K parts");
 constexpr int64_t kSplitMaxRows = 8192;
 
 struct Layer {

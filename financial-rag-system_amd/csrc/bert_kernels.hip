@@ -1007,6 +1007,7 @@ __global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
   // tiles per workgroup, where that serial latency was a visible part of the launch.
   constexpr int NBV = kPipeBiasMax / (TH * 4) > 0 ? kPipeBiasMax / (TH * 4) : 1;
   constexpr int NLN = EPI == kEpiAddLn ? (BN + TH * 4 - 1) / (TH * 4) : 0;
+  static_assert(NBV * TH * 4 >= kPipeBiasMax, "every staged bias float has a register slot");
   floatx4 bv[NBV], gv[NLN > 0 ? NLN : 1], ev[NLN > 0 ? NLN : 1];
 #pragma unroll
   for (int u = 0; u < NBV; ++u) {
