@@ -350,7 +350,7 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
     RAG_SELECT(false);
 #undef RAG_SELECT
   // tier 2 of the certificate, when select marked a query (returns at once otherwise): R
-  // workgroups split the shard's tiles, ~256 tiles each, at most kRescanMaxWG (two per CU)
+  // workgroups split the shard's tiles, ~1024 tiles each, at most kRescanMaxWG (two per CU)
   // RAGMI_RESCAN_WG (diagnostic A/B): workgroup cap of the rescan launch; 0 = not launched
   // (tier-2 queries are then left unanswered: timing only)
   static const int rescan_cap = [] {
@@ -359,7 +359,12 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
   }();
   if (rescan_cap > 0) {
     const int n_tiles = (int)((h->count + 15) / 16);
-    const int R = std::max(1, std::min(std::min(rescan_cap, ragmi::kRescanMaxWG), n_tiles / 256));
+    // ~1024 tiles per workgroup, at most kRescanMaxWG: the idle launch's cost follows its
+    // grid (1.25M rows, 4 in flight: 196-199K qps at 305 workgroups = tiles / 256, 203.5K at
+    // 76 = tiles / 1024, profiles/r03zz_rescan_wg.jsonl), and this keeps a tier-2 pass near
+    // the same ~10 ms at every shard size instead of scaling it down with small shards
+    // (10M rows is at the 512 cap either way)
+    const int R = std::max(1, std::min(std::min(rescan_cap, ragmi::kRescanMaxWG), n_tiles / 1024));
 #define RAG_RESCAN(F)                                                                            rescan_kernel<D, F><<<dim3(R), dim3(256), 0, st>>>(                                                w.fb_tier, w.t2, Bq, h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, w.qn, k, w.eps,       w.t2_s, w.t2_i, w.t2_tk, id_offset, out_s, out_i, out_packed, h->rows32)
     if (filt)
       RAG_RESCAN(true);
