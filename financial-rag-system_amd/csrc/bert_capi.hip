@@ -396,6 +396,16 @@ void gemm_add_ln(const _Float16* A, const _Float16* Al, const _Float16* W, const
                                            cu_count(), ln);
 }
 
+// RAGMI_CE_ROWS (A/B): CLS rows per workgroup of the cross-encoder head, 2, 4, 8 (ce_head_rows_kernel),
+// or 1 (default) = ce_head_kernel (one row per workgroup, whole W_p rows per thread)
+int ce_head_rows() {
+  static const int v = [] {
+    const char* s = std::getenv("RAGMI_CE_ROWS");
+    return s ? std::atoi(s) : 1;
+  }();
+  return v;
+}
+
 // RAGMI_ATTN_VAR (A/B): the forward's attention variant, 0 = kAttnVar (default) or 10
 int attn_var_override() {
   static const int v = [] {
@@ -850,6 +860,15 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
   // the final hidden states of the CLS tokens are rows 0 .. B-1 of w->xc (cu = null)
   if (c.head == RAG_HEAD_CLS_L2)
     cls_normalize_kernel<H><<<dim3(B), dim3(64), 0, st>>>(w->xc, nullptr, out);
+  else if (H % 128 == 0 && ce_head_rows() == 2)   // R CLS rows per workgroup
+    ce_head_rows_kernel<H, 2><<<dim3((B + 1) / 2), dim3(256), 0, st>>>(
+        w->xc, B, e->wp, e->bp, e->wc, e->bc, out);
+  else if (H % 128 == 0 && ce_head_rows() == 4)
+    ce_head_rows_kernel<H, 4><<<dim3((B + 3) / 4), dim3(256), 0, st>>>(
+        w->xc, B, e->wp, e->bp, e->wc, e->bc, out);
+  else if (H % 128 == 0 && ce_head_rows() == 8)
+    ce_head_rows_kernel<H, 8><<<dim3((B + 7) / 8), dim3(256), 0, st>>>(
+        w->xc, B, e->wp, e->bp, e->wc, e->bc, out);
   else
     ce_head_kernel<H><<<dim3(B), dim3(256), 0, st>>>(w->xc, nullptr, e->wp, e->bp, e->wc, e->bc,
                                                      out);

@@ -2411,5 +2411,58 @@ __global__ __launch_bounds__(256) void ce_head_kernel(const float* __restrict__ 
   if (tid == 0) out[b] = part[0] + part[1] + part[2] + part[3] + bc[0];
 }
 
+// The same head with the pooler dot products spread over the lanes (round 3). ce_head_kernel
+// gives every thread whole W_p rows: each float4 load of a wave touches 64 different rows, and
+// the 384-long FMA chain is serial (36 us for a 480-pair batch, latency-bound). Here a wave
+// reads one W_p row coalesced (lane l holds columns 2l, 2l+1 of each 128-column slice), dots it
+// with the R CLS rows held in registers and reduces over the wave (wave_sum64), so a row is one
+// coalesced 1.5 KB read shared by R pairs. Wave w takes outputs w, w+4, ... The summation order
+// differs from ce_head_kernel's (within the 1e-3 head contract) but is the same for every slot r,
+// so a pair scores identically alone and inside a batch.
+template <int H, int R>
+__global__ __launch_bounds__(256) void ce_head_rows_kernel(const float* __restrict__ x, int B,
+                                                           const float* __restrict__ wp,
+                                                           const float* __restrict__ bp,
+                                                           const float* __restrict__ wc,
+                                                           const float* __restrict__ bc,
+                                                           float* __restrict__ out) {
+  static_assert(H % 128 == 0, "lanes own column pairs of 128-column slices");
+  constexpr int NS = H / 128;
+  __shared__ float part[R][4];
+  const int b0 = blockIdx.x * R, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nr = min(R, B - b0);
+  float2 cl[R][NS];
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int k = 0; k < NS; ++k)
+      cl[r][k] = r < nr ? *reinterpret_cast<const float2*>(x + (int64_t)(b0 + r) * H + k * 128 +
+                                                            2 * lane)
+                        : make_float2(0.f, 0.f);
+  float acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] = 0.f;
+#pragma unroll 4
+  for (int o = wid; o < H; o += 4) {
+    float2 w2[NS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k)
+      w2[k] = *reinterpret_cast<const float2*>(wp + (int64_t)o * H + k * 128 + 2 * lane);
+    const float b = bp[o], w = wc[o];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      float d = 0.f;
+#pragma unroll
+      for (int k = 0; k < NS; ++k) d = fmaf(w2[k].y, cl[r][k].y, fmaf(w2[k].x, cl[r][k].x, d));
+      acc[r] = fmaf(tanhf(wave_sum64(d) + b), w, acc[r]);
+    }
+  }
+  if (lane == 0)
+#pragma unroll
+    for (int r = 0; r < R; ++r) part[r][wid] = acc[r];
+  __syncthreads();
+  if (tid < nr) out[b0 + tid] = part[tid][0] + part[tid][1] + part[tid][2] + part[tid][3] + bc[0];
+}
+
 }  // namespace bert
 }  // namespace ragmi
