@@ -317,6 +317,9 @@ def main():
                          "GPUs); 2 / 3: encode + search (+ rerank) pipeline over 1M x 384; "
                          "5: 50M x 1024 at batch 128; filtered: 10M x 384 with per-query "
                          "ticker filters (scripts/bench_modes.py)")
+    ap.add_argument("--diagnostic", action="store_true",
+                    help="create the index with RAG_CREATE_DIAGNOSTIC, so the RAGMI_* kernel "
+                         "A/B knobs are honoured (never for a reported line)")
     ap.add_argument("--precision", choices=["fp16x3", "fp16"], default="fp16x3",
                     help="encoder precision for --config 2/3 (fp16x3 = the 1e-3 contract)")
     args = ap.parse_args()
@@ -364,7 +367,8 @@ def main():
     from ragmi.index import busy_union_ms
 
     n_total = args.rows
-    sh = ShardedIndex(n_total, dim=D, device=dev, storage=args.storage, force_exchange=rehearsal)
+    sh = ShardedIndex(n_total, dim=D, device=dev, storage=args.storage, force_exchange=rehearsal,
+                      diagnostic=args.diagnostic)
     idx, lo, hi = sh.local, sh.lo, sh.hi
     build_shard(idx, lo, hi, n_total, dev)
     nb = args.warmup + args.steps

@@ -17,6 +17,7 @@
 namespace {
 
 using namespace ragmi::bert;
+using ragmi::launch_fixed;
 
 // largest static fp16 range bound accepted (fp16 max 65504; see range_bounds)
 constexpr double kF16Safe = 60000.0;
@@ -96,6 +97,9 @@ struct EncWorkspace {
   int64_t g_in_cap = 0;     // int32 elements
   float* g_out = nullptr;
   int64_t g_out_cap = 0;    // floats
+  // private capture stream: capturing on the caller's stream in relaxed mode would
+  // record any other thread's launches on that stream into the graph
+  hipStream_t cstream = nullptr;
 
   void drop_graphs() {   // (a replay may still run on the workspace's stream: wait for it)
     if (!graphs.empty() && stream) (void)hipStreamSynchronize(stream);
@@ -111,6 +115,7 @@ struct EncWorkspace {
                     (void*)xcl, (void*)cc, (void*)ccl, (void*)ffc, (void*)ffcl, (void*)sa,
                     (void*)sb, (void*)g_in, (void*)g_out})
       if (p) (void)hipFree(p);
+    if (cstream) (void)hipStreamDestroy(cstream);
     *this = EncWorkspace{};
   }
 };
@@ -293,15 +298,14 @@ int cu_count() {
   return n;
 }
 
+// RAGMI_* knobs below: diagnostic A/B only, honoured under RAG_CREATE_DIAGNOSTIC (ragmi::Knob)
 int gemm_variant_default() {
-  static int v = [] {
-    const char* s = std::getenv("RAGMI_GEMM");
-    if (s && std::strcmp(s, "tile") == 0) return (int)RAG_GEMM_TILE;
-    if (s && std::strcmp(s, "pipe") == 0) return (int)RAG_GEMM_PIPE;
-    if (s && std::strcmp(s, "small") == 0) return (int)RAG_GEMM_SMALL;
-    return (int)RAG_GEMM_AUTO;
-  }();
-  return v;
+  static ragmi::Knob k("RAGMI_GEMM");
+  const char* s = k.str();
+  if (s && std::strcmp(s, "tile") == 0) return (int)RAG_GEMM_TILE;
+  if (s && std::strcmp(s, "pipe") == 0) return (int)RAG_GEMM_PIPE;
+  if (s && std::strcmp(s, "small") == 0) return (int)RAG_GEMM_SMALL;
+  return (int)RAG_GEMM_AUTO;
 }
 
 // the DMA kernels address each operand and the output through 32-bit buffer extents
@@ -316,8 +320,8 @@ void launch_pipe(const _Float16* A, const _Float16* Al, const _Float16* W, const
                  int max_wg, const LnArgs& ln = LnArgs{}, int ksplit = 1) {
   const int tiles = (N / CFG::BN) * ((M + CFG::BM - 1) / CFG::BM) * ksplit;
   const dim3 grid((unsigned)std::min(max_wg, (tiles + 7) / 8 * 8));   // multiple of 8
-  gemm_pipe_kernel<EPI, SPLIT, CFG, PROBE><<<grid, dim3(CFG::THREADS), 0, st>>>(
-      A, Al, W, Wl, bias, M, N, K, C, Clo, ln, ksplit);
+  launch_fixed<kPipeBlock<CFG>>(gemm_pipe_kernel<EPI, SPLIT, CFG, PROBE>, grid, 0, st, A, Al, W,
+                                Wl, bias, M, N, K, C, Clo, ln, ksplit);
 }
 
 // split-K of the small-batch fp32-output GEMMs (O-proj, FFN2 of query batches: 64x64 tiles,
@@ -325,10 +329,8 @@ void launch_pipe(const _Float16* A, const _Float16* Al, const _Float16* W, const
 // never depends on what else is in its batch (tests/test_encoders_gpu.py batch independence).
 // The parts are summed in order by add_ln_kernel. 0 = no split for this shape.
 int small_ksplit(int K, int BK) {
-  static const int force = [] {
-    const char* v = std::getenv("RAGMI_KSPLIT");            // diagnostic: 1 = off, n = force
-    return v ? std::atoi(v) : 0;
-  }();
+  static ragmi::Knob k("RAGMI_KSPLIT");                     // diagnostic: 1 = off, n = force
+  const int force = k.get(0);
   const int nk = K / BK;
   int s = force > 0 ? force : K >= 1536 ? 3 : K >= 384 ? 2 : 1;
   s = std::min(s, kMaxKSplit);
@@ -345,14 +347,12 @@ void launch_ws(const _Float16* A, const _Float16* Al, const _Float16* W, const _
   const int per_cu = CFG::LOADERS < 4 ? 2 : 1;
   const dim3 grid((unsigned)std::min(per_cu * cu_count(), (tiles + 7) / 8 * 8));
   // RAGMI_WS_PHASE (A/B): start delay of the odd workgroups in units of ~3.4 us (DlArgs.phase)
-  static const int phase = [] {
-    const char* v = std::getenv("RAGMI_WS_PHASE");
-    return v ? std::max(0, std::atoi(v)) : 0;
-  }();
+  static ragmi::Knob k("RAGMI_WS_PHASE");
+  const int phase = std::max(0, k.get(0));
   DlArgs d = dl;
   if (d.phase == 0) d.phase = phase;
-  gemm_ws_kernel<EPI, SPLIT, CFG, PROBE, AUX><<<grid, dim3(CFG::THREADS + 64 * CFG::LOADERS), 0, st>>>(
-      A, Al, W, Wl, bias, M, N, K, C, Clo, d);
+  launch_fixed<kWsBlock<CFG>>(gemm_ws_kernel<EPI, SPLIT, CFG, PROBE, AUX>, grid, 0, st, A, Al, W,
+                              Wl, bias, M, N, K, C, Clo, d);
 }
 
 // shapes the deferred-LayerNorm WS GEMMs take: Ln* (K = 384 input rows; c1 | c2 staged in the
@@ -365,11 +365,8 @@ bool dl_gemm_ok(int epi, int M, int N, int K) {
 
 // deferred-LayerNorm mode of the forward: -1 auto, 0 off, 1 on (where the shapes allow)
 int defer_ln_default() {
-  static int v = [] {
-    const char* s = std::getenv("RAGMI_DEFER_LN");
-    return s ? std::atoi(s) : -1;
-  }();
-  return v;
+  static ragmi::Knob k("RAGMI_DEFER_LN");
+  return k.get(-1);
 }
 
 // the fused output projection + residual + LayerNorm (kEpiAddLn on PipeRow tiles)
@@ -399,29 +396,20 @@ void gemm_add_ln(const _Float16* A, const _Float16* Al, const _Float16* W, const
 // RAGMI_CE_ROWS (A/B): CLS rows per workgroup of the cross-encoder head, 2, 4, 8 (ce_head_rows_kernel),
 // or 1 (default) = ce_head_kernel (one row per workgroup, whole W_p rows per thread)
 int ce_head_rows() {
-  static const int v = [] {
-    const char* s = std::getenv("RAGMI_CE_ROWS");
-    return s ? std::atoi(s) : 1;
-  }();
-  return v;
+  static ragmi::Knob k("RAGMI_CE_ROWS");
+  return k.get(1);
 }
 
 // RAGMI_ATTN_VAR (A/B): the forward's attention variant, 0 = kAttnVar (default) or 10
 int attn_var_override() {
-  static const int v = [] {
-    const char* s = std::getenv("RAGMI_ATTN_VAR");
-    return s ? std::atoi(s) : 0;
-  }();
-  return v;
+  static ragmi::Knob k("RAGMI_ATTN_VAR");
+  return k.get(0);
 }
 
 // fusion mode of the forward: -1 auto (once the 128-row bands cover the CUs), 0 off, 1 on
 int fuse_ln_default() {
-  static int v = [] {
-    const char* s = std::getenv("RAGMI_FUSE_LN");
-    return s ? std::atoi(s) : -1;
-  }();
-  return v;
+  static ragmi::Knob k("RAGMI_FUSE_LN");
+  return k.get(-1);
 }
 
 int ensure_cls(const rag_bert_config& cfg, EncWorkspace* w, int64_t B) {
@@ -480,14 +468,9 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
   // batches' kernels off its CUs (profiles/r03b_small_gemm.jsonl); RAGMI_SMALL_BK=64 restores
   // SMALL_BK64. RAGMI_SMALL_WIDE=1 runs N >= 1024 GEMMs whose 64 x 64 tiles exceed the CUs on
   // 64 x 128 tiles (0.620 ms alone, 0.628 with BK 32: not kept)
-  static const int small_bk = [] {
-    const char* v = std::getenv("RAGMI_SMALL_BK");
-    return v ? std::atoi(v) : 32;
-  }();
-  static const bool small_wide = [] {
-    const char* v = std::getenv("RAGMI_SMALL_WIDE");
-    return v && std::atoi(v) == 1;
-  }();
+  static ragmi::Knob k_bk("RAGMI_SMALL_BK"), k_wide("RAGMI_SMALL_WIDE");
+  const int small_bk = k_bk.get(32);
+  const bool small_wide = k_wide.get(0) == 1;
   if (auto_pick && variant == RAG_GEMM_SMALL && Al && small_wide && N % 128 == 0 && N >= 1024 &&
       small_tiles > cu_count()) {
     launch_pipe<EPI, true, PipeSmallWide64>(A, Al, W, Wl, bias, M, N, K, C, Clo, st, cu_count());
@@ -499,10 +482,8 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
   // (profiles/r03zz_small_ws.jsonl, 782 tokens: QKV 9.8 vs 9.7 us, FFN1 14.3 vs 10.3,
   // encode_q 0.726 vs 0.686 ms): moving the DMA issue off the MFMA waves does not help a
   // GEMM of one or two tiles per workgroup
-  static const bool small_ws = [] {
-    const char* v = std::getenv("RAGMI_SMALL_WS");
-    return v && std::atoi(v) == 1;
-  }();
+  static ragmi::Knob k_ws("RAGMI_SMALL_WS");
+  const bool small_ws = k_ws.get(0) == 1;
   if (pipe_ok(M, N, K) &&
       (variant == RAG_GEMM_WS_SMALL ||
        (auto_pick && variant == RAG_GEMM_SMALL && Al && small_ws && EPI != kEpiF32))) {
@@ -550,7 +531,8 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
       variant == RAG_GEMM_WS_NOROT || variant == RAG_GEMM_WS_READS_FIRST ||
       variant == RAG_GEMM_WS_PROBE_NO_A_READS || variant == RAG_GEMM_WS_PROBE_NO_W_READS ||
       variant == RAG_GEMM_WS_PRIO_LOAD || variant == RAG_GEMM_WS_PRIO_MFMA ||
-      variant == RAG_GEMM_WS_FLAGS || variant == RAG_GEMM_WS_NOHALF) {
+      variant == RAG_GEMM_WS_FLAGS || variant == RAG_GEMM_WS_NOHALF ||
+      variant == RAG_GEMM_WS_BIG128) {
     // probes keep production's store policy (nt for fp16 outputs) since round 2's r02h runs
     auto go = [&](auto pc) {
       constexpr int P = decltype(pc)::value;
@@ -575,6 +557,11 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
     else if (variant == RAG_GEMM_WS_PRIO_LOAD) go(std::integral_constant<int, 16>{});
     else if (variant == RAG_GEMM_WS_PRIO_MFMA) go(std::integral_constant<int, 17>{});
     else if (variant == RAG_GEMM_WS_NOHALF) go(std::integral_constant<int, 19>{});
+    else if (variant == RAG_GEMM_WS_BIG128) {
+      constexpr int AX = EPI == kEpiF32 ? 0 : 2;
+      if (Al) launch_ws<EPI, true, PipeBig128, 0, AX>(A, Al, W, Wl, bias, M, N, K, C, Clo, st);
+      else launch_ws<EPI, false, PipeBig128, 0, AX>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st);
+    }
     else if (variant == RAG_GEMM_WS_FLAGS) {
       // the ring counters sit in the last 16 floats of the staged-vector area
       if (N <= kPipeBiasMax - 16) go(std::integral_constant<int, 18>{});
@@ -661,10 +648,8 @@ int forward_graph(rag_encoder* e, EncWorkspace* w, const int32_t* ids, const int
 constexpr int kGraphMaxT = 8192;
 constexpr int kGraphCache = 16;    // graphs per workspace (LRU)
 bool use_graphs(const rag_encoder* e, hipStream_t st, int T, bool null_ok = false) {
-  static const int env = [] {
-    const char* v = std::getenv("RAGMI_ENC_GRAPH");
-    return v ? std::atoi(v) : -1;
-  }();
+  static ragmi::Knob k("RAGMI_ENC_GRAPH");
+  const int env = k.get(-1);
   const int mode = e->graphs >= 0 ? e->graphs : env;
   if (mode == 0 || (st == nullptr && !null_ok)) return false;
   return mode > 0 || T <= kGraphMaxT;
@@ -672,10 +657,11 @@ bool use_graphs(const rag_encoder* e, hipStream_t st, int T, bool null_ok = fals
 
 template <int H, int HD>
 int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const int32_t* cu,
-              int B, int T, int max_len, float* out, hipStream_t st, bool capturing = false) {
+              int B, int T, int max_len, float* out, hipStream_t st, bool capturing = false,
+              EncWorkspace* w_in = nullptr) {
   const rag_bert_config& c = e->cfg;
   const int NH = H / HD, FF = c.intermediate;
-  EncWorkspace* w = workspace_for(e, st);
+  EncWorkspace* w = w_in ? w_in : workspace_for(e, st);
   if (!w) return ragmi::fail(RAG_EHIP, "device synchronize failed");
   if (!capturing && use_graphs(e, st, T))
     return forward_graph<H, HD>(e, w, ids, types, cu, B, T, max_len, out, st);
@@ -695,10 +681,8 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
   };
   // fp16x3 with the two-kernel projections: the token rows' residual stream is kept as the
   // operand planes xh + xl alone (add_ln_kernel<XF>), no fp32 copy
-  static const bool xf_on = [] {
-    const char* v = std::getenv("RAGMI_RESIDUAL_F32");      // diagnostic: keep the fp32 copy
-    return !(v && std::atoi(v) == 1);
-  }();
+  static ragmi::Knob k_f32("RAGMI_RESIDUAL_F32");           // diagnostic: keep the fp32 copy
+  const bool xf_on = k_f32.get(0) != 1;
   // deferred LayerNorm (DlArgs): auto once every token-row GEMM is a WS one (AUTO's choice:
   // the 384-wide projections' 256 x 128 tiles reach half the CUs, ~11K tokens)
   const bool dl = [&] {
@@ -743,16 +727,16 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
     const int max_qb = last ? 1 : 1 << 20;
     if (attn_var_override() == 10) {   // RAGMI_ATTN_VAR=10: the round-2 variant (A/B)
       if (w->xl)
-        attn_kernel<H, HD, true, 10><<<agrid, dim3(kAttnThreads<true>), alds, st>>>(
+        launch_fixed<kAttnThreads<true>>(attn_kernel<H, HD, true, 10>, agrid, alds, st,
             w->qkv, w->qkv_l, cu, max_len, kc, scale, w->ctx, w->ctx_l, max_qb);
       else
-        attn_kernel<H, HD, false, 10><<<agrid, dim3(kAttnThreads<false>), alds, st>>>(
+        launch_fixed<kAttnThreads<false>>(attn_kernel<H, HD, false, 10>, agrid, alds, st,
             w->qkv, nullptr, cu, max_len, kc, scale, w->ctx, nullptr, max_qb);
     } else if (w->xl)
-      attn_kernel<H, HD, true><<<agrid, dim3(kAttnThreads<true>), alds, st>>>(
+      launch_fixed<kAttnThreads<true>>(attn_kernel<H, HD, true>, agrid, alds, st,
           w->qkv, w->qkv_l, cu, max_len, kc, scale, w->ctx, w->ctx_l, max_qb);
     else
-      attn_kernel<H, HD, false><<<agrid, dim3(kAttnThreads<false>), alds, st>>>(
+      launch_fixed<kAttnThreads<false>>(attn_kernel<H, HD, false>, agrid, alds, st,
           w->qkv, nullptr, cu, max_len, kc, scale, w->ctx, nullptr, max_qb);
     if (dl && !last) {
       // z1 = LN2_{l-1}(z) + O-proj (stats -> sa); FFN1 with LN1 folded; z2 = LN1(z1) + FFN2
@@ -815,10 +799,8 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
       const int64_t ps = (int64_t)R * H;
       if constexpr (H == 384) {
         // 16-B accesses and DPP / permlane reductions (round 3; RAGMI_ADDLN_VEC=0: A/B)
-        static const bool vec = [] {
-          const char* v = std::getenv("RAGMI_ADDLN_VEC");
-          return !(v && std::atoi(v) == 0);
-        }();
+        static ragmi::Knob k_vec("RAGMI_ADDLN_VEC");
+        const bool vec = k_vec.get(1) != 0;
         if (vec) {
           if (row_xf)
             add_ln384_kernel<true><<<dim3(lg), dim3(256), 0, st>>>(nullptr, y, gam, bet,
@@ -895,7 +877,11 @@ __global__ void graph_stage_kernel(const int32_t* __restrict__ ids,
 // for the padded shape (T up to a multiple of 64, max_len up to a multiple of 32 — the
 // attention's key chunking depends on max_len only through that rounding, attn_chunk_keys),
 // copy the B output rows out. The graph is captured on first use of its shape from the same
-// eager code path (forward_t), so it launches the same kernels with the same arguments.
+// eager code path (forward_t), so it launches the same kernels with the same arguments. The
+// capture runs on the workspace's private capture stream (nothing executes during a capture;
+// the caller's stream stays free for other threads, whose launches would otherwise be
+// recorded into the graph), and a shape whose capture or instantiation fails runs eagerly on
+// the caller's stream instead of failing the call.
 template <int H, int HD>
 int forward_graph(rag_encoder* e, EncWorkspace* w, const int32_t* ids, const int32_t* types,
                   const int32_t* cu, int B, int T, int max_len, float* out, hipStream_t st) {
@@ -938,19 +924,25 @@ int forward_graph(rag_encoder* e, EncWorkspace* w, const int32_t* ids, const int
       (void)hipGraphExecDestroy(lru->exec);
       w->graphs.erase(lru);
     }
+    if (!w->cstream) RAG_HIP(hipStreamCreateWithFlags(&w->cstream, hipStreamNonBlocking));
     hipGraph_t graph = nullptr;
-    RAG_HIP(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
-    rc = forward_t<H, HD>(e, g, g + Tp, g + 2 * Tp, B, Tp, Lp, w->g_out, st, true);
-    const hipError_t ec = hipStreamEndCapture(st, &graph);
-    if (rc) {
-      if (graph) (void)hipGraphDestroy(graph);
-      return rc;
-    }
-    if (ec != hipSuccess) return ragmi::fail(RAG_EHIP, "graph capture failed");
     hipGraphExec_t exec = nullptr;
-    const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
-    (void)hipGraphDestroy(graph);
-    if (ei != hipSuccess) return ragmi::fail(RAG_EHIP, "graph instantiate failed");
+    bool ok = hipStreamBeginCapture(w->cstream, hipStreamCaptureModeRelaxed) == hipSuccess;
+    if (ok) {
+      // (recorded on the private stream, but into THIS workspace's buffers)
+      rc = forward_t<H, HD>(e, g, g + Tp, g + 2 * Tp, B, Tp, Lp, w->g_out, w->cstream, true, w);
+      ok = hipStreamEndCapture(w->cstream, &graph) == hipSuccess && rc == RAG_OK && graph;
+      ok = ok && hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0) == hipSuccess;
+      if (graph) (void)hipGraphDestroy(graph);
+    }
+    if (!ok) {
+      // a failed capture can leave its stream unusable: drop it (a new one next time)
+      (void)hipGetLastError();
+      (void)hipStreamDestroy(w->cstream);
+      w->cstream = nullptr;
+      ragmi::clear_error();
+      return forward_t<H, HD>(e, ids, types, cu, B, T, max_len, out, st, true, w);
+    }
     w->graphs.push_back(EncWorkspace::Graph{B, Tp, Lp, exec, 0});
     hit = &w->graphs.back();
   }
@@ -1059,6 +1051,14 @@ extern "C" {
 int rag_encoder_num_weights(const rag_bert_config* cfg) {
   if (!cfg) return -1;
   return 5 + 16 * cfg->layers + (cfg->head == RAG_HEAD_POOLER_CLS ? 4 : 0);
+}
+
+int rag_encoder_create_ex(const rag_bert_config* cfg, const float* const* w, int n_weights,
+                          int device, int flags, rag_encoder_t** out) {
+  ragmi::clear_error();
+  if (flags & ~RAG_CREATE_DIAGNOSTIC) return ragmi::fail(RAG_EINVAL, "unknown encoder flags");
+  if (flags & RAG_CREATE_DIAGNOSTIC) ragmi::diagnostics_on().store(true);
+  return rag_encoder_create(cfg, w, n_weights, device, out);
 }
 
 int rag_encoder_create(const rag_bert_config* cfg, const float* const* w, int n_weights,
@@ -1326,12 +1326,12 @@ int rag_bert_attention(int variant, const void* qkv, const void* qkv_lo, const i
     if (qkv_lo) {
       RAG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_kernel<H, HD, true, V>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, kAttnLdsMax));
-      attn_kernel<H, HD, true, V><<<agrid, dim3(kAttnThreads<true>), alds, st>>>(
+      launch_fixed<kAttnThreads<true>>(attn_kernel<H, HD, true, V>, agrid, alds, st,
           q, ql, cu, max_len, kc, scale, c, cl, 1 << 20);
     } else {
       RAG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_kernel<H, HD, false, V>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, kAttnLdsMax));
-      attn_kernel<H, HD, false, V><<<agrid, dim3(kAttnThreads<false>), alds, st>>>(
+      launch_fixed<kAttnThreads<false>>(attn_kernel<H, HD, false, V>, agrid, alds, st,
           q, nullptr, cu, max_len, kc, scale, c, nullptr, 1 << 20);
     }
     RAG_HIP(hipGetLastError());

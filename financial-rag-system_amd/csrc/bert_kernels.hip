@@ -943,8 +943,11 @@ struct LnArgs {
 // them; 5 = the same stores with S still counting the 8-B stores (more than are issued: the
 // post-epilogue vmcnt wait then passes before the next ring stage has landed).
 // (s_setprio around the MFMA clusters / for the younger waves measured +1-2%: not kept.)
+// block size of a gemm_pipe_kernel instance (launch_fixed; its __launch_bounds__)
+template <typename CFG> constexpr int kPipeBlock = CFG::THREADS;
+
 template <int EPI, bool SPLIT, typename CFG, int PROBE = 0>
-__global__ __launch_bounds__(CFG::THREADS, 1) void gemm_pipe_kernel(
+__global__ __launch_bounds__(kPipeBlock<CFG>, 1) void gemm_pipe_kernel(
     const _Float16* __restrict__ A, const _Float16* __restrict__ Al,
     const _Float16* __restrict__ W, const _Float16* __restrict__ Wl,
     const float* __restrict__ bias, int M, int N, int K, void* __restrict__ Cout,
@@ -1365,8 +1368,12 @@ __device__ __forceinline__ void lds_spin_ge(uint32_t* p, uint32_t target) {
   }
 }
 
+// block size of a gemm_ws_kernel instance: the MFMA waves plus one wave per loader
+// (launch_fixed; its __launch_bounds__)
+template <typename CFG> constexpr int kWsBlock = CFG::THREADS + 64 * CFG::LOADERS;
+
 template <int EPI, bool SPLIT, typename CFG, int PROBE = 0, int AUX = 0>
-__global__ __launch_bounds__(CFG::THREADS + 64 * CFG::LOADERS, 1) void gemm_ws_kernel(
+__global__ __launch_bounds__(kWsBlock<CFG>, 1) void gemm_ws_kernel(
     const _Float16* __restrict__ A, const _Float16* __restrict__ Al,
     const _Float16* __restrict__ W, const _Float16* __restrict__ Wl,
     const float* __restrict__ bias, int M, int N, int K, void* __restrict__ Cout,

@@ -10,6 +10,19 @@
 
 namespace ragmi {
 
+// Launch geometry. Every kernel whose LDS layout or wave roles assume a
+// block size (the LDS-ring GEMMs and scans, attention, the tier-2 rescan) takes that size from
+// ONE constexpr, which its __launch_bounds__ uses and which launch_fixed passes as the block:
+// no launch site spells a block size, so a launcher cannot size the block for a different
+// instance (round 3's RAG_GEMM_WS_SMALL fault: four loader waves launched for a one-loader
+// ring wrote past it).
+template <int BLOCK, typename... KArgs, typename... Args>
+inline void launch_fixed(void (*k)(KArgs...), dim3 grid, size_t lds, hipStream_t st,
+                         Args&&... args) {
+  static_assert(BLOCK > 0 && BLOCK % 64 == 0 && BLOCK <= 1024, "whole waves, <= 1024 threads");
+  k<<<grid, dim3(BLOCK), lds, st>>>(static_cast<Args&&>(args)...);
+}
+
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 

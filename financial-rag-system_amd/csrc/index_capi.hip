@@ -44,10 +44,10 @@ struct Workspace {
   int* progress = nullptr;      // [lists][groups] shared-group scan throttle words
   float* eps = nullptr;         // [groups][32] per-query |MFMA - exact| score bound (qprep)
   int* fb_tier = nullptr;       // [groups][32] certifying path per query of the last pass
-  unsigned long long* fb_cnt = nullptr;   // [2] tier-1 / tier-2 totals since creation
+  unsigned long long* fb_cnt = nullptr;   // [3] tier-1 / tier-2 / unanswered totals since creation
   int* tileq = nullptr;         // [8][kTileQStride] per-XCD tile-queue heads (dynamic scan)
   // tier-2 hand-off select -> rescan_kernel: (L, e_k) per query, the rescan workgroups' lists
-  // [query][kRescanMaxWG][32] and per-query arrival tickets (zero between passes)
+  // [query][kRescanMaxWG][32] and the launch's arrival ticket (zero between passes)
   float* t2 = nullptr;
   float* t2_s = nullptr;
   int* t2_i = nullptr;
@@ -77,6 +77,7 @@ struct rag_index {
   // rescoring reads — Qdrant's default Float32 datatype
   int storage = RAG_STORE_FP16;
   float* rows32 = nullptr;
+  int n_cu = 256;
   int max_wgs = 0;        // scan workgroups at full occupancy
   int scan_wgs = 0;       // D <= 384 scan grid cap: 3/4 of the CUs (launch_search_pass)
   int groups = 1;         // query groups of 32 per search pass
@@ -150,13 +151,28 @@ double store_eps(const rag_index* h) {
 // sample + thresh: seed thresholds for the scan (see sample_kernel). ~0.8% of the shard's
 // tiles, spread evenly, at least 256 tiles (all of them for small shards).
 // D <= 384 (one query group): qprep fused into the sample launch (qprep_sample_kernel);
-// RAGMI_FUSED_PREP=0 (diagnostic A/B) keeps the separate qprep launch
+// RAGMI_FUSED_PREP=0 (diagnostic A/B, ragmi::Knob) keeps the separate qprep launch
 bool fused_prep() {
-  static const bool on = [] {
-    const char* v = std::getenv("RAGMI_FUSED_PREP");
-    return !(v && std::atoi(v) == 0);
-  }();
-  return on;
+  static ragmi::Knob k("RAGMI_FUSED_PREP");
+  return k.get(1) != 0;
+}
+
+// Workgroups of the tier-2 rescan launch: ~128 tiles each, at most kRescanMaxWG (two per CU
+// on MI355X): a marked pass streams the shard at the chip's rate, and the idle launch (every
+// pass) is one round trip per workgroup. RAGMI_RESCAN_WG (diagnostic A/B) caps it; 0 = skip.
+int rescan_grid(const rag_index* h) {
+  static ragmi::Knob k("RAGMI_RESCAN_WG");
+  const int cap = k.get(ragmi::kRescanMaxWG);
+  if (cap <= 0) return 0;
+  const int64_t n_tiles = (h->count + 15) / 16;
+  return (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)cap, (int64_t)ragmi::kRescanMaxWG,
+                                                      (int64_t)2 * h->n_cu, n_tiles / 128}));
+}
+
+// RAGMI_SAMPLE_DIV (diagnostic A/B): 1 / the sampled fraction of the shard's tiles
+int sample_div() {
+  static ragmi::Knob k("RAGMI_SAMPLE_DIV");
+  return std::max(1, k.get(128));
 }
 
 template <int D, bool FILTER>
@@ -166,10 +182,7 @@ void launch_seed(rag_index* h, Workspace& w, int groups, hipStream_t st,
   const int n_tiles = (int)((h->count + 15) / 16);
   if (q) {     // fused: qprep inside the sample launch (also when there is nothing to sample)
     if constexpr (D <= 384) {
-      static const int div_f = [] {
-        const char* v = std::getenv("RAGMI_SAMPLE_DIV");
-        return v ? std::max(1, std::atoi(v)) : 128;
-      }();
+      const int div_f = sample_div();
       const int n_sample = n_tiles == 0 ? 0 : std::min({n_tiles, std::max(256, n_tiles / div_f),
                                                         kMaxSample});
       qprep_sample_kernel<D, FILTER><<<dim3(std::max(1, (n_sample + 7) / 8)), dim3(256), 0, st>>>(
@@ -182,10 +195,7 @@ void launch_seed(rag_index* h, Workspace& w, int groups, hipStream_t st,
     return;
   }
   if (n_tiles == 0) return;   // the scan visits no tile; seeds are never read
-  static const int div = [] {
-    const char* v = std::getenv("RAGMI_SAMPLE_DIV");   // tuning knob: 1 / sampled fraction
-    return v ? std::max(1, std::atoi(v)) : 128;
-  }();
+  const int div = sample_div();
   // D = 1024 tiles are 32 KB and config 5 shards hold up to 3.1M of them: a 4096-tile cap
   // would sample 0.13% of a 50M-row shard and let ~25K rows per query past the seed
   constexpr int kCap = D > 384 ? kMaxSampleWide : kMaxSample;
@@ -244,11 +254,9 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
     // wave streams keep HBM as busy as twice as many, each wave's fixed start / end-of-scan
     // list work is paid by 768 waves instead of 2048 (select merges that many fewer lists), and
     // the free CUs take the other streams' query prep, sampling and select beside the scan
-    // instead of behind it. RAGMI_SCAN_WGS overrides the cap (A/B).
-    static const int wg_env = [] {
-      const char* v = std::getenv("RAGMI_SCAN_WGS");
-      return v ? std::max(8, std::atoi(v)) : 0;
-    }();
+    // instead of behind it. RAGMI_SCAN_WGS overrides the cap (diagnostic A/B).
+    static ragmi::Knob k_wgs("RAGMI_SCAN_WGS");
+    const int wg_env = k_wgs.get(0) > 0 ? std::max(8, k_wgs.get(0)) : 0;
     // Filtered scans (a tag load and compare per row) keep two workgroups per CU: 10M rows,
     // per-query ticker filter, serial order: 26.8 / 27.0K qps at 512 vs 25.7 / 26.1K at 192
     // (scan 1.170 vs 1.21-1.24 ms, profiles/r03u_filtered_wgs.jsonl)
@@ -285,41 +293,43 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
       w.heads_s, w.heads_i, w.heads_n
   const bool wide = kLdsQ && groups > 1 && !filt;
   if (wide) {
-    // RAGMI_WIDE_WGS (A/B): workgroup cap of the wide scan (default one per CU)
-    static const int wide_env = [] {
-      const char* v = std::getenv("RAGMI_WIDE_WGS");
-      return v ? std::max(8, std::atoi(v)) : 0;
-    }();
+    // RAGMI_WIDE_WGS (diagnostic A/B): workgroup cap of the wide scan (default one per CU)
+    static ragmi::Knob k_wide("RAGMI_WIDE_WGS");
+    const int wide_env = k_wide.get(0) > 0 ? std::max(8, k_wide.get(0)) : 0;
     const int cap = wide_env ? std::min(wide_env, h->max_wgs / 2) : h->max_wgs / 2;
     grid = (int)std::min<int64_t>(cap, std::max<int64_t>(1, n_tiles));
   }
   if constexpr (kLdsQ) {
-    const dim3 g3(grid * groups), b3(64 * kLdsWaves);
+    const dim3 g3(grid * groups);
     if (wide) {
       // all groups in every workgroup, one pass over the corpus (scan_wide_kernel)
       // ring loads non-temporal (the corpus is read once per pass): 50M x 1024, B = 128
       // 70.3% -> 71.2% of the HBM roofline, loads-only 80.1% -> 85.8%
       // (profiles/r01h_wide_nt.jsonl). The diagnostic variants run only via rag_bench_scan.
-      scan_wide_kernel<D, 0, true><<<dim3(grid), dim3(64 * kWideWaves), 0, st>>>(
-          h->corpus, w.qfrag, (int)h->count, (int)n_tiles, w.seed, w.part_s, w.part_i,
-          w.heads_s, w.heads_i, w.heads_n, groups);
+      launch_fixed<kWideBlock>(scan_wide_kernel<D, 0, true>, dim3(grid), 0, st, h->corpus, w.qfrag,
+                               (int)h->count, (int)n_tiles, w.seed, w.part_s, w.part_i,
+                               w.heads_s, w.heads_i, w.heads_n, groups);
     } else if (groups == 1) {
       if (filt)
-        scan_lds_kernel<D, true, true><<<g3, b3, 0, st>>>(RAG_SCAN_ARGS, groups, w.progress);
+        launch_fixed<kLdsBlock>(scan_lds_kernel<D, true, true>, g3, 0, st, RAG_SCAN_ARGS, groups,
+                                w.progress);
       else
-        scan_lds_kernel<D, false, true><<<g3, b3, 0, st>>>(RAG_SCAN_ARGS, groups, w.progress);
+        launch_fixed<kLdsBlock>(scan_lds_kernel<D, false, true>, g3, 0, st, RAG_SCAN_ARGS, groups,
+                                w.progress);
     } else {
       RAG_HIP(hipMemsetAsync(w.progress, 0, (size_t)grid * kLdsWaves * groups * 4, st));
       if (filt)
-        scan_lds_kernel<D, true, false><<<g3, b3, 0, st>>>(RAG_SCAN_ARGS, groups, w.progress);
+        launch_fixed<kLdsBlock>(scan_lds_kernel<D, true, false>, g3, 0, st, RAG_SCAN_ARGS, groups,
+                                w.progress);
       else
-        scan_lds_kernel<D, false, false><<<g3, b3, 0, st>>>(RAG_SCAN_ARGS, groups, w.progress);
+        launch_fixed<kLdsBlock>(scan_lds_kernel<D, false, false>, g3, 0, st, RAG_SCAN_ARGS, groups,
+                                w.progress);
     }
   } else {
     if (filt)
-      scan_kernel<D, true><<<dim3(grid), dim3(256), 0, st>>>(RAG_SCAN_ARGS);
+      launch_fixed<kScanBlock>(scan_kernel<D, true>, dim3(grid), 0, st, RAG_SCAN_ARGS, nullptr);
     else
-      scan_kernel<D, false><<<dim3(grid), dim3(256), 0, st>>>(RAG_SCAN_ARGS);
+      launch_fixed<kScanBlock>(scan_kernel<D, false>, dim3(grid), 0, st, RAG_SCAN_ARGS, nullptr);
   }
 #undef RAG_SCAN_ARGS
   if (timed) {
@@ -349,28 +359,23 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
   else
     RAG_SELECT(false);
 #undef RAG_SELECT
-  // tier 2 of the certificate, when select marked a query (returns at once otherwise): R
-  // workgroups split the shard's tiles, ~1024 tiles each, at most kRescanMaxWG (two per CU)
-  // RAGMI_RESCAN_WG (diagnostic A/B): workgroup cap of the rescan launch; 0 = not launched
-  // (tier-2 queries are then left unanswered: timing only)
-  static const int rescan_cap = [] {
-    const char* v = std::getenv("RAGMI_RESCAN_WG");
-    return v ? std::atoi(v) : ragmi::kRescanMaxWG;
-  }();
-  if (rescan_cap > 0) {
-    const int n_tiles = (int)((h->count + 15) / 16);
-    // ~1024 tiles per workgroup, at most kRescanMaxWG: the idle launch's cost follows its
-    // grid (1.25M rows, 4 in flight: 196-199K qps at 305 workgroups = tiles / 256, 203.5K at
-    // 76 = tiles / 1024, profiles/r03zz_rescan_wg.jsonl), and this keeps a tier-2 pass near
-    // the same ~10 ms at every shard size instead of scaling it down with small shards
-    // (10M rows is at the 512 cap either way)
-    const int R = std::max(1, std::min(std::min(rescan_cap, ragmi::kRescanMaxWG), n_tiles / 1024));
-#define RAG_RESCAN(F)                                                                            rescan_kernel<D, F><<<dim3(R), dim3(256), 0, st>>>(                                                w.fb_tier, w.t2, Bq, h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, w.qn, k, w.eps,       w.t2_s, w.t2_i, w.t2_tk, id_offset, out_s, out_i, out_packed, h->rows32)
+  // tier 2 of the certificate (rescan_kernel): returns at once unless select marked a query
+  // of the pass; otherwise its R workgroups stream the shard once per 16 marked queries.
+  // RAGMI_RESCAN_WG (diagnostic A/B) caps R; 0 skips the launch, and mark_unanswered_kernel
+  // then records the marked queries as unanswered (tier 3, rag_index_unanswered): timing only
+  const int R = rescan_grid(h);
+  if (R > 0) {
+#define RAG_RESCAN(F)                                                                   \
+  launch_fixed<kScanBlock>(rescan_kernel<D, F>, dim3(R), 0, st, w.fb_tier, w.t2, Bq, h->corpus,  \
+                           h->tags, w.filt, w.qfrag, (int)h->count, w.qn, k, w.eps, w.t2_s,  \
+                           w.t2_i, w.t2_tk, id_offset, out_s, out_i, out_packed, h->rows32)
     if (filt)
       RAG_RESCAN(true);
     else
       RAG_RESCAN(false);
 #undef RAG_RESCAN
+  } else {
+    mark_unanswered_kernel<<<dim3(1), dim3(64), 0, st>>>(w.fb_tier, Bq, w.fb_cnt);
   }
   RAG_HIP(hipGetLastError());
   return RAG_OK;
@@ -486,9 +491,10 @@ void launch_variant(rag_index* h, Workspace& w, int grid, hipStream_t st) {
   constexpr bool NT = V != 5;
   constexpr bool SB = V != 6;
   constexpr int DYN = V == 9 || V == 12 ? 2 : V == 10 ? 1 : V == 11 ? 4 : 0;
-  scan_kernel<D, false, MODE, STRIDED, NT, SB, DYN><<<dim3(grid), dim3(256), 0, st>>>(
-      h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, n_tiles, V == 1 ? nullptr : w.seed,
-      w.part_s, w.part_i, w.heads_s, w.heads_i, w.heads_n, w.tileq);
+  launch_fixed<kScanBlock>(scan_kernel<D, false, MODE, STRIDED, NT, SB, DYN>, dim3(grid), 0, st,
+                           h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, n_tiles,
+                           V == 1 ? nullptr : w.seed, w.part_s, w.part_i, w.heads_s, w.heads_i,
+                           w.heads_n, w.tileq);
 }
 
 template <int D>
@@ -505,8 +511,8 @@ int bench_scan(rag_index* h, const float* q, int B, int variant, int reps, doubl
     RAG_HIP(hipMemsetD32(reinterpret_cast<hipDeviceptr_t>(w.seed), 0x7f800000, kQ));
   const int64_t n_tiles = (h->count + 15) / 16;
   // the production grid (launch_search_pass: 3/4 of the CUs); RAGMI_SCAN_WGS overrides
-  const char* wv = std::getenv("RAGMI_SCAN_WGS");
-  const int cap = wv ? std::max(8, std::atoi(wv)) : h->scan_wgs;
+  static ragmi::Knob k_wgs("RAGMI_SCAN_WGS");
+  const int cap = k_wgs.get(0) > 0 ? std::max(8, k_wgs.get(0)) : h->scan_wgs;
   int grid = (int)std::min<int64_t>(std::min(h->max_wgs, cap), std::max<int64_t>(1, (n_tiles + 3) / 4));
   grid = std::min(grid, kMaxLists / kWavesPerWG);
   // variant 8: the v_dot2 VALU ablation over a row-group-major copy of the corpus
@@ -599,9 +605,9 @@ int bench_wide(rag_index* h, const float* q, int B, int mode, int reps, double* 
   const int grid = (int)std::min<int64_t>(h->max_wgs / 2, std::max<int64_t>(1, n_tiles));
   auto one = [&]() {
 #define RAG_WIDE(MODE)                                                                     \
-  scan_wide_kernel<D, MODE, true><<<dim3(grid), dim3(64 * kWideWaves), 0, nullptr>>>(      \
-      h->corpus, w.qfrag, (int)h->count, (int)n_tiles, w.seed, w.part_s, w.part_i,         \
-      w.heads_s, w.heads_i, w.heads_n, groups)
+  launch_fixed<kWideBlock>(scan_wide_kernel<D, MODE, true>, dim3(grid), 0, nullptr,          \
+                           h->corpus, w.qfrag, (int)h->count, (int)n_tiles, w.seed, w.part_s, \
+                           w.part_i, w.heads_s, w.heads_i, w.heads_n, groups)
     switch (mode) {
       case 1: RAG_WIDE(1); break;
       case 2: RAG_WIDE(2); break;
@@ -645,6 +651,8 @@ int rag_index_create_ex(int dim, int64_t capacity_rows, int device, int storage,
   if (!out) return ragmi::fail(RAG_EINVAL, "out is NULL");
   *out = nullptr;
   if (dim != 384 && dim != 1024) return ragmi::fail(RAG_EINVAL, "dim must be 384 or 1024");
+  const bool diag = (storage & RAG_CREATE_DIAGNOSTIC) != 0;
+  storage &= ~RAG_CREATE_DIAGNOSTIC;
   if (storage != RAG_STORE_FP16 && storage != RAG_STORE_FP32)
     return ragmi::fail(RAG_EINVAL, "storage must be RAG_STORE_FP16 or RAG_STORE_FP32");
   if (capacity_rows < 0 || capacity_rows > (int64_t(1) << 31) - 16)
@@ -673,6 +681,7 @@ int rag_index_create_ex(int dim, int64_t capacity_rows, int device, int storage,
           hipSuccess ||
       n_cu <= 0)
     n_cu = 256;
+  h->n_cu = n_cu;
   h->max_wgs = n_cu * 2;  // 2 x 256-thread workgroups per CU (__launch_bounds__(256, 2))
   h->scan_wgs = std::max(8, (n_cu * 3 / 4) & ~7);
   // wide rows (LDS-query scan) take up to 4 query groups (128 queries) per pass
@@ -702,7 +711,7 @@ int rag_index_create_ex(int dim, int64_t capacity_rows, int device, int storage,
                         G * ragmi::kMaxLists * 4) == hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&w.eps), G * Q * 4) == hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&w.fb_tier), G * Q * 4) == hipSuccess &&
-              hipMalloc(reinterpret_cast<void**>(&w.fb_cnt), 16) == hipSuccess &&
+              hipMalloc(reinterpret_cast<void**>(&w.fb_cnt), 32) == hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&w.tileq), 8 * ragmi::kTileQStride * 4) ==
                   hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&w.t2), G * Q * 2 * 4) == hipSuccess &&
@@ -710,18 +719,25 @@ int rag_index_create_ex(int dim, int64_t capacity_rows, int device, int storage,
                         G * Q * ragmi::kRescanMaxWG * 32 * 4) == hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&w.t2_i),
                         G * Q * ragmi::kRescanMaxWG * 32 * 4) == hipSuccess &&
-              hipMalloc(reinterpret_cast<void**>(&w.t2_tk), G * Q * 4) == hipSuccess &&
-              hipMemset(w.t2_tk, 0, G * Q * 4) == hipSuccess &&
+              hipMalloc(reinterpret_cast<void**>(&w.t2_tk), 64) == hipSuccess &&
+              hipMemset(w.t2_tk, 0, 64) == hipSuccess &&
               hipMemset(w.tileq, 0, 8 * ragmi::kTileQStride * 4) == hipSuccess &&
-              hipMemset(w.fb_cnt, 0, 16) == hipSuccess &&
+              hipMemset(w.fb_cnt, 0, 32) == hipSuccess &&
               hipMemset(w.fb_tier, 0, G * Q * 4) == hipSuccess;
     if (!ok) {
       rag_index_destroy(h);
       return ragmi::fail(RAG_ENOMEM, "workspace allocation failed");
     }
   }
+  if (diag) ragmi::diagnostics_on().store(true);
   *out = h;
   return RAG_OK;
+}
+
+int rag_knob_probe(const char* name, int dflt) {
+  if (!name) return dflt;
+  ragmi::Knob k(name);
+  return k.get(dflt);
 }
 
 int rag_index_destroy(rag_index_t* h) {
@@ -1067,6 +1083,22 @@ int rag_index_exactness_stats(rag_index_t* h, int64_t* tier1, int64_t* tier2,
     if (n > 0)
       RAG_HIP(hipMemcpy(last_tiers, h->last_ws->fb_tier, (size_t)n * 4, hipMemcpyDeviceToHost));
   }
+  return RAG_OK;
+}
+
+int rag_index_unanswered(rag_index_t* h, int64_t* n) {
+  ragmi::clear_error();
+  if (!h || !n) return ragmi::fail(RAG_EINVAL, "bad args");
+  std::lock_guard<std::mutex> lk(h->mu);
+  RAG_HIP(hipSetDevice(h->device));
+  RAG_HIP(hipDeviceSynchronize());
+  unsigned long long tot = 0;
+  for (auto& w : h->ws) {
+    unsigned long long c[3];
+    RAG_HIP(hipMemcpy(c, w.fb_cnt, sizeof(c), hipMemcpyDeviceToHost));
+    tot += c[2];
+  }
+  *n = (int64_t)tot;
   return RAG_OK;
 }
 

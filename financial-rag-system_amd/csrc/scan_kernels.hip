@@ -21,6 +21,7 @@ constexpr int kQ = 32;            // queries per pass
 constexpr int kKS = 32;           // candidates kept per (wave, query)
 constexpr int kP = 8;             // pending slots per (lane, query tile)
 constexpr int kWavesPerWG = 4;
+constexpr int kScanBlock = 64 * kWavesPerWG;   // scan_kernel / rescan_kernel block (launch_fixed)
 constexpr int kMaxLists = 2048;   // max scan waves (= per-wave lists) per pass
 constexpr int kLdsPerWave = 4096; // dwords: keep_s[32][32] keep_i[32][32] pend_s[2][8][64] pend_i[2][8][64]
 constexpr int kTileQStride = 16;  // ints between the 8 per-XCD tile-queue heads (64 B apart)
@@ -502,7 +503,7 @@ __device__ __forceinline__ void tile_sequence(int gw, int nw, int n_tiles, int& 
 // Query B-operands live in VGPRs (2 x D/32 half8 per lane): the D = 384 production kernel.
 template <int D, bool FILTER, int MODE = 0, bool STRIDED = true, bool NT = true, bool SB = true,
           int DYN = 0>
-__global__ __launch_bounds__(256, 2) void scan_kernel(
+__global__ __launch_bounds__(kScanBlock, 2) void scan_kernel(
     const half8* __restrict__ corpus, const uint32_t* __restrict__ tags,
     const uint32_t* __restrict__ filt, const half8* __restrict__ qfrag, int n_rows, int n_tiles,
     const float* __restrict__ seed_thr, float* __restrict__ part_s, int* __restrict__ part_i,
@@ -648,6 +649,7 @@ __global__ __launch_bounds__(256, 2) void scan_kernel(
 // workgroup's 64 KB of query fragments (2 waves per SIMD).
 constexpr int kRP = 8;          // pending slots per (lane, query tile); flush at > kRP - 4
 constexpr int kLdsWaves = 8;    // waves per scan_lds_kernel workgroup
+constexpr int kLdsBlock = 64 * kLdsWaves;
 
 struct RegTopK {
   float* keep_s;   // LDS [32 queries][32] best-first
@@ -896,7 +898,7 @@ constexpr int kShareLead = 2;     // max tiles a wave may run ahead of its partn
 constexpr int kShareSpin = 256;   // bounded wait (x s_sleep 4 = 256 clocks each)
 
 template <int D, bool FILTER, bool NT>
-__global__ __launch_bounds__(64 * kLdsWaves, 1) void scan_lds_kernel(
+__global__ __launch_bounds__(kLdsBlock, 1) void scan_lds_kernel(
     const half8* __restrict__ corpus, const uint32_t* __restrict__ tags,
     const uint32_t* __restrict__ filt, const half8* __restrict__ qfrag, int n_rows, int n_tiles,
     const float* __restrict__ seed_thr, float* __restrict__ part_s, int* __restrict__ part_i,
@@ -1178,6 +1180,7 @@ __device__ __forceinline__ void wtopk_finish(WideTopK& st, int lane, int qt, int
 // next load reuses). The loop issues no VMEM besides the ring loads, so the counts are exact.
 constexpr int kWideBufs = 4;
 constexpr int kWideWaves = 8;
+constexpr int kWideBlock = 64 * kWideWaves;
 constexpr int kWidePre = 8;   // tile-fragment LDS reads in flight ahead of the MFMA chain
 
 // MODE (diagnostic timing variants, rag_bench_scan at dim 1024): 0 production; 1 no top-k (MFMA + a
@@ -1186,7 +1189,7 @@ constexpr int kWidePre = 8;   // tile-fragment LDS reads in flight ahead of the 
 // the tile-fragment LDS reads, no MFMA. NT: ring loads with the
 // non-temporal policy.
 template <int D, int MODE = 0, bool NT = false>
-__global__ __launch_bounds__(64 * kWideWaves, 1) void scan_wide_kernel(
+__global__ __launch_bounds__(kWideBlock, 1) void scan_wide_kernel(
     const half8* __restrict__ corpus, const half8* __restrict__ qfrag, int n_rows, int n_tiles,
     const float* __restrict__ seed_thr, float* __restrict__ part_s, int* __restrict__ part_i,
     float* __restrict__ heads_s, int* __restrict__ heads_i, int* __restrict__ heads_n,
@@ -2226,182 +2229,362 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
 }
 
 // ----------------------------------------------------------------------------------------
-// rescan (tier 2 of select's certificate): launched after every select with R workgroups; each
-// returns at once unless some query of the pass is marked tier 2. For such a query q,
-// workgroup r streams tiles t = 4 r + w, 4 r + w + 4 R, ... (wave w; rows increase per wave,
-// which the strict `> thr` tie rule needs), scores them approximately with v_dot2 over the
-// query's fp16 fragment (error within eps_q, the scan's bound), rescores rows with
-// a >= max(L, thr - eps_q) exactly into each wave's running exact top-32 (thr = its 32nd,
-// starting just below e_k: every true top-k row scores >= e_k), merges its 4 waves and
-// publishes its 32 best; the workgroup that arrives last (device-scope ticket) merges the R
-// lists and emits q's exact top-k. The global top-k lies in the union of the shares' top-32s
-// (k <= 32). Bounded: R workgroups over the shard instead of select's one.
-// Visibility: each workgroup's list stores, then __threadfence() (agent-scope release +
-// acquire: L2 write-back, L1 invalidate) before its ticket; the last arriver fences again
-// before it reads the other lists (MI355X_MICROARCH.md, inter-workgroup visibility).
-// Few registers and no dynamic LDS: the launch must fit beside full-occupancy scans of other
-// streams when it has nothing to do.
+// rescan (tier 2 of select's certificate; round 4): launched after every select with R
+// workgroups. Each returns at once (two loads and a ballot per wave) unless select marked a
+// query of the pass. Otherwise the workgroups split the shard's tiles (t = 4r + w, step 4R:
+// rows increase per wave, as the strict `> thr` tie rule needs) and serve ALL marked queries
+// in one stream of the shard per 16 of them (kRescanQ = one MFMA column tile; D = 384 passes
+// hold <= 32 queries, so at most two streams):
+//   * the marked queries' B-fragments are gathered from qprep's into LDS (column j = the j-th
+//     marked query), and every tile gets the scan's MFMA scores a(r) against all of them;
+//   * query j's rows with a >= band_j = max(L_j, thr_j - eps_j) may be in its top-k (L from
+//     select: every true top-k row has a >= L; thr_j = the wave's running 32nd exact score,
+//     starting just below e_k, the k-th exact score select saw); a tile with such a row for
+//     query j is re-scored exactly for j, all 16 rows at once (exact_tile_scores: the tile
+//     image re-read from L2, the canonical fp64 order), and its rows with e > thr_j merge into
+//     the wave's running exact top-32 of j (LDS; thr_j rises with it);
+//   * each workgroup merges its 4 waves' lists per query and publishes them; the workgroup that
+//     arrives last at the pass ticket (one per launch) merges the R lists of every marked query
+//     and emits its exact top-k. The global top-k lies in the union of the per-wave top-32s.
+// Round 3 streamed the shard once per marked query with v_dot2 and re-scored candidates two
+// rows per memory round trip: 4 marked queries cost 8.4 ms at 1.25M rows and 10.7 ms at 10M
+// (profiles/r03zz_tier2_latency.jsonl), and its 64-register budget spilled to scratch.
+// Visibility (MI355X_MICROARCH.md, inter-workgroup hand-off): list stores, every wave's
+// vmcnt(0), barrier, one lane's agent release fence + vmcnt(0), the ticket add; the last
+// arriver's one agent acquire + vmcnt(0), barrier, then plain loads.
 // ----------------------------------------------------------------------------------------
 constexpr int kRescanMaxWG = 512;
+constexpr int kRescanQ = 16;   // marked queries per stream of the shard (one MFMA column tile)
+
+// Canonical exact scores (exact_scores_pairs' arithmetic bit for bit) of the 16
+// rows of tile t against one normalised query qq, all rows at once. Lane (h, r) = (lane >> 4,
+// lane & 15) reads row 16t + r's chunks c = 4s + h: the tile16 image itself (fp16 storage) or
+// the fp32 rows. Canonical lane l = 4 sg + h of exact_scores_pairs sums the chunks l, l + 64,
+// ..., i.e. s = sg, sg + 16, ... in that order, so this lane keeps those partials p[sg]. The
+// canonical xor butterfly over l (d = 32 .. 1) is d = 32, 16, 8, 4 -> sg ^ 8, 4, 2, 1 inside the
+// lane, then d = 2, 1 -> h ^ 2, h ^ 1 = lane ^ 32, lane ^ 16. IEEE addition commutes, so each
+// pair sums to the canonical value whichever operand comes first. Every lane of row r returns
+// row r's score.
+template <int D, bool F32>
+__device__ __forceinline__ float exact_tile_scores(const half8* __restrict__ corpus,
+                                                   const float* __restrict__ rows32, int t,
+                                                   const float* __restrict__ qq, int lane) {
+  constexpr int S = steps<D>();
+  const int h = lane >> 4, r = lane & 15;
+  double p[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) p[i] = 0.0;
+  // opaque zero offset of every load: the tile's loads do not depend on the query, and
+  // without it the compiler hoisted them (and their fp32 conversions) out of the caller's
+  // loop over queries
+  int zoff = 0;
+  asm volatile("" : "+v"(zoff));
+  const half8* tp = corpus + (int64_t)t * (S * 64) + lane;
+  const float* rp = F32 ? rows32 + ((int64_t)t * kTileRows + r) * D + 8 * h : nullptr;
+  const float* qp = qq + 8 * h;
+  // G k-steps per group; the next group's addresses depend (opaque asm) on this group's
+  // last fp64 sum, so its loads issue after this group's registers are consumed: left free,
+  // the compiler hoisted every step's tile and query loads (S x 12 registers) to the top and
+  // spilled (sched_barrier did not stop it). One L2 round trip per group.
+  constexpr int G = S % 6 == 0 && S <= 12 ? 6 : 2;
+#pragma unroll
+  for (int s0 = 0; s0 < S; s0 += G) {
+    float x[G][8];
+    float4 qa[G], qb[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int s = s0 + g;
+      if constexpr (F32) {
+        const float4 u = *reinterpret_cast<const float4*>(rp + 32 * s + zoff);
+        const float4 v = *reinterpret_cast<const float4*>(rp + 32 * s + 4 + zoff);
+        x[g][0] = u.x; x[g][1] = u.y; x[g][2] = u.z; x[g][3] = u.w;
+        x[g][4] = v.x; x[g][5] = v.y; x[g][6] = v.z; x[g][7] = v.w;
+      } else {
+        const half8 v = tp[s * 64 + zoff];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x[g][i] = (float)v[i];
+      }
+      qa[g] = *reinterpret_cast<const float4*>(qp + 32 * s + zoff);
+      qb[g] = *reinterpret_cast<const float4*>(qp + 32 * s + 4 + zoff);
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      double a = p[(s0 + g) & 15];
+      a = fma((double)x[g][0], (double)qa[g].x, a);
+      a = fma((double)x[g][1], (double)qa[g].y, a);
+      a = fma((double)x[g][2], (double)qa[g].z, a);
+      a = fma((double)x[g][3], (double)qa[g].w, a);
+      a = fma((double)x[g][4], (double)qb[g].x, a);
+      a = fma((double)x[g][5], (double)qb[g].y, a);
+      a = fma((double)x[g][6], (double)qb[g].z, a);
+      a = fma((double)x[g][7], (double)qb[g].w, a);
+      p[(s0 + g) & 15] = a;
+    }
+    asm volatile("" : "+v"(zoff) : "v"(p[(s0 + G - 1) & 15]));
+  }
+#pragma unroll
+  for (int d = 8; d > 0; d >>= 1) {
+#pragma unroll
+    for (int i = 0; i < d; ++i) p[i] = p[i] + p[i + d];
+  }
+  double y = p[0] + __shfl_xor(p[0], 32, 64);
+  y = y + __shfl_xor(y, 16, 64);
+  return (float)y;
+}
 
 template <int D, bool FILTER>
-__global__ __launch_bounds__(256, 8) void rescan_kernel(
+__global__ __launch_bounds__(kScanBlock, 2) void rescan_kernel(
     const int* __restrict__ tier, const float* __restrict__ t2, int Bq,
     const half8* __restrict__ corpus, const uint32_t* __restrict__ tags,
     const uint32_t* __restrict__ filt, const half8* __restrict__ qfrag, int n_rows,
     const float* __restrict__ qn, int k, const float* __restrict__ eps,
-    float* __restrict__ lst_s, int* __restrict__ lst_i, int* __restrict__ tickets,
+    float* __restrict__ lst_s, int* __restrict__ lst_i, int* __restrict__ ticket,
     int64_t id_offset, float* __restrict__ out_s, int64_t* __restrict__ out_i,
     int32_t* __restrict__ out_packed, const float* __restrict__ rows32) {
-  __shared__ float c_s[4][32];
-  __shared__ int c_i[4][32];
-  __shared__ int last;
-  const int R = gridDim.x, r = blockIdx.x;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   constexpr int S = steps<D>();
-  const int n_tiles = (n_rows + kTileRows - 1) / kTileRows;
-  // the pass's tier-2 queries (Bq <= 128) from two loads per lane, not one dependent load
-  // per query: the common case (none) costs one round trip
-  uint64_t todo[2];
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int q = lane + 64 * h;
-    todo[h] = __ballot(q < Bq && tier[q < Bq ? q : 0] == 2);
+  constexpr int CS = S >= 16 ? 8 : S / 2;   // k-steps per streamed chunk (384: 6, 1024: 8)
+  constexpr int NCH = S / CS;               // chunks per tile: even, so every tile's chunk 0
+  static_assert(S % CS == 0 && NCH % 2 == 0, "two-slot chunk ring");   // lands in slot 0
+  __shared__ half8 bl[S * 64];                         // B-fragments of the marked queries
+  __shared__ float ws[kWavesPerWG][kRescanQ][kKS];     // per-wave running exact top-32s
+  __shared__ int wi[kWavesPerWG][kRescanQ][kKS];
+  __shared__ int fq[128];                              // marked queries, ascending
+  __shared__ int last;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // ---- the pass's marked queries (Bq <= 128): none -> return, the common case
+  const uint64_t todo0 = __ballot(lane < Bq && tier[lane < Bq ? lane : 0] == 2);
+  const uint64_t todo1 = __ballot(lane + 64 < Bq && tier[lane + 64 < Bq ? lane + 64 : 0] == 2);
+  if (!(todo0 | todo1)) return;
+  const int nf = __popcll(todo0) + __popcll(todo1);
+  if (tid < 128) {
+    const uint64_t m = tid < 64 ? todo0 : todo1;
+    if ((m >> lane) & 1)
+      fq[__popcll(m & ((1ull << lane) - 1)) + (tid < 64 ? 0 : __popcll(todo0))] = tid;
   }
-  for (int h = 0; h < 2; ++h)
-  while (todo[h]) {
-    const int bq = 64 * h + (int)__builtin_ctzll(todo[h]);
-    todo[h] &= todo[h] - 1;
-    const int grp = bq / kQ, b = bq % kQ;
-    const float L = t2[2 * bq], E = t2[2 * bq + 1];
-    const float e = eps[bq];
-    const float* qq = qn + (int64_t)bq * D;
+  const int R = gridDim.x;
+  const int gw = blockIdx.x * kWavesPerWG + wid, nw = R * kWavesPerWG;
+  const int n_tiles = (n_rows + kTileRows - 1) / kTileRows;
+  int t_first, t_step, n_mine;
+  tile_sequence<true>(gw, nw, n_tiles, t_first, t_step, n_mine);
+  const char* cbase = reinterpret_cast<const char*>(corpus);
+  const int voff = lane * 16;
+  const int j = lane & 15;   // the lane's MFMA column = marked query qb + j of the stream
+  // default cache policy: a tile with candidates is re-read from L2 by exact_tile_scores
+  auto load = [&](half8(&a)[CS], int t_in, int c) __attribute__((always_inline)) {
+    const int t = __builtin_amdgcn_readfirstlane(t_in);
+    const char* tp = cbase + (int64_t)t * (S * 1024) + c * (CS * 1024);
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(tp), 0, CS * 1024, 0x00020000);
+#pragma unroll
+    for (int s = 0; s < CS; ++s)
+      a[s] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, s * 1024, 0));
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  for (int qb = 0; qb < nf; qb += kRescanQ) {
+    const int nq = min(kRescanQ, nf - qb);
+    __syncthreads();   // fq written; the previous stream's list reads done
+    for (int idx = tid; idx < S * 64; idx += 256) {
+      const int jj = idx & 15;
+      half8 v = {};
+      if (jj < nq) {
+        const int q = fq[qb + jj], s = idx >> 6, hh = (idx >> 4) & 3;
+        v = qfrag[(q / kQ) * (2 * S * 64) + (((q % kQ) >> 4) * S + s) * 64 + hh * 16 + (q & 15)];
+      }
+      bl[idx] = v;
+    }
+#pragma unroll
+    for (int e = 0; e < kRescanQ * kKS / 64; ++e) {
+      (&ws[wid][0][0])[lane + 64 * e] = kNegInf;
+      (&wi[wid][0][0])[lane + 64 * e] = kIdNone32;
+    }
+    // column j's query: floor L, running threshold, bound, filter
+    const bool live = j < nq;
+    const int qj = live ? fq[qb + j] : 0;
+    const float L = t2[2 * qj], ej = eps[qj];
+    float thr = nextafterf(t2[2 * qj + 1], kNegInf);
     uint32_t fm = 0, fv = 0;
     if constexpr (FILTER) {
-      fm = filt[2 * bq];
-      fv = filt[2 * bq + 1];
+      fm = filt[2 * qj];
+      fv = filt[2 * qj + 1];
     }
-    const int hh = lane >> 4, rr = lane & 15;
-    // lane (hh, rr): dims 32 s + 8 hh .. + 7 of row 16 t + rr and of query b (qprep's
-    // B-fragment of query tile b >> 4, column b & 15)
-    const half8* qf = qfrag + grp * (2 * S * 64) + ((b >> 4) * S) * 64 + hh * 16 + (b & 15);
-    float thr = nextafterf(E, kNegInf);
-    float rs = kNegInf;
-    int ri = kIdNone32;
-    for (int t = 4 * r + wid; t < n_tiles; t += 4 * R) {
-      const half8* tp = corpus + (int64_t)t * (S * 64) + hh * 16 + rr;
-      float a = 0.f;
-#pragma unroll 2
-      for (int s2 = 0; s2 < S; ++s2) {
-        const half8 x = tp[s2 * 64], y = qf[s2 * 64];
-        a = __builtin_amdgcn_fdot2(half2v{x[0], x[1]}, half2v{y[0], y[1]}, a, false);
-        a = __builtin_amdgcn_fdot2(half2v{x[2], x[3]}, half2v{y[2], y[3]}, a, false);
-        a = __builtin_amdgcn_fdot2(half2v{x[4], x[5]}, half2v{y[4], y[5]}, a, false);
-        a = __builtin_amdgcn_fdot2(half2v{x[6], x[7]}, half2v{y[6], y[7]}, a, false);
-      }
-      a += __shfl_xor(a, 16, 64);
-      a += __shfl_xor(a, 32, 64);
-      const int row = t * kTileRows + rr;
-      bool ok = lane < 16 && row < n_rows;
-      if constexpr (FILTER) ok = ok && ((tags[row < n_rows ? row : 0] & fm) == fv);
-      uint64_t m = __ballot(ok && a >= fmaxf(L, thr - e));
-      while (m) {
-        int rows[2];
-        float es[2];
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int ln = m ? (int)__builtin_ctzll(m) : -1;
-          if (m) m &= m - 1;
-          rows[j] = ln >= 0 ? t * kTileRows + ln : -1;
-        }
-        exact_scores_wave<D, 2>(corpus, rows, qq, lane, es, rows32);
-        float ns = kNegInf;
-        int ni = kIdNone32;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          if (lane == 32 + j && rows[j] >= 0 && es[j] > thr) {
-            ns = es[j];
-            ni = rows[j];
-          }
-        }
-        if (lane >= 32) {
-          rs = ns;
-          ri = ni;
-        }
-        bitonic_sort64(rs, ri, lane);
-        thr = fmaxf(thr, __shfl(rs, 31, 64));
-      }
-    }
-    // this workgroup's 32 best: merge the 4 waves' lists
-    if (lane < 32) {
-      c_s[wid][lane] = rs;
-      c_i[wid][lane] = ri;
-    }
+    float band = live ? fmaxf(L, thr - ej) : __builtin_inff();
     __syncthreads();
-    float* ms = lst_s + ((int64_t)bq * kRescanMaxWG + r) * 32;
-    int* mi = lst_i + ((int64_t)bq * kRescanMaxWG + r) * 32;
-    if (wid == 0) {
-      float x = lane < 32 ? c_s[0][lane] : kNegInf;
-      int id = lane < 32 ? c_i[0][lane] : kIdNone32;
-      for (int v = 1; v < 4; ++v) {
-        if (lane >= 32) {
-          x = c_s[v][63 - lane];
-          id = c_i[v][63 - lane];
-        }
-        bitonic_merge64(x, id, lane);
-      }
-      if (lane < 32) {
-        ms[lane] = x;
-        mi[lane] = id;
-      }
-      __threadfence();                           // the list is visible before the ticket
-      if (lane == 0) last = atomicAdd(&tickets[bq], 1) == R - 1;
-    }
-    __syncthreads();
-    if (last) {
-      __threadfence();                           // acquire: the other workgroups' lists
-      // wave w merges lists w, w + 4, ...; wave 0 then merges the 4 results
-      float x = kNegInf;
-      int id = kIdNone32;
-      for (int w2 = wid; w2 < R; w2 += 4) {
-        const float* os = lst_s + ((int64_t)bq * kRescanMaxWG + w2) * 32;
-        const int* oi = lst_i + ((int64_t)bq * kRescanMaxWG + w2) * 32;
-        if (lane >= 32) {
-          x = os[63 - lane];
-          id = oi[63 - lane];
-        }
-        bitonic_merge64(x, id, lane);
-      }
-      if (lane < 32) {
-        c_s[wid][lane] = x;
-        c_i[wid][lane] = id;
-      }
-      __syncthreads();
-      if (wid == 0) {
-        x = lane < 32 ? c_s[0][lane] : kNegInf;
-        id = lane < 32 ? c_i[0][lane] : kIdNone32;
-        for (int v = 1; v < 4; ++v) {
-          if (lane >= 32) {
-            x = c_s[v][63 - lane];
-            id = c_i[v][63 - lane];
-          }
-          bitonic_merge64(x, id, lane);
-        }
-        if (lane < k) {
-          const bool ok = x != kNegInf;
-          if (out_packed) {
-            out_packed[((int64_t)bq * k + lane) * 2] = __float_as_int(x);
-            out_packed[((int64_t)bq * k + lane) * 2 + 1] = ok ? (int32_t)(id + id_offset) : -1;
+
+    if (n_mine > 0) {
+      half8 ra[CS], rb[CS];
+      load(ra, t_first, 0);
+      for (int jt = 0; jt < n_mine; ++jt) {
+        const int t = t_first + jt * t_step;
+        const int tn = t_first + min(jt + 1, n_mine - 1) * t_step;
+        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+          if (c % 2 == 0) {
+            load(rb, t, c + 1);
+#pragma unroll
+            for (int s = 0; s < CS; ++s)
+              acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ra[s], bl[(c * CS + s) * 64 + lane],
+                                                           acc, 0, 0, 0);
           } else {
-            out_s[(int64_t)bq * k + lane] = x;
-            out_i[(int64_t)bq * k + lane] = ok ? (int64_t)id + id_offset : (int64_t)-1;
+            if (c + 1 < NCH)
+              load(ra, t, c + 1);
+            else
+              load(ra, tn, 0);
+#pragma unroll
+            for (int s = 0; s < CS; ++s)
+              acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(rb[s], bl[(c * CS + s) * 64 + lane],
+                                                           acc, 0, 0, 0);
           }
         }
-        if (lane == 0) tickets[bq] = 0;          // re-armed for the slot's next pass
+        // rows 16t + 4(lane >> 4) + i of column j: any inside j's band?
+        const int rbase = t * kTileRows + 4 * (lane >> 4);
+        uint4 tg = {0u, 0u, 0u, 0u};
+        if constexpr (FILTER) tg = *reinterpret_cast<const uint4*>(tags + rbase);
+        bool hit = false;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          bool ok = rbase + i < n_rows && acc[i] >= band;
+          if constexpr (FILTER) {
+            const uint32_t tr = i == 0 ? tg.x : i == 1 ? tg.y : i == 2 ? tg.z : tg.w;
+            ok = ok && ((tr & fm) == fv);
+          }
+          hit = hit || ok;
+        }
+        const uint64_t bm = __ballot(hit);
+        uint32_t qm = (uint32_t)((bm | (bm >> 16) | (bm >> 32) | (bm >> 48)) & 0xffffu);
+        if (!qm) continue;
+        const int row = t * kTileRows + j;      // lanes 0..15 carry row 16t + lane below
+        uint32_t rt = 0;
+        if constexpr (FILTER) rt = tags[row < n_rows ? row : 0];
+        while (qm) {
+          const int c = __builtin_ctz(qm);
+          qm &= qm - 1;
+          const int q = __builtin_amdgcn_readlane(qj, c);
+          const float tc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(thr), c));
+          const float e =
+              rows32 ? exact_tile_scores<D, true>(corpus, rows32, t, qn + (int64_t)q * D, lane)
+                     : exact_tile_scores<D, false>(corpus, rows32, t, qn + (int64_t)q * D, lane);
+          bool cand = lane < 16 && row < n_rows && e > tc;
+          if constexpr (FILTER) {
+            const uint32_t fmc = __builtin_amdgcn_readlane(fm, c);
+            const uint32_t fvc = __builtin_amdgcn_readlane(fv, c);
+            cand = cand && ((rt & fmc) == fvc);
+          }
+          if (!__ballot(cand)) continue;
+          float s = cand ? e : kNegInf;
+          int id = cand ? row : kIdNone32;
+          if (lane >= 32) {
+            s = ws[wid][c][lane - 32];
+            id = wi[wid][c][lane - 32];
+          }
+          lds_fence();
+          bitonic_sort64(s, id, lane);
+          if (lane < 32) {
+            ws[wid][c][lane] = s;
+            wi[wid][c][lane] = id;
+          }
+          lds_fence();
+          const float nt = __shfl(s, 31, 64);
+          if (j == c) {
+            thr = fmaxf(thr, nt);
+            band = fmaxf(L, thr - ej);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // this workgroup's 32 best per query of the stream (wave w: queries w, w + 4, ...)
+    for (int c = wid; c < nq; c += kWavesPerWG) {
+      float x = lane < 32 ? ws[0][c][lane] : kNegInf;
+      int id = lane < 32 ? wi[0][c][lane] : kIdNone32;
+      for (int v = 1; v < kWavesPerWG; ++v) {
+        if (lane >= 32) {
+          x = ws[v][c][63 - lane];
+          id = wi[v][c][63 - lane];
+        }
+        bitonic_merge64(x, id, lane);
+      }
+      const int64_t o = ((int64_t)fq[qb + c] * kRescanMaxWG + blockIdx.x) * kKS;
+      if (lane < 32) {
+        lst_s[o + lane] = x;
+        lst_i[o + lane] = id;
+      }
+    }
+  }
+  // ---- publish: stores drained, agent release, then the ticket
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = atomicAdd(ticket, 1) == R - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  // ---- last arriver: each marked query's R lists -> its exact top-k (wave w merges lists
+  //      w, w + 4, ...; wave 0 the four results)
+  for (int i = 0; i < nf; ++i) {
+    const int q = fq[i];
+    float x = kNegInf;
+    int id = kIdNone32;
+    for (int w2 = wid; w2 < R; w2 += kWavesPerWG) {
+      const int64_t o = ((int64_t)q * kRescanMaxWG + w2) * kKS;
+      if (lane >= 32) {
+        x = lst_s[o + 63 - lane];
+        id = lst_i[o + 63 - lane];
+      }
+      bitonic_merge64(x, id, lane);
+    }
+    if (lane < 32) {
+      ws[wid][0][lane] = x;
+      wi[wid][0][lane] = id;
+    }
+    __syncthreads();
+    if (wid == 0) {
+      x = lane < 32 ? ws[0][0][lane] : kNegInf;
+      id = lane < 32 ? wi[0][0][lane] : kIdNone32;
+      for (int v = 1; v < kWavesPerWG; ++v) {
+        if (lane >= 32) {
+          x = ws[v][0][63 - lane];
+          id = wi[v][0][63 - lane];
+        }
+        bitonic_merge64(x, id, lane);
+      }
+      if (lane < k) {
+        const bool ok = x != kNegInf;
+        if (out_packed) {
+          out_packed[((int64_t)q * k + lane) * 2] = __float_as_int(x);
+          out_packed[((int64_t)q * k + lane) * 2 + 1] = ok ? (int32_t)(id + id_offset) : -1;
+        } else {
+          out_s[(int64_t)q * k + lane] = x;
+          out_i[(int64_t)q * k + lane] = ok ? (int64_t)id + id_offset : (int64_t)-1;
+        }
       }
     }
     __syncthreads();
   }
+  if (tid == 0) *ticket = 0;   // re-armed for the workspace's next pass (stream order)
+}
+
+// Diagnostic stand-in for a skipped rescan launch (RAGMI_RESCAN_WG=0 under
+// RAG_CREATE_DIAGNOSTIC): the pass's marked queries get no output, so they are re-marked
+// tier 3 and counted as unanswered (rag_index_unanswered) instead of passing as certified.
+__global__ __launch_bounds__(64) void mark_unanswered_kernel(int* __restrict__ tier, int Bq,
+                                                             unsigned long long* __restrict__ cnt) {
+  int n = 0;
+  for (int q = threadIdx.x; q < Bq; q += 64)
+    if (tier[q] == 2) {
+      tier[q] = 3;
+      ++n;
+    }
+  for (int d = 32; d > 0; d >>= 1) n += __shfl_xor(n, d, 64);
+  if (threadIdx.x == 0 && n > 0) atomicAdd(&cnt[2], (unsigned long long)n);
 }
 
 // ----------------------------------------------------------------------------------------

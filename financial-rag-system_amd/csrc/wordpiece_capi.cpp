@@ -16,8 +16,10 @@
 //                max_length as tokenizers 0.22 does it (budget n = max_length - 3: the shorter
 //                sequence keeps min(len, n / 2), ties count the first as shorter, the longer
 //                one the rest; a single text keeps max_length - 2).
-// A text (or pair) with any byte >= 0x80 is NOT encoded here: it is flagged and the caller
-// encodes it with the Rust tokenizer (Unicode normalisation tables stay out of this file).
+// A text (or pair) with any byte >= 0x80, or holding a literal special-token string such as
+// "[MASK]" (matched to one id by the Rust tokenizer before normalisation), is NOT encoded
+// here: it is flagged and the caller encodes it with the Rust tokenizer (Unicode
+// normalisation tables and the added-token matcher stay out of this file).
 // Why native: the Rust tokenizer's Python wrapper costs ~80 us per query string on one host
 // thread (~2.5 ms per 32-query batch) and holds the GIL while it builds Encoding objects, which
 // serialises a serving loop's kernel launches behind it; this path releases the GIL (ctypes)
@@ -175,6 +177,30 @@ bool ascii(const char* s, size_t n) {
   return true;
 }
 
+// A literal special-token string inside the text ([PAD] [UNK] [CLS] [SEP] [MASK], the tokens
+// BertWordPieceTokenizer registers as added special tokens): the Rust tokenizer maps it to ONE
+// id before normalisation, where the byte rules above would split it into '[' word ']'. Such a
+// text takes the fallback. Matched case-insensitively, which only sends a few more
+// texts to the fallback than needed (special tokens match case-sensitively there).
+bool has_special(const char* s, size_t n) {
+  static const char* const kSpecial[] = {"pad]", "unk]", "cls]", "sep]", "mask]"};
+  for (size_t i = 0; i < n; ++i) {
+    if (s[i] != '[') continue;
+    for (const char* sp : kSpecial) {
+      const size_t L = std::strlen(sp);
+      if (i + 1 + L > n) continue;
+      bool eq = true;
+      for (size_t k = 0; k < L && eq; ++k) {
+        char c = s[i + 1 + k];
+        if (c >= 'A' && c <= 'Z') c = (char)(c - 'A' + 'a');
+        eq = c == sp[k];
+      }
+      if (eq) return true;
+    }
+  }
+  return false;
+}
+
 }  // namespace
 
 extern "C" {
@@ -232,13 +258,13 @@ int rag_wordpiece_encode(const rag_wordpiece_t* t, const char* texts, const int6
   a.reserve(64);
   bb.reserve(512);
   int64_t T = 0;
-  cu[0] = 0;
+  if (cu) cu[0] = 0;   // n == 0 may pass no output arrays
   for (int j = 0; j < n; ++j) {
     const char* s = texts + text_off[j];
     const size_t sn = (size_t)(text_off[j + 1] - text_off[j]);
     const char* p = pairs ? pairs + pair_off[j] : nullptr;
     const size_t pn = pairs ? (size_t)(pair_off[j + 1] - pair_off[j]) : 0;
-    if (!ascii(s, sn) || (p && !ascii(p, pn))) {
+    if (!ascii(s, sn) || (p && !ascii(p, pn)) || has_special(s, sn) || (p && has_special(p, pn))) {
       fallback[j] = 1;
       cu[j + 1] = (int32_t)T;
       continue;

@@ -81,6 +81,8 @@ INDEX_API = {
                                       ctypes.POINTER(ctypes.c_double)]),
     "rag_index_set_scan_order": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "rag_index_exactness_stats": (ctypes.c_int, [c_vp, c_i64p, c_i64p, c_i32p, ctypes.c_int]),
+    "rag_index_unanswered": (ctypes.c_int, [c_vp, c_i64p]),
+    "rag_knob_probe": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int]),
     "rag_profile_enable": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "rag_profile_scan_ms": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_double), c_i64p]),
     "rag_profile_scan_intervals": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_double),
@@ -103,6 +105,10 @@ BERT_API = {
     "rag_encoder_create": (ctypes.c_int, [ctypes.POINTER(RagBertConfig),
                                           ctypes.POINTER(ctypes.POINTER(ctypes.c_float)),
                                           ctypes.c_int, ctypes.c_int, ctypes.POINTER(c_vp)]),
+    "rag_encoder_create_ex": (ctypes.c_int, [ctypes.POINTER(RagBertConfig),
+                                             ctypes.POINTER(ctypes.POINTER(ctypes.c_float)),
+                                             ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                             ctypes.POINTER(c_vp)]),
     "rag_encoder_destroy": (ctypes.c_int, [c_vp]),
     "rag_encoder_forward": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, ctypes.c_int, ctypes.c_int,
                                            ctypes.c_int, c_vp, c_vp]),

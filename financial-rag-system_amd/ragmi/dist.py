@@ -94,7 +94,8 @@ class ShardedIndex:
 
     def __init__(self, n_total: int, local=None, dim: int = 384, device=None, group=None,
                  merge: Callable | None = None, merge_packed: Callable | None = None,
-                 storage: str = "fp16", force_exchange: bool = False):
+                 storage: str = "fp16", force_exchange: bool = False,
+                 diagnostic: bool = False):
         self.group = group
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -103,7 +104,7 @@ class ShardedIndex:
         if local is None:
             from .index import FlatIndex
             local = FlatIndex(dim=dim, capacity=max(self.hi - self.lo, 16), device=device,
-                              storage=storage)
+                              storage=storage, diagnostic=diagnostic)
         self.local = local
         self.merge = merge or _gpu_merge
         self.merge_packed = merge_packed or _gpu_merge_packed

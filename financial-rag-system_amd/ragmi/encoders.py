@@ -300,7 +300,7 @@ class BertEncoder:
     """One encoder instance in HBM (fp16 GEMM weights, fp32 norms/embeddings)."""
 
     def __init__(self, cfg: dict, weights: dict, head: int, device=None,
-                 precision: str = "fp16x3"):
+                 precision: str = "fp16x3", diagnostic: bool = False):
         _lib.require_gpu()
         self._L = _lib.load()
         self.device = torch.device(device if device is not None else
@@ -311,8 +311,10 @@ class BertEncoder:
         self.precision = precision
         c, arrs, ptrs = _weight_ptrs(cfg, weights, head, precision)
         h = ctypes.c_void_p()
-        check(self._L.rag_encoder_create(ctypes.byref(c), ptrs, len(arrs), self.device.index,
-                                         ctypes.byref(h)))
+        # diagnostic=True (bench / profiling scripts): the process honours the RAGMI_* kernel
+        # A/B knobs (RAG_CREATE_DIAGNOSTIC, rag_encoder_create_ex); off in serving code
+        check(self._L.rag_encoder_create_ex(ctypes.byref(c), ptrs, len(arrs), self.device.index,
+                                            0x100 if diagnostic else 0, ctypes.byref(h)))
         self._h = h
         self.out_dim = cfg["hidden"] if head == HEAD_CLS_L2 else 1
 

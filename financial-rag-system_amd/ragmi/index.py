@@ -20,6 +20,7 @@ from ._lib import check
 MAX_K = 32          # RAG_MAX_K in include/ragmi.h
 QUERY_TILE = 32     # RAG_QUERY_TILE
 STORAGE = {"fp16": 0, "fp32": 1}   # RAG_STORE_FP16 / RAG_STORE_FP32
+CREATE_DIAGNOSTIC = 0x100          # RAG_CREATE_DIAGNOSTIC: honour the RAGMI_* A/B knobs
 
 
 def _stream_ptr(device: torch.device) -> int:
@@ -38,9 +39,13 @@ def _as_dev(x, dtype, device) -> torch.Tensor:
 class FlatIndex:
     """In-HBM flat index with exact (score desc, row asc) top-k search. storage "fp16": the
     fp16 rows only (what the scan streams); "fp32": the normalised fp32 rows too, which the
-    exact scores read (Qdrant's default Float32 vectors; rag_index_create_ex)."""
+    exact scores read (Qdrant's default Float32 vectors; rag_index_create_ex).
+    diagnostic=True (bench / profiling scripts only) lets the process honour the RAGMI_*
+    kernel A/B environment knobs (RAG_CREATE_DIAGNOSTIC); serving code leaves it off, and
+    the library then ignores (and reports) any such variable."""
 
-    def __init__(self, dim: int = 384, capacity: int = 0, device=None, storage: str = "fp16"):
+    def __init__(self, dim: int = 384, capacity: int = 0, device=None, storage: str = "fp16",
+                 diagnostic: bool = False):
         _lib.require_gpu()
         self._L = _lib.load()
         if device is None:
@@ -55,8 +60,9 @@ class FlatIndex:
             raise ValueError(f"storage must be one of {sorted(STORAGE)}")
         self.storage = storage
         h = ctypes.c_void_p()
-        check(self._L.rag_index_create_ex(self.dim, int(capacity), self.device.index,
-                                          STORAGE[storage], ctypes.byref(h)))
+        flags = STORAGE[storage] | (CREATE_DIAGNOSTIC if diagnostic else 0)
+        check(self._L.rag_index_create_ex(self.dim, int(capacity), self.device.index, flags,
+                                          ctypes.byref(h)))
         self._h = h
 
     # ---------------------------------------------------------------- lifetime
@@ -256,6 +262,14 @@ class FlatIndex:
             self._h, ctypes.byref(t1), ctypes.byref(t2),
             last.ctypes.data_as(_lib.c_i32p) if n_last > 0 else None, int(n_last)))
         return int(t1.value), int(t2.value), last
+
+    def unanswered(self) -> int:
+        """Marked (tier-2) queries since creation that got NO result because the second pass
+        was skipped (RAGMI_RESCAN_WG=0 on a diagnostic handle; their tier reads 3). Always 0
+        in production (rag_index_unanswered)."""
+        n = ctypes.c_int64()
+        check(self._L.rag_index_unanswered(self._h, ctypes.byref(n)))
+        return int(n.value)
 
     # ---------------------------------------------------------------- profiling
     def profile(self, every: int | bool) -> None:

@@ -87,6 +87,16 @@ int rag_index_create(int dim, int64_t capacity_rows, int device, rag_index_t** o
  * ranking identical to an fp32 store — while the scan still streams the fp16 copy (the
  * certified select's error bound grows by ||fp16(y) - y|| <= 2^-11 ||y||). */
 enum { RAG_STORE_FP16 = 0, RAG_STORE_FP32 = 1 };
+/* Flag OR-ed into rag_index_create_ex's `storage` (and rag_encoder_create_ex's `flags`): the
+ * process then honours the RAGMI_* environment knobs that switch kernels for A/B measurements
+ * (scan / rescan grids, seed sample, GEMM and attention variants). Without it every knob reads
+ * as its production default and a set knob is reported once on stderr. Diagnostic only:
+ * several knobs trade the worst-case latency or the certificate's fallback for timing. */
+#define RAG_CREATE_DIAGNOSTIC 0x100
+/* The value the library uses for the integer knob `name` (a RAGMI_* variable): the variable's
+ * value when it is set and diagnostics are on, else `dflt` (reporting an ignored variable
+ * once on stderr). Runs the same code path as every knob site; for tests. */
+int rag_knob_probe(const char* name, int dflt);
 /* rag_index_create with an explicit storage (rag_index_create = RAG_STORE_FP16). */
 int rag_index_create_ex(int dim, int64_t capacity_rows, int device, int storage,
                         rag_index_t** out);
@@ -162,13 +172,20 @@ int rag_merge_topk_packed(const int32_t* in_packed_dev, int n_lists, int B, int 
  * was created, whose top-k was certified by the list re-scoring fallback / needed the second
  * pass over the shard (all other queries passed the error-bound check directly).
  * last_tiers (host, may be NULL when n_last == 0) receives, for the first n_last queries of
- * the most recent search PASS, 0 / 1 / 2 = the path that certified them (-1 past the pass's
+ * the most recent search PASS, 0 / 1 / 2 = the path that certified them (3 = marked for the
+ * second pass but left unanswered, see rag_index_unanswered; -1 past the pass's
  * query count). Scope: a pass is one scan of <= 32 queries (<= 128 on the D = 1024 wide
  * scan); a search of more queries runs several passes and only its last one is reported, and
  * the state is per handle, so searches issued concurrently on several streams overwrite each
  * other's record (the tier1 / tier2 totals are exact in every case). Synchronises the device. */
 int rag_index_exactness_stats(rag_index_t* index, int64_t* tier1, int64_t* tier2,
                               int32_t* last_tiers, int n_last);
+
+/* Number of marked (tier-2) queries, since the index was created, that received NO result
+ * because the second pass was skipped (RAGMI_RESCAN_WG=0, honoured only under
+ * RAG_CREATE_DIAGNOSTIC; their last_tiers entry reads 3). Always 0 in production.
+ * Synchronises the device. */
+int rag_index_unanswered(rag_index_t* index, int64_t* n);
 
 /* Scan order across streams. serial = 1: each search pass's scan launch waits for the
  * previous pass's scan, whichever stream that ran on (one HIP event per handle), so passes

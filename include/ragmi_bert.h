@@ -58,6 +58,11 @@ int rag_encoder_num_weights(const rag_bert_config* cfg);
  *   RAG_HEAD_POOLER_CLS: pooler.dense.{weight [H][H], bias}, classifier.{weight [1][H], bias [1]}. */
 int rag_encoder_create(const rag_bert_config* cfg, const float* const* weights, int n_weights,
                        int device, rag_encoder_t** out);
+/* rag_encoder_create with flags: RAG_CREATE_DIAGNOSTIC (ragmi.h) makes the process honour the
+ * RAGMI_* kernel A/B knobs (GEMM / attention variants, split-K, fusion modes) — bench and
+ * profiling scripts only. */
+int rag_encoder_create_ex(const rag_bert_config* cfg, const float* const* weights, int n_weights,
+                          int device, int flags, rag_encoder_t** out);
 int rag_encoder_destroy(rag_encoder_t* enc);
 
 /* Device pointers, asynchronous on `stream` (hipStream_t). max_len must be >= the longest
@@ -115,7 +120,9 @@ int rag_build_pairs(const int32_t* q_ids, const int32_t* q_cu, int B, const int6
  * waves; _WS_NT the same with non-temporal output stores; _WS_* probes as the PIPE ones, and
  * _WS_L2_STORE with every tile stored over the first row band (L2-resident writes);
  * _WS_NOROT rotated-K-order-off A/B; _WS_READS_FIRST the MFMA waves' previous fragment order
- * (all reads of a K step before its MFMAs) for A/B against the interleaved one.
+ * (all reads of a K step before its MFMAs) for A/B against the interleaved one. _WS_BIG128
+ * (round 4, A/B): the WS ring with 4 MFMA waves of 128 x 64 (one per SIMD beside its loader
+ * wave, 256 registers each) instead of 8 of 64 x 64.
  * N % 128 == 0, K % 64 == 0 (PIPE/SMALL also N <= 4096). */
 enum { RAG_EPI_F16 = 0, RAG_EPI_GELU_F16 = 1, RAG_EPI_F32 = 2 };
 /* deferred-LayerNorm epilogues (rag_bert_gemm_dl) */
@@ -129,7 +136,7 @@ enum { RAG_GEMM_AUTO = 0, RAG_GEMM_TILE = 1, RAG_GEMM_PIPE = 2, RAG_GEMM_PROBE_N
        RAG_GEMM_WS_NT = 24, RAG_GEMM_WS_NOROT = 26, RAG_GEMM_WS_READS_FIRST = 27,
        RAG_GEMM_WS_PROBE_NO_A_READS = 28, RAG_GEMM_WS_PROBE_NO_W_READS = 29,
        RAG_GEMM_WS_PRIO_LOAD = 30, RAG_GEMM_WS_PRIO_MFMA = 31, RAG_GEMM_WS_FLAGS = 32,
-       RAG_GEMM_WS_NOHALF = 33, RAG_GEMM_WS_SMALL = 34 };
+       RAG_GEMM_WS_NOHALF = 33, RAG_GEMM_WS_SMALL = 34, RAG_GEMM_WS_BIG128 = 35 };
 int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, const void* W,
                   const void* W_lo, const float* bias, int M, int N, int K, void* C,
                   void* C_lo, void* stream);

@@ -110,7 +110,7 @@ def main():
     from ragmi.dist import ShardedIndex
 
     n = args.rows
-    sh = ShardedIndex(n, dim=D, device=dev)
+    sh = ShardedIndex(n, dim=D, device=dev, diagnostic=True)
     idx, lo, hi = sh.local, sh.lo, sh.hi
     t_build = time.perf_counter()
     build_shard(idx, lo, hi, n, dev)

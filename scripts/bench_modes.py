@@ -220,7 +220,7 @@ def run_pipeline(args, cfg_id):
     torch.cuda.set_device(dev)
     _init_dist(dev)
     n, D, prec = args.rows or 1_000_000, 384, args.precision
-    idx = FlatIndex(dim=D, capacity=n, device=dev)
+    idx = FlatIndex(dim=D, capacity=n, device=dev, diagnostic=True)
     build_shard(idx, 0, n, n, D, 1000, dev)
     g = torch.Generator(device=dev)
     g.manual_seed(77)
@@ -250,8 +250,8 @@ def run_pipeline(args, cfg_id):
     tok_ms = (time.perf_counter() - t_tok) / min(20, len(texts)) * 1e3
     q_lens = np.concatenate([np.diff(b[2]) for b in batches])
     bge_w, ce_w = R.make_weights(R.BGE_SMALL, 1), R.make_weights(R.MINILM_CE, 2)
-    bge = BertEncoder(R.BGE_SMALL, bge_w, HEAD_CLS_L2, dev, prec)
-    ce = BertEncoder(R.MINILM_CE, ce_w, HEAD_POOLER_CLS, dev, prec)
+    bge = BertEncoder(R.BGE_SMALL, bge_w, HEAD_CLS_L2, dev, prec, diagnostic=True)
+    ce = BertEncoder(R.MINILM_CE, ce_w, HEAD_POOLER_CLS, dev, prec, diagnostic=True)
     # 3 batches in flight: each stream takes one of the process's 4 hardware queues with the
     # null stream on the 4th (GPU_MAX_HW_QUEUES); a 4th stream would share a queue with
     # another and serialise behind it (config 2: 2 / 3 / 4 in flight 60.7K / 71.1K / 60.4K
@@ -583,7 +583,7 @@ def run_search(args, mode):
     def tags_fn(rows):            # ticker code 1..16 per global row (PayloadTags code space)
         return ((rows * 2654435761) % (1 << 32) // 7 % n_tick + 1).astype(np.uint32)
 
-    sh = ShardedIndex(n, dim=D, device=dev)
+    sh = ShardedIndex(n, dim=D, device=dev, diagnostic=True)
     idx, lo, hi = sh.local, sh.lo, sh.hi
     t_b = time.perf_counter()
     build_shard(idx, lo, hi, n, D, seed0, dev, tags_fn if mode == "filtered" else None)

@@ -47,7 +47,7 @@ def main():
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     steps = int(os.environ.get("STEPS", "20"))
-    idx = FlatIndex(dim=D, capacity=N, device=dev)
+    idx = FlatIndex(dim=D, capacity=N, device=dev, diagnostic=True)
     for c in range(N // 1_000_000):
         g = torch.Generator(device=dev)
         g.manual_seed(1000 + c)
@@ -63,8 +63,8 @@ def main():
         batches.append((ids.astype(np.int32), np.zeros(len(ids), np.int32),
                         np.r_[0, np.cumsum(lens)].astype(np.int32)))
     for prec in ("fp16x3", "fp16"):
-        bge = BertEncoder(R.BGE_SMALL, R.make_weights(R.BGE_SMALL, 1), HEAD_CLS_L2, dev, prec)
-        ce = BertEncoder(R.MINILM_CE, R.make_weights(R.MINILM_CE, 2), HEAD_POOLER_CLS, dev, prec)
+        bge = BertEncoder(R.BGE_SMALL, R.make_weights(R.BGE_SMALL, 1), HEAD_CLS_L2, dev, prec, diagnostic=True)
+        ce = BertEncoder(R.MINILM_CE, R.make_weights(R.MINILM_CE, 2), HEAD_POOLER_CLS, dev, prec, diagnostic=True)
         for cfg in (2, 3):
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
             acc = np.zeros(3)

@@ -110,7 +110,7 @@ def main():
             if only and name not in only.split(","):
                 continue
             w = R.make_weights(cfg, 1)
-            enc = BertEncoder(cfg, w, head, dev, prec)
+            enc = BertEncoder(cfg, w, head, dev, prec, diagnostic=True)
             ids, tt, cu = batch(rng, B, lo, hi, pair)
             # DEFERS=-1,0: the deferred LayerNorm (rag_encoder_set_defer_ln) auto, then off
             for defer in [int(v) for v in os.environ.get("DEFERS", "-1").split(",")]:

@@ -3,7 +3,9 @@ on a duplicate-heavy corpus (measure it at 1.25M and 10M rows).
 
 Corpus: torch randn rows (GPU generator), every `every`-th row replaced by base + 1e-5 noise
 (near-duplicates of one vector: each scan wave's list overflows inside the MFMA error band,
-so tier 1 cannot certify). Batch of 32: 4 queries near `base` (tier 2) + 28 random (tier 0).
+so tier 1 cannot certify). Batch of 32: M queries near `base` (tier 2; M = 4 by default, and
+16 / 32 with --marked) + 32 - M random (tier 0). Round 4: all marked queries of a pass share
+one rescan launch (csrc/scan_kernels.hip rescan_kernel).
 Reports the device time of one search call with and without the tier-2 queries, the tiers,
 and the ids of the tier-2 queries checked against an fp64 exact top-15 of the duplicate rows
 (the duplicates dominate every tier-2 query's top-15)."""
@@ -21,11 +23,11 @@ from ragmi.index import FlatIndex  # noqa: E402
 D, B, K = 384, 32, 15
 
 
-def run(n, every, reps=5):
+def run(n, every, reps=5, marked=4):
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev)
     g.manual_seed(11)
-    idx = FlatIndex(dim=D, capacity=n, device=dev)
+    idx = FlatIndex(dim=D, capacity=n, device=dev, diagnostic=True)
     base = torch.randn((1, D), generator=g, device=dev)
     chunk = 1 << 20
     dup_rows = []
@@ -38,8 +40,8 @@ def run(n, every, reps=5):
         dup_rows.append(rows[sel])
         idx.upsert(x, rows, new_count=r0 + m)
     dup_rows = torch.cat(dup_rows)
-    q_dup = base + 0.02 * torch.randn((4, D), generator=g, device=dev)
-    q_rnd = torch.randn((B - 4, D), generator=g, device=dev)
+    q_dup = base + 0.02 * torch.randn((marked, D), generator=g, device=dev)
+    q_rnd = torch.randn((B - marked, D), generator=g, device=dev)
     q_mix = torch.cat([q_dup, q_rnd])
     q_all_rnd = torch.randn((B, D), generator=g, device=dev)
 
@@ -65,9 +67,9 @@ def run(n, every, reps=5):
     import oracle_scan as O
     rows = dup_rows.cpu().numpy()
     stored = idx.export_rows(0, n).view(np.float16)[rows].astype(np.float64)
-    qn = O.normalize(q_mix[:4].cpu().numpy())
+    qn = O.normalize(q_mix[:marked].cpu().numpy())
     ok = 0
-    for j in range(4):
+    for j in range(marked):
         sc = (stored @ qn[j].astype(np.float64)).astype(np.float32)
         order = np.lexsort((rows, -sc.astype(np.float64)))[:K]
         ok += int(np.array_equal(rows[order], i[j].cpu().numpy()) and
@@ -75,12 +77,22 @@ def run(n, every, reps=5):
     idx.close()
     return {"rows": n, "duplicates": int(dup_rows.numel()), "dup_every": every,
             "search_ms_all_random": round(t_rnd, 4),
-            "search_ms_with_4_tier2_queries": round(t_mix, 4),
+            "marked": marked,
+            "search_ms_with_tier2_queries": round(t_mix, 4),
+            "tier2_added_ms": round(t_mix - t_rnd, 4),
+            "rescan_wg_knob": os.environ.get("RAGMI_RESCAN_WG"),
             "tier2_queries_per_call": int((t2b - t2a) / (reps + 1)),
             "tiers_first_8": tiers[:8].tolist(),
-            "tier2_ids_match_fp64_exact": f"{ok}/4"}
+            "tier2_ids_match_fp64_exact": f"{ok}/{marked}"}
 
 
 if __name__ == "__main__":
-    for n, every in ((1_250_000, 12), (10_000_000, 50)):
-        print(json.dumps(run(n, every)), flush=True)
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--marked", type=int, nargs="+", default=[4])
+    ap.add_argument("--rows", type=int, nargs="+", default=[1_250_000, 10_000_000])
+    a = ap.parse_args()
+    every = {1_250_000: 12, 10_000_000: 50}
+    for n in a.rows:
+        for m in a.marked:
+            print(json.dumps(run(n, every.get(n, 12), marked=m)), flush=True)

@@ -14,7 +14,7 @@ from ragmi.encoders import HEAD_POOLER_CLS, BertEncoder  # noqa: E402
 prec = os.environ.get("PREC", "fp16")
 reps = int(os.environ.get("REPS", "3"))
 dev = torch.device("cuda", 0)
-enc = BertEncoder(R.MINILM_CE, R.make_weights(R.MINILM_CE, 2), HEAD_POOLER_CLS, dev, prec)
+enc = BertEncoder(R.MINILM_CE, R.make_weights(R.MINILM_CE, 2), HEAD_POOLER_CLS, dev, prec, diagnostic=True)
 rng = np.random.default_rng(0)
 lens = rng.integers(200, 289, 480)
 ids = rng.integers(1000, 30000, int(lens.sum())).astype(np.int32)

@@ -26,7 +26,7 @@ def main():
     dev = torch.device("cuda:0")
     rng = np.random.default_rng(7)
     cfg = R.BGE_SMALL
-    enc = BertEncoder(cfg, R.make_weights(cfg, 1), HEAD_CLS_L2, dev, "fp16x3")
+    enc = BertEncoder(cfg, R.make_weights(cfg, 1), HEAD_CLS_L2, dev, "fp16x3", diagnostic=True)
     lens = rng.integers(16, 27, 32)
     ids = np.concatenate([rng.integers(1000, 30000, L).astype(np.int32) for L in lens])
     cu = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
@@ -42,7 +42,7 @@ def main():
         enc._L.rag_encoder_forward(enc._h, t_ids.data_ptr(), t_tt.data_ptr(), t_cu.data_ptr(),
                                    B, T, S, out.data_ptr(), st.cuda_stream)
 
-    idx = FlatIndex(384, capacity=1_000_000, device=dev)
+    idx = FlatIndex(384, capacity=1_000_000, device=dev, diagnostic=True)
     for c in range(4):
         x = torch.randn(250_000, 384, device=dev)
         idx.upsert(x, torch.arange(c * 250_000, (c + 1) * 250_000, device=dev))

@@ -49,7 +49,7 @@ def main():
         init_pg()
     from ragmi.dist import all_gather_packed
     from ragmi.index import FlatIndex, merge_topk_packed
-    idx = FlatIndex(bench.D, rows, dev)
+    idx = FlatIndex(bench.D, rows, dev, diagnostic=True)
     bench.build_shard(idx, 0, rows, rows, dev)
     qs, _ = bench.make_queries(warm + steps, rows, dev)
     if not no_pg and pg_mode == "late":

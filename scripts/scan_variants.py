@@ -32,7 +32,7 @@ def main():
     variants = [int(v) for v in os.environ.get("VARIANTS", "0,1,2,3,4,5,6").split(",")]
     rounds = int(os.environ.get("ROUNDS", "5"))
     dev = torch.device("cuda", 0)
-    idx = FlatIndex(bench.D, rows, dev)
+    idx = FlatIndex(bench.D, rows, dev, diagnostic=True)
     bench.build_shard(idx, 0, rows, rows, dev)
     qs, _ = bench.make_queries(1, rows, dev)
     res = {v: [] for v in variants}

@@ -70,3 +70,65 @@ def test_product_path_has_no_oracle_dependency():
             if f.endswith((".py", ".hip", ".hpp", ".h", ".cpp")):
                 text = open(os.path.join(dirpath, f), errors="ignore").read()
                 assert "oracle_scan" not in text and "liboracle" not in text, f
+
+
+KNOBS = ["RAGMI_SCAN_WGS", "RAGMI_RESCAN_WG", "RAGMI_SAMPLE_DIV", "RAGMI_WIDE_WGS",
+         "RAGMI_FUSED_PREP", "RAGMI_GEMM", "RAGMI_KSPLIT", "RAGMI_WS_PHASE", "RAGMI_DEFER_LN",
+         "RAGMI_CE_ROWS", "RAGMI_ATTN_VAR", "RAGMI_FUSE_LN", "RAGMI_SMALL_BK",
+         "RAGMI_SMALL_WIDE", "RAGMI_SMALL_WS", "RAGMI_ENC_GRAPH", "RAGMI_RESIDUAL_F32",
+         "RAGMI_ADDLN_VEC"]
+
+
+def test_ab_knobs_are_ignored_without_diagnostic_handle(libpath):
+    """a RAGMI_* kernel A/B variable set in a serving process (no handle
+    created with RAG_CREATE_DIAGNOSTIC) reads as the production default, and the library says
+    once on stderr that it ignored it. Run in a fresh process so the variables are seen at
+    load time; rag_knob_probe takes the same code path (ragmi::Knob) as every knob site."""
+    code = (
+        "import ctypes, sys\n"
+        f"L = ctypes.CDLL({libpath!r})\n"
+        "L.rag_knob_probe.argtypes = [ctypes.c_char_p, ctypes.c_int]\n"
+        "for n in sys.argv[1:]:\n"
+        "    print(n, L.rag_knob_probe(n.encode(), -7))\n")
+    env = dict(os.environ, **{k: "3" for k in KNOBS})
+    r = subprocess.run(["python3", "-c", code, *KNOBS], env=env, capture_output=True,
+                       text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    vals = dict(ln.split() for ln in r.stdout.splitlines())
+    assert all(vals[k] == "-7" for k in KNOBS), vals
+    for k in KNOBS:
+        assert f"{k}=3 ignored" in r.stderr, r.stderr
+    # unset variables are silent
+    r = subprocess.run(["python3", "-c", code, "RAGMI_SCAN_WGS"],
+                       env={k: v for k, v in os.environ.items() if not k.startswith("RAGMI_")},
+                       capture_output=True, text=True, timeout=60)
+    assert r.stdout.split() == ["RAGMI_SCAN_WGS", "-7"] and "ignored" not in r.stderr
+
+
+def test_every_env_knob_goes_through_the_gate():
+    """No kernel-switching getenv bypasses ragmi::Knob in the product sources."""
+    csrc = os.path.join(ROOT, "financial-rag-system_amd", "csrc")
+    for f in os.listdir(csrc):
+        text = open(os.path.join(csrc, f)).read()
+        if f == "common_host.hpp":
+            continue
+        assert "getenv" not in text, f"{f} reads the environment outside ragmi::Knob"
+
+
+def test_ring_kernels_launch_through_launch_fixed():
+    """the LDS-ring / fixed-wave kernels take their block size from the
+    constexpr their __launch_bounds__ uses (ragmi::launch_fixed); no launch site spells one."""
+    csrc = os.path.join(ROOT, "financial-rag-system_amd", "csrc")
+    ring = ("gemm_pipe_kernel", "gemm_ws_kernel", "scan_kernel", "scan_lds_kernel",
+            "scan_wide_kernel", "rescan_kernel", "attn_kernel")
+    for f in os.listdir(csrc):
+        text = open(os.path.join(csrc, f)).read()
+        for k in ring:
+            assert re.search(rf"\b{k}<[^;]*?>\s*<<<", text) is None, f"{f}: {k} launched by hand"
+    kern = open(os.path.join(csrc, "bert_kernels.hip")).read()
+    assert "__launch_bounds__(kPipeBlock<CFG>, 1) void gemm_pipe_kernel" in kern
+    assert "__launch_bounds__(kWsBlock<CFG>, 1) void gemm_ws_kernel" in kern
+    scan = open(os.path.join(csrc, "scan_kernels.hip")).read()
+    for b, k in (("kScanBlock, 2", "scan_kernel"), ("kLdsBlock, 1", "scan_lds_kernel"),
+                 ("kWideBlock, 1", "scan_wide_kernel"), ("kScanBlock, 2", "rescan_kernel")):
+        assert f"__launch_bounds__({b}) void {k}(" in scan

@@ -171,3 +171,50 @@ def test_second_pass_packed_output_and_shard_offset(gpu):
     p2 = idx.search_packed(q, 15, id_offset=off).cpu().numpy()
     np.testing.assert_array_equal(p2, p)
     idx.close()
+
+
+@pytest.mark.parametrize("dim,b", [(384, 20), (1024, 24)])
+def test_many_tier2_queries_share_the_second_pass(gpu, dim, b):
+    """Round 4: every marked query of a pass is served by the same rescan launch (16 per
+    stream of the shard, so 20 / 24 marked queries take two streams). Every query sits on a
+    saturated cluster, all are tier 2, and each top-k equals the exact oracle bit for bit."""
+    rng = np.random.default_rng(dim + b)
+    n = 160_000 if dim == 384 else 200_000   # (60K rows at D = 1024 stayed in tier 1)
+    base = rng.standard_normal((1, dim)).astype(np.float32)
+    x = rng.standard_normal((n, dim)).astype(np.float32)
+    x[::2] = base + 1e-5 * rng.standard_normal((n // 2, dim)).astype(np.float32)
+    q = base + 0.02 * rng.standard_normal((b, dim)).astype(np.float32)
+    idx = _index(gpu, x)
+    t1a, t2a, _ = idx.exactness_stats()
+    s, i = _search(idx, q, 15)
+    t1, t2, tiers = idx.exactness_stats(b)
+    assert (tiers == 2).all() and t2 - t2a == b, tiers
+    assert idx.unanswered() == 0
+    s2, i2 = O.search(idx.export_rows(), q, 15)
+    np.testing.assert_array_equal(i, i2)
+    np.testing.assert_array_equal(s, s2)
+    idx.close()
+
+
+@pytest.mark.parametrize("k", [15, 32])
+def test_second_pass_exact_duplicates_tie_by_row(gpu, k):
+    """Identical rows score identically: the rescan's per-wave lists, workgroup merges and the
+    last arriver's merge must keep the (score desc, row asc) order across all of them, i.e.
+    return the k lowest rows of the duplicate set."""
+    rng = np.random.default_rng(k)
+    n, dim = 120_000, 384
+    base = rng.standard_normal((1, dim)).astype(np.float32)
+    x = rng.standard_normal((n, dim)).astype(np.float32)
+    dup = np.sort(rng.choice(n, 40_000, replace=False))
+    x[dup] = base
+    q = np.concatenate([base + 0.01 * rng.standard_normal((3, dim)).astype(np.float32),
+                        rng.standard_normal((3, dim)).astype(np.float32)])
+    idx = _index(gpu, x)
+    s, i = _search(idx, q, k)
+    _, _, tiers = idx.exactness_stats(6)
+    s2, i2 = O.search(idx.export_rows(), q, k)
+    np.testing.assert_array_equal(i, i2)
+    np.testing.assert_array_equal(s, s2)
+    np.testing.assert_array_equal(i[:3], np.broadcast_to(dup[:k], (3, k)))
+    assert (tiers[:3] >= 1).all(), tiers
+    idx.close()

@@ -241,3 +241,26 @@ def test_native_vocab_rules(tmp_path):
     bad = b"[PAD]\n[CLS]\n[SEP]\n"
     with pytest.raises(_lib.RagmiError):
         _lib.check(L.rag_wordpiece_create(bad, len(bad), 512, 1, ctypes.byref(h)))
+
+
+def test_native_path_defers_literal_special_tokens(vocab_file):
+    """the Rust tokenizer maps a literal "[MASK]" / "[SEP]" / ... in the text to ONE
+    special-token id before normalisation; the native byte rules would split it into '[' word
+    ']'. Texts and pairs holding one go to the fallback, so ids match the Rust path."""
+    from ragmi.encoders import WordPiece
+    wp = WordPiece(vocab_file, 64)
+    texts = ["what is [MASK] here", "a [SEP] b", "[CLS][cls] Apple [UNK] inc [PAD]",
+             "plain text only", "[mask] lower and [Sep] mixed", "bracket [ MASK ] spaced",
+             "[MASKED] word", "net income"]
+    pairs = ["x [SEP] y", "plain", "q", "[PAD] pad [PAD]", "r", "s", "t", "[MASK]"]
+    a = wp.encode_packed(texts)
+    b = wp._encode_rust(texts)
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x, y)
+    a = wp.encode_packed(texts, pairs)
+    b = wp._encode_rust(texts, pairs)
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x, y)
+    # the special token really is one id on the Rust path (what the native split would miss)
+    ids = wp._encode_rust(["what is [MASK] here"])[0].tolist()
+    assert R.load_vocab(vocab_file)["[MASK]"] in ids
