@@ -120,7 +120,8 @@ def cpu_baseline(corpus16_sample: np.ndarray, q: np.ndarray, n_total: int, budge
                       f"scaled linearly to {n_total} rows"}
 
 
-def scan_traffic(rows_per_gpu: int, storage: str = "fp16", path: str | None = None):
+def scan_traffic(rows_per_gpu: int, storage: str = "fp16", path: str | None = None,
+                 kind: str = "scan_384"):
     """HBM bytes per scan launch from the committed rocprofv3 --pmc FETCH_SIZE passes
     (profiles/scan_pmc.json, written by scripts/profile.sh; x2 gfx950 correction), keyed by
     the rows one launch scans: a rank's shard of R rows runs the same launch as a 1-GPU run
@@ -131,9 +132,12 @@ def scan_traffic(rows_per_gpu: int, storage: str = "fp16", path: str | None = No
             p = json.load(f)
     except (OSError, ValueError):
         return None, None
-    table = dict(p.get("by_rows_per_gpu", {}))
-    if "hbm_bytes_per_launch" in p:                 # the headline pass (10M rows per GPU)
-        table.setdefault(str(p.get("rows_per_gpu", 10_000_000)), p)
+    if kind == "scan_384":
+        table = dict(p.get("by_rows_per_gpu", {}))
+        if "hbm_bytes_per_launch" in p:             # the headline pass (10M rows per GPU)
+            table.setdefault(str(p.get("rows_per_gpu", 10_000_000)), p)
+    else:                                           # wide_1024 (config 5), filtered_384
+        table = dict(p.get(f"by_rows_{kind}", {}))
     e = table.get(str(int(rows_per_gpu)))
     if storage != "fp16" or not e or e.get("hbm_bytes_per_launch") is None:
         return None, None
@@ -536,6 +540,10 @@ def main():
             "recall_at_5_vs_fp32_corpus_min": check and check["recall_at_5_vs_fp32_corpus_min"],
             "exactness_fallbacks": {"queries": B * args.steps, "tier1_list_rescoring": tier1,
                                     "tier2_second_pass": tier2},
+            # a diagnostic run (--diagnostic: the RAGMI_* kernel A/B knobs honoured) says which
+            # knobs it ran with; production lines carry null
+            "diagnostic_knobs": ({k: v for k, v in os.environ.items() if k.startswith("RAGMI_")}
+                                 if args.diagnostic else None),
             "roofline": {"bound": "hbm", "achieved": round(achieved / 1e9, 1),
                          "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK, 4),

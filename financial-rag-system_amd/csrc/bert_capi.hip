@@ -355,6 +355,24 @@ void launch_ws(const _Float16* A, const _Float16* Al, const _Float16* W, const _
                               Wl, bias, M, N, K, C, Clo, d);
 }
 
+// RAGMI_WS_BIG128=1 (diagnostic A/B, round 4): the large-batch WS GEMMs (plain AUTO picks and
+// the deferred-LN ones) on PipeBig128 — 4 MFMA waves of 128 x 64, one per SIMD beside its
+// loader wave (256 registers each), instead of PipeLarge's 8 of 64 x 64
+bool ws_big128() {
+  static ragmi::Knob k("RAGMI_WS_BIG128");
+  return k.get(0) == 1;
+}
+
+template <int EPI, bool SPLIT, int AUX = 0>
+void launch_ws_large(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float16* Wl,
+                     const float* bias, int M, int N, int K, void* C, _Float16* Clo,
+                     hipStream_t st, const DlArgs& dl = DlArgs{}) {
+  if (ws_big128())
+    launch_ws<EPI, SPLIT, PipeBig128, 0, AUX>(A, Al, W, Wl, bias, M, N, K, C, Clo, st, dl);
+  else
+    launch_ws<EPI, SPLIT, PipeLarge, 0, AUX>(A, Al, W, Wl, bias, M, N, K, C, Clo, st, dl);
+}
+
 // shapes the deferred-LayerNorm WS GEMMs take: Ln* (K = 384 input rows; c1 | c2 staged in the
 // 4096-float bias area) and ResLn (N = 384 output rows; bias | gamma | beta)
 bool dl_gemm_ok(int epi, int M, int N, int K) {
@@ -545,8 +563,8 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
       // 0.310 ms, the streamed 540 MB no longer evicting the A panels the n-tiles of an XCD
       // share); the fp32 ones (O / FFN2, read back at once by add_ln) keep the default policy
       constexpr int AX = EPI == kEpiF32 ? 0 : 2;
-      if (Al) launch_ws<EPI, true, PipeLarge, 0, AX>(A, Al, W, Wl, bias, M, N, K, C, Clo, st);
-      else launch_ws<EPI, false, PipeLarge, 0, AX>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st);
+      if (Al) launch_ws_large<EPI, true, AX>(A, Al, W, Wl, bias, M, N, K, C, Clo, st);
+      else launch_ws_large<EPI, false, AX>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st);
     }
     else if (variant == RAG_GEMM_WS_MFMA_ONLY) go(std::integral_constant<int, 7>{});
     else if (variant == RAG_GEMM_WS_NO_STORE) go(std::integral_constant<int, 6>{});
@@ -719,8 +737,8 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
       a.st_in = w->sb;
       a.c1 = L.qkv_c1;
       a.eps = c.layer_norm_eps;
-      launch_ws<kEpiLnF16, true, PipeLarge, 0, 2>(w->xh, w->xl, L.wqkv_f, L.wqkv_fl, L.qkv_c2, T,
-                                                  3 * H, H, w->qkv, w->qkv_l, st, a);
+      launch_ws_large<kEpiLnF16, true, 2>(w->xh, w->xl, L.wqkv_f, L.wqkv_fl, L.qkv_c2, T, 3 * H,
+                                          H, w->qkv, w->qkv_l, st, a);
     } else {
       gemm<kEpiF16>(w->xh, w->xl, L.wqkv, L.wqkv_l, L.bqkv, T, 3 * H, H, w->qkv, w->qkv_l, st);
     }
@@ -747,22 +765,22 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
       o.beta = P ? P->be2 : nullptr;
       o.st_out = w->sa;
       o.eps = c.layer_norm_eps;
-      launch_ws<kEpiResLn, true, PipeLarge>(w->ctx, w->ctx_l, L.wo, L.wo_l, L.bo, T, H, H, w->xh,
-                                            w->xl, st, o);
+      launch_ws_large<kEpiResLn, true>(w->ctx, w->ctx_l, L.wo, L.wo_l, L.bo, T, H, H, w->xh,
+                                       w->xl, st, o);
       DlArgs f;
       f.st_in = w->sa;
       f.c1 = L.w1_c1;
       f.eps = c.layer_norm_eps;
-      launch_ws<kEpiLnGeluF16, true, PipeLarge, 0, 2>(w->xh, w->xl, L.w1_f, L.w1_fl, L.w1_c2, T,
-                                                      FF, H, w->ff, w->ff_l, st, f);
+      launch_ws_large<kEpiLnGeluF16, true, 2>(w->xh, w->xl, L.w1_f, L.w1_fl, L.w1_c2, T, FF, H,
+                                              w->ff, w->ff_l, st, f);
       DlArgs r;
       r.st_in = w->sa;
       r.gamma = L.g1;
       r.beta = L.be1;
       r.st_out = w->sb;
       r.eps = c.layer_norm_eps;
-      launch_ws<kEpiResLn, true, PipeLarge>(w->ff, w->ff_l, L.w2, L.w2_l, L.bi2, T, H, FF, w->xh,
-                                            w->xl, st, r);
+      launch_ws_large<kEpiResLn, true>(w->ff, w->ff_l, L.w2, L.w2_l, L.bi2, T, H, FF, w->xh,
+                                       w->xl, st, r);
       continue;
     }
     // rows the rest of the layer runs on: all T tokens, or the B gathered CLS rows
@@ -1240,7 +1258,7 @@ int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, co
                      variant == RAG_GEMM_WS_NOROT || variant == RAG_GEMM_WS_READS_FIRST ||
                      variant == RAG_GEMM_WS_PRIO_LOAD || variant == RAG_GEMM_WS_PRIO_MFMA ||
                      variant == RAG_GEMM_WS_FLAGS || variant == RAG_GEMM_WS_NOHALF ||
-                     variant == RAG_GEMM_WS_SMALL || probe;
+                     variant == RAG_GEMM_WS_SMALL || variant == RAG_GEMM_WS_BIG128 || probe;
   if (!known || (probe && !pipe_ok(M, N, K)))
     return ragmi::fail(RAG_EINVAL, "unknown GEMM variant, or a probe on a non-pipe shape");
   auto* a = static_cast<const _Float16*>(A);
@@ -1477,11 +1495,11 @@ int rag_bert_gemm_dl(int epilogue, const void* A, const void* A_lo, const void* 
   auto* cl = static_cast<_Float16*>(C_lo);
   const auto st = static_cast<hipStream_t>(stream);
   if (epilogue == RAG_EPI_LN_F16)
-    launch_ws<kEpiLnF16, true, PipeLarge, 0, 2>(a, al, w, wl, bias, M, N, K, C, cl, st, d);
+    launch_ws_large<kEpiLnF16, true, 2>(a, al, w, wl, bias, M, N, K, C, cl, st, d);
   else if (epilogue == RAG_EPI_LN_GELU_F16)
-    launch_ws<kEpiLnGeluF16, true, PipeLarge, 0, 2>(a, al, w, wl, bias, M, N, K, C, cl, st, d);
+    launch_ws_large<kEpiLnGeluF16, true, 2>(a, al, w, wl, bias, M, N, K, C, cl, st, d);
   else
-    launch_ws<kEpiResLn, true, PipeLarge>(a, al, w, wl, bias, M, N, K, C, cl, st, d);
+    launch_ws_large<kEpiResLn, true>(a, al, w, wl, bias, M, N, K, C, cl, st, d);
   RAG_HIP(hipGetLastError());
   return RAG_OK;
 }

@@ -2256,6 +2256,19 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ p
 constexpr int kRescanMaxWG = 512;
 constexpr int kRescanQ = 16;   // marked queries per stream of the shard (one MFMA column tile)
 
+// the canonical butterfly of exact_tile_scores on a lane's 16 partials: sg ^ 8, 4, 2, 1 in the
+// lane, then lane ^ 32, lane ^ 16; fp32 rounding of the fp64 sum
+__device__ __forceinline__ float exact_tree(double (&p)[16]) {
+#pragma unroll
+  for (int d = 8; d > 0; d >>= 1) {
+#pragma unroll
+    for (int i = 0; i < d; ++i) p[i] = p[i] + p[i + d];
+  }
+  double y = p[0] + __shfl_xor(p[0], 32, 64);
+  y = y + __shfl_xor(y, 16, 64);
+  return (float)y;
+}
+
 // Canonical exact scores (exact_scores_pairs' arithmetic bit for bit) of the 16
 // rows of tile t against one normalised query qq, all rows at once. Lane (h, r) = (lane >> 4,
 // lane & 15) reads row 16t + r's chunks c = 4s + h: the tile16 image itself (fp16 storage) or
@@ -2286,7 +2299,7 @@ __device__ __forceinline__ float exact_tile_scores(const half8* __restrict__ cor
   // last fp64 sum, so its loads issue after this group's registers are consumed: left free,
   // the compiler hoisted every step's tile and query loads (S x 12 registers) to the top and
   // spilled (sched_barrier did not stop it). One L2 round trip per group.
-  constexpr int G = S % 6 == 0 && S <= 12 ? 6 : 2;
+  constexpr int G = 2;
 #pragma unroll
   for (int s0 = 0; s0 < S; s0 += G) {
     float x[G][8];
@@ -2322,14 +2335,49 @@ __device__ __forceinline__ float exact_tile_scores(const half8* __restrict__ cor
     }
     asm volatile("" : "+v"(zoff) : "v"(p[(s0 + G - 1) & 15]));
   }
+  return exact_tree(p);
+}
+
+// exact_tile_scores for D <= 384 with the tile already in registers (the scan-order image a
+// lane streamed: a[s] = row 16t + r, dims 32s + 8h .. +7 = chunk 4s + h) and the query as
+// fp64 in LDS (qd = its D values): no memory round trip besides the LDS reads. Groups of G
+// steps chained by the opaque asm dependency of exact_tile_scores (LDS reads hoisted above
+// the fp64 FMAs spilled the same way).
+template <int D>
+__device__ __forceinline__ float exact_tile_scores_reg(const half8 (&a)[steps<D>()],
+                                                       const double* qd, int lane) {
+  constexpr int S = steps<D>();
+  static_assert(S <= 16, "one chunk per canonical lane");
+  const int h = lane >> 4;
+  double p[16];
 #pragma unroll
-  for (int d = 8; d > 0; d >>= 1) {
+  for (int i = 0; i < 16; ++i) p[i] = 0.0;
+  int zoff = 0;
+  asm volatile("" : "+v"(zoff));
+  constexpr int G = 2;
 #pragma unroll
-    for (int i = 0; i < d; ++i) p[i] = p[i] + p[i + d];
+  for (int s0 = 0; s0 < S; s0 += G) {
+    double2 qv[G][4];
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        qv[g][i] = *reinterpret_cast<const double2*>(qd + 32 * (s0 + g) + 8 * h + 2 * i + zoff);
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      half8 v = a[s0 + g];
+      asm volatile("" : "+v"(v));   // per call: no fp32 / fp64 copy of the tile hoisted
+      double x = 0.0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        x = fma((double)(float)v[2 * i], qv[g][i].x, x);
+        x = fma((double)(float)v[2 * i + 1], qv[g][i].y, x);
+      }
+      p[s0 + g] = x;
+    }
+    asm volatile("" : "+v"(zoff) : "v"(p[s0 + G - 1]));
   }
-  double y = p[0] + __shfl_xor(p[0], 32, 64);
-  y = y + __shfl_xor(y, 16, 64);
-  return (float)y;
+  return exact_tree(p);
 }
 
 template <int D, bool FILTER>
@@ -2342,12 +2390,17 @@ __global__ __launch_bounds__(kScanBlock, 2) void rescan_kernel(
     int64_t id_offset, float* __restrict__ out_s, int64_t* __restrict__ out_i,
     int32_t* __restrict__ out_packed, const float* __restrict__ rows32) {
   constexpr int S = steps<D>();
-  constexpr int CS = S >= 16 ? 8 : S / 2;   // k-steps per streamed chunk (384: 6, 1024: 8)
-  constexpr int NCH = S / CS;               // chunks per tile: even, so every tile's chunk 0
-  static_assert(S % CS == 0 && NCH % 2 == 0, "two-slot chunk ring");   // lands in slot 0
+  // D <= 384: a whole tile per chunk (48 registers) in a two-slot ring, and fp16-storage exact
+  // scores straight from those registers with the queries in LDS as fp64 (exact_tile_scores_reg);
+  // D = 1024: chunks of 8 k-steps and the exact scores from an L2 re-read (exact_tile_scores)
+  constexpr bool REG = S <= 12;
+  constexpr int CS = REG ? S : 8;          // k-steps per streamed chunk
+  constexpr int NCH = S / CS;              // chunks per tile: 1, or even (two-slot ring)
+  static_assert(S % CS == 0 && (NCH == 1 || NCH % 2 == 0), "two-slot chunk ring");
   __shared__ half8 bl[S * 64];                         // B-fragments of the marked queries
   __shared__ float ws[kWavesPerWG][kRescanQ][kKS];     // per-wave running exact top-32s
   __shared__ int wi[kWavesPerWG][kRescanQ][kKS];
+  __shared__ double qd[REG ? kRescanQ * D : 2];        // marked queries' qn as fp64 (REG)
   __shared__ int fq[128];                              // marked queries, ascending
   __shared__ int last;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -2383,8 +2436,8 @@ __global__ __launch_bounds__(kScanBlock, 2) void rescan_kernel(
 
   for (int qb = 0; qb < nf; qb += kRescanQ) {
     const int nq = min(kRescanQ, nf - qb);
-    __syncthreads();   // fq written; the previous stream's list reads done
-    for (int idx = tid; idx < S * 64; idx += 256) {
+    __syncthreads();   // fq written; the previous stream's LDS reads done
+    for (int idx = tid; idx < S * 64; idx += kScanBlock) {
       const int jj = idx & 15;
       half8 v = {};
       if (jj < nq) {
@@ -2393,6 +2446,9 @@ __global__ __launch_bounds__(kScanBlock, 2) void rescan_kernel(
       }
       bl[idx] = v;
     }
+    if constexpr (REG)
+      for (int idx = tid; idx < nq * D; idx += kScanBlock)
+        qd[idx] = (double)qn[(int64_t)fq[qb + idx / D] * D + idx % D];
 #pragma unroll
     for (int e = 0; e < kRescanQ * kKS / 64; ++e) {
       (&ws[wid][0][0])[lane + 64 * e] = kNegInf;
@@ -2411,85 +2467,118 @@ __global__ __launch_bounds__(kScanBlock, 2) void rescan_kernel(
     float band = live ? fmaxf(L, thr - ej) : __builtin_inff();
     __syncthreads();
 
+    // one tile's MFMA scores -> its marked-query candidates (cur: the tile's registers, REG)
+    auto candidates = [&](const floatx4& acc, int t, const half8* cur)
+                          __attribute__((always_inline)) {
+      // rows 16t + 4(lane >> 4) + i of column j: any inside j's band?
+      const int rbase = t * kTileRows + 4 * (lane >> 4);
+      uint4 tg = {0u, 0u, 0u, 0u};
+      if constexpr (FILTER) tg = *reinterpret_cast<const uint4*>(tags + rbase);
+      bool hit = false;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        bool ok = rbase + i < n_rows && acc[i] >= band;
+        if constexpr (FILTER) {
+          const uint32_t tr = i == 0 ? tg.x : i == 1 ? tg.y : i == 2 ? tg.z : tg.w;
+          ok = ok && ((tr & fm) == fv);
+        }
+        hit = hit || ok;
+      }
+      const uint64_t bm = __ballot(hit);
+      uint32_t qm = (uint32_t)((bm | (bm >> 16) | (bm >> 32) | (bm >> 48)) & 0xffffu);
+      if (!qm) return;
+      const int row = t * kTileRows + j;      // lanes 0..15 carry row 16t + lane below
+      uint32_t rt = 0;
+      if constexpr (FILTER) rt = tags[row < n_rows ? row : 0];
+      while (qm) {
+        const int c = __builtin_ctz(qm);
+        qm &= qm - 1;
+        const float tc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(thr), c));
+        float e;
+        const int q = __builtin_amdgcn_readlane(qj, c);
+        if (rows32) {
+          e = exact_tile_scores<D, true>(corpus, rows32, t, qn + (int64_t)q * D, lane);
+        } else {
+          if constexpr (REG)
+            e = exact_tile_scores_reg<D>(*reinterpret_cast<const half8(*)[S]>(cur), qd + c * D,
+                                         lane);
+          else
+            e = exact_tile_scores<D, false>(corpus, rows32, t, qn + (int64_t)q * D, lane);
+        }
+        bool cand = lane < 16 && row < n_rows && e > tc;
+        if constexpr (FILTER) {
+          const uint32_t fmc = __builtin_amdgcn_readlane(fm, c);
+          const uint32_t fvc = __builtin_amdgcn_readlane(fv, c);
+          cand = cand && ((rt & fmc) == fvc);
+        }
+        if (!__ballot(cand)) continue;
+        float s = cand ? e : kNegInf;
+        int id = cand ? row : kIdNone32;
+        if (lane >= 32) {
+          s = ws[wid][c][lane - 32];
+          id = wi[wid][c][lane - 32];
+        }
+        lds_fence();
+        bitonic_sort64(s, id, lane);
+        if (lane < 32) {
+          ws[wid][c][lane] = s;
+          wi[wid][c][lane] = id;
+        }
+        lds_fence();
+        const float nt = __shfl(s, 31, 64);
+        if (j == c) {
+          thr = fmaxf(thr, nt);
+          band = fmaxf(L, thr - ej);
+        }
+      }
+    };
+
     if (n_mine > 0) {
       half8 ra[CS], rb[CS];
-      load(ra, t_first, 0);
-      for (int jt = 0; jt < n_mine; ++jt) {
-        const int t = t_first + jt * t_step;
-        const int tn = t_first + min(jt + 1, n_mine - 1) * t_step;
-        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (NCH == 1) {
+        // whole tiles, slots alternating per tile (REG)
+        auto tile_of = [&](int jt) { return t_first + min(jt, n_mine - 1) * t_step; };
+        auto score = [&](const half8(&a)[CS]) __attribute__((always_inline)) {
+          floatx4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int c = 0; c < NCH; ++c) {
-          if (c % 2 == 0) {
-            load(rb, t, c + 1);
-#pragma unroll
-            for (int s = 0; s < CS; ++s)
-              acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ra[s], bl[(c * CS + s) * 64 + lane],
-                                                           acc, 0, 0, 0);
-          } else {
-            if (c + 1 < NCH)
-              load(ra, t, c + 1);
-            else
-              load(ra, tn, 0);
-#pragma unroll
-            for (int s = 0; s < CS; ++s)
-              acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(rb[s], bl[(c * CS + s) * 64 + lane],
-                                                           acc, 0, 0, 0);
-          }
+          for (int s = 0; s < CS; ++s)
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[s], bl[s * 64 + lane], acc, 0, 0, 0);
+          return acc;
+        };
+        load(ra, t_first, 0);
+        for (int jt = 0; jt < n_mine; jt += 2) {
+          load(rb, tile_of(jt + 1), 0);
+          candidates(score(ra), tile_of(jt), ra);
+          if (jt + 1 >= n_mine) break;
+          load(ra, tile_of(jt + 2), 0);
+          candidates(score(rb), tile_of(jt + 1), rb);
         }
-        // rows 16t + 4(lane >> 4) + i of column j: any inside j's band?
-        const int rbase = t * kTileRows + 4 * (lane >> 4);
-        uint4 tg = {0u, 0u, 0u, 0u};
-        if constexpr (FILTER) tg = *reinterpret_cast<const uint4*>(tags + rbase);
-        bool hit = false;
+      } else {
+        load(ra, t_first, 0);
+        for (int jt = 0; jt < n_mine; ++jt) {
+          const int t = t_first + jt * t_step;
+          const int tn = t_first + min(jt + 1, n_mine - 1) * t_step;
+          floatx4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          bool ok = rbase + i < n_rows && acc[i] >= band;
-          if constexpr (FILTER) {
-            const uint32_t tr = i == 0 ? tg.x : i == 1 ? tg.y : i == 2 ? tg.z : tg.w;
-            ok = ok && ((tr & fm) == fv);
+          for (int c = 0; c < NCH; ++c) {
+            if (c % 2 == 0) {
+              load(rb, t, c + 1);
+#pragma unroll
+              for (int s = 0; s < CS; ++s)
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ra[s], bl[(c * CS + s) * 64 + lane],
+                                                             acc, 0, 0, 0);
+            } else {
+              if (c + 1 < NCH)
+                load(ra, t, c + 1);
+              else
+                load(ra, tn, 0);
+#pragma unroll
+              for (int s = 0; s < CS; ++s)
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(rb[s], bl[(c * CS + s) * 64 + lane],
+                                                             acc, 0, 0, 0);
+            }
           }
-          hit = hit || ok;
-        }
-        const uint64_t bm = __ballot(hit);
-        uint32_t qm = (uint32_t)((bm | (bm >> 16) | (bm >> 32) | (bm >> 48)) & 0xffffu);
-        if (!qm) continue;
-        const int row = t * kTileRows + j;      // lanes 0..15 carry row 16t + lane below
-        uint32_t rt = 0;
-        if constexpr (FILTER) rt = tags[row < n_rows ? row : 0];
-        while (qm) {
-          const int c = __builtin_ctz(qm);
-          qm &= qm - 1;
-          const int q = __builtin_amdgcn_readlane(qj, c);
-          const float tc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(thr), c));
-          const float e =
-              rows32 ? exact_tile_scores<D, true>(corpus, rows32, t, qn + (int64_t)q * D, lane)
-                     : exact_tile_scores<D, false>(corpus, rows32, t, qn + (int64_t)q * D, lane);
-          bool cand = lane < 16 && row < n_rows && e > tc;
-          if constexpr (FILTER) {
-            const uint32_t fmc = __builtin_amdgcn_readlane(fm, c);
-            const uint32_t fvc = __builtin_amdgcn_readlane(fv, c);
-            cand = cand && ((rt & fmc) == fvc);
-          }
-          if (!__ballot(cand)) continue;
-          float s = cand ? e : kNegInf;
-          int id = cand ? row : kIdNone32;
-          if (lane >= 32) {
-            s = ws[wid][c][lane - 32];
-            id = wi[wid][c][lane - 32];
-          }
-          lds_fence();
-          bitonic_sort64(s, id, lane);
-          if (lane < 32) {
-            ws[wid][c][lane] = s;
-            wi[wid][c][lane] = id;
-          }
-          lds_fence();
-          const float nt = __shfl(s, 31, 64);
-          if (j == c) {
-            thr = fmaxf(thr, nt);
-            band = fmaxf(L, thr - ej);
-          }
+          candidates(acc, t, nullptr);
         }
       }
     }

@@ -677,6 +677,11 @@ def run_search(args, mode):
     if rank == 0:
         per_row = D * 2 + (4 if mode == "filtered" else 0)
         algo = (hi - lo) * per_row
+        # HBM bytes per launch from a committed rocprofv3 --pmc FETCH_SIZE pass of the same
+        # launch size (scripts/pmc_table.py; not measured inside this run)
+        from bench import scan_traffic
+        traffic, traffic_source = scan_traffic(hi - lo, "fp16",
+                                               kind="wide_1024" if mode == "5" else "filtered_384")
         ach = algo / (busy * 1e-3)
         kern = ("scan_wide_kernel<1024,0,true>" if mode == "5" else
                 "scan_kernel<384,true>")
@@ -696,8 +701,8 @@ def run_search(args, mode):
              "parallelism": f"corpus-shard{world}", "batches_in_flight": n_streams,
              "scan_order": "serial" if serial else "free"},
             roofline={"bound": "hbm", "achieved": round(ach / 1e9, 1), "peak": HBM_PEAK / 1e9,
-                      "unit": "GB/s", "frac": round(ach / HBM_PEAK, 4), "traffic": None,
-                      "kernel": kern,
+                      "unit": "GB/s", "frac": round(ach / HBM_PEAK, 4), "traffic": traffic,
+                      "traffic_source": traffic_source, "kernel": kern,
                       "time_basis": ("union of the scan launches' HIP-event intervals over "
                                      "the timed region / launches" if n_streams > 1 and
                                      not serial else "average scan launch duration (HIP "

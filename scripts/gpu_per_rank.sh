@@ -5,7 +5,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out; out=gpurun_out/per_rank.jsonl; : > $out
 for rows in 5000000 2500000 1250000; do
-  RAGMI_DIST_REHEARSAL=1 timeout -k 10 300 python3 -u bench.py --rows $rows --steps 200 --warmup 10 --no-cpu 2> gpurun_out/pr.err | grep '^{' >> $out || { tail -20 gpurun_out/pr.err; exit 1; }
+  RAGMI_DIST_REHEARSAL=1 timeout -k 10 300 python3 -u bench.py --rows $rows --steps 200 --warmup 10 2> gpurun_out/pr.err | grep '^{' >> $out || { tail -20 gpurun_out/pr.err; exit 1; }
 done
 timeout -k 10 400 python3 -u bench.py --config 5 --rows 6250000 --no-cpu 2> gpurun_out/pr5.err | grep '^{' >> $out || { tail -20 gpurun_out/pr5.err; exit 1; }
 python3 -c "

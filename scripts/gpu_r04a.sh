@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out; O=gpurun_out
 timeout -k 10 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread \
   tests/test_exactness_gpu.py tests/test_storage32_gpu.py tests/test_scan_gpu.py \
-  tests/test_encoder_graph_gpu.py tests/test_gemm_exact_gpu.py tests/test_attention_gpu.py > $O/t_exact.log 2>&1 \
+  tests/test_encoder_graph_gpu.py tests/test_attention_gpu.py > $O/t_exact.log 2>&1 \
   || { tail -40 $O/t_exact.log; exit 1; }
 tail -3 $O/t_exact.log
 timeout -k 10 300 python3 -u scripts/bench_tier2.py --marked 4 16 32 > $O/tier2.jsonl 2> $O/tier2.err \
