@@ -56,9 +56,19 @@ def main():
                     "hbm_bytes_per_launch": kb * 1024 * 2,
                     "note": "FETCH_SIZE (kB) x 1024 x 2: gfx950 reports half the bytes of "
                             "16 B/lane streaming reads (MI355X_MICROARCH.md §HBM)"})
-        json.dump({"hbm_bytes_per_launch": kb * 1024 * 2, "source": f"profiles/{tag}_pmc_fetch_size.csv",
-                   "fetch_size_kB_raw": kb, "commit": os.environ.get("COMMIT", "")},
-                  open(os.path.join(out, "scan_pmc.json"), "w"), indent=1)
+        # headline entry updated in place: the by-rows / by-kind tables of earlier passes
+        # (scripts/pmc_table.py) are kept
+        path = os.path.join(out, "scan_pmc.json")
+        base = os.path.join(ROOT, "profiles", "scan_pmc.json")
+        table = {}
+        for src in (path, base):
+            if os.path.exists(src):
+                table = json.load(open(src))
+                break
+        table.update({"hbm_bytes_per_launch": kb * 1024 * 2,
+                      "source": f"profiles/{tag}_pmc_fetch_size.csv",
+                      "fetch_size_kB_raw": kb, "commit": os.environ.get("COMMIT", "")})
+        json.dump(table, open(path, "w"), indent=1)
     if bench_log and os.path.exists(bench_log):
         lines = [l for l in open(bench_log) if l.startswith("{")]
         if lines:
