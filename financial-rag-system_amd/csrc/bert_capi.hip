@@ -550,7 +550,8 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
       variant == RAG_GEMM_WS_PROBE_NO_A_READS || variant == RAG_GEMM_WS_PROBE_NO_W_READS ||
       variant == RAG_GEMM_WS_PRIO_LOAD || variant == RAG_GEMM_WS_PRIO_MFMA ||
       variant == RAG_GEMM_WS_FLAGS || variant == RAG_GEMM_WS_NOHALF ||
-      variant == RAG_GEMM_WS_BIG128) {
+      variant == RAG_GEMM_WS_BIG128 || variant == RAG_GEMM_WS_BIG128_MFMA_ONLY ||
+      variant == RAG_GEMM_WS_BIG128_DMA_ONLY || variant == RAG_GEMM_WS_BIG128_NO_STORE) {
     // probes keep production's store policy (nt for fp16 outputs) since round 2's r02h runs
     auto go = [&](auto pc) {
       constexpr int P = decltype(pc)::value;
@@ -575,10 +576,18 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
     else if (variant == RAG_GEMM_WS_PRIO_LOAD) go(std::integral_constant<int, 16>{});
     else if (variant == RAG_GEMM_WS_PRIO_MFMA) go(std::integral_constant<int, 17>{});
     else if (variant == RAG_GEMM_WS_NOHALF) go(std::integral_constant<int, 19>{});
-    else if (variant == RAG_GEMM_WS_BIG128) {
+    else if (variant == RAG_GEMM_WS_BIG128 || variant == RAG_GEMM_WS_BIG128_MFMA_ONLY ||
+             variant == RAG_GEMM_WS_BIG128_DMA_ONLY || variant == RAG_GEMM_WS_BIG128_NO_STORE) {
       constexpr int AX = EPI == kEpiF32 ? 0 : 2;
-      if (Al) launch_ws<EPI, true, PipeBig128, 0, AX>(A, Al, W, Wl, bias, M, N, K, C, Clo, st);
-      else launch_ws<EPI, false, PipeBig128, 0, AX>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st);
+      auto gb = [&](auto pc) {
+        constexpr int P = decltype(pc)::value;
+        if (Al) launch_ws<EPI, true, PipeBig128, P, AX>(A, Al, W, Wl, bias, M, N, K, C, Clo, st);
+        else launch_ws<EPI, false, PipeBig128, P, AX>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st);
+      };
+      if (variant == RAG_GEMM_WS_BIG128) gb(std::integral_constant<int, 0>{});
+      else if (variant == RAG_GEMM_WS_BIG128_MFMA_ONLY) gb(std::integral_constant<int, 7>{});
+      else if (variant == RAG_GEMM_WS_BIG128_DMA_ONLY) gb(std::integral_constant<int, 8>{});
+      else gb(std::integral_constant<int, 6>{});
     }
     else if (variant == RAG_GEMM_WS_FLAGS) {
       // the ring counters sit in the last 16 floats of the staged-vector area
@@ -1258,7 +1267,10 @@ int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, co
                      variant == RAG_GEMM_WS_NOROT || variant == RAG_GEMM_WS_READS_FIRST ||
                      variant == RAG_GEMM_WS_PRIO_LOAD || variant == RAG_GEMM_WS_PRIO_MFMA ||
                      variant == RAG_GEMM_WS_FLAGS || variant == RAG_GEMM_WS_NOHALF ||
-                     variant == RAG_GEMM_WS_SMALL || variant == RAG_GEMM_WS_BIG128 || probe;
+                     variant == RAG_GEMM_WS_SMALL || variant == RAG_GEMM_WS_BIG128 ||
+                     variant == RAG_GEMM_WS_BIG128_MFMA_ONLY ||
+                     variant == RAG_GEMM_WS_BIG128_DMA_ONLY ||
+                     variant == RAG_GEMM_WS_BIG128_NO_STORE || probe;
   if (!known || (probe && !pipe_ok(M, N, K)))
     return ragmi::fail(RAG_EINVAL, "unknown GEMM variant, or a probe on a non-pipe shape");
   auto* a = static_cast<const _Float16*>(A);

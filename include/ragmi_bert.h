@@ -136,7 +136,9 @@ enum { RAG_GEMM_AUTO = 0, RAG_GEMM_TILE = 1, RAG_GEMM_PIPE = 2, RAG_GEMM_PROBE_N
        RAG_GEMM_WS_NT = 24, RAG_GEMM_WS_NOROT = 26, RAG_GEMM_WS_READS_FIRST = 27,
        RAG_GEMM_WS_PROBE_NO_A_READS = 28, RAG_GEMM_WS_PROBE_NO_W_READS = 29,
        RAG_GEMM_WS_PRIO_LOAD = 30, RAG_GEMM_WS_PRIO_MFMA = 31, RAG_GEMM_WS_FLAGS = 32,
-       RAG_GEMM_WS_NOHALF = 33, RAG_GEMM_WS_SMALL = 34, RAG_GEMM_WS_BIG128 = 35 };
+       RAG_GEMM_WS_NOHALF = 33, RAG_GEMM_WS_SMALL = 34, RAG_GEMM_WS_BIG128 = 35,
+       RAG_GEMM_WS_BIG128_MFMA_ONLY = 36, RAG_GEMM_WS_BIG128_DMA_ONLY = 37,
+       RAG_GEMM_WS_BIG128_NO_STORE = 38 };
 int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, const void* W,
                   const void* W_lo, const float* bias, int M, int N, int K, void* C,
                   void* C_lo, void* stream);
