@@ -1391,9 +1391,13 @@ __global__ __launch_bounds__(kWsBlock<CFG>, 1) void gemm_ws_kernel(
   constexpr int STAGE_H8 = NPL * (A_H8 + W_H8);
   constexpr int LA = A_H8 / LTH, LW = W_H8 / LTH;  // DMAs per loader wave per plane
   constexpr int L = NPL * (LA + LW);               // DMAs per loader wave per stage
-  constexpr bool P_NO_MFMA = PROBE == 1 || PROBE == 8;
+  constexpr bool P_NO_MFMA = PROBE == 1 || PROBE == 8 || PROBE == 23;
   constexpr bool P_NO_DMA = PROBE == 2 || PROBE == 7;
-  constexpr bool P_NO_STORE = PROBE == 6 || PROBE == 7 || PROBE == 8;
+  constexpr bool P_NO_STORE = PROBE == 6 || PROBE == 7 || PROBE == 8 || PROBE == 23;
+  // PROBE 22 / 23 (round 4, A/B): the loader waves stage through registers (buffer_load to
+  // VGPRs one K step ahead, then ds_write_b128 into the ring slot) instead of LDS-DMA; 23 =
+  // the same without MFMAs and stores (the intake alone, as PROBE 8 for the DMA path)
+  constexpr bool REGST = PROBE == 22 || PROBE == 23;
   constexpr int OUT_B = EPI == kEpiF32 ? 4 : 2;
   static_assert(A_H8 % LTH == 0 && W_H8 % LTH == 0 && FN % 2 == 0, "tile shape");
   static_assert((NS - 2) * L <= 63, "vmcnt range");
@@ -1488,6 +1492,68 @@ __global__ __launch_bounds__(kWsBlock<CFG>, 1) void gemm_ws_kernel(
     }
     int it_i = 0, kt_i = 0, kr_i = 0, slot_i = 0;
     __amdgpu_buffer_rsrc_t rA0 = panel(A, 0), rA1 = rA0, rW0 = rA0, rW1 = rA0;
+    if constexpr (REGST) {
+      u32x4 rb0[L], rb1[L];
+      auto load_stage = [&](u32x4 (&r)[L]) __attribute__((always_inline)) {
+        if (it_i >= n_mine) return;
+        if (kt_i == 0) {
+          int m0, nt, m_end;
+          tile_mn(it_i, m0, nt, m_end);
+          const int n0 = nt * BN;
+          kr_i = aligned ? 0 : nt % nk;
+          const int64_t abytes = (int64_t)(m_end - m0) * K * 2, wbytes = (int64_t)BN * K * 2;
+          rA0 = panel(A + (int64_t)m0 * K, abytes);
+          rW0 = panel(W + (int64_t)n0 * K, wbytes);
+          if constexpr (SPLIT) {
+            rA1 = panel(Al + (int64_t)m0 * K, abytes);
+            rW1 = panel(Wl + (int64_t)n0 * K, wbytes);
+          }
+        }
+        const uint32_t soff = __builtin_amdgcn_readfirstlane((uint32_t)kr_i * (BK * 2));
+        if (++kr_i == nk) kr_i = 0;
+#pragma unroll
+        for (int i = 0; i < LA; ++i) {
+          r[i * NPL] = __builtin_amdgcn_raw_buffer_load_b128(rA0, voA[i], soff, 0);
+          if constexpr (SPLIT) r[i * NPL + 1] = __builtin_amdgcn_raw_buffer_load_b128(rA1, voA[i], soff, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < LW; ++i) {
+          r[NPL * LA + i * NPL] = __builtin_amdgcn_raw_buffer_load_b128(rW0, voW[i], soff, 0);
+          if constexpr (SPLIT)
+            r[NPL * LA + i * NPL + 1] = __builtin_amdgcn_raw_buffer_load_b128(rW1, voW[i], soff, 0);
+        }
+        if (++kt_i == nk) { kt_i = 0; ++it_i; }
+      };
+      // stage g's registers -> ring slot g % NS, then the step's barrier. The slot was last
+      // read at step g - NS, whose reads every MFMA wave finished before barrier g - NS + 1.
+      auto write_stage = [&](const u32x4 (&r)[L]) __attribute__((always_inline)) {
+        u32x4* base = reinterpret_cast<u32x4*>(lds + slot_i * STAGE_H8);
+#pragma unroll
+        for (int i = 0; i < LA; ++i) {
+          base[(lw * LA + i) * 64 + lane] = r[i * NPL];
+          if constexpr (SPLIT) base[A_H8 + (lw * LA + i) * 64 + lane] = r[i * NPL + 1];
+        }
+#pragma unroll
+        for (int i = 0; i < LW; ++i) {
+          base[NPL * A_H8 + (lw * LW + i) * 64 + lane] = r[NPL * LA + i * NPL];
+          if constexpr (SPLIT)
+            base[NPL * A_H8 + W_H8 + (lw * LW + i) * 64 + lane] = r[NPL * LA + i * NPL + 1];
+        }
+        if (++slot_i == NS) slot_i = 0;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      };
+      load_stage(rb0);
+      for (int g = 0; g < steps; g += 2) {
+        load_stage(rb1);                  // stage g + 1 in flight while stage g is written
+        write_stage(rb0);
+        if (g + 1 >= steps) break;
+        load_stage(rb0);
+        write_stage(rb1);
+      }
+      return;
+    }
     auto issue_next = [&]() __attribute__((always_inline)) {
       if (it_i >= n_mine) return;
       if constexpr (P_NO_DMA) {
@@ -1557,6 +1623,7 @@ __global__ __launch_bounds__(kWsBlock<CFG>, 1) void gemm_ws_kernel(
   // (declared outside the step loop only so the PROBE 14 / 15 timing probes can keep stale
   // fragments: every production step overwrites them all before use)
   half8 af[KSN][NPL][FM], wf[KSN][NPL][FN];
+  half8 a_st[FM], w_st[FN];   // PROBE 21: the even step's lo16 fragments
   // deferred LN: the current tile's row statistics, loaded right after the previous tile's
   // epilogue (a whole tile before they are used; loaded at the tile's first K step instead, the
   // compiler's waitcnt model put a vmcnt(0) there — a wait for the previous tile's stores)
@@ -1608,6 +1675,29 @@ __global__ __launch_bounds__(kWsBlock<CFG>, 1) void gemm_ws_kernel(
             wf[ks][p][j] = sw[p * W_H8 + swz<CPR>(wc * WTN + j * 16 + (lane & 15), ks * 4 + (lane >> 4))];
     };
     auto mma = [&](int ks, int i, int j) __attribute__((always_inline)) {
+      if constexpr (PROBE == 20) {   // timing: the hi x hi MFMA alone (fp16x3 bytes and reads)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[ks][0][j], af[ks][0][i], acc[i][j], 0, 0, 0);
+        return;
+      }
+      if constexpr (PROBE == 21) {
+        // timing: hi x hi per step + the two correction products of 2 steps as ONE block-scaled
+        // fp8 MFMA (16x16x128: 2 K steps x [A_hi8 | A_lo8] . [W_lo8 ; W_hi8]); the lo16
+        // fragments of the even step stand in for the fp8 ones (same LDS bytes)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[ks][0][j], af[ks][0][i], acc[i][j], 0, 0, 0);
+        if (kt_c & 1) {
+          typedef int i4 __attribute__((ext_vector_type(4)));
+          typedef int i8 __attribute__((ext_vector_type(8)));
+          const i8 a8 = __builtin_shufflevector(__builtin_bit_cast(i4, a_st[i]),
+                                                __builtin_bit_cast(i4, af[ks][1][i]),
+                                                0, 1, 2, 3, 4, 5, 6, 7);
+          const i8 w8 = __builtin_shufflevector(__builtin_bit_cast(i4, w_st[j]),
+                                                __builtin_bit_cast(i4, wf[ks][1][j]),
+                                                0, 1, 2, 3, 4, 5, 6, 7);
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(w8, a8, acc[i][j], 0, 0,
+                                                                       0, 127, 0, 127);
+        }
+        return;
+      }
       if constexpr (!P_NO_MFMA) {
         if constexpr (SPLIT) {   // small terms first: W_lo A_hi + W_hi A_lo + W_hi A_hi
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[ks][1][j], af[ks][0][i], acc[i][j], 0, 0, 0);
@@ -1645,6 +1735,13 @@ __global__ __launch_bounds__(kWsBlock<CFG>, 1) void gemm_ws_kernel(
   #pragma unroll
             for (int j = 0; j < FN; ++j) mma(ks, i, j);
         }
+        if constexpr (PROBE == 21)
+          if (!(kt_c & 1)) {
+#pragma unroll
+            for (int i = 0; i < FM; ++i) a_st[i] = af[0][1][i];
+#pragma unroll
+            for (int j = 0; j < FN; ++j) w_st[j] = wf[0][1][j];
+          }
       } else {
         if constexpr (!P_NO_MFMA) {
   #pragma unroll

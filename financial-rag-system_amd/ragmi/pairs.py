@@ -14,9 +14,11 @@ longest pair, ready for BertEncoder.forward_device.
 
 build_pairs_gpu: the production form — two HIP kernels (rag_build_pairs: lengths + scan,
 then one workgroup per pair) and one 8-byte read-back of {T, longest} (the forward's launch
-grids need T on the host). build_pairs: the same assembly in pure torch ops (works on CPU
-tensors too, which is how tests/test_pairs_cpu.py checks it against a per-pair loop; the GPU
-test checks build_pairs_gpu against it bit for bit).
+grids need T on the host). build_pairs_gpu_async moves that read-back off the critical path:
+the 8 bytes go to pinned memory behind an event and the caller collects them after it has
+enqueued the next batch. build_pairs: the same assembly in pure torch ops
+(works on CPU tensors too, which is how tests/test_pairs_cpu.py checks it against a per-pair
+loop; the GPU test checks build_pairs_gpu against it bit for bit).
 """
 from __future__ import annotations
 
@@ -57,9 +59,26 @@ def build_pairs(q_ids, q_cu, rows, c_toks, c_lens, max_len: int = 512):
         int(plen.max())
 
 
-def build_pairs_gpu(q_ids, q_cu, rows, c_toks, c_lens, max_len: int = 512):
-    """Same contract as build_pairs for cuda tensors (c_toks int16, c_lens int32), through the
-    rag_build_pairs kernels."""
+class PendingPairs:
+    """build_pairs_gpu_async's result: the packed pair tensors are enqueued on the stream; the
+    8-byte {T, longest} travels to pinned host memory behind an event. result() waits for
+    that event only — by the time a pipelined caller asks (after enqueueing the next batch's
+    encode + search), the assembly has long finished and the wait costs nothing."""
+
+    def __init__(self, ids, types, cu, stats_host, event):
+        self._ids, self._types, self.cu = ids, types, cu
+        self._stats, self._event = stats_host, event
+
+    def ready(self) -> bool:
+        return self._event.query()
+
+    def result(self):
+        self._event.synchronize()
+        T, longest = (int(v) for v in self._stats)
+        return self._ids[:T], self._types[:T], self.cu, longest
+
+
+def _launch_pairs(q_ids, q_cu, rows, c_toks, c_lens, max_len):
     from . import _lib
     dev = rows.device
     Bq, Kq = rows.shape
@@ -77,5 +96,25 @@ def build_pairs_gpu(q_ids, q_cu, rows, c_toks, c_lens, max_len: int = 512):
         q_ids.data_ptr(), q_cu.data_ptr(), Bq, rows.data_ptr(), Kq, c_toks.data_ptr(),
         c_toks.shape[1], c_lens.data_ptr(), max_len, ids.data_ptr(), types.data_ptr(),
         cu.data_ptr(), stats.data_ptr(), torch.cuda.current_stream(dev).cuda_stream))
-    T, longest = (int(v) for v in stats.cpu())          # one host sync per batch
+    return ids, types, cu, stats
+
+
+def build_pairs_gpu(q_ids, q_cu, rows, c_toks, c_lens, max_len: int = 512):
+    """Same contract as build_pairs for cuda tensors (c_toks int16, c_lens int32), through the
+    rag_build_pairs kernels. Reads {T, longest} back at once (one host sync per call); a
+    pipelined caller uses build_pairs_gpu_async instead."""
+    ids, types, cu, stats = _launch_pairs(q_ids, q_cu, rows, c_toks, c_lens, max_len)
+    T, longest = (int(v) for v in stats.cpu())
     return ids[:T], types[:T], cu, longest
+
+
+def build_pairs_gpu_async(q_ids, q_cu, rows, c_toks, c_lens, max_len: int = 512):
+    """build_pairs_gpu without the blocking read: returns a PendingPairs whose result() is the
+    same tuple. The host can enqueue batch i+1's encode and search before it asks for batch
+    i's pair count, so the GPU queue never drains behind the read-back."""
+    ids, types, cu, stats = _launch_pairs(q_ids, q_cu, rows, c_toks, c_lens, max_len)
+    host = torch.empty(2, dtype=torch.int32, pin_memory=True)
+    host.copy_(stats, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(rows.device))
+    return PendingPairs(ids, types, cu, host, ev)

@@ -122,7 +122,11 @@ int rag_build_pairs(const int32_t* q_ids, const int32_t* q_cu, int B, const int6
  * _WS_NOROT rotated-K-order-off A/B; _WS_READS_FIRST the MFMA waves' previous fragment order
  * (all reads of a K step before its MFMAs) for A/B against the interleaved one. _WS_BIG128
  * (round 4, A/B): the WS ring with 4 MFMA waves of 128 x 64 (one per SIMD beside its loader
- * wave, 256 registers each) instead of 8 of 64 x 64.
+ * wave, 256 registers each) instead of 8 of 64 x 64. _WS_PROBE_HI_ONLY / _WS_PROBE_FP8_CORR
+ * (round 4 timing probes, fp16x3 only, results meaningless): the hi x hi MFMA alone; hi x hi
+ * plus one block-scaled fp8 16x16x128 MFMA per 2 K steps standing in for the two corrections.
+ * _WS_REGSTAGE (A/B): the loader waves stage through registers (buffer_load to VGPRs, then
+ * ds_write_b128) instead of LDS-DMA; _WS_REGSTAGE_INTAKE its loads alone (timing probe).
  * N % 128 == 0, K % 64 == 0 (PIPE/SMALL also N <= 4096). */
 enum { RAG_EPI_F16 = 0, RAG_EPI_GELU_F16 = 1, RAG_EPI_F32 = 2 };
 /* deferred-LayerNorm epilogues (rag_bert_gemm_dl) */
@@ -138,7 +142,9 @@ enum { RAG_GEMM_AUTO = 0, RAG_GEMM_TILE = 1, RAG_GEMM_PIPE = 2, RAG_GEMM_PROBE_N
        RAG_GEMM_WS_PRIO_LOAD = 30, RAG_GEMM_WS_PRIO_MFMA = 31, RAG_GEMM_WS_FLAGS = 32,
        RAG_GEMM_WS_NOHALF = 33, RAG_GEMM_WS_SMALL = 34, RAG_GEMM_WS_BIG128 = 35,
        RAG_GEMM_WS_BIG128_MFMA_ONLY = 36, RAG_GEMM_WS_BIG128_DMA_ONLY = 37,
-       RAG_GEMM_WS_BIG128_NO_STORE = 38 };
+       RAG_GEMM_WS_BIG128_NO_STORE = 38, RAG_GEMM_WS_PROBE_HI_ONLY = 39,
+       RAG_GEMM_WS_PROBE_FP8_CORR = 40, RAG_GEMM_WS_REGSTAGE = 41,
+       RAG_GEMM_WS_REGSTAGE_INTAKE = 42 };
 int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, const void* W,
                   const void* W_lo, const float* bias, int M, int N, int K, void* C,
                   void* C_lo, void* stream);

@@ -28,7 +28,9 @@ VNAME = {0: "auto", 1: "tile", 2: "pipe", 3: "probe_no_mfma", 4: "probe_no_dma",
          28: "ws_probe_no_a_reads", 29: "ws_probe_no_w_reads", 30: "ws_prio_load",
          31: "ws_prio_mfma", 32: "ws_flags",
          33: "ws_nohalf", 34: "ws_small", 35: "ws_big128",
-         36: "ws_big128_mfma_only", 37: "ws_big128_dma_only", 38: "ws_big128_no_store"}
+         36: "ws_big128_mfma_only", 37: "ws_big128_dma_only", 38: "ws_big128_no_store",
+         39: "ws_probe_hi_only", 40: "ws_probe_fp8_corr", 41: "ws_regstage",
+         42: "ws_regstage_intake"}
 LAYERS = {
     "small": [("qkv", 1152, 384, EPI_F16), ("o", 384, 384, EPI_F32),
               ("ffn1", 1536, 384, EPI_GELU_F16), ("ffn2", 384, 1536, EPI_F32)],

@@ -144,7 +144,7 @@ def test_build_pairs_gpu_matches_torch(gpu):
     """rag_build_pairs (HIP) == ragmi.pairs.build_pairs (torch, itself CPU-tested against a
     per-pair loop), bit for bit, incl. truncation to max_len and -1 rows."""
     import torch
-    from ragmi.pairs import build_pairs, build_pairs_gpu
+    from ragmi.pairs import build_pairs, build_pairs_gpu, build_pairs_gpu_async
     g = torch.Generator(device="cuda")
     g.manual_seed(5)
     rows_n, lmax = 5000, 300
@@ -161,7 +161,15 @@ def test_build_pairs_gpu_matches_torch(gpu):
         rows = torch.randint(-1, rows_n, (B, K), generator=g, device="cuda")
         a = build_pairs(q_ids, q_cu, rows, c_toks, c_lens, max_len)
         b = build_pairs_gpu(q_ids, q_cu, rows, c_toks, c_lens, max_len)
+        # the pipelined form: enqueue on a side stream, collect after more work was queued
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            pend = build_pairs_gpu_async(q_ids, q_cu, rows, c_toks, c_lens, max_len)
+            _ = torch.randn(1 << 20, device="cuda").sum()
+            c = pend.result()
         torch.cuda.synchronize()
-        for x, y in zip(a[:3], b[:3]):
+        for x, y, z in zip(a[:3], b[:3], c[:3]):
             assert torch.equal(x.cpu(), y.cpu())
-        assert a[3] == b[3]
+            assert torch.equal(x.cpu(), z.cpu())
+        assert a[3] == b[3] == c[3]
