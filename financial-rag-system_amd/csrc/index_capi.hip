@@ -157,16 +157,20 @@ bool fused_prep() {
   return k.get(1) != 0;
 }
 
-// Workgroups of the tier-2 rescan launch: ~128 tiles each, at most kRescanMaxWG (two per CU
-// on MI355X): a marked pass streams the shard at the chip's rate, and the idle launch (every
-// pass) is one round trip per workgroup. RAGMI_RESCAN_WG (diagnostic A/B) caps it; 0 = skip.
+// Workgroups of the tier-2 rescan launch: ~128 tiles each, at most one per CU. A marked pass
+// streams the shard at the chip's rate with that many, and the idle launch (every pass) costs
+// one dispatch per workgroup, each needing a CU with the rescan's 79 KB of LDS free beside the
+// other streams' scans. Round 4 sweep (profiles/r04m_rescan_grid.jsonl), 1.25M rows, 4 in
+// flight, qps / 4 marked queries' added ms at 1.25M / 10M rows: 512 workgroups (two per CU)
+// 209.3K / 0.45 / 1.36, 256: 210.4K / 0.53 / 1.21, 128: 210.7K / 0.80 / 2.18.
+// RAGMI_RESCAN_WG (diagnostic A/B) caps it; 0 = skip (queries left tier 3, unanswered).
 int rescan_grid(const rag_index* h) {
   static ragmi::Knob k("RAGMI_RESCAN_WG");
   const int cap = k.get(ragmi::kRescanMaxWG);
   if (cap <= 0) return 0;
   const int64_t n_tiles = (h->count + 15) / 16;
   return (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)cap, (int64_t)ragmi::kRescanMaxWG,
-                                                      (int64_t)2 * h->n_cu, n_tiles / 128}));
+                                                      (int64_t)h->n_cu, n_tiles / 128}));
 }
 
 // RAGMI_SAMPLE_DIV (diagnostic A/B): 1 / the sampled fraction of the shard's tiles
@@ -286,7 +290,9 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
   if (timed) {
     RAG_HIP(hipEventCreate(&pp.a));
     RAG_HIP(hipEventCreate(&pp.b));
-    RAG_HIP(hipEventRecord(pp.a, st));
+    // the LDS-query / wide scans (a memset + launch, or one launch): marker events around them;
+    // the 384-d scan times its own dispatch (launch_fixed_timed below)
+    if constexpr (kLdsQ) RAG_HIP(hipEventRecord(pp.a, st));
   }
 #define RAG_SCAN_ARGS                                                                    \
   h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, (int)n_tiles, w.seed, w.part_s, w.part_i, \
@@ -325,6 +331,14 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
         launch_fixed<kLdsBlock>(scan_lds_kernel<D, false, false>, g3, 0, st, RAG_SCAN_ARGS, groups,
                                 w.progress);
     }
+  } else if (timed) {
+    // the timed launch carries its own start / end timestamps (launch_fixed_timed)
+    if (filt)
+      RAG_HIP(launch_fixed_timed<kScanBlock>(scan_kernel<D, true>, dim3(grid), 0, st, pp.a, pp.b,
+                                             RAG_SCAN_ARGS, nullptr));
+    else
+      RAG_HIP(launch_fixed_timed<kScanBlock>(scan_kernel<D, false>, dim3(grid), 0, st, pp.a, pp.b,
+                                             RAG_SCAN_ARGS, nullptr));
   } else {
     if (filt)
       launch_fixed<kScanBlock>(scan_kernel<D, true>, dim3(grid), 0, st, RAG_SCAN_ARGS, nullptr);
@@ -333,7 +347,7 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
   }
 #undef RAG_SCAN_ARGS
   if (timed) {
-    RAG_HIP(hipEventRecord(pp.b, st));
+    if constexpr (kLdsQ) RAG_HIP(hipEventRecord(pp.b, st));
     h->prof_pairs.push_back(pp);
   }
   if (h->serial_scans == 1) {
