@@ -373,6 +373,33 @@ void launch_ws_large(const _Float16* A, const _Float16* Al, const _Float16* W, c
     launch_ws<EPI, SPLIT, PipeLarge, 0, AUX>(A, Al, W, Wl, bias, M, N, K, C, Clo, st, dl);
 }
 
+// Deferred LayerNorm for query batches (round 4; diagnostic A/B,
+// RAGMI_DL_SMALL=1): token counts up to kDlSmallT run the DL forward on PipeDlSmall's
+// 64 x 128 tiles. Its residual-add epilogue (kEpiResLn) adds the residual and writes the row
+// statistics in the GEMM itself, so the O-proj / FFN2 split-K parts, their fp32 round trip
+// and the 24 add_ln launches of a bge-small forward go away. Parity-green, but slower at 32
+// queries (782 tokens): 0.889 vs 0.685 ms per forward (profiles/r04o_dl_small_ab.jsonl). A
+// tile's serial K loop runs ~0.6 us per 32-deep step at these sizes, so the unsplit FFN2
+// (48 steps on 39 workgroups) takes 30 us against 9.7 (3-way split-K) + 5.0 (add_ln); at
+// query-batch sizes the K split is what keeps the GEMMs short, and its seam is the add_ln.
+// (at most 63 row blocks of 64: the small tiles keep the rotated K order, as PipeLarge does
+// up to 16K tokens, so both give every element the same MFMA chain)
+constexpr int kDlSmallT = 63 * 64;
+bool dl_small_on() {
+  static ragmi::Knob k("RAGMI_DL_SMALL");
+  return k.get(0) == 1;
+}
+
+template <int EPI, bool SPLIT, int AUX = 0>
+void launch_dl(bool small, const _Float16* A, const _Float16* Al, const _Float16* W,
+               const _Float16* Wl, const float* bias, int M, int N, int K, void* C,
+               _Float16* Clo, hipStream_t st, const DlArgs& dl) {
+  if (small)
+    launch_ws<EPI, SPLIT, PipeDlSmall, 0, AUX>(A, Al, W, Wl, bias, M, N, K, C, Clo, st, dl);
+  else
+    launch_ws_large<EPI, SPLIT, AUX>(A, Al, W, Wl, bias, M, N, K, C, Clo, st, dl);
+}
+
 // shapes the deferred-LayerNorm WS GEMMs take: Ln* (K = 384 input rows; c1 | c2 staged in the
 // 4096-float bias area) and ResLn (N = 384 output rows; bias | gamma | beta)
 bool dl_gemm_ok(int epi, int M, int N, int K) {
@@ -720,13 +747,18 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
   const bool xf_on = k_f32.get(0) != 1;
   // deferred LayerNorm (DlArgs): auto once every token-row GEMM is a WS one (AUTO's choice:
   // the 384-wide projections' 256 x 128 tiles reach half the CUs, ~11K tokens)
-  const bool dl = [&] {
+  const bool dl_shapes = [&] {
     if (e->defer_ln == 0 || H != kDlH || !w->xl || !w->sa || !e->layers[0].w1_f ||
         e->bound_defer > kF16Safe)
       return false;
-    if (!dl_gemm_ok(kEpiLnF16, T, 3 * H, H) || !dl_gemm_ok(kEpiLnGeluF16, T, FF, H) ||
-        !dl_gemm_ok(kEpiResLn, T, H, H) || !dl_gemm_ok(kEpiResLn, T, H, FF))
-      return false;
+    return dl_gemm_ok(kEpiLnF16, T, 3 * H, H) && dl_gemm_ok(kEpiLnGeluF16, T, FF, H) &&
+           dl_gemm_ok(kEpiResLn, T, H, H) && dl_gemm_ok(kEpiResLn, T, H, FF);
+  }();
+  // query batches: the DL forward on the 64 x 128 tiles (kDlSmallT)
+  const bool dl_small = dl_shapes && T <= kDlSmallT && e->defer_ln != 0 && dl_small_on() &&
+                        gemm_variant_default() == RAG_GEMM_AUTO;
+  const bool dl = dl_small || [&] {
+    if (!dl_shapes) return false;
     if (e->defer_ln > 0) return true;
     const int tiles384 = (H / PBN) * ((T + PBM - 1) / PBM);
     return gemm_variant_default() == RAG_GEMM_AUTO && 2 * tiles384 >= cu_count() &&
@@ -754,8 +786,8 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
       a.st_in = w->sb;
       a.c1 = L.qkv_c1;
       a.eps = c.layer_norm_eps;
-      launch_ws_large<kEpiLnF16, true, 2>(w->xh, w->xl, L.wqkv_f, L.wqkv_fl, L.qkv_c2, T, 3 * H,
-                                          H, w->qkv, w->qkv_l, st, a);
+      launch_dl<kEpiLnF16, true, 2>(dl_small, w->xh, w->xl, L.wqkv_f, L.wqkv_fl, L.qkv_c2, T,
+                                    3 * H, H, w->qkv, w->qkv_l, st, a);
     } else {
       gemm<kEpiF16>(w->xh, w->xl, L.wqkv, L.wqkv_l, L.bqkv, T, 3 * H, H, w->qkv, w->qkv_l, st);
     }
@@ -782,22 +814,22 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
       o.beta = P ? P->be2 : nullptr;
       o.st_out = w->sa;
       o.eps = c.layer_norm_eps;
-      launch_ws_large<kEpiResLn, true>(w->ctx, w->ctx_l, L.wo, L.wo_l, L.bo, T, H, H, w->xh,
-                                       w->xl, st, o);
+      launch_dl<kEpiResLn, true>(dl_small, w->ctx, w->ctx_l, L.wo, L.wo_l, L.bo, T, H, H, w->xh,
+                                 w->xl, st, o);
       DlArgs f;
       f.st_in = w->sa;
       f.c1 = L.w1_c1;
       f.eps = c.layer_norm_eps;
-      launch_ws_large<kEpiLnGeluF16, true, 2>(w->xh, w->xl, L.w1_f, L.w1_fl, L.w1_c2, T, FF, H,
-                                              w->ff, w->ff_l, st, f);
+      launch_dl<kEpiLnGeluF16, true, 2>(dl_small, w->xh, w->xl, L.w1_f, L.w1_fl, L.w1_c2, T, FF,
+                                        H, w->ff, w->ff_l, st, f);
       DlArgs r;
       r.st_in = w->sa;
       r.gamma = L.g1;
       r.beta = L.be1;
       r.st_out = w->sb;
       r.eps = c.layer_norm_eps;
-      launch_ws_large<kEpiResLn, true>(w->ff, w->ff_l, L.w2, L.w2_l, L.bi2, T, H, FF, w->xh,
-                                       w->xl, st, r);
+      launch_dl<kEpiResLn, true>(dl_small, w->ff, w->ff_l, L.w2, L.w2_l, L.bi2, T, H, FF, w->xh,
+                                 w->xl, st, r);
       continue;
     }
     // rows the rest of the layer runs on: all T tokens, or the B gathered CLS rows
@@ -1519,12 +1551,14 @@ int rag_bert_gemm_dl(int epilogue, const void* A, const void* A_lo, const void* 
   auto* wl = static_cast<const _Float16*>(W_lo);
   auto* cl = static_cast<_Float16*>(C_lo);
   const auto st = static_cast<hipStream_t>(stream);
+  // the forward's tile choice: query-batch tiles up to kDlSmallT rows
+  const bool small = M <= kDlSmallT && dl_small_on();
   if (epilogue == RAG_EPI_LN_F16)
-    launch_ws_large<kEpiLnF16, true, 2>(a, al, w, wl, bias, M, N, K, C, cl, st, d);
+    launch_dl<kEpiLnF16, true, 2>(small, a, al, w, wl, bias, M, N, K, C, cl, st, d);
   else if (epilogue == RAG_EPI_LN_GELU_F16)
-    launch_ws_large<kEpiLnGeluF16, true, 2>(a, al, w, wl, bias, M, N, K, C, cl, st, d);
+    launch_dl<kEpiLnGeluF16, true, 2>(small, a, al, w, wl, bias, M, N, K, C, cl, st, d);
   else
-    launch_ws_large<kEpiResLn, true>(a, al, w, wl, bias, M, N, K, C, cl, st, d);
+    launch_dl<kEpiResLn, true>(small, a, al, w, wl, bias, M, N, K, C, cl, st, d);
   RAG_HIP(hipGetLastError());
   return RAG_OK;
 }

@@ -560,6 +560,10 @@ using PipeWide192 = PipeCfg<256, 192, 4, 2, 2>;
 // slower than SMALL, not AUTO's pick): SMALL's 64 x 64 tiles and 3-stage BK-32 ring, the
 // DMAs moved to ONE loader wave beside the 4 MFMA waves, two workgroups per CU.
 using PipeWsSmall = PipeCfg<64, 64, 2, 2, 3, 0, 1>;
+// deferred-LayerNorm GEMMs of query batches (round 4): the large-batch DL
+// epilogues on 64 x 128 tiles — 4 MFMA waves of 32 x 64 (a wave's 64 columns are one stats
+// block, as ws_dl_epilogue needs), 2 loader waves, a 4-stage BK-32 ring (96 KB)
+using PipeDlSmall = PipeCfg<64, 128, 2, 2, 4, 32, 2>;
 constexpr int PBM = PipeLarge::BM, PBN = PipeLarge::BN;
 constexpr int kPipeThreads = PipeLarge::THREADS;
 constexpr int kPipeBiasMax = 4096;            // floats of bias staged in LDS (N <= 4096)
