@@ -580,7 +580,8 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
       variant == RAG_GEMM_WS_BIG128 || variant == RAG_GEMM_WS_BIG128_MFMA_ONLY ||
       variant == RAG_GEMM_WS_BIG128_DMA_ONLY || variant == RAG_GEMM_WS_BIG128_NO_STORE ||
       variant == RAG_GEMM_WS_PROBE_HI_ONLY || variant == RAG_GEMM_WS_PROBE_FP8_CORR ||
-      variant == RAG_GEMM_WS_REGSTAGE || variant == RAG_GEMM_WS_REGSTAGE_INTAKE) {
+      variant == RAG_GEMM_WS_REGSTAGE || variant == RAG_GEMM_WS_REGSTAGE_INTAKE ||
+      variant == RAG_GEMM_WS_L2PF || variant == RAG_GEMM_WS_L2PF_INTAKE) {
     // probes keep production's store policy (nt for fp16 outputs) since round 2's r02h runs
     auto go = [&](auto pc) {
       constexpr int P = decltype(pc)::value;
@@ -608,6 +609,8 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
     else if (variant == RAG_GEMM_WS_PROBE_HI_ONLY) go(std::integral_constant<int, 20>{});
     else if (variant == RAG_GEMM_WS_REGSTAGE) go(std::integral_constant<int, 22>{});
     else if (variant == RAG_GEMM_WS_REGSTAGE_INTAKE) go(std::integral_constant<int, 23>{});
+    else if (variant == RAG_GEMM_WS_L2PF) go(std::integral_constant<int, 24>{});
+    else if (variant == RAG_GEMM_WS_L2PF_INTAKE) go(std::integral_constant<int, 25>{});
     else if (variant == RAG_GEMM_WS_PROBE_FP8_CORR) {
       if (Al) launch_ws<EPI, true, PipeLarge, 21, (EPI == kEpiF32 ? 0 : 2)>(A, Al, W, Wl, bias, M, N, K, C, Clo, st);
     }
@@ -1289,7 +1292,7 @@ int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, co
        variant == RAG_GEMM_WS_READS_FIRST || variant == RAG_GEMM_WS_PRIO_LOAD ||
        variant == RAG_GEMM_WS_PRIO_MFMA || variant == RAG_GEMM_WS_FLAGS ||
        variant == RAG_GEMM_WS_NOHALF || variant == RAG_GEMM_WS_SMALL ||
-       variant == RAG_GEMM_WS_REGSTAGE) &&
+       variant == RAG_GEMM_WS_REGSTAGE || variant == RAG_GEMM_WS_L2PF) &&
       !pipe_ok(M, N, K))
     return ragmi::fail(RAG_EINVAL, "pipe/small/wide variants need N % 128 == 0, K % 64 == 0, "
                                    "N <= 4096, M*K*2 and M*N*4 < 2^31");
@@ -1302,7 +1305,8 @@ int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, co
                      variant == RAG_GEMM_WS_PROBE_NO_W_READS ||
                      variant == RAG_GEMM_WS_PROBE_HI_ONLY ||
                      variant == RAG_GEMM_WS_PROBE_FP8_CORR ||
-                     variant == RAG_GEMM_WS_REGSTAGE_INTAKE;
+                     variant == RAG_GEMM_WS_REGSTAGE_INTAKE ||
+                     variant == RAG_GEMM_WS_L2PF_INTAKE;
   const bool known = variant == RAG_GEMM_AUTO || variant == RAG_GEMM_TILE ||
                      variant == RAG_GEMM_PIPE || variant == RAG_GEMM_SMALL ||
                      variant == RAG_GEMM_WIDE || variant == RAG_GEMM_SMALL_BK64 ||
@@ -1315,7 +1319,7 @@ int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, co
                      variant == RAG_GEMM_WS_BIG128_MFMA_ONLY ||
                      variant == RAG_GEMM_WS_BIG128_DMA_ONLY ||
                      variant == RAG_GEMM_WS_BIG128_NO_STORE ||
-                     variant == RAG_GEMM_WS_REGSTAGE || probe;
+                     variant == RAG_GEMM_WS_REGSTAGE || variant == RAG_GEMM_WS_L2PF || probe;
   if (!known || (probe && !pipe_ok(M, N, K)))
     return ragmi::fail(RAG_EINVAL, "unknown GEMM variant, or a probe on a non-pipe shape");
   auto* a = static_cast<const _Float16*>(A);

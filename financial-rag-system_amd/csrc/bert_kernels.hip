@@ -584,6 +584,19 @@ __device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t rs, uint32_t voff,
       : "memory");
 }
 
+// 4 B per lane buffer -> LDS DMA into a sink: used only for the line fetch it causes (an L2
+// prefetch that occupies no VGPR; lane l's dword lands at lds_addr + 4 l)
+__device__ __forceinline__ void blds4(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff,
+                                      uint32_t lds_addr) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+      "buffer_load_dword %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(rs), "s"(lds_addr), "s"(soff)
+      : "memory");
+}
+
 // raw buffer resource over [base, base + bytes) from wave-uniform inputs (reads past the
 // end return zeros, stores past it are dropped); bytes < 2^31 (checked by the launcher)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t panel(const void* base, int64_t bytes) {
@@ -1395,16 +1408,22 @@ __global__ __launch_bounds__(kWsBlock<CFG>, 1) void gemm_ws_kernel(
   constexpr int STAGE_H8 = NPL * (A_H8 + W_H8);
   constexpr int LA = A_H8 / LTH, LW = W_H8 / LTH;  // DMAs per loader wave per plane
   constexpr int L = NPL * (LA + LW);               // DMAs per loader wave per stage
-  constexpr bool P_NO_MFMA = PROBE == 1 || PROBE == 8 || PROBE == 23;
+  constexpr bool P_NO_MFMA = PROBE == 1 || PROBE == 8 || PROBE == 23 || PROBE == 25;
   constexpr bool P_NO_DMA = PROBE == 2 || PROBE == 7;
-  constexpr bool P_NO_STORE = PROBE == 6 || PROBE == 7 || PROBE == 8 || PROBE == 23;
+  constexpr bool P_NO_STORE = PROBE == 6 || PROBE == 7 || PROBE == 8 || PROBE == 23 || PROBE == 25;
   // PROBE 22 / 23 (round 4, A/B): the loader waves stage through registers (buffer_load to
   // VGPRs one K step ahead, then ds_write_b128 into the ring slot) instead of LDS-DMA; 23 =
   // the same without MFMAs and stores (the intake alone, as PROBE 8 for the DMA path)
   constexpr bool REGST = PROBE == 22 || PROBE == 23;
+  // PROBE 24 / 25 (round 4, A/B): every loader wave also issues one 4-B-per-lane LDS-DMA per
+  // stage into a sink, touching the A panel's lines kPrefD K steps ahead (an L2 prefetch: the
+  // long-K FFN2 streams its A panel from HBM at the ring's depth); 25 = with PROBE 8's cuts
+  constexpr bool PREF = PROBE == 24 || PROBE == 25;
+  constexpr int kPrefD = 6;
+  constexpr int LP = L + (PREF ? 1 : 0);   // vector-memory ops per loader wave per stage
   constexpr int OUT_B = EPI == kEpiF32 ? 4 : 2;
   static_assert(A_H8 % LTH == 0 && W_H8 % LTH == 0 && FN % 2 == 0, "tile shape");
-  static_assert((NS - 2) * L <= 63, "vmcnt range");
+  static_assert((NS - 2) * (L + 1) <= 63, "vmcnt range");
   __shared__ half8 lds[NS * STAGE_H8 + kPipeBiasMax / 4];
   float* bias_l = reinterpret_cast<float*>(lds + NS * STAGE_H8);
   // PROBE 18: FULL[s] (loader waves' landed stages) and FREE[s] (MFMA waves' released
@@ -1577,6 +1596,7 @@ __global__ __launch_bounds__(kWsBlock<CFG>, 1) void gemm_ws_kernel(
           rW1 = panel(Wl + (int64_t)n0 * K, wbytes);
         }
       }
+      const int kr_cur = kr_i;
       const uint32_t soff = __builtin_amdgcn_readfirstlane((uint32_t)kr_i * (BK * 2));
       if (++kr_i == nk) kr_i = 0;
       const uint32_t slot = lbase + (uint32_t)slot_i * (STAGE_H8 * 16);
@@ -1592,13 +1612,27 @@ __global__ __launch_bounds__(kWsBlock<CFG>, 1) void gemm_ws_kernel(
         blds16(rW0, voW[i], soff, d);
         if constexpr (SPLIT) blds16(rW1, voW[i], soff, d + W_H8 * 16);
       }
+      if constexpr (PREF) {
+        // rows lw*64 + lane of the panel (4 loader waves x 64 = BM rows), the 128-B line
+        // holding K steps 2m, 2m+1 of one plane: hi at even kp, lo at odd (a wrap past the
+        // tile's last step touches its first lines again: hits)
+        // (BK 64, one plane: one line per row per step)
+        static_assert(LTH == BM && (BK * 2 == 64 || BK * 2 == 128), "a line per row per 1-2 steps");
+        int kp = kr_cur + kPrefD;
+        if (kp >= nk) kp -= nk;
+        const int kl = BK * 2 == 64 ? (kp & ~1) : kp;
+        const uint32_t vo = (uint32_t)(((lw * 64 + lane) * K + kl * BK) * 2);
+        const uint32_t sink = lbase + (uint32_t)(NS * STAGE_H8 * 16 + (kPipeBiasMax - 64) * 4);
+        if (SPLIT && BK * 2 == 64 && (kp & 1)) blds4(rA1, vo, 0, sink);
+        else blds4(rA0, vo, 0, sink);
+      }
       if (++kt_i == nk) { kt_i = 0; ++it_i; }
       if (++slot_i == NS) slot_i = 0;
     };
 #pragma unroll
     for (int p = 0; p < NS - 1; ++p) issue_next();
     for (int g = 0; g < steps; ++g) {
-      wait_ring<L, 0, NS - 2>(min(NS - 2, steps - 1 - g), false);   // stage g landed
+      wait_ring<LP, 0, NS - 2>(min(NS - 2, steps - 1 - g), false);   // stage g landed
       if constexpr (FLAGS) {
         // publish stage g, then take slot (g-1) % NS once all 8 MFMA waves released stage g-1
         if (lane == 0)

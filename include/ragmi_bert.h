@@ -127,6 +127,8 @@ int rag_build_pairs(const int32_t* q_ids, const int32_t* q_cu, int B, const int6
  * plus one block-scaled fp8 16x16x128 MFMA per 2 K steps standing in for the two corrections.
  * _WS_REGSTAGE (A/B): the loader waves stage through registers (buffer_load to VGPRs, then
  * ds_write_b128) instead of LDS-DMA; _WS_REGSTAGE_INTAKE its loads alone (timing probe).
+ * _WS_L2PF (A/B): the loader waves also touch the A panel's lines 6 K steps ahead (one 4-B
+ * LDS-DMA per lane and stage into a sink: an L2 prefetch); _WS_L2PF_INTAKE its loads alone.
  * N % 128 == 0, K % 64 == 0 (PIPE/SMALL also N <= 4096). */
 enum { RAG_EPI_F16 = 0, RAG_EPI_GELU_F16 = 1, RAG_EPI_F32 = 2 };
 /* deferred-LayerNorm epilogues (rag_bert_gemm_dl) */
@@ -144,7 +146,7 @@ enum { RAG_GEMM_AUTO = 0, RAG_GEMM_TILE = 1, RAG_GEMM_PIPE = 2, RAG_GEMM_PROBE_N
        RAG_GEMM_WS_BIG128_MFMA_ONLY = 36, RAG_GEMM_WS_BIG128_DMA_ONLY = 37,
        RAG_GEMM_WS_BIG128_NO_STORE = 38, RAG_GEMM_WS_PROBE_HI_ONLY = 39,
        RAG_GEMM_WS_PROBE_FP8_CORR = 40, RAG_GEMM_WS_REGSTAGE = 41,
-       RAG_GEMM_WS_REGSTAGE_INTAKE = 42 };
+       RAG_GEMM_WS_REGSTAGE_INTAKE = 42, RAG_GEMM_WS_L2PF = 43, RAG_GEMM_WS_L2PF_INTAKE = 44 };
 int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, const void* W,
                   const void* W_lo, const float* bias, int M, int N, int K, void* C,
                   void* C_lo, void* stream);

@@ -30,7 +30,7 @@ VNAME = {0: "auto", 1: "tile", 2: "pipe", 3: "probe_no_mfma", 4: "probe_no_dma",
          33: "ws_nohalf", 34: "ws_small", 35: "ws_big128",
          36: "ws_big128_mfma_only", 37: "ws_big128_dma_only", 38: "ws_big128_no_store",
          39: "ws_probe_hi_only", 40: "ws_probe_fp8_corr", 41: "ws_regstage",
-         42: "ws_regstage_intake"}
+         42: "ws_regstage_intake", 43: "ws_l2pf", 44: "ws_l2pf_intake"}
 LAYERS = {
     "small": [("qkv", 1152, 384, EPI_F16), ("o", 384, 384, EPI_F32),
               ("ffn1", 1536, 384, EPI_GELU_F16), ("ffn2", 384, 1536, EPI_F32)],
