@@ -1387,8 +1387,10 @@ int rag_bert_attention(int variant, const void* qkv, const void* qkv_lo, const i
     return ragmi::fail(RAG_EINVAL, "qkv_lo and ctx_lo: both (fp16x3) or neither (fp16)");
   if (variant == -1) variant = kAttnVar;
   if ((variant < 0 || variant > 15) && variant != 18 && variant != 26 &&
-      (variant < 40 || variant > 46 || variant % 2))
-    return ragmi::fail(RAG_EINVAL, "variant: -1, 0..15, 18, 26, 40, 42, 44 or 46");
+      (variant < 40 || variant > 46 || variant % 2) && variant != 43 && variant != 106 &&
+      variant != 107)
+    return ragmi::fail(RAG_EINVAL,
+                       "variant: -1, 0..15, 18, 26, 40, 42, 43, 44, 46, 106 or 107");
   constexpr int H = 384, HD = 32, NH = H / HD;
   const int planes = qkv_lo ? 2 : 1;
   const int kc = attn_chunk_keys<HD>(max_len, planes);
@@ -1438,6 +1440,9 @@ int rag_bert_attention(int variant, const void* qkv, const void* qkv_lo, const i
     case 42: return go(std::integral_constant<int, 42>{});
     case 44: return go(std::integral_constant<int, 44>{});
     case 46: return go(std::integral_constant<int, 46>{});
+    case 43: return go(std::integral_constant<int, 43>{});   // + 1 = rolling Q prefetch
+    case 106: return go(std::integral_constant<int, 106>{});  // + 64 = staging loads first
+    case 107: return go(std::integral_constant<int, 107>{});
     default: return go(std::integral_constant<int, 15>{});
   }
 }

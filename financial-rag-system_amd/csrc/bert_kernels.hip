@@ -1952,6 +1952,43 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) 
   // ---- stage keys [k0, k0 + n) (n multiple of 32; zeros past len): K and V row-major,
   // 16-B chunks (swizzled: swz_chunk for K's row reads, attn_vsw for V's transposed reads)
   auto stage = [&](int k0, int n) {
+    if constexpr ((VAR & 64) != 0) {
+      // VAR bit 64 (round 4): every staging load of up to SU passes issued before any LDS
+      // store (one memory round trip per SU passes instead of one per pass); same bytes to
+      // the same LDS places
+      constexpr int SU = 2;
+      constexpr int T = kAttnThreads<SPLIT>;
+      const int total = n * (HD / 8);
+      for (int c0 = tid; c0 < total; c0 += SU * T) {
+        half8 kv[SU][NP], vv[SU][NP];
+#pragma unroll
+        for (int u = 0; u < SU; ++u) {
+          const int c = c0 + u * T, kl = c / (HD / 8), ch = c % (HD / 8), key = k0 + kl;
+#pragma unroll
+          for (int p = 0; p < NP; ++p) {
+            kv[u][p] = half8{};
+            vv[u][p] = half8{};
+            if (c < total && key < len) {
+              const _Float16* src = planes[p] + (int64_t)(base + key) * (3 * H) + h * HD + 8 * ch;
+              kv[u][p] = *reinterpret_cast<const half8*>(src + H);
+              vv[u][p] = *reinterpret_cast<const half8*>(src + 2 * H);
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < SU; ++u) {
+          const int c = c0 + u * T, kl = c / (HD / 8), ch = c % (HD / 8);
+          if (c < total) {
+#pragma unroll
+            for (int p = 0; p < NP; ++p) {
+              *reinterpret_cast<half8*>(kls[p] + kl * KROW + 8 * swz_chunk<KCPR>(kl, ch)) = kv[u][p];
+              *reinterpret_cast<half8*>(vls[p] + kl * HD + 8 * (ch ^ attn_vsw<HD>(kl))) = vv[u][p];
+            }
+          }
+        }
+      }
+      return;
+    }
     for (int c = tid; c < n * (HD / 8); c += kAttnThreads<SPLIT>) {
       const int kl = c / (HD / 8), ch = c % (HD / 8), key = k0 + kl;
 #pragma unroll

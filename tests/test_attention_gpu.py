@@ -43,7 +43,7 @@ def data():
     return x, hi, lo, cu
 
 
-@pytest.mark.parametrize("variant", list(range(16)) + [18, 26, 40, 42, 44, 46])
+@pytest.mark.parametrize("variant", list(range(16)) + [18, 26, 40, 42, 43, 44, 46, 106, 107])
 @pytest.mark.parametrize("split", [True, False], ids=["fp16x3", "fp16"])
 def test_attention_matches_fp32(gpu, data, variant, split):
     from ragmi.encoders import attention
@@ -114,6 +114,21 @@ def test_peeled_prefetch_is_bitwise_identical(gpu, data, variant, split):
     cu_t = torch.from_numpy(cu).cuda()
     a = attention(hi, cu_t, max(LENS), lo if split else None, variant)
     b = attention(hi, cu_t, max(LENS), lo if split else None, variant | 32)
+    torch.cuda.synchronize()
+    for x1, x2 in (zip(a, b) if split else [(a, b)]):
+        assert torch.equal(x1.view(torch.int16), x2.view(torch.int16))
+
+
+@pytest.mark.parametrize("pair", [(42, 106), (42, 43), (43, 107)], ids=lambda p: f"{p[0]}-{p[1]}")
+@pytest.mark.parametrize("split", [True, False], ids=["fp16x3", "fp16"])
+def test_staging_and_q_prefetch_are_bitwise_identical(gpu, data, pair, split):
+    """VAR bit 64 (staging loads all issued before the LDS stores) and bit 1 (rolling Q
+    prefetch) change when bytes move, not the arithmetic: outputs equal bit for bit."""
+    from ragmi.encoders import attention
+    x, hi, lo, cu = data
+    cu_t = torch.from_numpy(cu).cuda()
+    a = attention(hi, cu_t, max(LENS), lo if split else None, pair[0])
+    b = attention(hi, cu_t, max(LENS), lo if split else None, pair[1])
     torch.cuda.synchronize()
     for x1, x2 in (zip(a, b) if split else [(a, b)]):
         assert torch.equal(x1.view(torch.int16), x2.view(torch.int16))
