@@ -26,8 +26,10 @@ namespace {
 // same stream are ordered by the stream itself, so the hot path records no events at all (an
 // event record idles the queue for ~5 us between kernels). Up to kRing streams search
 // concurrently without interference; a further stream drains the device once and rebinds
-// the least recently used slot.
-constexpr int kRing = 4;
+// the least recently used slot. (Round 4: 8 slots. With 4, a fifth stream in flight rebinds on
+// every pass: 1.25M rows, 5-8 streams 137-141K qps; with 8, 5 / 6 / 8 streams 186-205K, and
+// 4 streams stay the fastest at 209-210K, profiles/r04t_streams_hwqueues.jsonl.)
+constexpr int kRing = 8;
 constexpr int kMaxGroups = 4;   // query groups of 32 per pass (wide rows)
 
 struct Workspace {
