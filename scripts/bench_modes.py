@@ -252,11 +252,13 @@ def run_pipeline(args, cfg_id):
     bge_w, ce_w = R.make_weights(R.BGE_SMALL, 1), R.make_weights(R.MINILM_CE, 2)
     bge = BertEncoder(R.BGE_SMALL, bge_w, HEAD_CLS_L2, dev, prec, diagnostic=True)
     ce = BertEncoder(R.MINILM_CE, ce_w, HEAD_POOLER_CLS, dev, prec, diagnostic=True)
-    # 3 batches in flight: each stream takes one of the process's 4 hardware queues with the
-    # null stream on the 4th (GPU_MAX_HW_QUEUES); a 4th stream would share a queue with
-    # another and serialise behind it (config 2: 2 / 3 / 4 in flight 60.7K / 71.1K / 60.4K
-    # qps, profiles/r03b_small_gemm.jsonl)
-    S = args.streams or 3
+    # batches in flight: config 2 four, config 3 three. Round 3 measured config 2 at 2 / 3 / 4
+    # in flight 60.7K / 71.1K / 60.4K qps (profiles/r03b_small_gemm.jsonl); on the round-4
+    # build (graphs captured on a private stream) 4 beat 3 in four of four pairs (70.5-72.8K
+    # vs 68.4-71.6K) and config 3 is 1% better at 3 (profiles/r04v_config23_streams.jsonl).
+    # More hardware queues per process (GPU_MAX_HW_QUEUES=8) drop config 2 to 30-45K
+    # (profiles/r04u_config2_streams_hwq.jsonl).
+    S = args.streams or (4 if cfg_id == 2 else 3)
     streams = [torch.cuda.Stream(dev) for _ in range(S)]
     ev_every = 4                        # CE forward events on every 4th batch (sampled)
     evs, flops = [], []
