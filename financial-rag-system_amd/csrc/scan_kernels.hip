@@ -1266,42 +1266,45 @@ __global__ __launch_bounds__(kWideBlock, 1) void scan_wide_kernel(
     };
 #pragma unroll
     for (int p = 0; p < HB - 1; ++p) issue_h(p);
-    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int jh = 0; jh < n_half; ++jh) {
-      const int later = min(HB - 2, n_half - 1 - jh);            // halves issued after jh
-      switch (later) {                                           // HS / 8 DMAs per half
-        case 6: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-        case 5: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-        case 4: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-        case 3: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-        case 2: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-        case 1: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-      }
-      __builtin_amdgcn_s_barrier();   // half jh landed for all; everyone is past half jh-1
-      asm volatile("" ::: "memory");
-      issue_h(jh + HB - 1);           // slot (jh+7)%8 == (jh-1)%8
-      if (active) {
-        const half8* tb = ring + (jh % HB) * (HS * 64) + lane;
-        const int s0 = (jh & 1) * HS;
-        half8 a[HS];
-#pragma unroll
-        for (int s = 0; s < HS; ++s) a[s] = tb[s * 64];
-#pragma unroll
-        for (int s = 0; s < HS; ++s)
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[s], qf[s0 + s], acc, 0, 0, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, kWidePre, 0);    // DS reads
-#pragma unroll
-        for (int s = 0; s < HS - kWidePre; ++s) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);         // one MFMA
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);         // one DS read
+    // one tile per iteration, its two halves unrolled (compile-time query-fragment offsets)
+    for (int j = 0; j < n_mine; ++j) {
+      floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+      auto half_step = [&](auto uc) __attribute__((always_inline)) {
+        constexpr int U = decltype(uc)::value;
+        const int jh = 2 * j + U;
+        const int later = min(HB - 2, n_half - 1 - jh);          // halves issued after jh
+        switch (later) {                                         // HS / 8 DMAs per half
+          case 6: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+          case 5: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+          case 4: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+          case 3: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+          case 2: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+          case 1: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+          default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
         }
-        __builtin_amdgcn_sched_group_barrier(0x008, kWidePre, 0);
-        if (jh & 1) {
-          wtopk_tile(st, acc, b + (jh >> 1) * nb, n_rows, lane);
-          acc = floatx4{0.f, 0.f, 0.f, 0.f};
+        __builtin_amdgcn_s_barrier();   // half jh landed for all; everyone is past half jh-1
+        asm volatile("" ::: "memory");
+        issue_h(jh + HB - 1);           // slot (jh+7)%8 == (jh-1)%8
+        if (active) {
+          const half8* tb = ring + (jh % HB) * (HS * 64) + lane;
+          half8 a[HS];
+#pragma unroll
+          for (int s = 0; s < HS; ++s) a[s] = tb[s * 64];
+#pragma unroll
+          for (int s = 0; s < HS; ++s)
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[s], qf[U * HS + s], acc, 0, 0, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, kWidePre, 0);    // DS reads
+#pragma unroll
+          for (int s = 0; s < HS - kWidePre; ++s) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);         // one MFMA
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);         // one DS read
+          }
+          __builtin_amdgcn_sched_group_barrier(0x008, kWidePre, 0);
         }
-      }
+      };
+      half_step(std::integral_constant<int, 0>{});
+      half_step(std::integral_constant<int, 1>{});
+      if (active) wtopk_tile(st, acc, b + j * nb, n_rows, lane);
     }
     if (active) wtopk_finish(st, lane, qt, b, nw, part_s, part_i, heads_s, heads_i, heads_n);
     return;
