@@ -385,6 +385,13 @@ void launch_ws_large(const _Float16* A, const _Float16* Al, const _Float16* W, c
 // (at most 63 row blocks of 64: the small tiles keep the rotated K order, as PipeLarge does
 // up to 16K tokens, so both give every element the same MFMA chain)
 constexpr int kDlSmallT = 63 * 64;
+
+// RAGMI_CLS_ATTN=0 (diagnostic A/B, round 4): the last layer's all-token QKV + attention
+// instead of the K|V projection + CLS-only attention
+bool cls_attn_on() {
+  static ragmi::Knob k("RAGMI_CLS_ATTN");
+  return k.get(1) != 0;
+}
 bool dl_small_on() {
   static ragmi::Knob k("RAGMI_DL_SMALL");
   return k.get(0) == 1;
@@ -783,7 +790,29 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
     const Layer& L = e->layers[l];
     const bool last = l == nl - 1;                  // CLS rows only after the attention
     const Layer* P = l > 0 ? &e->layers[l - 1] : nullptr;
-    if (dl && P) {
+    // Last layer, deferred LayerNorm (fp16x3 large batches): only the [CLS] rows leave the
+    // layer, so only their Q is needed. K|V for every token (the folded QKV weights' rows
+    // H .. 3H-1, N = 2H), the CLS rows gathered with their pending LN2 applied, their Q by a
+    // B-row GEMM, and a CLS-only attention (attn_cls_kernel) straight into the CLS context.
+    // RAGMI_CLS_ATTN=0 (diagnostic A/B): the all-token QKV + attention path.
+    if (last && dl && P && H == kDlH && HD == 32 && cls_attn_on()) {
+      DlArgs a;
+      a.st_in = w->sb;
+      a.c1 = L.qkv_c1 + H;
+      a.eps = c.layer_norm_eps;
+      launch_dl<kEpiLnF16, true, 2>(dl_small, w->xh, w->xl, L.wqkv_f + (int64_t)H * H,
+                                    L.wqkv_fl + (int64_t)H * H, L.qkv_c2 + H, T, 2 * H, H,
+                                    w->qkv, w->qkv_l, st, a);
+      gather_cls_kernel<H><<<dim3(B), dim3(64), 0, st>>>(
+          nullptr, w->xh, w->xl, nullptr, nullptr, cu, w->xc, nullptr, nullptr, w->sb, P->g2,
+          P->be2, c.layer_norm_eps, w->xch, w->xcl);
+      // Q of the CLS rows into the CLS FFN buffers (free until this layer's FFN1)
+      gemm<kEpiF16>(w->xch, w->xcl, L.wqkv, L.wqkv_l, L.bqkv, B, H, H, w->ffc, w->ffcl, st);
+      constexpr int kGroups = (H / HD) / kAttnClsHeads;
+      launch_fixed<kAttnClsBlock>(attn_cls_kernel<H, HD>, dim3((unsigned)(B * kGroups)), 0, st,
+                                  w->qkv, w->qkv_l, w->ffc, w->ffcl, cu, B, max_len, scale,
+                                  w->cc, w->ccl);
+    } else if (dl && P) {
       // LN2 of layer l-1 pending on z: folded into QKV (kEpiLnF16)
       DlArgs a;
       a.st_in = w->sb;
@@ -794,8 +823,11 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
     } else {
       gemm<kEpiF16>(w->xh, w->xl, L.wqkv, L.wqkv_l, L.bqkv, T, 3 * H, H, w->qkv, w->qkv_l, st);
     }
+    const bool cls_done = last && dl && P && H == kDlH && HD == 32 && cls_attn_on();
     const int max_qb = last ? 1 : 1 << 20;
-    if (attn_var_override() == 10) {   // RAGMI_ATTN_VAR=10: the round-2 variant (A/B)
+    if (cls_done) {
+      // (the CLS context is in w->cc / w->ccl already)
+    } else if (attn_var_override() == 10) {   // RAGMI_ATTN_VAR=10: the round-2 variant (A/B)
       if (w->xl)
         launch_fixed<kAttnThreads<true>>(attn_kernel<H, HD, true, 10>, agrid, alds, st,
             w->qkv, w->qkv_l, cu, max_len, kc, scale, w->ctx, w->ctx_l, max_qb);
@@ -843,12 +875,14 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
              *ffl = w->ff_l;
     bool row_xf = xf;
     if (last) {
-      // (deferred LayerNorm: x_cls = LN2_{l-1}(z) of the CLS rows)
+      // (deferred LayerNorm: x_cls = LN2_{l-1}(z) of the CLS rows; the CLS-only path
+      // gathered them before its attention)
       const bool dlp = dl && P;
-      gather_cls_kernel<H><<<dim3(B), dim3(64), 0, st>>>(
-          x, w->xh, w->xl, w->ctx, w->ctx_l, cu, w->xc, w->cc, w->xl ? w->ccl : nullptr,
-          dlp ? w->sb : nullptr, dlp ? P->g2 : nullptr, dlp ? P->be2 : nullptr,
-          c.layer_norm_eps);
+      if (!cls_done)
+        gather_cls_kernel<H><<<dim3(B), dim3(64), 0, st>>>(
+            x, w->xh, w->xl, w->ctx, w->ctx_l, cu, w->xc, w->cc, w->xl ? w->ccl : nullptr,
+            dlp ? w->sb : nullptr, dlp ? P->g2 : nullptr, dlp ? P->be2 : nullptr,
+            c.layer_norm_eps);
       row_xf = false;                                 // the B CLS rows keep an fp32 copy
       R = B;
       x = w->xc;

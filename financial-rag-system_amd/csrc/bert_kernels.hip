@@ -2435,7 +2435,10 @@ __global__ __launch_bounds__(64) void gather_cls_kernel(
     const _Float16* __restrict__ ctx_lo, const int* __restrict__ cu, float* __restrict__ x_cls,
     _Float16* __restrict__ ctx_cls, _Float16* __restrict__ ctx_cls_lo,
     const float* __restrict__ st = nullptr, const float* __restrict__ g = nullptr,
-    const float* __restrict__ bt = nullptr, float eps = 0.f) {
+    const float* __restrict__ bt = nullptr, float eps = 0.f,
+    _Float16* __restrict__ xh_cls = nullptr, _Float16* __restrict__ xl_cls = nullptr) {
+  // (ctx null: the CLS rows only, before a CLS-only attention, attn_cls_kernel; xh_cls /
+  // xl_cls: also their hi / lo fp16 planes, the Q projection's operands)
   const int b = blockIdx.x, lane = threadIdx.x;
   const int64_t r = cu[b];
   float mu = 0.f, rs = 1.f;
@@ -2450,8 +2453,113 @@ __global__ __launch_bounds__(64) void gather_cls_kernel(
     float v = x ? x[r * H + c] : (float)xh[r * H + c] + (float)xl[r * H + c];
     if (st) v = (v - mu) * rs * g[c] + bt[c];
     x_cls[(int64_t)b * H + c] = v;
-    ctx_cls[(int64_t)b * H + c] = ctx[r * H + c];
-    if (ctx_lo) ctx_cls_lo[(int64_t)b * H + c] = ctx_lo[r * H + c];
+    if (xh_cls) {
+      const _Float16 hv = (_Float16)v;
+      xh_cls[(int64_t)b * H + c] = hv;
+      if (xl_cls) xl_cls[(int64_t)b * H + c] = (_Float16)(v - (float)hv);
+    }
+    if (ctx) {
+      ctx_cls[(int64_t)b * H + c] = ctx[r * H + c];
+      if (ctx_lo) ctx_cls_lo[(int64_t)b * H + c] = ctx_lo[r * H + c];
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// CLS-only attention of the last encoder layer (round 4): the cross-encoder / bge heads read
+// only the [CLS] row, so the last layer needs the attention output of one query per
+// (sequence, head). One wave per (sequence, head), 4 heads per workgroup: lane j takes keys
+// j, j + 64, ... of the sequence; scores from the fp16x3 planes in fp32 (the MFMA path's
+// three products: k_hi q_hi + k_lo q_hi + k_hi q_lo), softmax in base 2 with the 1/sqrt(d)
+// scale folded in, P . V against v_hi + v_lo, then one cross-lane combine (max, rescale, sum).
+// kv: [T][2H] planes (K | V of every token: the last layer's K|V-only projection); q: [B][H]
+// planes of the CLS rows' Q; out: [B][H] planes of the CLS rows' context.
+// ----------------------------------------------------------------------------------------
+constexpr int kAttnClsHeads = 4;
+constexpr int kAttnClsBlock = 64 * kAttnClsHeads;   // launch_fixed / __launch_bounds__
+template <int H, int HD>
+__global__ __launch_bounds__(kAttnClsBlock) void attn_cls_kernel(
+    const _Float16* __restrict__ kv, const _Float16* __restrict__ kv_lo,
+    const _Float16* __restrict__ q, const _Float16* __restrict__ q_lo,
+    const int* __restrict__ cu, int B, int max_len, float scale, _Float16* __restrict__ out,
+    _Float16* __restrict__ out_lo) {
+  static_assert(HD % 8 == 0 && (H / HD) % kAttnClsHeads == 0, "head groups");
+  constexpr int NH = H / HD;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int b = blockIdx.x / (NH / kAttnClsHeads);
+  const int h = (blockIdx.x % (NH / kAttnClsHeads)) * kAttnClsHeads + wv;
+  if (b >= B) return;
+  const int base = cu[b], len = min(cu[b + 1] - cu[b], max_len);
+  float qh[HD], ql[HD];
+#pragma unroll
+  for (int c = 0; c < HD / 8; ++c) {
+    const half8 a = *reinterpret_cast<const half8*>(q + (int64_t)b * H + h * HD + 8 * c);
+    const half8 l = *reinterpret_cast<const half8*>(q_lo + (int64_t)b * H + h * HD + 8 * c);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      qh[8 * c + e] = (float)a[e];
+      ql[8 * c + e] = (float)l[e];
+    }
+  }
+  const float c2 = scale * 1.44269504088896341f;
+  float m = kNegInf, l = 0.f, o[HD];
+#pragma unroll
+  for (int d = 0; d < HD; ++d) o[d] = 0.f;
+  for (int j = lane; j < len; j += 64) {
+    const _Float16* kr = kv + (int64_t)(base + j) * (2 * H) + h * HD;
+    const _Float16* krl = kv_lo + (int64_t)(base + j) * (2 * H) + h * HD;
+    half8 k8[HD / 8], kl8[HD / 8], v8[HD / 8], vl8[HD / 8];
+#pragma unroll
+    for (int c = 0; c < HD / 8; ++c) {
+      k8[c] = *reinterpret_cast<const half8*>(kr + 8 * c);
+      kl8[c] = *reinterpret_cast<const half8*>(krl + 8 * c);
+      v8[c] = *reinterpret_cast<const half8*>(kr + H + 8 * c);
+      vl8[c] = *reinterpret_cast<const half8*>(krl + H + 8 * c);
+    }
+    float s0 = 0.f, s1 = 0.f;   // k_hi q_hi and the two correction products
+#pragma unroll
+    for (int c = 0; c < HD / 8; ++c)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float kh = (float)k8[c][e], klo = (float)kl8[c][e];
+        s0 = fmaf(kh, qh[8 * c + e], s0);
+        s1 = fmaf(klo, qh[8 * c + e], fmaf(kh, ql[8 * c + e], s1));
+      }
+    const float sc = (s0 + s1) * c2;
+    const float mn = fmaxf(m, sc);
+    const float corr = __builtin_amdgcn_exp2f(m - mn);   // m = -inf: 0
+    const float p = __builtin_amdgcn_exp2f(sc - mn);
+    l = l * corr + p;
+#pragma unroll
+    for (int c = 0; c < HD / 8; ++c)
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        o[8 * c + e] = fmaf(p, (float)v8[c][e] + (float)vl8[c][e], o[8 * c + e] * corr);
+    m = mn;
+  }
+  // combine the 64 lanes: common max, rescale, sums
+  float mw = m;
+#pragma unroll
+  for (int sh = 32; sh >= 1; sh >>= 1) mw = fmaxf(mw, __shfl_xor(mw, sh, 64));
+  const float f = m == kNegInf ? 0.f : __builtin_amdgcn_exp2f(m - mw);
+  l *= f;
+#pragma unroll
+  for (int sh = 32; sh >= 1; sh >>= 1) l += __shfl_xor(l, sh, 64);
+#pragma unroll
+  for (int d = 0; d < HD; ++d) {
+    float x = o[d] * f;
+#pragma unroll
+    for (int sh = 32; sh >= 1; sh >>= 1) x += __shfl_xor(x, sh, 64);
+    o[d] = x;
+  }
+  if (lane < HD) {
+    float v = 0.f;
+#pragma unroll
+    for (int d = 0; d < HD; ++d) v = lane == d ? o[d] : v;
+    v = v / l;
+    const _Float16 hv = (_Float16)v;
+    out[(int64_t)b * H + h * HD + lane] = hv;
+    out_lo[(int64_t)b * H + h * HD + lane] = (_Float16)(v - (float)hv);
   }
 }
 

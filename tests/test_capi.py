@@ -77,7 +77,7 @@ KNOBS = ["RAGMI_SCAN_WGS", "RAGMI_RESCAN_WG", "RAGMI_SAMPLE_DIV", "RAGMI_WIDE_WG
          "RAGMI_CE_ROWS", "RAGMI_ATTN_VAR", "RAGMI_FUSE_LN", "RAGMI_SMALL_BK",
          "RAGMI_SMALL_WIDE", "RAGMI_SMALL_WS", "RAGMI_ENC_GRAPH", "RAGMI_RESIDUAL_F32",
          "RAGMI_ADDLN_VEC", "RAGMI_WS_BIG128", "RAGMI_DL_SMALL",
-         "RAGMI_WIDE_HALF"]
+         "RAGMI_WIDE_HALF", "RAGMI_CLS_ATTN"]
 
 
 def test_ab_knobs_are_ignored_without_diagnostic_handle(libpath):
@@ -121,7 +121,7 @@ def test_ring_kernels_launch_through_launch_fixed():
     constexpr their __launch_bounds__ uses (ragmi::launch_fixed); no launch site spells one."""
     csrc = os.path.join(ROOT, "financial-rag-system_amd", "csrc")
     ring = ("gemm_pipe_kernel", "gemm_ws_kernel", "scan_kernel", "scan_lds_kernel",
-            "scan_wide_kernel", "rescan_kernel", "attn_kernel")
+            "scan_wide_kernel", "rescan_kernel", "attn_kernel", "attn_cls_kernel")
     for f in os.listdir(csrc):
         text = open(os.path.join(csrc, f)).read()
         for k in ring:
