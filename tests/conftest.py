@@ -24,7 +24,13 @@ def gpu():
     assert torch.cuda.is_available(), "GPU test run without a HIP device"
     from ragmi import _lib
     _lib.load()   # fail loudly if libragmi.so is missing
-    return torch.device("cuda", 0)
+    dev = torch.device("cuda", 0)
+    if os.environ.get("RAGMI_TEST_DIAGNOSTIC") == "1":
+        # A/B runs of the GPU suite under a RAGMI_* kernel variant (scripts/gpu_*.sh): one
+        # diagnostic handle for the session, so the library honours the variables
+        from ragmi.index import FlatIndex
+        pytest.ragmi_diag_handle = FlatIndex(384, 16, dev, diagnostic=True)
+    return dev
 
 
 @pytest.fixture(scope="session")
