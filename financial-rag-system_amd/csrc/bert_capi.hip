@@ -386,11 +386,12 @@ void launch_ws_large(const _Float16* A, const _Float16* Al, const _Float16* W, c
 // up to 16K tokens, so both give every element the same MFMA chain)
 constexpr int kDlSmallT = 63 * 64;
 
-// RAGMI_CLS_ATTN=1 (diagnostic A/B, round 4): the last layer as K|V projection + CLS-only
-// attention instead of the all-token QKV + attention
+// RAGMI_CLS_ATTN=0 (diagnostic A/B): the last layer's all-token QKV + attention instead of
+// the K|V projection + CLS-only attention (round 4: rerank forward 9.17-9.19 vs 9.30-9.32 ms,
+// profiles/r04aa_cls_attention_ab.jsonl)
 bool cls_attn_on() {
   static ragmi::Knob k("RAGMI_CLS_ATTN");
-  return k.get(0) == 1;
+  return k.get(1) != 0;
 }
 bool dl_small_on() {
   static ragmi::Knob k("RAGMI_DL_SMALL");
@@ -794,7 +795,7 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
     // layer, so only their Q is needed. K|V for every token (the folded QKV weights' rows
     // H .. 3H-1, N = 2H), the CLS rows gathered with their pending LN2 applied, their Q by a
     // B-row GEMM, and a CLS-only attention (attn_cls_kernel) straight into the CLS context.
-    // Off unless RAGMI_CLS_ATTN=1 (diagnostic A/B) until measured.
+    // RAGMI_CLS_ATTN=0 (diagnostic A/B): the all-token QKV + attention path.
     if (last && dl && P && H == kDlH && HD == 32 && cls_attn_on()) {
       DlArgs a;
       a.st_in = w->sb;
