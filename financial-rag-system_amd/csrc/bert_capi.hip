@@ -363,10 +363,39 @@ bool ws_big128() {
   return k.get(0) == 1;
 }
 
+// the ping-pong GEMM (gemm_pp_kernel, round 5): fp16x3, N % 192 == 0 (every token-row GEMM of
+// the 384-hidden encoders). RAGMI_GEMM_PP=0 (diagnostic A/B): the WS kernel instead.
+bool pp_on() {
+  static ragmi::Knob k("RAGMI_GEMM_PP");
+  return k.get(1) != 0;
+}
+bool pp_ok(int M, int N, int K) { return N % PipePP::BN == 0 && K % 32 == 0 && pipe_ok(M, N, K); }
+
+template <int EPI, int AUX = 0, int PROBE = 0>
+void launch_pp(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float16* Wl,
+               const float* bias, int M, int N, int K, void* C, _Float16* Clo, hipStream_t st,
+               const DlArgs& dl = DlArgs{}) {
+  const int tiles = (N / PipePP::BN) * ((M + PipePP::BM - 1) / PipePP::BM);
+  const dim3 grid((unsigned)std::min(cu_count(), (tiles + 7) / 8 * 8));   // one per CU
+  // RAGMI_PP_STAGGER (A/B): start stagger of the workgroups (DlArgs.phase, gemm_pp_kernel)
+  static ragmi::Knob k("RAGMI_PP_STAGGER");
+  DlArgs d = dl;
+  d.phase = std::max(0, k.get(0));
+  launch_fixed<kPpBlock>(gemm_pp_kernel<EPI, PipePP, PROBE, AUX>, grid, 0, st, A, Al, W, Wl, bias,
+                         M, N, K, C, Clo, d);
+}
+
 template <int EPI, bool SPLIT, int AUX = 0>
 void launch_ws_large(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float16* Wl,
                      const float* bias, int M, int N, int K, void* C, _Float16* Clo,
-                     hipStream_t st, const DlArgs& dl = DlArgs{}) {
+                     hipStream_t st, const DlArgs& dl = DlArgs{}, bool allow_pp = true) {
+  // (the residual-add deferred-LN epilogue stays on the WS kernel: in the ping-pong kernel's
+  // 256 registers its residual planes and staged vectors spill beside the accumulators)
+  if constexpr (SPLIT && EPI != kEpiResLn)
+    if (allow_pp && pp_on() && pp_ok(M, N, K)) {
+      launch_pp<EPI, AUX>(A, Al, W, Wl, bias, M, N, K, C, Clo, st, dl);
+      return;
+    }
   if (ws_big128())
     launch_ws<EPI, SPLIT, PipeBig128, 0, AUX>(A, Al, W, Wl, bias, M, N, K, C, Clo, st, dl);
   else
@@ -578,6 +607,16 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
     }
     return;
   }
+  if (variant >= RAG_GEMM_PP && variant <= RAG_GEMM_PP_PRIO) {
+    // (rag_bert_gemm checks fp16x3 and N % 192 == 0 for these)
+    constexpr int AX = EPI == kEpiF32 ? 0 : 2;
+    if (variant == RAG_GEMM_PP) launch_pp<EPI, AX>(A, Al, W, Wl, bias, M, N, K, C, Clo, st);
+    else if (variant == RAG_GEMM_PP_MFMA_ONLY) launch_pp<EPI, AX, 7>(A, Al, W, Wl, bias, M, N, K, C, Clo, st);
+    else if (variant == RAG_GEMM_PP_DMA_ONLY) launch_pp<EPI, AX, 8>(A, Al, W, Wl, bias, M, N, K, C, Clo, st);
+    else if (variant == RAG_GEMM_PP_NO_STORE) launch_pp<EPI, AX, 6>(A, Al, W, Wl, bias, M, N, K, C, Clo, st);
+    else launch_pp<EPI, 0, 0>(A, Al, W, Wl, bias, M, N, K, C, Clo, st);   // default store policy
+    return;
+  }
   if (variant == RAG_GEMM_WS || variant == RAG_GEMM_WS_MFMA_ONLY ||
       variant == RAG_GEMM_WS_NO_STORE || variant == RAG_GEMM_WS_DMA_ONLY ||
       variant == RAG_GEMM_WS_L2_STORE || variant == RAG_GEMM_WS_NT ||
@@ -602,7 +641,8 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
       // 0.310 ms, the streamed 540 MB no longer evicting the A panels the n-tiles of an XCD
       // share); the fp32 ones (O / FFN2, read back at once by add_ln) keep the default policy
       constexpr int AX = EPI == kEpiF32 ? 0 : 2;
-      if (Al) launch_ws_large<EPI, true, AX>(A, Al, W, Wl, bias, M, N, K, C, Clo, st);
+      // (an explicit RAG_GEMM_WS stays on the WS kernel; AUTO's pick may take the PP one)
+      if (Al) launch_ws_large<EPI, true, AX>(A, Al, W, Wl, bias, M, N, K, C, Clo, st, DlArgs{}, auto_pick);
       else launch_ws_large<EPI, false, AX>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st);
     }
     else if (variant == RAG_GEMM_WS_MFMA_ONLY) go(std::integral_constant<int, 7>{});
@@ -1355,7 +1395,11 @@ int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, co
                      variant == RAG_GEMM_WS_BIG128_DMA_ONLY ||
                      variant == RAG_GEMM_WS_BIG128_NO_STORE ||
                      variant == RAG_GEMM_WS_REGSTAGE || variant == RAG_GEMM_WS_L2PF || probe;
-  if (!known || (probe && !pipe_ok(M, N, K)))
+  const bool pp = variant >= RAG_GEMM_PP && variant <= RAG_GEMM_PP_PRIO;
+  if (pp && (!A_lo || !pp_ok(M, N, K)))
+    return ragmi::fail(RAG_EINVAL, "PP variants: fp16x3, N % 192 == 0, K % 64 == 0, "
+                                   "M*K*2 and M*N*4 < 2^31");
+  if ((!known && !pp) || (probe && !pipe_ok(M, N, K)))
     return ragmi::fail(RAG_EINVAL, "unknown GEMM variant, or a probe on a non-pipe shape");
   auto* a = static_cast<const _Float16*>(A);
   auto* al = static_cast<const _Float16*>(A_lo);

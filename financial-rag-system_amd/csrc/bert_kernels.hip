@@ -1829,6 +1829,484 @@ __global__ __launch_bounds__(kWsBlock<CFG>, 1) void gemm_ws_kernel(
 }
 
 // ----------------------------------------------------------------------------------------
+// GEMM, ping-pong (gemm_pp_kernel; round 5): fp16x3 token-row GEMMs of large batches with
+// N % 192 == 0 (MiniLM / bge-small: Q|K|V 1152, FFN1 1536, O-proj / FFN2 384, last-layer
+// K|V 768). Same arithmetic as gemm_ws_kernel in its panel-aligned order — per output element
+// the same MFMA sequence (K steps in order; per step W_lo A_hi, W_hi A_lo, W_hi A_hi), so the
+// two kernels agree bit for bit from 64 row panels up — on a different structure:
+//  * 256 x 192 tiles (the WS kernel's 256 x 128): 448 operand rows per K step instead of 384
+//    for 1.5x the products, -22% L2 -> LDS bytes per FLOP. The WS probes put the LDS-DMA intake
+//    (~24-30 B/clk per CU) on the critical path of these GEMMs; with
+//    the hi + lo output stream that intake is what bounds a tile, not the MFMA pipe.
+//  * no loader waves: 8 waves, two per SIMD (256 registers each), each computing 32 rows x
+//    the 192 columns (three whole 64-column stats blocks, as the deferred-LN epilogue needs)
+//    and each taking a share of the DMAs. Waves 0-3 (group 0: tile rows 0-127) and 4-7
+//    (group 1: rows 128-255) sit on the same four SIMDs and run half a step apart: between two
+//    consecutive s_barriers one group issues its MFMAs (C phase: 72 MFMAs of 16x16x32, the
+//    step's fragments already in registers) while the other reads the next step's fragments
+//    from LDS, issues its half of a coming stage's DMAs and runs any tile epilogue (M phase).
+//    The matrix pipe of each SIMD alternates between the two waves it hosts instead of idling
+//    while both read (the WS kernel's MFMA waves read their fragments in lockstep after each
+//    step's barrier: 0.59 of the pipe even with no DMA and no stores).
+//  * a two-stage LDS ring (2 x 56 KB) + the staged bias area. Group 1 streams the A planes of
+//    stage s during its M phase of step s - 2 (right after its own reads of the slot), group 0
+//    the W planes during its M phase of step s - 1; each group retires its own DMAs with a
+//    counted vmcnt before the barrier that precedes the slot's first read (group 0: end of its
+//    C phase; group 1: end of its M phase, the next stage's DMAs left in flight).
+// Barriers: group 1 passes one extra barrier at the start and skips the last, so every wave
+// arrives at every barrier (2 per K step). LDS reads of a stage finish (lgkmcnt(0)) before the
+// barrier that ends the M phase, so no DMA into a slot can overtake a read of it.
+// ----------------------------------------------------------------------------------------
+using PipePP = PipeCfg<256, 192, 8, 1, 2, 32, 0>;
+constexpr int kPpBlock = 512;
+
+// the deferred-LN epilogues for wave tiles of several 64-column stats blocks (WTN % 64 == 0):
+// ws_dl_epilogue's arithmetic per element (same formulas, same order), block by block; the
+// residual planes of one row group are loaded at a time (the ping-pong kernel's register budget)
+template <int EPI, typename CFG, int AUX>
+__device__ __forceinline__ void pp_dl_epilogue(floatx4 (&acc)[CFG::FM][CFG::FN],
+                                               const float* lds_f, __amdgpu_buffer_rsrc_t rc,
+                                               __amdgpu_buffer_rsrc_t rl,
+                                               const floatx4 (&dls)[CFG::FM],
+                                               __amdgpu_buffer_rsrc_t rs_out, bool has_stats,
+                                               int N, int n0, int wr, int wc, int lane,
+                                               float eps) {
+  constexpr int FM = CFG::FM, FN = CFG::FN, WTM = 16 * FM, WTN = 16 * FN;
+  static_assert(WTN % 64 == 0 && FN % 4 == 0, "whole 64-column stats blocks per wave");
+  const int g = lane >> 4;
+  const int cofs = 8 * ((g & 1) * 2 + (g >> 1));
+  const float* bias_l = lds_f;
+  const float* c1_l = lds_f + N;                          // Ln*
+  const float *gam_l = lds_f + N, *bet_l = lds_f + 2 * N;  // ResLn
+  float mu[FM], rs[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    mu[i] = 0.f;
+    rs[i] = 1.f;
+    if (EPI != kEpiResLn || has_stats) dl_lane_stats(dls[i], g, eps, mu[i], rs[i]);
+  }
+  // column-block outer, row group inner: a block's staged vectors are read once for all the
+  // wave's rows and are dead after it (rows outer, the compiler kept every block's vectors
+  // live beside the accumulators and spilled)
+  if constexpr (EPI == kEpiResLn) {
+    // row group by row group: the residual z of a group's 16 rows x WTN columns in flight at
+    // once (one round trip per group; both groups' 96 registers would not fit)
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int ml = wr * WTM + i * 16 + (lane & 15);
+      u32x2 zh[FN], zl[FN];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int vo = (ml * N + n0 + wc * WTN + j * 16 + 4 * g) * 2;
+        zh[j] = __builtin_amdgcn_raw_buffer_load_b64(rc, vo, 0, 0);
+        zl[j] = __builtin_amdgcn_raw_buffer_load_b64(rl, vo, 0, 0);
+      }
+      const floatx4 a4 = {rs[i], rs[i], rs[i], rs[i]};
+      const floatx4 b4 = {-mu[i] * rs[i], -mu[i] * rs[i], -mu[i] * rs[i], -mu[i] * rs[i]};
+#pragma unroll
+      for (int bb = 0; bb < FN / 4; ++bb) {
+        floatx4 s4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int j = 4 * bb + jj;
+          const int nl = n0 + wc * WTN + j * 16 + 4 * g;
+          const floatx4 z = mix_f16x4(zh[j], zl[j]);
+          const floatx4 b = *reinterpret_cast<const floatx4*>(bias_l + nl);
+          floatx4 xr = z;
+          if (has_stats)
+            xr = __builtin_elementwise_fma(__builtin_elementwise_fma(z, a4, b4),
+                                           *reinterpret_cast<const floatx4*>(gam_l + nl),
+                                           *reinterpret_cast<const floatx4*>(bet_l + nl));
+          acc[i][j] = (acc[i][j] + b) + xr;
+          s4 += acc[i][j];
+          if (jj & 1) __builtin_amdgcn_sched_barrier(0);   // staged vectors of 2 frags live
+        }
+        float s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+        s += __shfl_xor(s, 16, 64);
+        s += __shfl_xor(s, 32, 64);
+        const float mw = s * (1.0f / 64);
+        const floatx4 m4 = {mw, mw, mw, mw};
+        floatx4 q4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const floatx4 d = acc[i][4 * bb + jj] - m4;
+          q4 = __builtin_elementwise_fma(d, d, q4);
+        }
+        float q = (q4[0] + q4[1]) + (q4[2] + q4[3]);
+        q += __shfl_xor(q, 16, 64);
+        q += __shfl_xor(q, 32, 64);
+        if (g == 0) {
+          const u32x2 d = {__builtin_bit_cast(uint32_t, mw), __builtin_bit_cast(uint32_t, q)};
+          __builtin_amdgcn_raw_buffer_store_b64(
+              d, rs_out, (ml * kDlParts + (n0 + wc * WTN) / 64 + bb) * 8, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // z planes (default policy), row group by row group (ws_dl_epilogue's order)
+#pragma unroll
+      for (int jp = 0; jp < FN; jp += 2) dl_store_pair<AUX>(acc, i, jp, ml, N, n0, wc, cofs, rc, rl);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
+#pragma unroll
+    for (int bb = 0; bb < FN / 4; ++bb) {
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int j = 4 * bb + jj;
+        const int nl = n0 + wc * WTN + j * 16 + 4 * g;
+        const floatx4 c1 = *reinterpret_cast<const floatx4*>(c1_l + nl);
+        const floatx4 c2 = *reinterpret_cast<const floatx4*>(bias_l + nl);
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const floatx4 nm4 = {-mu[i], -mu[i], -mu[i], -mu[i]}, rs4 = {rs[i], rs[i], rs[i], rs[i]};
+          acc[i][j] = __builtin_elementwise_fma(rs4, __builtin_elementwise_fma(nm4, c1, acc[i][j]), c2);
+          if constexpr (EPI == kEpiLnGeluF16) acc[i][j] = gelu_erf4(acc[i][j]);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // QKV / FFN1 outputs: the plain epilogue's order (see ws_dl_epilogue)
+#pragma unroll
+    for (int jp = 0; jp < FN; jp += 2)
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+        dl_store_pair<AUX>(acc, i, jp, wr * WTM + i * 16 + (lane & 15), N, n0, wc, cofs, rc, rl);
+  }
+}
+
+// PROBE (diagnostic timing probes, results meaningless): 6 = no stores, 7 = no DMAs and no
+// stores (MFMAs, LDS reads and barriers only), 8 = no MFMAs and no stores (the DMA ring alone);
+// 31 (A/B, results valid) = s_setprio 1 around every C phase.
+template <int EPI, typename CFG, int PROBE = 0, int AUX = 0>
+__global__ __launch_bounds__(kPpBlock, 1) void gemm_pp_kernel(
+    const _Float16* __restrict__ A, const _Float16* __restrict__ Al,
+    const _Float16* __restrict__ W, const _Float16* __restrict__ Wl,
+    const float* __restrict__ bias, int M, int N, int K, void* __restrict__ Cout,
+    _Float16* __restrict__ Clo, DlArgs dl) {
+  static_assert(EPI != kEpiAddLn, "plain and deferred-LN epilogues");
+  constexpr bool DL = EPI == kEpiLnF16 || EPI == kEpiLnGeluF16 || EPI == kEpiResLn;
+  constexpr int BM = CFG::BM, BN = CFG::BN;
+  constexpr int FM = CFG::FM, FN = CFG::FN, WTM = 16 * FM;
+  static_assert(BM == 256 && CFG::WAVES_M == 8 && CFG::WAVES_N == 1 && CFG::NS == 2 &&
+                    CFG::BK == 32 && kPpBlock == 64 * CFG::WAVES_M,
+                "8 waves of 32 rows x BN, two-stage BK-32 ring");
+  constexpr int BK = 32, CPR = BK / 8, NPL = 2;
+  constexpr int A_H8 = BM * CPR, W_H8 = BN * CPR;
+  constexpr int STAGE_H8 = NPL * (A_H8 + W_H8);
+  // DMAs per wave and plane: group 1's four waves stream the A planes, group 0's the W planes
+  constexpr int LA = A_H8 / 256, LW = W_H8 / 256;
+  static_assert(A_H8 % 256 == 0 && W_H8 % 256 == 0 && FN % 2 == 0, "tile shape");
+  constexpr int OUT_B = EPI == kEpiF32 ? 4 : 2;
+  constexpr bool P_NO_MFMA = PROBE == 8, P_NO_DMA = PROBE == 7;
+  constexpr bool P_NO_STORE = PROBE == 6 || PROBE == 7 || PROBE == 8;
+  __shared__ half8 lds[2 * STAGE_H8 + kPipeBiasMax / 4];
+  float* bias_l = reinterpret_cast<float*>(lds + 2 * STAGE_H8);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wid >> 2, lw = wid & 3;
+  const uint32_t lbase = lds_addr_of(lds);
+  const int nN = N / BN, nM = (M + BM - 1) / BM;
+  const int nk = K / BK;
+  // tile schedule: gemm_ws_kernel's (panel-aligned XCD placement from 64 row panels up, split
+  // last round), K steps always in order
+  const int G = gridDim.x, per_xcd = G >> 3;    // G: a multiple of 8 (launcher)
+  const int xcd = blockIdx.x & 7, lx = blockIdx.x >> 3;
+  const bool aligned = nM >= 64;
+  const int t_x = aligned ? (nM > xcd ? (nM - xcd + 7) >> 3 : 0) * nN : nM * nN;
+  const int l0 = aligned ? lx : xcd * per_xcd + lx, stride = aligned ? per_xcd : G;
+  const int r_x = aligned ? t_x % stride : 0;
+  const bool halves = aligned && r_x > 0 && 2 * r_x <= stride;
+  const int n_full = halves ? t_x / stride : l0 < t_x ? (t_x - l0 + stride - 1) / stride : 0;
+  const int n_mine = n_full + (halves && lx < 2 * r_x ? 1 : 0);
+  const int steps = n_mine * nk;
+  auto tile_mn = [&](int it, int& m0, int& nt, int& m_end) __attribute__((always_inline)) {
+    if (it < n_full) {
+      const int t = it * stride + l0;
+      m0 = (aligned ? xcd + 8 * (t / nN) : t / nN) * BM;
+      nt = t % nN;
+      m_end = min(M, m0 + BM);
+    } else {                                  // the half tile of the split last round
+      const int t = n_full * stride + (lx >> 1);
+      m0 = (xcd + 8 * (t / nN)) * BM + (lx & 1) * (BM / 2);
+      nt = t % nN;
+      m_end = min(M, m0 + BM / 2);
+    }
+  };
+
+  for (int i = tid * 4; i < N; i += kPpBlock * 4) {
+    *reinterpret_cast<floatx4*>(bias_l + i) = *reinterpret_cast<const floatx4*>(bias + i);
+    if constexpr (EPI == kEpiLnF16 || EPI == kEpiLnGeluF16)
+      *reinterpret_cast<floatx4*>(bias_l + N + i) = *reinterpret_cast<const floatx4*>(dl.c1 + i);
+    if constexpr (EPI == kEpiResLn)
+      if (dl.st_in) {
+        *reinterpret_cast<floatx4*>(bias_l + N + i) = *reinterpret_cast<const floatx4*>(dl.gamma + i);
+        *reinterpret_cast<floatx4*>(bias_l + 2 * N + i) = *reinterpret_cast<const floatx4*>(dl.beta + i);
+      }
+  }
+  __syncthreads();
+  // start stagger (dl.phase > 0, A/B): workgroup lx starts (lx % 4) x dl.phase x ~3.9 us late,
+  // spreading the chip's tile epilogues (each CU's output burst) over a tile's time
+  if (dl.phase > 0)
+    for (int i = 0; i < dl.phase * (lx & 3); ++i) __builtin_amdgcn_s_sleep(127);
+
+  // ---- DMA duties ----
+  // A planes: every wave streams ITS OWN 32 rows (LA2 = 2 DMAs per plane), which no other wave
+  // reads, so refilling them right after its own reads needs no barrier, and landing them needs
+  // only its own counted vmcnt. W planes (read by all 8 waves): group 0, LW = 3 DMAs per plane
+  // per wave, into the slot both groups finished reading a barrier ago. DMA i covers 16 rows:
+  // row 16 b + lane / 4, source chunk swz_chunk(row, lane % 4), which depends on the lane only
+  // (row bit 3 is lane bit 5), so one per-lane byte offset serves every DMA and the row block
+  // goes into soffset. (Round 5's first form split the A planes over group 1's waves: a wave
+  // could refill rows another wave of its group was still reading — wrong tiles under load.)
+  static_assert(CPR == 4, "64-B rows: 4 chunks per row, 16 rows per DMA");
+  constexpr int LA2 = WTM / 16;
+  const uint32_t vo = (uint32_t)(((lane >> 2) * K + swz_chunk<CPR>(lane >> 2, lane & 3) * 8) * 2);
+  struct Feed {
+    int s = 0, it = 0, kt = 0;
+    __amdgpu_buffer_rsrc_t r0, r1;
+  };
+  Feed fa, fw;
+  fa.r0 = fa.r1 = fw.r0 = fw.r1 = panel(A, 0);
+  // the next stage of feed f (A: this wave's rows; W: group 0's share) into slot s & 1; false
+  // once every stage is issued
+  auto issue = [&](Feed& f, bool is_w) __attribute__((always_inline)) -> bool {
+    if (f.it >= n_mine) return false;
+    if (f.kt == 0) {
+      int m0, nt, m_end;
+      tile_mn(f.it, m0, nt, m_end);
+      if (is_w) {
+        const int64_t wbytes = (int64_t)BN * K * 2;
+        f.r0 = panel(W + (int64_t)nt * BN * K, wbytes);
+        f.r1 = panel(Wl + (int64_t)nt * BN * K, wbytes);
+      } else {
+        const int64_t abytes = (int64_t)(m_end - m0) * K * 2;
+        f.r0 = panel(A + (int64_t)m0 * K, abytes);
+        f.r1 = panel(Al + (int64_t)m0 * K, abytes);
+      }
+    }
+    const uint32_t slot = lbase + (uint32_t)(f.s & 1) * (STAGE_H8 * 16);
+    if constexpr (!P_NO_DMA) {
+      if (is_w) {
+#pragma unroll
+        for (int i = 0; i < LW; ++i) {
+          const uint32_t d = slot + (uint32_t)((NPL * A_H8 + (lw * LW + i) * 64) * 16);
+          const uint32_t soff = __builtin_amdgcn_readfirstlane(
+              (uint32_t)f.kt * (BK * 2) + (uint32_t)((lw * LW + i) * 16 * K * 2));
+          blds16(f.r0, vo, soff, d);
+          blds16(f.r1, vo, soff, d + W_H8 * 16);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < LA2; ++i) {
+          const uint32_t d = slot + (uint32_t)((wid * LA2 + i) * 64 * 16);
+          const uint32_t soff = __builtin_amdgcn_readfirstlane(
+              (uint32_t)f.kt * (BK * 2) + (uint32_t)((wid * LA2 + i) * 16 * K * 2));
+          blds16(f.r0, vo, soff, d);
+          blds16(f.r1, vo, soff, d + A_H8 * 16);
+        }
+      }
+    }
+    ++f.s;
+    if (++f.kt == nk) { f.kt = 0; ++f.it; }
+    return true;
+  };
+
+  // ---- compute state: rows wid * 32 .. + 31 of the tile, all BN columns ----
+  const int wr = wid, wc = 0;
+  const int lane_sw = swz<CPR>(lane & 15, lane >> 4);   // fragment read offset in a 16-row block
+  floatx4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  floatx4 dls[FM];
+  // (the residual epilogue loads its rows' statistics itself, beside the residual planes:
+  // held through the tile, the 8 registers were spilled)
+  auto prefetch = [&](int it) __attribute__((always_inline)) {
+    if constexpr (DL && EPI != kEpiResLn) {
+      if (dl.st_in && it < n_mine) {
+        int m0, nt, m_end;
+        tile_mn(it, m0, nt, m_end);
+        const __amdgpu_buffer_rsrc_t rsi =
+            panel(dl.st_in + (int64_t)m0 * kDlParts * 2, (int64_t)(m_end - m0) * kDlParts * 8);
+        dl_prefetch_stats<FM>(dls, rsi, wr, lane);
+      }
+    }
+  };
+  // the epilogue of tile `it` (this wave's 32 rows; none in the upper half of a half tile)
+  auto epilogue = [&](int it) __attribute__((always_inline)) {
+    int m0, nt, m_end;
+    tile_mn(it, m0, nt, m_end);
+    const bool idle_t = it >= n_full && grp == 1;
+    const int n0 = nt * BN;
+    const __amdgpu_buffer_rsrc_t rc = panel(static_cast<char*>(Cout) + (int64_t)m0 * N * OUT_B,
+                                            (int64_t)(m_end - m0) * N * OUT_B);
+    __amdgpu_buffer_rsrc_t rl = rc;
+    if constexpr (EPI != kEpiF32)
+      rl = panel(Clo + (int64_t)m0 * N, (int64_t)(m_end - m0) * N * 2);
+    if (!idle_t) {
+      // the lane index laundered per call: every lane-derived address of the epilogue is then
+      // computed in the epilogue, not hoisted out of the step loop (hoisted, ~20 such values
+      // lived through the loop and the residual epilogue spilled them)
+      int ln = lane;
+      asm volatile("" : "+v"(ln));
+      if constexpr (DL) {
+        const int64_t sb = (int64_t)(m_end - m0) * kDlParts * 8;
+        const __amdgpu_buffer_rsrc_t rso =
+            panel(dl.st_out + (int64_t)m0 * kDlParts * 2, dl.st_out ? sb : 0);
+        if constexpr (EPI == kEpiResLn)
+          if (dl.st_in)
+            dl_prefetch_stats<FM>(
+                dls, panel(dl.st_in + (int64_t)m0 * kDlParts * 2, (int64_t)(m_end - m0) * kDlParts * 8),
+                wr, ln);
+        pp_dl_epilogue<EPI, CFG, AUX>(acc, bias_l, rc, rl, dls, rso, dl.st_in != nullptr, N, n0,
+                                      wr, wc, ln, dl.eps);
+      } else {
+        pipe_plain_epilogue<EPI, true, CFG, P_NO_STORE, AUX>(acc, bias_l, rc, rl, N, n0, wr, wc,
+                                                             ln);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  };
+
+  prefetch(0);
+  issue(fa, false);                              // stages 0 and 1
+  issue(fa, false);
+  if (grp == 0) {
+    issue(fw, true);
+    issue(fw, true);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (grp == 1 && steps > 0) __builtin_amdgcn_s_barrier();   // half a step behind group 0
+  asm volatile("" ::: "memory");
+  int it_c = 0, kt_c = 0;
+  bool pending = false;                          // a finished tile awaits its epilogue
+  // vector-memory ops an epilogue issues (all unconditional for a wave with rows): the counted
+  // waits below leave them in flight instead of draining them with the DMAs they wait for
+  // (vmcnt is positional: "all but the N youngest done")
+  constexpr int S_EPI = FM * FN;
+  constexpr int DA = 2 * LA2;                    // own-A DMAs per stage (both planes)
+  bool prev_epi_stores = false;                  // the previous M phase ran a storing epilogue
+  for (int g = 0; g < steps; ++g) {
+    // ---------------- M phase ----------------
+    const bool epi = pending;
+    const bool epi_stores = epi && !P_NO_STORE && !(it_c - 1 >= n_full && grp == 1);
+    // own A rows of stage g (issued at the end of M phase g - 2; younger than them: the
+    // previous M phase's epilogue ops and its own-A DMAs of stage g + 1 — group 0's are also
+    // covered by its W wait at the end of the previous C phase)
+    if (grp == 1) {
+      if (prev_epi_stores) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(S_EPI + DA) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DA) : "memory");
+    }
+    prev_epi_stores = epi_stores;
+    bool w_issued = false;
+    if (grp == 0 && g >= 1) {
+      // W planes of stage g + 1 (their slot: both groups read stage g - 1 a barrier ago), before
+      // the epilogue's stores, so waiting for them does not wait for those
+      if constexpr (DL)
+        if (epi)
+#pragma unroll
+          for (int i = 0; i < FM; ++i) asm volatile("" ::"v"(dls[i]));   // (its loads done)
+      w_issued = issue(fw, true);
+    }
+    if (pending) {
+      if constexpr (P_NO_STORE) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            asm volatile("" ::"v"(acc[i][j]));
+            acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+          }
+      } else {
+        epilogue(it_c - 1);
+      }
+      prefetch(it_c);
+      pending = false;
+      // (the next step's fragment reads stay below the epilogue: interleaved with it, its
+      // temporaries, the accumulators and 112 fragment registers would not fit in 256)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const bool idle = halves && it_c == n_full && grp == 1;
+    // (declared per step: nothing carries fragments across steps, so they are dead during
+    // the epilogue; declared outside the loop, the compiler kept all 112 registers live)
+    half8 af[NPL][FM], wf[NPL][FN];
+    if (!idle) {
+      // swz<CPR>(16 b + (lane & 15), lane >> 4) = 64 b + lane_sw for every 16-row block b:
+      // one base address per operand, the rest immediate offsets (computed per fragment, the
+      // compiler kept ~20 loop-invariant address registers, which the in-loop deferred-LN
+      // epilogues could not spare)
+      const half8* sa = lds + (g & 1) * STAGE_H8 + lane_sw + wr * (WTM * CPR);
+      const half8* sw = lds + (g & 1) * STAGE_H8 + NPL * A_H8 + lane_sw;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int p = 0; p < NPL; ++p) af[p][i] = sa[p * A_H8 + i * 16 * CPR];
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int p = 0; p < NPL; ++p) wf[p][j] = sw[p * W_H8 + j * 16 * CPR];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // own reads done
+    // own A rows of stage g + 2 into the slot just read (nobody else reads them)
+    const bool a_issued = issue(fa, false);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    // ---------------- C phase ----------------
+    if constexpr (PROBE == 31) __builtin_amdgcn_s_setprio(1);
+    if (!idle && !P_NO_MFMA) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {   // small terms first: W_lo A_hi + W_hi A_lo + W_hi A_hi
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[1][j], af[0][i], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[0][j], af[1][i], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[0][j], af[0][i], acc[i][j], 0, 0, 0);
+        }
+    }
+    if constexpr (P_NO_MFMA) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) asm volatile("" ::"v"(wf[0][j]), "v"(wf[1][j]));
+#pragma unroll
+      for (int i = 0; i < FM; ++i) asm volatile("" ::"v"(af[0][i]), "v"(af[1][i]));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (PROBE == 31) __builtin_amdgcn_s_setprio(0);
+    if (w_issued) {   // W planes of stage g + 1 (younger: the epilogue ops, own-A DMAs)
+      if (epi_stores) {
+        if (a_issued) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(S_EPI + DA) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(S_EPI) : "memory");
+      } else {
+        if (a_issued) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DA) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
+    if (++kt_c == nk) {
+      kt_c = 0;
+      ++it_c;
+      pending = true;
+    }
+    if (grp == 0 || g + 1 < steps) __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+  if (pending) {
+    if constexpr (P_NO_STORE) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) asm volatile("" ::"v"(acc[i][j]));
+    } else {
+      epilogue(it_c - 1);
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------------
 // attention (varlen, one workgroup per (head, sequence), 8 waves (fp16) / 16 (fp16x3)).
 // K and V of the sequence's keys are staged into LDS (all of them when they fit — always for
 // head_dim 32, and for head_dim 64 up to ~288 keys in fp16x3 — else in chunks of kc keys),

@@ -54,6 +54,15 @@ struct Workspace {
   float* t2_s = nullptr;
   int* t2_i = nullptr;
   int* t2_tk = nullptr;
+  // large-k path (k > RAG_MAX_K; lk_* kernels), allocated on first use: sample maxima
+  // [32][kLkSampleMax], per query thr / count / round flag, round flags, candidates
+  // [32][kLkCap]
+  float* lk_smax = nullptr;
+  float* lk_thr = nullptr;
+  int* lk_cnt = nullptr;
+  int* lk_again = nullptr;
+  int* lk_need = nullptr;
+  int* lk_cand = nullptr;
   hipEvent_t ev_in = nullptr;   // scan-stream order: caller stream -> scan stream -> caller
   hipEvent_t ev_out = nullptr;
   hipStream_t owner = nullptr;  // stream of the last pass that used this slot
@@ -404,6 +413,67 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
   return RAG_OK;
 }
 
+// One search pass of <= 32 queries for RAG_MAX_K < k <= RAG_MAX_K_LARGE (scan_kernels.hip,
+// "Exact top-k for RAG_MAX_K < k"): qprep, a sample of the shard's tiles for the bound, then
+// kLkRounds (collect, final) launch pairs; rounds after the first return at once unless a
+// query's candidate list overflowed in the previous one.
+int ensure_lk(Workspace& w) {
+  using namespace ragmi;
+  if (w.lk_cand) return RAG_OK;
+  const size_t Q = kQ;
+  const bool ok =
+      hipMalloc(reinterpret_cast<void**>(&w.lk_smax), Q * kLkSampleMax * 4) == hipSuccess &&
+      hipMalloc(reinterpret_cast<void**>(&w.lk_thr), Q * 4) == hipSuccess &&
+      hipMalloc(reinterpret_cast<void**>(&w.lk_cnt), Q * 4) == hipSuccess &&
+      hipMalloc(reinterpret_cast<void**>(&w.lk_again), Q * 4) == hipSuccess &&
+      hipMalloc(reinterpret_cast<void**>(&w.lk_need), 64) == hipSuccess &&
+      hipMalloc(reinterpret_cast<void**>(&w.lk_cand), Q * kLkCap * 4) == hipSuccess;
+  if (!ok) return ragmi::fail(RAG_ENOMEM, "large-k workspace allocation failed");
+  return RAG_OK;
+}
+
+template <int D>
+int launch_large_k_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k,
+                        const uint32_t* filt, int64_t id_offset, float* out_s, int64_t* out_i,
+                        int32_t* out_packed, hipStream_t st) {
+  using namespace ragmi;
+  int rc = ensure_lk(w);
+  if (rc) return rc;
+  qprep_kernel<D><<<dim3(kQ), dim3(64), 0, st>>>(q, Bq, filt, w.qn, w.qfrag, w.filt, w.eps,
+                                                  store_eps(h));
+  const int n_tiles = (int)((h->count + 15) / 16);
+  // bound sample: >= 4k tiles (so k distinct-row maxima exist with margin), >= 1/32 of the
+  // shard, at most kLkSampleMax
+  const int n_sample = n_tiles == 0 ? 0 : std::min({n_tiles, std::max(4 * k, n_tiles / 32),
+                                                    kLkSampleMax});
+  if (n_sample > 0) {
+    if (filt)
+      sample_kernel<D, true><<<dim3((n_sample + 7) / 8, 1), dim3(256), 0, st>>>(
+          h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, n_tiles, n_sample, w.lk_smax);
+    else
+      sample_kernel<D, false><<<dim3((n_sample + 7) / 8, 1), dim3(256), 0, st>>>(
+          h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, n_tiles, n_sample, w.lk_smax);
+  }
+  lk_bound_kernel<<<dim3(Bq), dim3(256), 0, st>>>(w.lk_smax, n_sample, k, w.eps, w.lk_thr,
+                                                  w.lk_cnt, w.lk_again, w.lk_need);
+  const int cgrid = (int)std::max<int64_t>(1, std::min<int64_t>(4 * h->n_cu, (n_tiles + 3) / 4));
+  for (int r = 0; r < kLkRounds; ++r) {
+    if (filt)
+      lk_collect_kernel<D, true><<<dim3(cgrid), dim3(256), 0, st>>>(
+          h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, n_tiles, Bq, w.lk_thr, w.lk_cnt,
+          w.lk_cand, w.lk_again, w.lk_need, r);
+    else
+      lk_collect_kernel<D, false><<<dim3(cgrid), dim3(256), 0, st>>>(
+          h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, n_tiles, Bq, w.lk_thr, w.lk_cnt,
+          w.lk_cand, w.lk_again, w.lk_need, r);
+    lk_final_kernel<D><<<dim3(Bq), dim3(256), 0, st>>>(
+        h->corpus, w.qn, k, w.lk_cnt, w.lk_cand, w.eps, w.lk_thr, w.lk_again, w.lk_need, r,
+        w.fb_tier, w.fb_cnt, id_offset, out_s, out_i, out_packed, h->rows32);
+  }
+  RAG_HIP(hipGetLastError());
+  return RAG_OK;
+}
+
 template <int D>
 void launch_import(rag_index* h, const half8* in, int64_t row0, int64_t n, hipStream_t st) {
   const int64_t total = n * (D / 8);
@@ -455,9 +525,11 @@ int search_locked(rag_index* h, const float* q, int B, int k, const uint32_t* fi
                   hipStream_t st) {
   if (B < 0 || (B > 0 && (!q || (!out_packed && (!out_s || !out_i)))))
     return ragmi::fail(RAG_EINVAL, "bad search args");
-  if (k < 1 || k > RAG_MAX_K) return ragmi::fail(RAG_ERANGE, "k must be in [1, RAG_MAX_K=32]");
+  if (k < 1 || k > RAG_MAX_K_LARGE)
+    return ragmi::fail(RAG_ERANGE, "k must be in [1, RAG_MAX_K_LARGE=4096]");
   RAG_HIP(hipSetDevice(h->device));
-  const int per_pass = ragmi::kQ * h->groups;
+  const bool large = k > RAG_MAX_K;
+  const int per_pass = large ? ragmi::kQ : ragmi::kQ * h->groups;
   for (int b0 = 0; b0 < B; b0 += per_pass) {
     const int Bq = std::min(per_pass, B - b0);
     Workspace* wp = nullptr;
@@ -480,6 +552,19 @@ int search_locked(rag_index* h, const float* q, int B, int k, const uint32_t* fi
     int rc;
     h->last_ws = &w;
     h->last_bq = Bq;
+    if (large) {
+      float* os = out_packed ? nullptr : out_s + (int64_t)b0 * k;
+      int64_t* oi = out_packed ? nullptr : out_i + (int64_t)b0 * k;
+      int32_t* op = out_packed ? out_packed + (int64_t)b0 * k * 2 : nullptr;
+      const uint32_t* fq = filt ? filt + 2 * b0 : nullptr;
+      rc = h->dim == 384
+               ? launch_large_k_pass<384>(h, w, q + (int64_t)b0 * h->dim, Bq, k, fq, id_offset, os,
+                                          oi, op, st)
+               : launch_large_k_pass<1024>(h, w, q + (int64_t)b0 * h->dim, Bq, k, fq, id_offset,
+                                           os, oi, op, st);
+      if (rc) return rc;
+      continue;
+    }
     if (h->dim == 384)
       rc = launch_search_pass<384>(
           h, w, q + (int64_t)b0 * h->dim, Bq, k, filt ? filt + 2 * b0 : nullptr, id_offset,
@@ -786,6 +871,9 @@ int rag_index_destroy(rag_index_t* h) {
     if (w.tileq) (void)hipFree(w.tileq);
     for (void* p : {(void*)w.t2, (void*)w.t2_s, (void*)w.t2_i, (void*)w.t2_tk})
       if (p) (void)hipFree(p);
+    for (void* p : {(void*)w.lk_smax, (void*)w.lk_thr, (void*)w.lk_cnt, (void*)w.lk_again,
+                    (void*)w.lk_need, (void*)w.lk_cand})
+      if (p) (void)hipFree(p);
     if (w.ev_in) (void)hipEventDestroy(w.ev_in);
     if (w.ev_out) (void)hipEventDestroy(w.ev_out);
   }
@@ -919,7 +1007,8 @@ int rag_index_search_host(rag_index_t* h, const float* q, int B, int k,
   ragmi::clear_error();
   if (!h) return ragmi::fail(RAG_EINVAL, "index is NULL");
   if (B < 0 || (B > 0 && (!q || !out_s || !out_i))) return ragmi::fail(RAG_EINVAL, "bad search args");
-  if (k < 1 || k > RAG_MAX_K) return ragmi::fail(RAG_ERANGE, "k must be in [1, RAG_MAX_K=32]");
+  if (k < 1 || k > RAG_MAX_K_LARGE)
+    return ragmi::fail(RAG_ERANGE, "k must be in [1, RAG_MAX_K_LARGE=4096]");
   if (B == 0) return RAG_OK;
   std::lock_guard<std::mutex> lk(h->mu);
   RAG_HIP(hipSetDevice(h->device));
@@ -1048,11 +1137,15 @@ int rag_index_export_tags(rag_index_t* h, int64_t row0, int64_t n, uint32_t* out
 int rag_merge_topk(const float* in_s, const int64_t* in_i, int n_lists, int B, int k,
                    float* out_s, int64_t* out_i, void* stream) {
   ragmi::clear_error();
-  if (n_lists < 1 || B < 0 || k < 1 || k > RAG_MAX_K)
+  if (n_lists < 1 || B < 0 || k < 1 || k > RAG_MAX_K_LARGE)
     return ragmi::fail(RAG_EINVAL, "bad merge args");
   if (B == 0) return RAG_OK;
-  ragmi::merge_exact_kernel<false><<<dim3(B), dim3(64), 0, static_cast<hipStream_t>(stream)>>>(
-      in_s, in_i, n_lists, B, k, out_s, out_i);
+  if (k > RAG_MAX_K)
+    ragmi::merge_large_kernel<false><<<dim3(B), dim3(256), 0, static_cast<hipStream_t>(stream)>>>(
+        in_s, in_i, n_lists, B, k, out_s, out_i);
+  else
+    ragmi::merge_exact_kernel<false><<<dim3(B), dim3(64), 0, static_cast<hipStream_t>(stream)>>>(
+        in_s, in_i, n_lists, B, k, out_s, out_i);
   RAG_HIP(hipGetLastError());
   return RAG_OK;
 }
@@ -1060,11 +1153,15 @@ int rag_merge_topk(const float* in_s, const int64_t* in_i, int n_lists, int B, i
 int rag_merge_topk_packed(const int32_t* in_packed, int n_lists, int B, int k, float* out_s,
                           int64_t* out_i, void* stream) {
   ragmi::clear_error();
-  if (n_lists < 1 || B < 0 || k < 1 || k > RAG_MAX_K || (B > 0 && !in_packed))
+  if (n_lists < 1 || B < 0 || k < 1 || k > RAG_MAX_K_LARGE || (B > 0 && !in_packed))
     return ragmi::fail(RAG_EINVAL, "bad merge args");
   if (B == 0) return RAG_OK;
-  ragmi::merge_exact_kernel<true><<<dim3(B), dim3(64), 0, static_cast<hipStream_t>(stream)>>>(
-      reinterpret_cast<const float*>(in_packed), nullptr, n_lists, B, k, out_s, out_i);
+  if (k > RAG_MAX_K)
+    ragmi::merge_large_kernel<true><<<dim3(B), dim3(256), 0, static_cast<hipStream_t>(stream)>>>(
+        reinterpret_cast<const float*>(in_packed), nullptr, n_lists, B, k, out_s, out_i);
+  else
+    ragmi::merge_exact_kernel<true><<<dim3(B), dim3(64), 0, static_cast<hipStream_t>(stream)>>>(
+        reinterpret_cast<const float*>(in_packed), nullptr, n_lists, B, k, out_s, out_i);
   RAG_HIP(hipGetLastError());
   return RAG_OK;
 }

@@ -2836,6 +2836,86 @@ __global__ __launch_bounds__(64) void merge_exact_kernel(const float* __restrict
   }
 }
 
+// the same merge for 32 < k <= kLkMerge (the large-k path's exchange, round 5): one 256-thread
+// workgroup per query keeps the running best k in LDS; each further list's k entries go beside
+// them and a bitonic sort of the 2k by (score desc, row asc) keeps the first k
+constexpr int kLkMerge = 4096;
+template <bool PACKED>
+__global__ __launch_bounds__(256) void merge_large_kernel(const float* __restrict__ in_s,
+                                                          const int64_t* __restrict__ in_i,
+                                                          int n_lists, int B, int k,
+                                                          float* __restrict__ out_s,
+                                                          int64_t* __restrict__ out_i) {
+  __shared__ float ms[2 * kLkMerge];
+  __shared__ int64_t mi[2 * kLkMerge];
+  const int b = blockIdx.x;
+  int P = 1;
+  while (P < 2 * k) P <<= 1;
+  auto fetch = [&](int l, int pos, float& s, int64_t& id) {
+    s = kNegInf;
+    id = INT64_MAX;
+    const int64_t off = ((int64_t)l * B + b) * k + pos;
+    if constexpr (PACKED) {
+      const int2 pv = reinterpret_cast<const int2*>(in_s)[off];
+      if (pv.y >= 0) {
+        s = __int_as_float(pv.x);
+        id = pv.y;
+      }
+    } else {
+      const int64_t v = in_i[off];
+      if (v >= 0) {
+        s = in_s[off];
+        id = v;
+      }
+    }
+  };
+  for (int i = threadIdx.x; i < P; i += 256) {
+    float s = kNegInf;
+    int64_t id = INT64_MAX;
+    if (i < k) fetch(0, i, s, id);
+    ms[i] = s;
+    mi[i] = id;
+  }
+  // (each per-shard list is sorted best-first already: one list needs no sort)
+  for (int l = 1; l < n_lists; ++l) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < P - k; i += 256) {
+      float s = kNegInf;
+      int64_t id = INT64_MAX;
+      if (i < k) fetch(l, i, s, id);
+      ms[k + i] = s;
+      mi[k + i] = id;
+    }
+    __syncthreads();
+    for (int size = 2; size <= P; size <<= 1)
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        for (int i = threadIdx.x; i < P; i += 256) {
+          const int j = i ^ stride;
+          if (j > i) {
+            const bool best_first = (i & size) == 0;
+            const float a = ms[i], c = ms[j];
+            const int64_t ia = mi[i], ic = mi[j];
+            const bool a_better = (a > c) || (a == c && ia < ic);
+            if (best_first != a_better) {
+              ms[i] = c;
+              ms[j] = a;
+              mi[i] = ic;
+              mi[j] = ia;
+            }
+          }
+        }
+        __syncthreads();
+      }
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < k; j += 256) {
+    const float s = ms[j];
+    const bool ok = s != kNegInf;
+    out_s[(int64_t)b * k + j] = s;
+    out_i[(int64_t)b * k + j] = ok ? mi[j] : (int64_t)-1;
+  }
+}
+
 // ----------------------------------------------------------------------------------------
 // export: tile16 -> row-major fp16 (one thread per 8-half chunk)
 // ----------------------------------------------------------------------------------------
@@ -2886,6 +2966,343 @@ __global__ void import32_kernel(const float* __restrict__ in, int64_t row0, int6
     h[j] = f32_to_f16(src[j]);
   }
   corpus[(row >> 4) * (steps<D>() * 64) + (c >> 2) * 64 + (c & 3) * 16 + (row & 15)] = h;
+}
+
+// ----------------------------------------------------------------------------------------
+// Exact top-k for RAG_MAX_K < k <= RAG_MAX_K_LARGE (round 5): Qdrant's
+// query_points takes any `limit` (reference main.py:215,232-237); the scan's per-wave lists
+// hold 32. A pass of <= 32 queries runs, after qprep:
+//  1. sample_kernel over n_sample tiles spread over the shard (per tile and query the max MFMA
+//     score a of its matching rows) and lk_bound_kernel: T = the k-th largest of those maxima.
+//     They come from k distinct rows, each with exact score e >= a - eps (qprep's bound), so
+//     the k-th best exact score e_k >= T - eps and every exact top-k row has
+//     a >= e - eps >= T - 2 eps = thr. (Fewer than k finite maxima: thr = -inf.)
+//  2. lk_collect_kernel: every tile MFMA-scored; each matching row with a >= thr is appended
+//     to its query's candidate list (at most kLkCap kept; the counter counts them all).
+//  3. lk_final_kernel: per query, the candidates are rescored exactly (exact_scores_wave: the
+//     canonical fp64 order of select / the oracle) and the k best by (score desc, row asc) are
+//     emitted. They contain the exact top-k, so the result is exact. If the list overflowed,
+//     the k-th best exact score e' among the kept candidates (real rows: e_k >= e') gives a
+//     tighter thr = e' - eps, and steps 2-3 run again for that query (kLkRounds launches in
+//     all; later ones return at once unless a query was marked). A query still overflowing in
+//     the last round (more than kLkCap rows tied within 2 eps of its k-th best) is recorded
+//     as unanswered (tier 3, rag_index_unanswered), never silently truncated.
+// ----------------------------------------------------------------------------------------
+constexpr int kLkMax = 4096;       // largest k (ragmi.h RAG_MAX_K_LARGE)
+constexpr int kLkCap = 16384;      // candidates kept per query and round (exact scores in LDS)
+constexpr int kLkRounds = 3;
+constexpr int kLkSampleMax = 16384;
+
+// order-preserving uint32 key of a float (larger float -> larger key; -inf smallest finite)
+__device__ __forceinline__ uint32_t fkey(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float fkey_inv(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+// the largest key t with #{i < n : keys[i] >= t} >= k (keys in LDS; 256 threads); sets *ge
+// to that count. Requires n >= k.
+__device__ uint32_t lk_kth_key(const uint32_t* keys, int n, int k, int* red) {
+  uint32_t t = 0;
+  for (int bit = 31; bit >= 0; --bit) {
+    const uint32_t c = t | (1u << bit);
+    int m = 0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) m += keys[i] >= c;
+    __syncthreads();
+    if (threadIdx.x == 0) *red = 0;
+    __syncthreads();
+    atomicAdd(red, m);
+    __syncthreads();
+    if (*red >= k) t = c;
+  }
+  return t;
+}
+
+// per query q < B: thr[q] from the sample maxima smax [32][n_sample]; resets the round state
+__global__ __launch_bounds__(256) void lk_bound_kernel(const float* __restrict__ smax,
+                                                       int n_sample, int k,
+                                                       const float* __restrict__ eps,
+                                                       float* __restrict__ thr,
+                                                       int* __restrict__ cnt,
+                                                       int* __restrict__ again,
+                                                       int* __restrict__ need) {
+  __shared__ uint32_t keys[kLkSampleMax];
+  __shared__ int red;
+  const int q = blockIdx.x;
+  int fin = 0;
+  for (int i = threadIdx.x; i < n_sample; i += 256) {
+    const float v = smax[(int64_t)q * n_sample + i];
+    keys[i] = fkey(v);
+    fin += v != kNegInf;
+  }
+  if (threadIdx.x == 0) red = 0;
+  __syncthreads();
+  atomicAdd(&red, fin);
+  __syncthreads();
+  const int n_fin = red;
+  __syncthreads();
+  float th = kNegInf;
+  if (n_fin >= k) {
+    const float T = fkey_inv(lk_kth_key(keys, n_sample, k, &red));
+    const double d = (double)T - 2.0 * (double)eps[q];
+    th = (float)d;
+    if ((double)th > d) th = nextafterf(th, kNegInf);   // round toward -inf
+  }
+  if (threadIdx.x == 0) {
+    thr[q] = th;
+    cnt[q] = 0;
+    again[q] = 1;     // round 0 processes every query
+  }
+  if (q == 0 && threadIdx.x < kLkRounds) need[threadIdx.x] = threadIdx.x == 0 ? 1 : 0;
+}
+
+// every tile against the pass's queries: append matching rows with a >= thr[q]. One wave per
+// tile per step (grid-stride). round > 0: only if the previous round marked a query, and only
+// the marked queries.
+template <int D, bool FILTER>
+__global__ __launch_bounds__(256) void lk_collect_kernel(const half8* __restrict__ corpus,
+                                                         const uint32_t* __restrict__ tags,
+                                                         const uint32_t* __restrict__ filt,
+                                                         const half8* __restrict__ qfrag,
+                                                         int n_rows, int n_tiles, int B,
+                                                         const float* __restrict__ thr,
+                                                         int* __restrict__ cnt,
+                                                         int* __restrict__ cand,
+                                                         const int* __restrict__ again,
+                                                         const int* __restrict__ need, int round) {
+  constexpr int S = steps<D>();
+  if (!need[round]) return;
+  const int lane = threadIdx.x & 63;
+  const int nw = gridDim.x * 4;
+  const int w0 = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // this lane's two queries: (l & 15) and 16 + (l & 15)
+  const int qa = lane & 15, qb = 16 + (lane & 15);
+  const bool la = qa < B && again[qa], lb = qb < B && again[qb];
+  const float ta = la ? thr[qa] : __builtin_inff(), tb = lb ? thr[qb] : __builtin_inff();
+  uint32_t fma_ = 0, fva = 0, fmb = 0, fvb = 0;
+  if constexpr (FILTER) {
+    fma_ = filt[2 * qa];
+    fva = filt[2 * qa + 1];
+    fmb = filt[2 * qb];
+    fvb = filt[2 * qb + 1];
+  }
+  for (int t = w0; t < n_tiles; t += nw) {
+    const half8* p = corpus + (int64_t)t * (S * 64) + lane;
+    floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    constexpr int CH = S <= 12 ? S : 8;
+    static_assert(S % CH == 0, "k-step chunks");
+    for (int c = 0; c < S / CH; ++c) {
+      half8 a[CH], b0[CH], b1[CH];
+#pragma unroll
+      for (int s = 0; s < CH; ++s) {
+        a[s] = __builtin_nontemporal_load(p + (c * CH + s) * 64);
+        b0[s] = qfrag[(c * CH + s) * 64 + lane];
+        b1[s] = qfrag[(S + c * CH + s) * 64 + lane];
+      }
+#pragma unroll
+      for (int s = 0; s < CH; ++s) {
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[s], b0[s], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[s], b1[s], acc1, 0, 0, 0);
+      }
+    }
+    const int rbase = t * kTileRows + 4 * (lane >> 4);
+    uint4 tg = {0u, 0u, 0u, 0u};
+    if constexpr (FILTER) tg = *reinterpret_cast<const uint4*>(tags + rbase);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = rbase + r;
+      if (row >= n_rows) break;
+      bool oka = acc0[r] >= ta, okb = acc1[r] >= tb;
+      if constexpr (FILTER) {
+        const uint32_t tr = r == 0 ? tg.x : r == 1 ? tg.y : r == 2 ? tg.z : tg.w;
+        oka = oka && ((tr & fma_) == fva);
+        okb = okb && ((tr & fmb) == fvb);
+      }
+      if (oka) {
+        const int pos = atomicAdd(&cnt[qa], 1);
+        if (pos < kLkCap) cand[qa * kLkCap + pos] = row;
+      }
+      if (okb) {
+        const int pos = atomicAdd(&cnt[qb], 1);
+        if (pos < kLkCap) cand[qb * kLkCap + pos] = row;
+      }
+    }
+  }
+}
+
+// per query (workgroup q < B): exact rescoring of the candidates, then the top-k by
+// (score desc, row asc) -> output; on overflow a tighter thr and another round (see above).
+template <int D>
+__global__ __launch_bounds__(256) void lk_final_kernel(const half8* __restrict__ corpus,
+                                                       const float* __restrict__ qn, int k,
+                                                       int* __restrict__ cnt,
+                                                       const int* __restrict__ cand,
+                                                       const float* __restrict__ eps,
+                                                       float* __restrict__ thr,
+                                                       int* __restrict__ again,
+                                                       int* __restrict__ need, int round,
+                                                       int* __restrict__ tier,
+                                                       unsigned long long* __restrict__ fb_cnt,
+                                                       int64_t id_offset,
+                                                       float* __restrict__ out_s,
+                                                       int64_t* __restrict__ out_i,
+                                                       int32_t* __restrict__ out_packed,
+                                                       const float* __restrict__ rows32) {
+  __shared__ float es[kLkCap];            // exact scores of the kept candidates
+  __shared__ float ss[kLkMax];            // the selected entries (sorted in place)
+  __shared__ int si[kLkMax];
+  __shared__ int red, red2, verdict;
+  const int q = blockIdx.x, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (!need[round] || !again[q]) return;
+  const int total = cnt[q];
+  const int n = min(total, kLkCap);
+  const int* cq = cand + (int64_t)q * kLkCap;
+  const float* qq = qn + (int64_t)q * D;
+  // 1. exact scores of the kept candidates, 8 rows per wave per round trip
+  constexpr int NC = 8;
+  for (int i0 = wid * NC; i0 < n; i0 += 4 * NC) {
+    int rows[NC];
+#pragma unroll
+    for (int j = 0; j < NC; ++j) rows[j] = i0 + j < n ? cq[i0 + j] : -1;
+    float sc[NC];
+    exact_scores_wave<D, NC>(corpus, rows, qq, lane, sc, rows32);
+    if (lane == 0)
+#pragma unroll
+      for (int j = 0; j < NC; ++j)
+        if (i0 + j < n) es[i0 + j] = sc[j];
+  }
+  __syncthreads();
+  // block-wide count of the candidates passing pred(i)
+  auto count_if = [&](auto pred) -> int {
+    int m = 0;
+    for (int i = threadIdx.x; i < n; i += 256) m += pred(i) ? 1 : 0;
+    if (threadIdx.x == 0) red = 0;
+    __syncthreads();
+    atomicAdd(&red, m);
+    __syncthreads();
+    const int r = red;
+    __syncthreads();
+    return r;
+  };
+  // 2. tkey = the key of the kk-th best exact score among the kept candidates
+  const int kk = min(k, n);
+  uint32_t tkey = 0;
+  if (kk > 0)
+    for (int bit = 31; bit >= 0; --bit) {
+      const uint32_t c = tkey | (1u << bit);
+      if (count_if([&](int i) { return fkey(es[i]) >= c; }) >= kk) tkey = c;
+    }
+  if (total > kLkCap) {
+    // overflow: the kept candidates are real rows, so e_k >= fkey_inv(tkey) and every exact
+    // top-k row has a >= that - eps: a tighter threshold for the next round
+    if (threadIdx.x == 0) {
+      verdict = 0;                            // 0: unanswered, 1: another round
+      if (round + 1 < kLkRounds && n >= k) {
+        const double d = (double)fkey_inv(tkey) - (double)eps[q];
+        float th = (float)d;
+        if ((double)th > d) th = nextafterf(th, kNegInf);
+        if (th > thr[q]) {
+          thr[q] = th;
+          cnt[q] = 0;
+          need[round + 1] = 1;                // (again[q] stays 1)
+          verdict = 1;
+        }
+      }
+      if (!verdict) {                         // no progress possible: tier 3
+        tier[q] = 3;
+        atomicAdd(&fb_cnt[2], 1ull);
+        again[q] = 0;
+      }
+    }
+    __syncthreads();
+    if (verdict) return;
+    for (int j = threadIdx.x; j < k; j += 256) {
+      if (out_packed) {
+        out_packed[((int64_t)q * k + j) * 2] = __float_as_int(kNegInf);
+        out_packed[((int64_t)q * k + j) * 2 + 1] = -1;
+      } else {
+        out_s[(int64_t)q * k + j] = kNegInf;
+        out_i[(int64_t)q * k + j] = -1;
+      }
+    }
+    return;
+  }
+  // 3. the selected set: every candidate with key > tkey, then the ties (key == tkey) by row
+  //    ascending up to kk — rcut = the largest admitted tie row
+  const int gt = kk > 0 ? count_if([&](int i) { return fkey(es[i]) > tkey; }) : 0;
+  const int need_eq = kk - gt;
+  int rcut = -1;
+  if (need_eq > 0) {
+    // the largest r with #{ties with row < r} < need_eq: then row r is a tie row and exactly
+    // need_eq ties have row <= r (rows are distinct within a round)
+    uint32_t r = 0;
+    for (int bit = 30; bit >= 0; --bit) {
+      const uint32_t c = r | (1u << bit);
+      if (count_if([&](int i) { return fkey(es[i]) == tkey && (uint32_t)cq[i] < c; }) < need_eq)
+        r = c;
+    }
+    rcut = (int)r;
+  }
+  if (threadIdx.x == 0) red2 = 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += 256) {
+    const float s = es[i];
+    const uint32_t key = fkey(s);
+    const int row = cq[i];
+    if (kk > 0 && (key > tkey || (key == tkey && row <= rcut))) {
+      const int p = atomicAdd(&red2, 1);
+      if (p < kLkMax) {
+        ss[p] = s;
+        si[p] = row;
+      }
+    }
+  }
+  __syncthreads();
+  // 4. bitonic sort of the kk selected entries by (score desc, row asc), padded to P
+  int P = 1;
+  while (P < kk) P <<= 1;
+  for (int i = kk + threadIdx.x; i < P; i += 256) {
+    ss[i] = kNegInf;
+    si[i] = kIdNone32;
+  }
+  __syncthreads();
+  for (int size = 2; size <= P; size <<= 1)
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = threadIdx.x; i < P; i += 256) {
+        const int j = i ^ stride;
+        if (j > i) {
+          const bool best_first = (i & size) == 0;
+          const float a = ss[i], b = ss[j];
+          const int ia = si[i], ib = si[j];
+          const bool a_better = (a > b) || (a == b && ia < ib);
+          if (best_first != a_better) {
+            ss[i] = b;
+            ss[j] = a;
+            si[i] = ib;
+            si[j] = ia;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  for (int j = threadIdx.x; j < k; j += 256) {
+    const bool ok = j < kk;
+    const float s = ok ? ss[j] : kNegInf;
+    const int id = ok ? si[j] : -1;
+    if (out_packed) {
+      out_packed[((int64_t)q * k + j) * 2] = __float_as_int(s);
+      out_packed[((int64_t)q * k + j) * 2 + 1] = ok ? (int32_t)(id + id_offset) : -1;
+    } else {
+      out_s[(int64_t)q * k + j] = s;
+      out_i[(int64_t)q * k + j] = ok ? (int64_t)id + id_offset : (int64_t)-1;
+    }
+  }
+  if (threadIdx.x == 0) {
+    tier[q] = 0;
+    again[q] = 0;
+  }
 }
 
 }  // namespace ragmi

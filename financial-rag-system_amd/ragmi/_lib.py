@@ -29,6 +29,42 @@ class RagmiUnavailable(RuntimeError):
     """libragmi.so is not built or cannot be loaded (no CPU fallback exists)."""
 
 
+class RagmiDeviceError(ValueError):
+    """A device the HIP-only build cannot run on — notably the reference's USE_GPU=false
+    "cpu" (main.py:83,89) — or a HIP device index that does not exist."""
+
+
+def resolve_device(device) -> torch.device | None:
+    """The HIP device behind a reference-style `device` argument (main.py:83,89:
+    ``device = "cuda" if USE_GPU else "cpu"``; sentence-transformers takes a str, an int or a
+    torch.device). None -> None (the caller takes the current HIP device); "cuda" / "cuda:N" /
+    N / torch.device("cuda", N) -> that device. Any other type — "cpu" above all — raises
+    RagmiDeviceError instead of silently running on the GPU: this build has no CPU path.
+    Checked before any HIP call, so the refusal is the same with or without a GPU."""
+    if device is None:
+        return None
+    try:
+        d = device if isinstance(device, torch.device) else torch.device(device)
+    except (RuntimeError, TypeError) as e:
+        raise RagmiDeviceError(f"device {device!r}: {e}") from e
+    if d.type != "cuda":
+        raise RagmiDeviceError(
+            f"device {str(d)!r}: ragmi is a HIP-only build (MI355X, gfx950) with no CPU path; "
+            "the reference's USE_GPU=false / device='cpu' cannot be honoured — pass "
+            "device='cuda' or 'cuda:N' (or None for the current HIP device)")
+    return d
+
+
+def device_index(d: torch.device | None) -> int:
+    """Index of a resolved HIP device (resolve_device), the current one for None / 'cuda'."""
+    if d is None or d.index is None:
+        return torch.cuda.current_device()
+    n = torch.cuda.device_count()
+    if not 0 <= d.index < n:
+        raise RagmiDeviceError(f"device {str(d)!r}: {n} HIP device(s) visible")
+    return d.index
+
+
 class RagmiError(RuntimeError):
     def __init__(self, code: int, msg: str):
         super().__init__(f"libragmi error {code}: {msg}")

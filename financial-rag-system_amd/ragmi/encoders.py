@@ -301,12 +301,12 @@ class BertEncoder:
 
     def __init__(self, cfg: dict, weights: dict, head: int, device=None,
                  precision: str = "fp16x3", diagnostic: bool = False):
+        # the reference's device argument (main.py:83,89): "cuda[:N]" / None run on that HIP
+        # device; "cpu" (USE_GPU=false) is refused, never remapped (_lib.resolve_device)
+        dev = _lib.resolve_device(device)
         _lib.require_gpu()
         self._L = _lib.load()
-        self.device = torch.device(device if device is not None else
-                                   torch.device("cuda", torch.cuda.current_device()))
-        if self.device.index is None:
-            self.device = torch.device("cuda", torch.cuda.current_device())
+        self.device = torch.device("cuda", _lib.device_index(dev))
         self.cfg, self.head = dict(cfg), head
         self.precision = precision
         c, arrs, ptrs = _weight_ptrs(cfg, weights, head, precision)
@@ -566,6 +566,7 @@ class SentenceTransformer:
 
     def __init__(self, model_dir: str | None = None, device=None, *, cfg=None, weights=None,
                  vocab_file=None, max_seq_length: int | None = None, precision: str = "fp16x3"):
+        _lib.resolve_device(device)                # "cpu" refused before the checkpoint loads
         if model_dir is not None:
             st_head_from_dir(model_dir)            # refuses any head but CLS + Normalize
             cfg, weights, vocab_file, _ = _load_dir(model_dir)
@@ -611,6 +612,7 @@ class CrossEncoder:
     def __init__(self, model_dir: str | None = None, device=None, *, cfg=None, weights=None,
                  vocab_file=None, max_length: int | None = None, precision: str = "fp16x3",
                  activation_fn=None, default_activation_function=None):
+        _lib.resolve_device(device)                # "cpu" refused before the checkpoint loads
         hf = None
         if model_dir is not None:
             cfg, weights, vocab_file, hf = _load_dir(model_dir)

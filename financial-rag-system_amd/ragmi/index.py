@@ -17,7 +17,8 @@ import torch
 from . import _lib
 from ._lib import check
 
-MAX_K = 32          # RAG_MAX_K in include/ragmi.h
+MAX_K = 32          # RAG_MAX_K in include/ragmi.h: the scan's certified top-k path
+MAX_K_LARGE = 4096  # RAG_MAX_K_LARGE: k in (32, 4096] takes the exact large-k pass
 QUERY_TILE = 32     # RAG_QUERY_TILE
 STORAGE = {"fp16": 0, "fp32": 1}   # RAG_STORE_FP16 / RAG_STORE_FP32
 CREATE_DIAGNOSTIC = 0x100          # RAG_CREATE_DIAGNOSTIC: honour the RAGMI_* A/B knobs
@@ -46,15 +47,10 @@ class FlatIndex:
 
     def __init__(self, dim: int = 384, capacity: int = 0, device=None, storage: str = "fp16",
                  diagnostic: bool = False):
+        dev = _lib.resolve_device(device)        # "cpu" refused before any HIP call
         _lib.require_gpu()
         self._L = _lib.load()
-        if device is None:
-            device = torch.device("cuda", torch.cuda.current_device())
-        device = torch.device(device)
-        if device.type != "cuda":
-            raise ValueError("FlatIndex lives on a HIP device (torch 'cuda' device)")
-        self.device = torch.device("cuda", device.index if device.index is not None
-                                   else torch.cuda.current_device())
+        self.device = torch.device("cuda", _lib.device_index(dev))
         self.dim = int(dim)
         if storage not in STORAGE:
             raise ValueError(f"storage must be one of {sorted(STORAGE)}")
@@ -119,8 +115,8 @@ class FlatIndex:
 
     # ---------------------------------------------------------------- search
     def _search_args(self, queries, k, filters):
-        if not 1 <= k <= MAX_K:
-            raise ValueError(f"k must be in [1, {MAX_K}]")
+        if not 1 <= k <= MAX_K_LARGE:
+            raise ValueError(f"k must be in [1, {MAX_K_LARGE}]")
         q = _as_dev(queries, torch.float32, self.device)
         if q.dim() == 1:
             q = q.unsqueeze(0)

@@ -31,7 +31,7 @@ import numpy as np
 import torch
 
 from . import qdrant_models as models
-from .index import MAX_K, FlatIndex
+from .index import MAX_K, MAX_K_LARGE, FlatIndex
 
 DEFAULT_TAG_FIELDS = ("ticker", "document_type")
 
@@ -57,7 +57,8 @@ class UnsupportedFilter(NotImplementedError):
 
 
 class LimitTooLarge(ValueError):
-    """query_points(limit > RAG_MAX_K): refused loudly, never answered with empty points."""
+    """query_points(limit > RAG_MAX_K_LARGE on a collection of more points): refused loudly,
+    never answered with empty points (ragmi.rag lets it through the reference's swallow)."""
 
 
 class PayloadTags:
@@ -294,10 +295,13 @@ class Collection:
             B = len(filters)
             if limit < 1:
                 return [[] for _ in range(B)]
-            if limit > MAX_K:
-                raise LimitTooLarge(f"limit {limit} > {MAX_K} is not supported by the GPU "
-                                    f"top-k (the reference uses limit=15, main.py:215)")
-            k = limit
+            # Qdrant answers at most the collection's points: a limit past them is the whole
+            # collection, which fits any k once it holds <= RAG_MAX_K_LARGE points
+            k = min(limit, max(1, self.index.count))
+            if k > MAX_K_LARGE:
+                raise LimitTooLarge(f"limit {limit} > {MAX_K_LARGE} (RAG_MAX_K_LARGE) over "
+                                    f"{self.index.count} points (the reference uses "
+                                    f"limit=15, main.py:215)")
             live = [i for i, f in enumerate(filters) if f is not None]
             out = [[] for _ in range(B)]
             if not live or self.index.count == 0:

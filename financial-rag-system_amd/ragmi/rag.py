@@ -39,6 +39,13 @@ EMBED_BATCH = 64                                 # ingest.py:27
 UPSERT_BATCH = 256                               # ingest.py:28
 RETRIEVE_LIMIT = 15                              # main.py:215
 PRECISION = os.getenv("RAGMI_PRECISION", "fp16x3")
+# main.py:23 — the loaders pass device = "cuda" if USE_GPU else "cpu" (main.py:83,89), read per
+# call here so tests can set it; "cpu" makes the encoders raise RagmiDeviceError (this build
+# has no CPU path): set USE_GPU=true, as the reference needs on a GPU host.
+
+
+def _device() -> str:
+    return "cuda" if os.getenv("USE_GPU", "false").lower() == "true" else "cpu"
 
 
 def _testing() -> bool:
@@ -55,7 +62,7 @@ def get_embedder():
     if not d:
         raise RuntimeError("set RAGMI_BGE_DIR to a local bge-small-en-v1.5 directory "
                            "(config.json, model.safetensors, vocab.txt)")
-    return SentenceTransformer(d, precision=PRECISION)
+    return SentenceTransformer(d, device=_device(), precision=PRECISION)
 
 
 @lru_cache()
@@ -66,7 +73,7 @@ def get_reranker():
     d = os.environ.get("RAGMI_CE_DIR")
     if not d:
         raise RuntimeError("set RAGMI_CE_DIR to a local ms-marco-MiniLM-L-6-v2 directory")
-    return CrossEncoder(d, precision=PRECISION)
+    return CrossEncoder(d, device=_device(), precision=PRECISION)
 
 
 @lru_cache()
@@ -115,16 +122,16 @@ def _filter(ticker, document_type=None):
 def retrieve_from_qdrant(query_vector, ticker, document_type=None, limit=RETRIEVE_LIMIT):
     if _testing():
         return type("obj", (object,), {"points": []})
-    from .index import MAX_K
-    if int(limit) > MAX_K:
-        # outside the reference's swallow-to-empty (main.py:238-239): an unsupported limit
-        # must not look like "no matching documents"
-        from .qdrant import LimitTooLarge
-        raise LimitTooLarge(f"limit {limit} > {MAX_K} (RAG_MAX_K)")
+    from .qdrant import LimitTooLarge
     try:
         return get_qdrant().query_points(collection_name=COLLECTION_NAME, query=query_vector,
                                          limit=limit,
                                          query_filter=_filter(ticker, document_type))
+    except LimitTooLarge:
+        # past the reference's swallow-to-empty (main.py:238-239): a limit the build cannot
+        # answer (> RAG_MAX_K_LARGE over a larger collection) must not look like "no matching
+        # documents"
+        raise
     except Exception:
         return type("obj", (object,), {"points": []})
 

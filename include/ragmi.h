@@ -63,6 +63,13 @@ enum {
  * re-scored exactly, from the scan's per-wave lists when they provably hold all of them,
  * otherwise by a second pass over the shard (see rag_index_exactness_stats). */
 #define RAG_MAX_K 32
+/* Largest k overall (round 5; Qdrant's query_points takes any `limit`, main.py:215,232-237).
+ * RAG_MAX_K < k <= RAG_MAX_K_LARGE runs a separate exact pass per 32 queries: a sampled
+ * certified lower bound of each query's k-th best score, every row whose MFMA score can reach
+ * it collected, all of those re-scored exactly, the k best by (score desc, row asc) emitted —
+ * the same exact result and canonical scores as the k <= 32 path (scan_kernels.hip, "Exact
+ * top-k for RAG_MAX_K < k"). rag_merge_topk[_packed] accept the same k. */
+#define RAG_MAX_K_LARGE 4096
 /* Queries handled per scan pass; larger batches run ceil(B/32) passes. */
 #define RAG_QUERY_TILE 32
 

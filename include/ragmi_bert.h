@@ -146,7 +146,9 @@ enum { RAG_GEMM_AUTO = 0, RAG_GEMM_TILE = 1, RAG_GEMM_PIPE = 2, RAG_GEMM_PROBE_N
        RAG_GEMM_WS_BIG128_MFMA_ONLY = 36, RAG_GEMM_WS_BIG128_DMA_ONLY = 37,
        RAG_GEMM_WS_BIG128_NO_STORE = 38, RAG_GEMM_WS_PROBE_HI_ONLY = 39,
        RAG_GEMM_WS_PROBE_FP8_CORR = 40, RAG_GEMM_WS_REGSTAGE = 41,
-       RAG_GEMM_WS_REGSTAGE_INTAKE = 42, RAG_GEMM_WS_L2PF = 43, RAG_GEMM_WS_L2PF_INTAKE = 44 };
+       RAG_GEMM_WS_REGSTAGE_INTAKE = 42, RAG_GEMM_WS_L2PF = 43, RAG_GEMM_WS_L2PF_INTAKE = 44,
+       RAG_GEMM_PP = 45, RAG_GEMM_PP_MFMA_ONLY = 46, RAG_GEMM_PP_DMA_ONLY = 47,
+       RAG_GEMM_PP_NO_STORE = 48, RAG_GEMM_PP_PRIO = 49 };
 int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, const void* W,
                   const void* W_lo, const float* bias, int M, int N, int K, void* C,
                   void* C_lo, void* stream);

@@ -63,6 +63,7 @@ def main():
     tmp = tempfile.mkdtemp(prefix="cfg1_")
     write_model(os.path.join(tmp, "bge"), cfg, w, vocab)
     os.environ["TESTING"] = "False"
+    os.environ["USE_GPU"] = "true"
     os.environ["RAGMI_BGE_DIR"] = os.path.join(tmp, "bge")
     import ragmi.rag as rag
 

@@ -30,7 +30,9 @@ VNAME = {0: "auto", 1: "tile", 2: "pipe", 3: "probe_no_mfma", 4: "probe_no_dma",
          33: "ws_nohalf", 34: "ws_small", 35: "ws_big128",
          36: "ws_big128_mfma_only", 37: "ws_big128_dma_only", 38: "ws_big128_no_store",
          39: "ws_probe_hi_only", 40: "ws_probe_fp8_corr", 41: "ws_regstage",
-         42: "ws_regstage_intake", 43: "ws_l2pf", 44: "ws_l2pf_intake"}
+         42: "ws_regstage_intake", 43: "ws_l2pf", 44: "ws_l2pf_intake",
+         45: "pp", 46: "pp_mfma_only", 47: "pp_dma_only",
+         48: "pp_no_store", 49: "pp_wb_stores"}
 LAYERS = {
     "small": [("qkv", 1152, 384, EPI_F16), ("o", 384, 384, EPI_F32),
               ("ffn1", 1536, 384, EPI_GELU_F16), ("ffn2", 384, 1536, EPI_F32)],
@@ -62,8 +64,9 @@ def main():
     Ms = [int(x) for x in os.environ.get("GEMM_M", "117000,14800,782").split(",")]
     variants = [int(x) for x in os.environ.get("GEMM_VARIANTS", "1,2").split(",")]
     for M in Ms:
-        for prec in ("fp16", "fp16x3"):
-            tot = {v: 0.0 for v in variants}
+        for prec in os.environ.get("GEMM_PRECS", "fp16,fp16x3").split(","):
+            vs = [v for v in variants if prec == "fp16x3" or v < 45]   # PP: fp16x3 only
+            tot = {v: 0.0 for v in vs}
             for name, N, K, epi in LAYERS[os.environ.get("GEMM_LAYER", "small")]:
                 g = torch.Generator(device="cuda")
                 g.manual_seed(0)
@@ -74,7 +77,7 @@ def main():
                     if prec == "fp16x3" else None
                 wl = (torch.randn((N, K), generator=g, device="cuda") * 1e-5).half() \
                     if prec == "fp16x3" else None
-                for v in variants:
+                for v in vs:
                     ms = timeit(lambda: linear(a, w, bias, epi, al, wl, v))
                     fl = 2.0 * M * N * K
                     pipe_fl = fl * (3 if prec == "fp16x3" else 1)

@@ -2,6 +2,7 @@
 216, 242-243), payload-filter compilation, point ids, ingest point construction. No GPU."""
 import hashlib
 import importlib
+import os
 import uuid
 
 import numpy as np
@@ -86,15 +87,35 @@ def test_reference_model_constructors():
     assert m.Filter(must=[fc]).must[0].match.value == "AAPL"
 
 
-def test_limit_above_max_k_fails_loudly(monkeypatch):
-    """limit > RAG_MAX_K is refused before the reference's swallow-to-empty wrapper
-    (main.py:238-239): an unsupported limit must not read as 'no documents'."""
+def test_limit_too_large_fails_loudly(monkeypatch):
+    """A limit the build cannot answer (> RAG_MAX_K_LARGE over a larger collection) passes the
+    reference's swallow-to-empty wrapper (main.py:238-239) as LimitTooLarge: it must not read
+    as 'no documents'. Any other query error still gives empty points, as in the reference."""
     monkeypatch.setenv("TESTING", "False")
     import ragmi.rag as rag
     rag = importlib.reload(rag)
     from ragmi.qdrant import LimitTooLarge
+
+    class Fake:
+        def __init__(self, exc):
+            self.exc = exc
+
+        def query_points(self, **kw):
+            raise self.exc
+
+    monkeypatch.setattr(rag, "get_qdrant", lambda: Fake(LimitTooLarge("limit 5000")))
     with pytest.raises(LimitTooLarge):
-        rag.retrieve_from_qdrant([0.0] * 384, "aapl", limit=33)
+        rag.retrieve_from_qdrant([0.0] * 384, "aapl", limit=5000)
+    monkeypatch.setattr(rag, "get_qdrant", lambda: Fake(RuntimeError("down")))
+    assert rag.retrieve_from_qdrant([0.0] * 384, "aapl", limit=5000).points == []
+
+
+def test_limit_range_constants():
+    from ragmi import index
+    assert index.MAX_K == 32 and index.MAX_K_LARGE == 4096
+    hdr = open(os.path.join(os.path.dirname(os.path.dirname(__file__)), "include",
+                            "ragmi.h")).read()
+    assert "#define RAG_MAX_K 32" in hdr and "#define RAG_MAX_K_LARGE 4096" in hdr
 
 
 def test_rerank_batch_is_one_forward(monkeypatch):

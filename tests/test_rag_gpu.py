@@ -41,6 +41,7 @@ def rag(gpu, tmp_path_factory):
     _write_model(root / "ce", cc, wc, vocab, "ce")
     mp = pytest.MonkeyPatch()
     mp.setenv("TESTING", "False")
+    mp.setenv("USE_GPU", "true")                   # main.py:23,83: device = "cuda"
     mp.setenv("RAGMI_BGE_DIR", str(root / "bge"))
     mp.setenv("RAGMI_CE_DIR", str(root / "ce"))
     import ragmi.rag as rag
