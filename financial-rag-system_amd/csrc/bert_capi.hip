@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <cstdio>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -123,6 +125,7 @@ struct EncWorkspace {
 struct rag_encoder {
   rag_bert_config cfg{};
   int device = 0;
+  bool diagnostic = false;   // counted in ragmi::diagnostic_handles() (common_host.hpp)
   std::mutex mu;
   std::vector<void*> allocs;
   float *wemb = nullptr, *pemb = nullptr, *temb = nullptr, *eg = nullptr, *eb = nullptr;
@@ -284,9 +287,9 @@ EncWorkspace* workspace_for(rag_encoder* e, hipStream_t st) {
 }
 
 // GEMM variants: RAG_GEMM_TILE (gemm_kernel: one 128x128 tile per workgroup, 2 per CU),
-// RAG_GEMM_PIPE (gemm_pipe_kernel<PipeLarge>: persistent, one 8-wave workgroup per CU, LDS-DMA
-// ring across 256x128 tiles) and RAG_GEMM_SMALL (gemm_pipe_kernel<PipeSmall>: 64x64 tiles,
-// the K panel in flight at once); AUTO's choice is below.
+// RAG_GEMM_SMALL (gemm_pipe_kernel<PipeSmall>: 64x64 tiles, the K panel in flight at once) and
+// RAG_GEMM_WS (gemm_ws_kernel<PipeLarge>: persistent, one workgroup per CU, 8 MFMA waves fed
+// by 4 loader waves through an LDS-DMA ring of 256x128 tiles); AUTO's choice is in gemm().
 int cu_count() {
   static int n = [] {
     int dev = 0, v = 0;
@@ -303,7 +306,7 @@ int gemm_variant_default() {
   static ragmi::Knob k("RAGMI_GEMM");
   const char* s = k.str();
   if (s && std::strcmp(s, "tile") == 0) return (int)RAG_GEMM_TILE;
-  if (s && std::strcmp(s, "pipe") == 0) return (int)RAG_GEMM_PIPE;
+  if (s && std::strcmp(s, "ws") == 0) return (int)RAG_GEMM_WS;
   if (s && std::strcmp(s, "small") == 0) return (int)RAG_GEMM_SMALL;
   return (int)RAG_GEMM_AUTO;
 }
@@ -314,13 +317,13 @@ bool pipe_ok(int M, int N, int K) {
          (int64_t)M * K * 2 < (int64_t(1) << 31) && (int64_t)M * N * 4 < (int64_t(1) << 31);
 }
 
-template <int EPI, bool SPLIT, typename CFG, int PROBE = 0>
+template <int EPI, bool SPLIT, typename CFG>
 void launch_pipe(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float16* Wl,
                  const float* bias, int M, int N, int K, void* C, _Float16* Clo, hipStream_t st,
                  int max_wg, const LnArgs& ln = LnArgs{}, int ksplit = 1) {
   const int tiles = (N / CFG::BN) * ((M + CFG::BM - 1) / CFG::BM) * ksplit;
   const dim3 grid((unsigned)std::min(max_wg, (tiles + 7) / 8 * 8));   // multiple of 8
-  launch_fixed<kPipeBlock<CFG>>(gemm_pipe_kernel<EPI, SPLIT, CFG, PROBE>, grid, 0, st, A, Al, W,
+  launch_fixed<kPipeBlock<CFG>>(gemm_pipe_kernel<EPI, SPLIT, CFG>, grid, 0, st, A, Al, W,
                                 Wl, bias, M, N, K, C, Clo, ln, ksplit);
 }
 
@@ -343,77 +346,18 @@ void launch_ws(const _Float16* A, const _Float16* Al, const _Float16* W, const _
                const float* bias, int M, int N, int K, void* C, _Float16* Clo, hipStream_t st,
                const DlArgs& dl = DlArgs{}) {
   const int tiles = (N / CFG::BN) * ((M + CFG::BM - 1) / CFG::BM);
-  // one workgroup per CU; the single-loader small-tile instance fits two (64 KB LDS each)
-  const int per_cu = CFG::LOADERS < 4 ? 2 : 1;
-  const dim3 grid((unsigned)std::min(per_cu * cu_count(), (tiles + 7) / 8 * 8));
-  // RAGMI_WS_PHASE (A/B): start delay of the odd workgroups in units of ~3.4 us (DlArgs.phase)
-  static ragmi::Knob k("RAGMI_WS_PHASE");
-  const int phase = std::max(0, k.get(0));
-  DlArgs d = dl;
-  if (d.phase == 0) d.phase = phase;
-  launch_fixed<kWsBlock<CFG>>(gemm_ws_kernel<EPI, SPLIT, CFG, PROBE, AUX>, grid, 0, st, A, Al, W,
-                              Wl, bias, M, N, K, C, Clo, d);
-}
-
-// RAGMI_WS_BIG128=1 (diagnostic A/B, round 4): the large-batch WS GEMMs (plain AUTO picks and
-// the deferred-LN ones) on PipeBig128 — 4 MFMA waves of 128 x 64, one per SIMD beside its
-// loader wave (256 registers each), instead of PipeLarge's 8 of 64 x 64
-bool ws_big128() {
-  static ragmi::Knob k("RAGMI_WS_BIG128");
-  return k.get(0) == 1;
-}
-
-// the ping-pong GEMM (gemm_pp_kernel, round 5): fp16x3, N % 192 == 0 (every token-row GEMM of
-// the 384-hidden encoders). RAGMI_GEMM_PP=0 (diagnostic A/B): the WS kernel instead.
-bool pp_on() {
-  static ragmi::Knob k("RAGMI_GEMM_PP");
-  return k.get(1) != 0;
-}
-bool pp_ok(int M, int N, int K) { return N % PipePP::BN == 0 && K % 32 == 0 && pipe_ok(M, N, K); }
-
-template <int EPI, int AUX = 0, int PROBE = 0>
-void launch_pp(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float16* Wl,
-               const float* bias, int M, int N, int K, void* C, _Float16* Clo, hipStream_t st,
-               const DlArgs& dl = DlArgs{}) {
-  const int tiles = (N / PipePP::BN) * ((M + PipePP::BM - 1) / PipePP::BM);
   const dim3 grid((unsigned)std::min(cu_count(), (tiles + 7) / 8 * 8));   // one per CU
-  // RAGMI_PP_STAGGER (A/B): start stagger of the workgroups (DlArgs.phase, gemm_pp_kernel)
-  static ragmi::Knob k("RAGMI_PP_STAGGER");
-  DlArgs d = dl;
-  d.phase = std::max(0, k.get(0));
-  launch_fixed<kPpBlock>(gemm_pp_kernel<EPI, PipePP, PROBE, AUX>, grid, 0, st, A, Al, W, Wl, bias,
-                         M, N, K, C, Clo, d);
+  launch_fixed<kWsBlock<CFG>>(gemm_ws_kernel<EPI, SPLIT, CFG, PROBE, AUX>, grid, 0, st, A, Al, W,
+                              Wl, bias, M, N, K, C, Clo, dl);
 }
 
+// the large-batch GEMMs (the WS kernel on PipeLarge: 8 MFMA waves of 64 x 64 + 4 loader waves)
 template <int EPI, bool SPLIT, int AUX = 0>
 void launch_ws_large(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float16* Wl,
                      const float* bias, int M, int N, int K, void* C, _Float16* Clo,
-                     hipStream_t st, const DlArgs& dl = DlArgs{}, bool allow_pp = true) {
-  // (the residual-add deferred-LN epilogue stays on the WS kernel: in the ping-pong kernel's
-  // 256 registers its residual planes and staged vectors spill beside the accumulators)
-  if constexpr (SPLIT && EPI != kEpiResLn)
-    if (allow_pp && pp_on() && pp_ok(M, N, K)) {
-      launch_pp<EPI, AUX>(A, Al, W, Wl, bias, M, N, K, C, Clo, st, dl);
-      return;
-    }
-  if (ws_big128())
-    launch_ws<EPI, SPLIT, PipeBig128, 0, AUX>(A, Al, W, Wl, bias, M, N, K, C, Clo, st, dl);
-  else
-    launch_ws<EPI, SPLIT, PipeLarge, 0, AUX>(A, Al, W, Wl, bias, M, N, K, C, Clo, st, dl);
+                     hipStream_t st, const DlArgs& dl = DlArgs{}) {
+  launch_ws<EPI, SPLIT, PipeLarge, 0, AUX>(A, Al, W, Wl, bias, M, N, K, C, Clo, st, dl);
 }
-
-// Deferred LayerNorm for query batches (round 4; diagnostic A/B,
-// RAGMI_DL_SMALL=1): token counts up to kDlSmallT run the DL forward on PipeDlSmall's
-// 64 x 128 tiles. Its residual-add epilogue (kEpiResLn) adds the residual and writes the row
-// statistics in the GEMM itself, so the O-proj / FFN2 split-K parts, their fp32 round trip
-// and the 24 add_ln launches of a bge-small forward go away. Parity-green, but slower at 32
-// queries (782 tokens): 0.889 vs 0.685 ms per forward (profiles/r04o_dl_small_ab.jsonl). A
-// tile's serial K loop runs ~0.6 us per 32-deep step at these sizes, so the unsplit FFN2
-// (48 steps on 39 workgroups) takes 30 us against 9.7 (3-way split-K) + 5.0 (add_ln); at
-// query-batch sizes the K split is what keeps the GEMMs short, and its seam is the add_ln.
-// (at most 63 row blocks of 64: the small tiles keep the rotated K order, as PipeLarge does
-// up to 16K tokens, so both give every element the same MFMA chain)
-constexpr int kDlSmallT = 63 * 64;
 
 // RAGMI_CLS_ATTN=0 (diagnostic A/B): the last layer's all-token QKV + attention instead of
 // the K|V projection + CLS-only attention (round 4: rerank forward 9.17-9.19 vs 9.30-9.32 ms,
@@ -421,20 +365,6 @@ constexpr int kDlSmallT = 63 * 64;
 bool cls_attn_on() {
   static ragmi::Knob k("RAGMI_CLS_ATTN");
   return k.get(1) != 0;
-}
-bool dl_small_on() {
-  static ragmi::Knob k("RAGMI_DL_SMALL");
-  return k.get(0) == 1;
-}
-
-template <int EPI, bool SPLIT, int AUX = 0>
-void launch_dl(bool small, const _Float16* A, const _Float16* Al, const _Float16* W,
-               const _Float16* Wl, const float* bias, int M, int N, int K, void* C,
-               _Float16* Clo, hipStream_t st, const DlArgs& dl) {
-  if (small)
-    launch_ws<EPI, SPLIT, PipeDlSmall, 0, AUX>(A, Al, W, Wl, bias, M, N, K, C, Clo, st, dl);
-  else
-    launch_ws_large<EPI, SPLIT, AUX>(A, Al, W, Wl, bias, M, N, K, C, Clo, st, dl);
 }
 
 // shapes the deferred-LayerNorm WS GEMMs take: Ln* (K = 384 input rows; c1 | c2 staged in the
@@ -473,19 +403,6 @@ void gemm_add_ln(const _Float16* A, const _Float16* Al, const _Float16* W, const
   else
     launch_pipe<kEpiAddLn, false, PipeRow>(A, nullptr, W, nullptr, bias, M, N, K, x, nullptr, st,
                                            cu_count(), ln);
-}
-
-// RAGMI_CE_ROWS (A/B): CLS rows per workgroup of the cross-encoder head, 2, 4, 8 (ce_head_rows_kernel),
-// or 1 (default) = ce_head_kernel (one row per workgroup, whole W_p rows per thread)
-int ce_head_rows() {
-  static ragmi::Knob k("RAGMI_CE_ROWS");
-  return k.get(1);
-}
-
-// RAGMI_ATTN_VAR (A/B): the forward's attention variant, 0 = kAttnVar (default) or 10
-int attn_var_override() {
-  static ragmi::Knob k("RAGMI_ATTN_VAR");
-  return k.get(0);
 }
 
 // fusion mode of the forward: -1 auto (once the 128-row bands cover the CUs), 0 off, 1 on
@@ -528,7 +445,6 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
   const int ks_room = ksplit_io ? *ksplit_io : 1;
   if (ksplit_io) *ksplit_io = 1;
   if (variant == RAG_GEMM_AUTO) variant = gemm_variant_default();
-  const bool auto_pick = variant == RAG_GEMM_AUTO;
   const int pipe_tiles = (N / PBN) * ((M + PBM - 1) / PBM);
   // SMALL while its 64x64 tiles fit about two per CU (every query-batch GEMM; the N = 384
   // ones up to ~5K tokens), then WS (the loader-specialised pipe) once its 256x128 tiles reach
@@ -543,176 +459,25 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
               : 2 * pipe_tiles >= cu_count()     ? RAG_GEMM_WS
                                                  : RAG_GEMM_TILE;
   if (variant != RAG_GEMM_TILE && !pipe_ok(M, N, K)) variant = RAG_GEMM_TILE;
-  // knobs of the small-batch fp16x3 GEMMs (A/B): the BK-32 SMALL kernel (64 KB LDS, 2
-  // workgroups per CU, split-K) is the default since round 3 — 782-token bge-small forward
-  // 0.637 / 0.644 ms with SMALL_BK64 (160 KB, 1 per CU) vs 0.628 / 0.627, and the config-2
-  // line at 3 batches in flight 65.9K vs 71.1K qps, where a 1-per-CU GEMM keeps the other
-  // batches' kernels off its CUs (profiles/r03b_small_gemm.jsonl); RAGMI_SMALL_BK=64 restores
-  // SMALL_BK64. RAGMI_SMALL_WIDE=1 runs N >= 1024 GEMMs whose 64 x 64 tiles exceed the CUs on
-  // 64 x 128 tiles (0.620 ms alone, 0.628 with BK 32: not kept)
-  static ragmi::Knob k_bk("RAGMI_SMALL_BK"), k_wide("RAGMI_SMALL_WIDE");
-  const int small_bk = k_bk.get(32);
-  const bool small_wide = k_wide.get(0) == 1;
-  if (auto_pick && variant == RAG_GEMM_SMALL && Al && small_wide && N % 128 == 0 && N >= 1024 &&
-      small_tiles > cu_count()) {
-    launch_pipe<EPI, true, PipeSmallWide64>(A, Al, W, Wl, bias, M, N, K, C, Clo, st, cu_count());
-    return;
-  }
-  if (auto_pick && variant == RAG_GEMM_SMALL && Al && small_bk != 32) variant = RAG_GEMM_SMALL_BK64;
-  // RAGMI_SMALL_WS=1 (A/B, off): query-batch fp16-output GEMMs (QKV, FFN1 at fp16x3) on the
-  // loader-specialised small tiles (PipeWsSmall, RAG_GEMM_WS_SMALL). Measured slower
-  // (profiles/r03zz_small_ws.jsonl, 782 tokens: QKV 9.8 vs 9.7 us, FFN1 14.3 vs 10.3,
-  // encode_q 0.726 vs 0.686 ms): moving the DMA issue off the MFMA waves does not help a
-  // GEMM of one or two tiles per workgroup
-  static ragmi::Knob k_ws("RAGMI_SMALL_WS");
-  const bool small_ws = k_ws.get(0) == 1;
-  if (pipe_ok(M, N, K) &&
-      (variant == RAG_GEMM_WS_SMALL ||
-       (auto_pick && variant == RAG_GEMM_SMALL && Al && small_ws && EPI != kEpiF32))) {
-    if (Al) launch_ws<EPI, true, PipeWsSmall, 0, 0>(A, Al, W, Wl, bias, M, N, K, C, Clo, st);
-    else launch_ws<EPI, false, PipeWsSmall, 0, 0>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st);
-    return;
-  }
-  // diagnostic probes of the PIPE kernel (parts removed; bert_kernels.hip PROBE)
-  const int probe = variant == RAG_GEMM_PROBE_NO_MFMA           ? 1
-                    : variant == RAG_GEMM_PROBE_NO_DMA          ? 2
-                    : variant == RAG_GEMM_PROBE_NO_SYNC         ? 3
-                    : variant == RAG_GEMM_PROBE_NO_STORE        ? 6
-                    : variant == RAG_GEMM_PROBE_MFMA_ONLY       ? 7
-                    : variant == RAG_GEMM_PROBE_DMA_ONLY        ? 8
-                                                                : 0;
-  if (probe) {
-    auto go = [&](auto pc) {
-      constexpr int P = decltype(pc)::value;
-      if (Al) launch_pipe<EPI, true, PipeLarge, P>(A, Al, W, Wl, bias, M, N, K, C, Clo, st, cu_count());
-      else launch_pipe<EPI, false, PipeLarge, P>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st, cu_count());
-    };
-    switch (probe) {
-      case 1: go(std::integral_constant<int, 1>{}); break;
-      case 2: go(std::integral_constant<int, 2>{}); break;
-      case 3: go(std::integral_constant<int, 3>{}); break;
-      case 6: go(std::integral_constant<int, 6>{}); break;
-      case 7: go(std::integral_constant<int, 7>{}); break;
-      default: go(std::integral_constant<int, 8>{}); break;
-    }
-    return;
-  }
-  // (256x192 fp16x3 would split a stage's W rows unevenly over the waves: fp16 only)
-  if (variant == RAG_GEMM_WIDE && (N % 256 == 0 || (N % 192 == 0 && !Al))) {
-    if (N % 256 == 0) {
-      if (Al) launch_pipe<EPI, true, PipeWide256>(A, Al, W, Wl, bias, M, N, K, C, Clo, st, cu_count());
-      else launch_pipe<EPI, false, PipeWide256>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st, cu_count());
-    } else {
-      launch_pipe<EPI, false, PipeWide192>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st, cu_count());
-    }
-    return;
-  }
-  if (variant >= RAG_GEMM_PP && variant <= RAG_GEMM_PP_PRIO) {
-    // (rag_bert_gemm checks fp16x3 and N % 192 == 0 for these)
-    constexpr int AX = EPI == kEpiF32 ? 0 : 2;
-    if (variant == RAG_GEMM_PP) launch_pp<EPI, AX>(A, Al, W, Wl, bias, M, N, K, C, Clo, st);
-    else if (variant == RAG_GEMM_PP_MFMA_ONLY) launch_pp<EPI, AX, 7>(A, Al, W, Wl, bias, M, N, K, C, Clo, st);
-    else if (variant == RAG_GEMM_PP_DMA_ONLY) launch_pp<EPI, AX, 8>(A, Al, W, Wl, bias, M, N, K, C, Clo, st);
-    else if (variant == RAG_GEMM_PP_NO_STORE) launch_pp<EPI, AX, 6>(A, Al, W, Wl, bias, M, N, K, C, Clo, st);
-    else launch_pp<EPI, 0, 0>(A, Al, W, Wl, bias, M, N, K, C, Clo, st);   // default store policy
-    return;
-  }
+  // (the small-batch A/B forms — BK-64 tiles, 64 x 128 tiles, loader-specialised small tiles —
+  // and the PIPE / WIDE / BIG large-batch forms were measured and removed in round 5:
+  // DESIGN.md §R5 lists their numbers)
   if (variant == RAG_GEMM_WS || variant == RAG_GEMM_WS_MFMA_ONLY ||
-      variant == RAG_GEMM_WS_NO_STORE || variant == RAG_GEMM_WS_DMA_ONLY ||
-      variant == RAG_GEMM_WS_L2_STORE || variant == RAG_GEMM_WS_NT ||
-      variant == RAG_GEMM_WS_NOROT || variant == RAG_GEMM_WS_READS_FIRST ||
-      variant == RAG_GEMM_WS_PROBE_NO_A_READS || variant == RAG_GEMM_WS_PROBE_NO_W_READS ||
-      variant == RAG_GEMM_WS_PRIO_LOAD || variant == RAG_GEMM_WS_PRIO_MFMA ||
-      variant == RAG_GEMM_WS_FLAGS || variant == RAG_GEMM_WS_NOHALF ||
-      variant == RAG_GEMM_WS_BIG128 || variant == RAG_GEMM_WS_BIG128_MFMA_ONLY ||
-      variant == RAG_GEMM_WS_BIG128_DMA_ONLY || variant == RAG_GEMM_WS_BIG128_NO_STORE ||
-      variant == RAG_GEMM_WS_PROBE_HI_ONLY || variant == RAG_GEMM_WS_PROBE_FP8_CORR ||
-      variant == RAG_GEMM_WS_REGSTAGE || variant == RAG_GEMM_WS_REGSTAGE_INTAKE ||
-      variant == RAG_GEMM_WS_L2PF || variant == RAG_GEMM_WS_L2PF_INTAKE) {
-    // probes keep production's store policy (nt for fp16 outputs) since round 2's r02h runs
+      variant == RAG_GEMM_WS_NO_STORE || variant == RAG_GEMM_WS_DMA_ONLY) {
+    // non-temporal stores for the fp16 outputs (QKV / FFN1: 117K x 1152 fp16x3 0.354 ->
+    // 0.310 ms, the streamed 540 MB no longer evicting the A panels the n-tiles of an XCD
+    // share); the fp32 ones (O / FFN2, read back at once by add_ln) keep the default policy.
+    // The probes keep production's store policy.
+    constexpr int AX = EPI == kEpiF32 ? 0 : 2;
     auto go = [&](auto pc) {
       constexpr int P = decltype(pc)::value;
-      constexpr int AX = EPI == kEpiF32 ? 0 : 2;
       if (Al) launch_ws<EPI, true, PipeLarge, P, AX>(A, Al, W, Wl, bias, M, N, K, C, Clo, st);
       else launch_ws<EPI, false, PipeLarge, P, AX>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st);
     };
-    if (variant == RAG_GEMM_WS) {
-      // non-temporal stores for the fp16 outputs (QKV / FFN1: 117K x 1152 fp16x3 0.354 ->
-      // 0.310 ms, the streamed 540 MB no longer evicting the A panels the n-tiles of an XCD
-      // share); the fp32 ones (O / FFN2, read back at once by add_ln) keep the default policy
-      constexpr int AX = EPI == kEpiF32 ? 0 : 2;
-      // (an explicit RAG_GEMM_WS stays on the WS kernel; AUTO's pick may take the PP one)
-      if (Al) launch_ws_large<EPI, true, AX>(A, Al, W, Wl, bias, M, N, K, C, Clo, st, DlArgs{}, auto_pick);
-      else launch_ws_large<EPI, false, AX>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st);
-    }
+    if (variant == RAG_GEMM_WS) go(std::integral_constant<int, 0>{});
     else if (variant == RAG_GEMM_WS_MFMA_ONLY) go(std::integral_constant<int, 7>{});
     else if (variant == RAG_GEMM_WS_NO_STORE) go(std::integral_constant<int, 6>{});
-    else if (variant == RAG_GEMM_WS_L2_STORE) go(std::integral_constant<int, 9>{});
-    else if (variant == RAG_GEMM_WS_DMA_ONLY) go(std::integral_constant<int, 8>{});
-    else if (variant == RAG_GEMM_WS_PROBE_NO_A_READS) go(std::integral_constant<int, 14>{});
-    else if (variant == RAG_GEMM_WS_PROBE_NO_W_READS) go(std::integral_constant<int, 15>{});
-    else if (variant == RAG_GEMM_WS_PRIO_LOAD) go(std::integral_constant<int, 16>{});
-    else if (variant == RAG_GEMM_WS_PRIO_MFMA) go(std::integral_constant<int, 17>{});
-    else if (variant == RAG_GEMM_WS_NOHALF) go(std::integral_constant<int, 19>{});
-    else if (variant == RAG_GEMM_WS_PROBE_HI_ONLY) go(std::integral_constant<int, 20>{});
-    else if (variant == RAG_GEMM_WS_REGSTAGE) go(std::integral_constant<int, 22>{});
-    else if (variant == RAG_GEMM_WS_REGSTAGE_INTAKE) go(std::integral_constant<int, 23>{});
-    else if (variant == RAG_GEMM_WS_L2PF) go(std::integral_constant<int, 24>{});
-    else if (variant == RAG_GEMM_WS_L2PF_INTAKE) go(std::integral_constant<int, 25>{});
-    else if (variant == RAG_GEMM_WS_PROBE_FP8_CORR) {
-      if (Al) launch_ws<EPI, true, PipeLarge, 21, (EPI == kEpiF32 ? 0 : 2)>(A, Al, W, Wl, bias, M, N, K, C, Clo, st);
-    }
-    else if (variant == RAG_GEMM_WS_BIG128 || variant == RAG_GEMM_WS_BIG128_MFMA_ONLY ||
-             variant == RAG_GEMM_WS_BIG128_DMA_ONLY || variant == RAG_GEMM_WS_BIG128_NO_STORE) {
-      constexpr int AX = EPI == kEpiF32 ? 0 : 2;
-      auto gb = [&](auto pc) {
-        constexpr int P = decltype(pc)::value;
-        if (Al) launch_ws<EPI, true, PipeBig128, P, AX>(A, Al, W, Wl, bias, M, N, K, C, Clo, st);
-        else launch_ws<EPI, false, PipeBig128, P, AX>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st);
-      };
-      if (variant == RAG_GEMM_WS_BIG128) gb(std::integral_constant<int, 0>{});
-      else if (variant == RAG_GEMM_WS_BIG128_MFMA_ONLY) gb(std::integral_constant<int, 7>{});
-      else if (variant == RAG_GEMM_WS_BIG128_DMA_ONLY) gb(std::integral_constant<int, 8>{});
-      else gb(std::integral_constant<int, 6>{});
-    }
-    else if (variant == RAG_GEMM_WS_FLAGS) {
-      // the ring counters sit in the last 16 floats of the staged-vector area
-      if (N <= kPipeBiasMax - 16) go(std::integral_constant<int, 18>{});
-      else go(std::integral_constant<int, 0>{});
-    }
-    else if (variant == RAG_GEMM_WS_READS_FIRST) {
-      constexpr int AX = EPI == kEpiF32 ? 0 : 2;
-      // the all-reads-first fragment order (PROBE 13) the WS kernel used before its interleaved one
-      if (Al) launch_ws<EPI, true, PipeLarge, 13, AX>(A, Al, W, Wl, bias, M, N, K, C, Clo, st);
-      else launch_ws<EPI, false, PipeLarge, 13, AX>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st);
-    }
-    else if (variant == RAG_GEMM_WS_NOROT) {
-      constexpr int AX = EPI == kEpiF32 ? 0 : 2;
-      if (Al) launch_ws<EPI, true, PipeLarge, 11, AX>(A, Al, W, Wl, bias, M, N, K, C, Clo, st);
-      else launch_ws<EPI, false, PipeLarge, 11, AX>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st);
-    }
-    else if (variant == RAG_GEMM_WS_NT) {
-      if (Al) launch_ws<EPI, true, PipeLarge, 0, 2>(A, Al, W, Wl, bias, M, N, K, C, Clo, st);
-      else launch_ws<EPI, false, PipeLarge, 0, 2>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st);
-    }
-    return;
-  }
-  if (variant == RAG_GEMM_BIG && N % 256 == 0) {
-    if (Al) launch_pipe<EPI, true, PipeBig>(A, Al, W, Wl, bias, M, N, K, C, Clo, st, cu_count());
-    else launch_pipe<EPI, false, PipeBig>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st, cu_count());
-    return;
-  }
-  if (variant == RAG_GEMM_BIG128 || variant == RAG_GEMM_BIG) {
-    if (Al) launch_pipe<EPI, true, PipeBig128>(A, Al, W, Wl, bias, M, N, K, C, Clo, st, cu_count());
-    else launch_pipe<EPI, false, PipeBig128>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st, cu_count());
-    return;
-  }
-  if (variant == RAG_GEMM_PIPE || variant == RAG_GEMM_WIDE) {
-    if (Al)
-      launch_pipe<EPI, true, PipeLarge>(A, Al, W, Wl, bias, M, N, K, C, Clo, st, cu_count());
-    else
-      launch_pipe<EPI, false, PipeLarge>(A, nullptr, W, nullptr, bias, M, N, K, C, nullptr, st,
-                                         cu_count());
+    else go(std::integral_constant<int, 8>{});
     return;
   }
   // split-K parts for the small fp32-output GEMMs (small_ksplit), where the caller has room
@@ -721,17 +486,10 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
     if (ks_room <= 1 || N > kPipeBiasMax / 2) return 1;
     return std::min(ks_room, small_ksplit(K, BK));
   };
-  if (variant == RAG_GEMM_SMALL_BK64 && Al) {
-    const int ks = ks_for(PipeSmallSplit64::BK);
-    launch_pipe<EPI, true, PipeSmallSplit64>(A, Al, W, Wl, bias, M, N, K, C, Clo, st, cu_count(),
-                                             LnArgs{}, ks);
-    if (ksplit_io) *ksplit_io = ks;
-    return;
-  }
-  if (variant == RAG_GEMM_SMALL || variant == RAG_GEMM_SMALL_BK64) {
-    // fp16: 80 KB LDS -> 2 workgroups per CU; fp16x3 (AUTO's choice is SMALL_BK64, above:
-    // one MiniLM layer's four GEMMs at 782 / 3056 tokens 49.1 -> 46.6 / 96.3 -> 87.5 us):
-    // 112 KB -> 1
+  if (variant == RAG_GEMM_SMALL) {
+    // BK-32 tiles (64 KB LDS: 2 workgroups per CU; round 3: 782-token bge-small forward 0.628
+    // vs 0.637 ms with BK-64 tiles at 1 per CU, and the config-2 line at 3 batches in flight
+    // 71.1K vs 65.9K qps, where a 1-per-CU GEMM keeps the other batches' kernels off its CUs)
     const int ks = ks_for(Al ? kBK<true> : kBK<false>);
     if (Al)   // 48 KB ring + 16 KB bias area: two workgroups per CU
       launch_pipe<EPI, true, PipeSmall<true>>(A, Al, W, Wl, bias, M, N, K, C, Clo, st,
@@ -794,8 +552,6 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
   };
   // fp16x3 with the two-kernel projections: the token rows' residual stream is kept as the
   // operand planes xh + xl alone (add_ln_kernel<XF>), no fp32 copy
-  static ragmi::Knob k_f32("RAGMI_RESIDUAL_F32");           // diagnostic: keep the fp32 copy
-  const bool xf_on = k_f32.get(0) != 1;
   // deferred LayerNorm (DlArgs): auto once every token-row GEMM is a WS one (AUTO's choice:
   // the 384-wide projections' 256 x 128 tiles reach half the CUs, ~11K tokens)
   const bool dl_shapes = [&] {
@@ -805,17 +561,14 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
     return dl_gemm_ok(kEpiLnF16, T, 3 * H, H) && dl_gemm_ok(kEpiLnGeluF16, T, FF, H) &&
            dl_gemm_ok(kEpiResLn, T, H, H) && dl_gemm_ok(kEpiResLn, T, H, FF);
   }();
-  // query batches: the DL forward on the 64 x 128 tiles (kDlSmallT)
-  const bool dl_small = dl_shapes && T <= kDlSmallT && e->defer_ln != 0 && dl_small_on() &&
-                        gemm_variant_default() == RAG_GEMM_AUTO;
-  const bool dl = dl_small || [&] {
+  const bool dl = [&] {
     if (!dl_shapes) return false;
     if (e->defer_ln > 0) return true;
     const int tiles384 = (H / PBN) * ((T + PBM - 1) / PBM);
     return gemm_variant_default() == RAG_GEMM_AUTO && 2 * tiles384 >= cu_count() &&
            (H / 64) * ((T + 63) / 64) > 2 * cu_count();
   }();
-  const bool xf = dl || (xf_on && w->xl && !fuse_for(T));
+  const bool xf = dl || (w->xl && !fuse_for(T));
   embed_ln_kernel<H><<<dim3((max_len + 3) / 4, B), dim3(256), 0, st>>>(
       ids, types, cu, e->wemb, e->pemb, e->temb, e->eg, e->eb, c.layer_norm_eps, c.vocab,
       c.type_vocab, c.max_position, xf ? nullptr : w->x, w->xh, w->xl);
@@ -841,7 +594,7 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
       a.st_in = w->sb;
       a.c1 = L.qkv_c1 + H;
       a.eps = c.layer_norm_eps;
-      launch_dl<kEpiLnF16, true, 2>(dl_small, w->xh, w->xl, L.wqkv_f + (int64_t)H * H,
+      launch_ws_large<kEpiLnF16, true, 2>(w->xh, w->xl, L.wqkv_f + (int64_t)H * H,
                                     L.wqkv_fl + (int64_t)H * H, L.qkv_c2 + H, T, 2 * H, H,
                                     w->qkv, w->qkv_l, st, a);
       gather_cls_kernel<H><<<dim3(B), dim3(64), 0, st>>>(
@@ -859,7 +612,7 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
       a.st_in = w->sb;
       a.c1 = L.qkv_c1;
       a.eps = c.layer_norm_eps;
-      launch_dl<kEpiLnF16, true, 2>(dl_small, w->xh, w->xl, L.wqkv_f, L.wqkv_fl, L.qkv_c2, T,
+      launch_ws_large<kEpiLnF16, true, 2>(w->xh, w->xl, L.wqkv_f, L.wqkv_fl, L.qkv_c2, T,
                                     3 * H, H, w->qkv, w->qkv_l, st, a);
     } else {
       gemm<kEpiF16>(w->xh, w->xl, L.wqkv, L.wqkv_l, L.bqkv, T, 3 * H, H, w->qkv, w->qkv_l, st);
@@ -868,13 +621,6 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
     const int max_qb = last ? 1 : 1 << 20;
     if (cls_done) {
       // (the CLS context is in w->cc / w->ccl already)
-    } else if (attn_var_override() == 10) {   // RAGMI_ATTN_VAR=10: the round-2 variant (A/B)
-      if (w->xl)
-        launch_fixed<kAttnThreads<true>>(attn_kernel<H, HD, true, 10>, agrid, alds, st,
-            w->qkv, w->qkv_l, cu, max_len, kc, scale, w->ctx, w->ctx_l, max_qb);
-      else
-        launch_fixed<kAttnThreads<false>>(attn_kernel<H, HD, false, 10>, agrid, alds, st,
-            w->qkv, nullptr, cu, max_len, kc, scale, w->ctx, nullptr, max_qb);
     } else if (w->xl)
       launch_fixed<kAttnThreads<true>>(attn_kernel<H, HD, true>, agrid, alds, st,
           w->qkv, w->qkv_l, cu, max_len, kc, scale, w->ctx, w->ctx_l, max_qb);
@@ -890,13 +636,13 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
       o.beta = P ? P->be2 : nullptr;
       o.st_out = w->sa;
       o.eps = c.layer_norm_eps;
-      launch_dl<kEpiResLn, true>(dl_small, w->ctx, w->ctx_l, L.wo, L.wo_l, L.bo, T, H, H, w->xh,
+      launch_ws_large<kEpiResLn, true>(w->ctx, w->ctx_l, L.wo, L.wo_l, L.bo, T, H, H, w->xh,
                                  w->xl, st, o);
       DlArgs f;
       f.st_in = w->sa;
       f.c1 = L.w1_c1;
       f.eps = c.layer_norm_eps;
-      launch_dl<kEpiLnGeluF16, true, 2>(dl_small, w->xh, w->xl, L.w1_f, L.w1_fl, L.w1_c2, T, FF,
+      launch_ws_large<kEpiLnGeluF16, true, 2>(w->xh, w->xl, L.w1_f, L.w1_fl, L.w1_c2, T, FF,
                                         H, w->ff, w->ff_l, st, f);
       DlArgs r;
       r.st_in = w->sa;
@@ -904,7 +650,7 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
       r.beta = L.be1;
       r.st_out = w->sb;
       r.eps = c.layer_norm_eps;
-      launch_dl<kEpiResLn, true>(dl_small, w->ff, w->ff_l, L.w2, L.w2_l, L.bi2, T, H, FF, w->xh,
+      launch_ws_large<kEpiResLn, true>(w->ff, w->ff_l, L.w2, L.w2_l, L.bi2, T, H, FF, w->xh,
                                  w->xl, st, r);
       continue;
     }
@@ -943,20 +689,16 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
     auto add_ln = [&](const float* gam, const float* bet, int parts) {
       const int64_t ps = (int64_t)R * H;
       if constexpr (H == 384) {
-        // 16-B accesses and DPP / permlane reductions (round 3; RAGMI_ADDLN_VEC=0: A/B)
-        static ragmi::Knob k_vec("RAGMI_ADDLN_VEC");
-        const bool vec = k_vec.get(1) != 0;
-        if (vec) {
-          if (row_xf)
-            add_ln384_kernel<true><<<dim3(lg), dim3(256), 0, st>>>(nullptr, y, gam, bet,
-                                                                  c.layer_norm_eps, xh, xl, R,
-                                                                  parts, ps);
-          else
-            add_ln384_kernel<false><<<dim3(lg), dim3(256), 0, st>>>(x, y, gam, bet,
-                                                                   c.layer_norm_eps, xh, xl, R,
-                                                                   parts, ps);
-          return;
-        }
+        // 16-B accesses and DPP / permlane reductions (round 3)
+        if (row_xf)
+          add_ln384_kernel<true><<<dim3(lg), dim3(256), 0, st>>>(nullptr, y, gam, bet,
+                                                                c.layer_norm_eps, xh, xl, R,
+                                                                parts, ps);
+        else
+          add_ln384_kernel<false><<<dim3(lg), dim3(256), 0, st>>>(x, y, gam, bet,
+                                                                 c.layer_norm_eps, xh, xl, R,
+                                                                 parts, ps);
+        return;
       }
       if (row_xf)
         add_ln_kernel<H, true><<<dim3(lg), dim3(256), 0, st>>>(nullptr, y, gam, bet,
@@ -987,15 +729,6 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
   // the final hidden states of the CLS tokens are rows 0 .. B-1 of w->xc (cu = null)
   if (c.head == RAG_HEAD_CLS_L2)
     cls_normalize_kernel<H><<<dim3(B), dim3(64), 0, st>>>(w->xc, nullptr, out);
-  else if (H % 128 == 0 && ce_head_rows() == 2)   // R CLS rows per workgroup
-    ce_head_rows_kernel<H, 2><<<dim3((B + 1) / 2), dim3(256), 0, st>>>(
-        w->xc, B, e->wp, e->bp, e->wc, e->bc, out);
-  else if (H % 128 == 0 && ce_head_rows() == 4)
-    ce_head_rows_kernel<H, 4><<<dim3((B + 3) / 4), dim3(256), 0, st>>>(
-        w->xc, B, e->wp, e->bp, e->wc, e->bc, out);
-  else if (H % 128 == 0 && ce_head_rows() == 8)
-    ce_head_rows_kernel<H, 8><<<dim3((B + 7) / 8), dim3(256), 0, st>>>(
-        w->xc, B, e->wp, e->bp, e->wc, e->bc, out);
   else
     ce_head_kernel<H><<<dim3(B), dim3(256), 0, st>>>(w->xc, nullptr, e->wp, e->bp, e->wc, e->bc,
                                                      out);
@@ -1066,7 +799,7 @@ int forward_graph(rag_encoder* e, EncWorkspace* w, const int32_t* ids, const int
                                     return a.last < b.last;
                                   });
       RAG_HIP(hipStreamSynchronize(st));      // its last replay was on this stream
-      (void)hipGraphExecDestroy(lru->exec);
+      if (lru->exec) (void)hipGraphExecDestroy(lru->exec);
       w->graphs.erase(lru);
     }
     if (!w->cstream) RAG_HIP(hipStreamCreateWithFlags(&w->cstream, hipStreamNonBlocking));
@@ -1081,17 +814,27 @@ int forward_graph(rag_encoder* e, EncWorkspace* w, const int32_t* ids, const int
       if (graph) (void)hipGraphDestroy(graph);
     }
     if (!ok) {
-      // a failed capture can leave its stream unusable: drop it (a new one next time)
-      (void)hipGetLastError();
+      // a failed capture can leave its stream unusable: drop it (a new one next time). The
+      // shape is remembered as eager (exec = null), so it is not captured again on every call,
+      // and the first failure of the process is reported once on stderr.
+      const hipError_t err = hipGetLastError();
+      static std::atomic<bool> said{false};
+      if (!said.exchange(true))
+        std::fprintf(stderr, "ragmi: encoder graph capture failed (%s%s%s); shape B=%d T=%d "
+                     "runs eagerly\n", hipGetErrorString(err), rc ? ": " : "",
+                     rc ? rag_last_error() : "", B, Tp);
       (void)hipStreamDestroy(w->cstream);
       w->cstream = nullptr;
       ragmi::clear_error();
+      w->graphs.push_back(EncWorkspace::Graph{B, Tp, Lp, nullptr, e->uses});
       return forward_t<H, HD>(e, ids, types, cu, B, T, max_len, out, st, true, w);
     }
     w->graphs.push_back(EncWorkspace::Graph{B, Tp, Lp, exec, 0});
     hit = &w->graphs.back();
   }
   hit->last = e->uses;
+  if (!hit->exec)     // a shape whose capture failed: eager on the caller's stream
+    return forward_t<H, HD>(e, ids, types, cu, B, T, max_len, out, st, true, w);
   RAG_HIP(hipGraphLaunch(hit->exec, st));
   RAG_HIP(hipMemcpyAsync(out, w->g_out, (size_t)B * od * 4, hipMemcpyDeviceToDevice, st));
   return RAG_OK;
@@ -1173,10 +916,6 @@ int set_attn_lds_attr() {
                               hipFuncAttributeMaxDynamicSharedMemorySize, kAttnLdsMax));
   RAG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_kernel<H, HD, false>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, kAttnLdsMax));
-  RAG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_kernel<H, HD, true, 10>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, kAttnLdsMax));
-  RAG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_kernel<H, HD, false, 10>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, kAttnLdsMax));
   return RAG_OK;
 }
 
@@ -1202,8 +941,15 @@ int rag_encoder_create_ex(const rag_bert_config* cfg, const float* const* w, int
                           int device, int flags, rag_encoder_t** out) {
   ragmi::clear_error();
   if (flags & ~RAG_CREATE_DIAGNOSTIC) return ragmi::fail(RAG_EINVAL, "unknown encoder flags");
-  if (flags & RAG_CREATE_DIAGNOSTIC) ragmi::diagnostics_on().store(true);
-  return rag_encoder_create(cfg, w, n_weights, device, out);
+  const int rc = rag_encoder_create(cfg, w, n_weights, device, out);
+  if (rc == RAG_OK && (flags & RAG_CREATE_DIAGNOSTIC)) {
+    (*out)->diagnostic = true;
+    ragmi::diagnostic_acquire();
+    // knobs read at create time (the LayerNorm modes) see the handle as diagnostic
+    (*out)->fuse_ln = fuse_ln_default();
+    (*out)->defer_ln = defer_ln_default();
+  }
+  return rc;
 }
 
 int rag_encoder_create(const rag_bert_config* cfg, const float* const* w, int n_weights,
@@ -1311,6 +1057,7 @@ int rag_encoder_create(const rag_bert_config* cfg, const float* const* w, int n_
 int rag_encoder_destroy(rag_encoder_t* e) {
   ragmi::clear_error();
   if (!e) return RAG_OK;
+  if (e->diagnostic) ragmi::diagnostic_release();
   (void)hipSetDevice(e->device);
   (void)hipDeviceSynchronize();
   for (void* p : e->allocs) (void)hipFree(p);
@@ -1361,46 +1108,14 @@ int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, co
     return ragmi::fail(RAG_EINVAL, "A_lo and W_lo: both (fp16x3) or neither (fp16)");
   if (A_lo && epilogue != kEpiF32 && !C_lo)
     return ragmi::fail(RAG_EINVAL, "fp16x3 fp16-output GEMM needs C_lo");
-  if ((variant == RAG_GEMM_PIPE || variant == RAG_GEMM_SMALL || variant == RAG_GEMM_WIDE ||
-       variant == RAG_GEMM_SMALL_BK64 || variant == RAG_GEMM_BIG || variant == RAG_GEMM_BIG128 ||
-       variant == RAG_GEMM_WS || variant == RAG_GEMM_WS_NT || variant == RAG_GEMM_WS_NOROT ||
-       variant == RAG_GEMM_WS_READS_FIRST || variant == RAG_GEMM_WS_PRIO_LOAD ||
-       variant == RAG_GEMM_WS_PRIO_MFMA || variant == RAG_GEMM_WS_FLAGS ||
-       variant == RAG_GEMM_WS_NOHALF || variant == RAG_GEMM_WS_SMALL ||
-       variant == RAG_GEMM_WS_REGSTAGE || variant == RAG_GEMM_WS_L2PF) &&
-      !pipe_ok(M, N, K))
-    return ragmi::fail(RAG_EINVAL, "pipe/small/wide variants need N % 128 == 0, K % 64 == 0, "
-                                   "N <= 4096, M*K*2 and M*N*4 < 2^31");
-  const bool probe = variant == RAG_GEMM_PROBE_NO_MFMA || variant == RAG_GEMM_PROBE_NO_DMA ||
-                     variant == RAG_GEMM_PROBE_NO_SYNC || variant == RAG_GEMM_PROBE_NO_STORE ||
-                     variant == RAG_GEMM_PROBE_MFMA_ONLY || variant == RAG_GEMM_PROBE_DMA_ONLY ||
-                     variant == RAG_GEMM_WS_MFMA_ONLY || variant == RAG_GEMM_WS_NO_STORE ||
-                     variant == RAG_GEMM_WS_DMA_ONLY || variant == RAG_GEMM_WS_L2_STORE ||
-                     variant == RAG_GEMM_WS_PROBE_NO_A_READS ||
-                     variant == RAG_GEMM_WS_PROBE_NO_W_READS ||
-                     variant == RAG_GEMM_WS_PROBE_HI_ONLY ||
-                     variant == RAG_GEMM_WS_PROBE_FP8_CORR ||
-                     variant == RAG_GEMM_WS_REGSTAGE_INTAKE ||
-                     variant == RAG_GEMM_WS_L2PF_INTAKE;
   const bool known = variant == RAG_GEMM_AUTO || variant == RAG_GEMM_TILE ||
-                     variant == RAG_GEMM_PIPE || variant == RAG_GEMM_SMALL ||
-                     variant == RAG_GEMM_WIDE || variant == RAG_GEMM_SMALL_BK64 ||
-                     variant == RAG_GEMM_BIG || variant == RAG_GEMM_BIG128 ||
-                     variant == RAG_GEMM_WS || variant == RAG_GEMM_WS_NT ||
-                     variant == RAG_GEMM_WS_NOROT || variant == RAG_GEMM_WS_READS_FIRST ||
-                     variant == RAG_GEMM_WS_PRIO_LOAD || variant == RAG_GEMM_WS_PRIO_MFMA ||
-                     variant == RAG_GEMM_WS_FLAGS || variant == RAG_GEMM_WS_NOHALF ||
-                     variant == RAG_GEMM_WS_SMALL || variant == RAG_GEMM_WS_BIG128 ||
-                     variant == RAG_GEMM_WS_BIG128_MFMA_ONLY ||
-                     variant == RAG_GEMM_WS_BIG128_DMA_ONLY ||
-                     variant == RAG_GEMM_WS_BIG128_NO_STORE ||
-                     variant == RAG_GEMM_WS_REGSTAGE || variant == RAG_GEMM_WS_L2PF || probe;
-  const bool pp = variant >= RAG_GEMM_PP && variant <= RAG_GEMM_PP_PRIO;
-  if (pp && (!A_lo || !pp_ok(M, N, K)))
-    return ragmi::fail(RAG_EINVAL, "PP variants: fp16x3, N % 192 == 0, K % 64 == 0, "
-                                   "M*K*2 and M*N*4 < 2^31");
-  if ((!known && !pp) || (probe && !pipe_ok(M, N, K)))
-    return ragmi::fail(RAG_EINVAL, "unknown GEMM variant, or a probe on a non-pipe shape");
+                     variant == RAG_GEMM_SMALL || variant == RAG_GEMM_WS ||
+                     variant == RAG_GEMM_WS_MFMA_ONLY || variant == RAG_GEMM_WS_NO_STORE ||
+                     variant == RAG_GEMM_WS_DMA_ONLY;
+  if (!known) return ragmi::fail(RAG_EINVAL, "unknown GEMM variant");
+  if ((variant == RAG_GEMM_SMALL || variant >= RAG_GEMM_WS) && !pipe_ok(M, N, K))
+    return ragmi::fail(RAG_EINVAL, "SMALL / WS variants need N % 128 == 0, K % 64 == 0, "
+                                   "N <= 4096, M*K*2 and M*N*4 < 2^31");
   auto* a = static_cast<const _Float16*>(A);
   auto* al = static_cast<const _Float16*>(A_lo);
   auto* w = static_cast<const _Float16*>(W);
@@ -1424,8 +1139,8 @@ int rag_bert_gemm_splitk(int variant, const void* A, const void* A_lo, const voi
   if (!A || !W || !bias || !C || !parts) return ragmi::fail(RAG_EINVAL, "NULL argument");
   if ((A_lo == nullptr) != (W_lo == nullptr))
     return ragmi::fail(RAG_EINVAL, "A_lo and W_lo: both (fp16x3) or neither (fp16)");
-  if (variant != RAG_GEMM_AUTO && variant != RAG_GEMM_SMALL && variant != RAG_GEMM_SMALL_BK64)
-    return ragmi::fail(RAG_EINVAL, "split-K runs on the SMALL GEMMs (AUTO, SMALL, SMALL_BK64)");
+  if (variant != RAG_GEMM_AUTO && variant != RAG_GEMM_SMALL)
+    return ragmi::fail(RAG_EINVAL, "split-K runs on the SMALL GEMMs (AUTO, SMALL)");
   if (M < 1 || max_parts < 1 || N % BN != 0 || K % 64 != 0 || !pipe_ok(M, N, K))
     return ragmi::fail(RAG_EINVAL, "bad shape");
   int ks = std::min(max_parts, kMaxKSplit);
@@ -1526,40 +1241,6 @@ int rag_bert_attention(int variant, const void* qkv, const void* qkv_lo, const i
   }
 }
 
-int rag_bert_gemm_add_ln_probe(int probe, const void* A, const void* A_lo, const void* W,
-                               const void* W_lo, const float* bias, const float* gamma,
-                               const float* beta, float eps, int M, int N, int K, float* x,
-                               void* xh, void* xl, void* stream) {
-  ragmi::clear_error();
-  if (probe != 4 && probe != 5) return ragmi::fail(RAG_EINVAL, "probe: 4 or 5");
-  if (!A || !W || !bias || !gamma || !beta || !x || !xh)
-    return ragmi::fail(RAG_EINVAL, "NULL argument");
-  if ((A_lo == nullptr) != (W_lo == nullptr) || (A_lo != nullptr) != (xl != nullptr))
-    return ragmi::fail(RAG_EINVAL, "A_lo, W_lo and xl: all three (fp16x3) or none (fp16)");
-  if (M < 1 || !add_ln_ok(M, N, K))
-    return ragmi::fail(RAG_EINVAL, "N == 384, K % 64 == 0, M*K*2 and M*N*4 < 2^31 required");
-  LnArgs ln;
-  ln.gamma = gamma;
-  ln.beta = beta;
-  ln.xh = static_cast<_Float16*>(xh);
-  ln.eps = eps;
-  const auto* a = static_cast<const _Float16*>(A);
-  const auto* al = static_cast<const _Float16*>(A_lo);
-  const auto* w = static_cast<const _Float16*>(W);
-  const auto* wl = static_cast<const _Float16*>(W_lo);
-  auto* l = static_cast<_Float16*>(xl);
-  const auto st = static_cast<hipStream_t>(stream);
-  if (probe == 4) {
-    if (al) launch_pipe<kEpiAddLn, true, PipeRow, 4>(a, al, w, wl, bias, M, N, K, x, l, st, cu_count(), ln);
-    else launch_pipe<kEpiAddLn, false, PipeRow, 4>(a, nullptr, w, nullptr, bias, M, N, K, x, nullptr, st, cu_count(), ln);
-  } else {
-    if (al) launch_pipe<kEpiAddLn, true, PipeRow, 5>(a, al, w, wl, bias, M, N, K, x, l, st, cu_count(), ln);
-    else launch_pipe<kEpiAddLn, false, PipeRow, 5>(a, nullptr, w, nullptr, bias, M, N, K, x, nullptr, st, cu_count(), ln);
-  }
-  RAG_HIP(hipGetLastError());
-  return RAG_OK;
-}
-
 int rag_encoder_set_fusion(rag_encoder_t* e, int mode) {
   ragmi::clear_error();
   if (!e || mode < -1 || mode > 1) return ragmi::fail(RAG_EINVAL, "mode: -1 auto, 0 off, 1 on");
@@ -1639,14 +1320,12 @@ int rag_bert_gemm_dl(int epilogue, const void* A, const void* A_lo, const void* 
   auto* wl = static_cast<const _Float16*>(W_lo);
   auto* cl = static_cast<_Float16*>(C_lo);
   const auto st = static_cast<hipStream_t>(stream);
-  // the forward's tile choice: query-batch tiles up to kDlSmallT rows
-  const bool small = M <= kDlSmallT && dl_small_on();
   if (epilogue == RAG_EPI_LN_F16)
-    launch_dl<kEpiLnF16, true, 2>(small, a, al, w, wl, bias, M, N, K, C, cl, st, d);
+    launch_ws_large<kEpiLnF16, true, 2>(a, al, w, wl, bias, M, N, K, C, cl, st, d);
   else if (epilogue == RAG_EPI_LN_GELU_F16)
-    launch_dl<kEpiLnGeluF16, true, 2>(small, a, al, w, wl, bias, M, N, K, C, cl, st, d);
+    launch_ws_large<kEpiLnGeluF16, true, 2>(a, al, w, wl, bias, M, N, K, C, cl, st, d);
   else
-    launch_dl<kEpiResLn, true>(small, a, al, w, wl, bias, M, N, K, C, cl, st, d);
+    launch_ws_large<kEpiResLn, true>(a, al, w, wl, bias, M, N, K, C, cl, st, d);
   RAG_HIP(hipGetLastError());
   return RAG_OK;
 }

@@ -540,30 +540,9 @@ using PipeLarge = PipeCfg<256, 128, 4, 2, 3>;
 // residual + LayerNorm fused into the epilogue (kEpiAddLn); 2 x 4 waves of 64 x 96
 using PipeRow = PipeCfg<128, 384, 2, 4, 2>;
 template <bool SPLIT> using PipeSmall = PipeCfg<64, 64, 2, 2, SPLIT ? 3 : 4>;
-// fp16x3 query-batch GEMMs at BK 64 (4 planes, 4-stage ring, 128 KB LDS, 1 workgroup per
-// CU): half the K steps of PipeSmall<true> — a query-batch GEMM is a few dozen tiles whose
-// time is the serial K loop's per-step latency
-using PipeSmallSplit64 = PipeCfg<64, 64, 2, 2, 4, 64>;
-// 64 x 128 tiles at BK 64, 3 stages (fp16x3: 144 KB ring + the bias area = the whole 160 KB):
-// the N = 1536 FFN1 of a query batch in one round of tiles (156 at 782 tokens vs 312 64 x 64)
-using PipeSmallWide64 = PipeCfg<64, 128, 2, 2, 3, 64>;
-// wider N tiles: fewer panel bytes per FLOP (256x256: 128 FLOP/B fp16 vs 85 at 256x128) at
-// the price of a 2-stage ring (one stage in flight)
-using PipeWide256 = PipeCfg<256, 256, 4, 2, 2>;
-// register-blocked shapes (round 2): 4 waves, each 128 x 128 (BIG) or 128 x 64 (BIG128) —
-// half / three quarters of the LDS fragment bytes per MFMA of the 64 x 64-per-wave tiles,
-// one wave per SIMD (256 / 128 accumulator registers)
-using PipeBig = PipeCfg<256, 256, 2, 2, 2>;
-using PipeBig128 = PipeCfg<256, 128, 2, 2, 3>;
-using PipeWide192 = PipeCfg<256, 192, 4, 2, 2>;
-// query-batch tiles on the loader-specialised kernel (round 3, RAG_GEMM_WS_SMALL; measured
-// slower than SMALL, not AUTO's pick): SMALL's 64 x 64 tiles and 3-stage BK-32 ring, the
-// DMAs moved to ONE loader wave beside the 4 MFMA waves, two workgroups per CU.
-using PipeWsSmall = PipeCfg<64, 64, 2, 2, 3, 0, 1>;
-// deferred-LayerNorm GEMMs of query batches (round 4): the large-batch DL
-// epilogues on 64 x 128 tiles — 4 MFMA waves of 32 x 64 (a wave's 64 columns are one stats
-// block, as ws_dl_epilogue needs), 2 loader waves, a 4-stage BK-32 ring (96 KB)
-using PipeDlSmall = PipeCfg<64, 128, 2, 2, 4, 32, 2>;
+// (Measured and removed in round 5 — numbers in DESIGN.md §R5: 256x256 / 256x192 PIPE tiles,
+// register-blocked BIG / BIG128 shapes, BK-64 and 64x128 query-batch tiles, the one-loader and
+// deferred-LN query-batch WS tiles, and the 256x192 ping-pong kernel.)
 constexpr int PBM = PipeLarge::BM, PBN = PipeLarge::BN;
 constexpr int kPipeThreads = PipeLarge::THREADS;
 constexpr int kPipeBiasMax = 4096;            // floats of bias staged in LDS (N <= 4096)
@@ -742,7 +721,6 @@ struct DlArgs {
   const float* beta = nullptr;
   const float* c1 = nullptr;       // Ln*: [N] column sums of W' (the bias argument is c2)
   float eps = 0.f;
-  int phase = 0;                   // WS kernel: start delay of the odd workgroups (see there)
 };
 
 // hi + lo fp16 planes (4 values each, as loaded) -> fp32 by v_fma_mix_f32 (hi * 1 + lo in one
@@ -950,20 +928,10 @@ struct LnArgs {
   float eps = 0.f;
 };
 
-// PROBE (diagnostic builds only, rag_bert_gemm variants 3/4/9): timing probes of the same
-// kernel with parts removed — 1 = no MFMAs, 2 = no DMAs, 3 = no DMAs and no barriers.
-// 6 = epilogue without its stores (bias, GELU and conversions run; nothing is written):
-// the cost of the epilogue's store stream; 7 = no DMAs and no stores (MFMAs, LDS reads and
-// barriers only); 8 = no MFMAs and no stores (the DMA ring alone).
-// kEpiAddLn only (rag_bert_gemm_add_ln_probe): 4 = the fp16 copy [+ lo plane] stored with
-// the plain epilogue's paired 16-B stores (store_f16_pair) and a store count S matching
-// them; 5 = the same stores with S still counting the 8-B stores (more than are issued: the
-// post-epilogue vmcnt wait then passes before the next ring stage has landed).
-// (s_setprio around the MFMA clusters / for the younger waves measured +1-2%: not kept.)
 // block size of a gemm_pipe_kernel instance (launch_fixed; its __launch_bounds__)
 template <typename CFG> constexpr int kPipeBlock = CFG::THREADS;
 
-template <int EPI, bool SPLIT, typename CFG, int PROBE = 0>
+template <int EPI, bool SPLIT, typename CFG>
 __global__ __launch_bounds__(kPipeBlock<CFG>, 1) void gemm_pipe_kernel(
     const _Float16* __restrict__ A, const _Float16* __restrict__ Al,
     const _Float16* __restrict__ W, const _Float16* __restrict__ Wl,
@@ -981,13 +949,8 @@ __global__ __launch_bounds__(kPipeBlock<CFG>, 1) void gemm_pipe_kernel(
   // (kEpiAddLn: the fp32 rows and the fp16 copy [+ lo plane], 8-B stores for the latter).
   // The count is capped at what vmcnt can express: waiting until fewer ops are outstanding
   // than were issued after the awaited stage is only stricter.
-  constexpr bool P_NO_MFMA = PROBE == 1 || PROBE == 8;
-  constexpr bool P_NO_DMA = PROBE == 2 || PROBE == 3 || PROBE == 7;
-  constexpr bool P_NO_STORE = PROBE == 6 || PROBE == 7 || PROBE == 8;
-  constexpr int S_ISSUED = P_NO_STORE           ? 0
-                           : EPI == kEpiF32     ? FM * FN
-                           : EPI == kEpiAddLn ? (PROBE == 4 ? FM * FN + FM * FN / 2 * (SPLIT ? 2 : 1)
-                                                            : FM * FN * (SPLIT ? 3 : 2))
+  constexpr int S_ISSUED = EPI == kEpiF32   ? FM * FN
+                           : EPI == kEpiAddLn ? FM * FN * (SPLIT ? 3 : 2)
                                               : FM * FN / 2 * (SPLIT ? 2 : 1);
   constexpr int S = S_ISSUED < 63 - (NS - 2) * L ? S_ISSUED : 63 - (NS - 2) * L;
   constexpr int OUT_B = EPI == kEpiF32 || EPI == kEpiAddLn ? 4 : 2;   // Cout element bytes
@@ -1084,10 +1047,6 @@ __global__ __launch_bounds__(kPipeBlock<CFG>, 1) void gemm_pipe_kernel(
   __amdgpu_buffer_rsrc_t rA0 = panel(A, 0), rA1 = rA0, rW0 = rA0, rW1 = rA0;
   auto issue_next = [&]() {
     if (it_i >= n_mine) return;
-    if constexpr (P_NO_DMA) {
-      if (++kt_i == nk) { kt_i = 0; ++it_i; }
-      return;
-    }
     if (kt_i == 0) {
       const int unit = it_i * G + off;
       const int tile = unit % n_tiles;
@@ -1135,16 +1094,14 @@ __global__ __launch_bounds__(kPipeBlock<CFG>, 1) void gemm_pipe_kernel(
   for (int g = 0; g < steps; ++g) {
     // stages issued after step g: min(NS - 2, steps - 1 - g); plus the last epilogue's
     // stores when it ran at the end of step g-1
-    if constexpr (PROBE != 3) {
-      wait_ring<L, S, NS - 2>(min(NS - 2, steps - 1 - g), g > 0 && kt_c == 0);
-      __builtin_amdgcn_s_barrier();   // step g landed for all waves; all are past step g-1
-    }
+    wait_ring<L, S, NS - 2>(min(NS - 2, steps - 1 - g), g > 0 && kt_c == 0);
+    __builtin_amdgcn_s_barrier();     // step g landed for all waves; all are past step g-1
     asm volatile("" ::: "memory");    // no LDS read of step g may be scheduled above it
     issue_next();                     // step g+NS-1 -> slot (g-1) % NS
 
     const half8* sa = lds + slot_c * STAGE_H8;
     const half8* sw = sa + NPL * A_H8;
-    if constexpr (!P_NO_MFMA && CFG::PRELOAD) {
+    if constexpr (CFG::PRELOAD) {
       // every fragment of the K step issued back to back, then the MFMAs (left alone, the
       // compiler loads each fragment just before its first use and waits every few MFMAs;
       // this order measured ~3% faster on the 256-row tiles)
@@ -1178,7 +1135,7 @@ __global__ __launch_bounds__(kPipeBlock<CFG>, 1) void gemm_pipe_kernel(
           }
     }
 #pragma unroll
-    for (int ks = 0; ks < (P_NO_MFMA || CFG::PRELOAD ? 0 : BK / 32); ++ks) {
+    for (int ks = 0; ks < (CFG::PRELOAD ? 0 : BK / 32); ++ks) {
       const int ch = ks * 4 + (lane >> 4);
       half8 af[FM], wf[FN];
 #pragma unroll
@@ -1278,43 +1235,8 @@ __global__ __launch_bounds__(kPipeBlock<CFG>, 1) void gemm_pipe_kernel(
           }
         }
         // fp16 copy [+ lo plane]: 8-B stores straight from the fragment layout. (Paired 16-B
-        // stores — PROBE 4 — issue fewer stores than the 8-B count S; with S unchanged the
-        // next tile's first ring stage was read before it landed: wrong dwords. PROBE 5.)
-        if constexpr (PROBE == 4 || PROBE == 5) {
-          const int cofs = 8 * ((g & 1) * 2 + (g >> 1));
-#pragma unroll
-          for (int jp = 0; jp < FN; jp += 2) {
-            const floatx4 ga = *reinterpret_cast<const floatx4*>(gam + wc * WTN + jp * 16 + 4 * g);
-            const floatx4 ea = *reinterpret_cast<const floatx4*>(bet + wc * WTN + jp * 16 + 4 * g);
-            const floatx4 gb = *reinterpret_cast<const floatx4*>(gam + wc * WTN + jp * 16 + 16 + 4 * g);
-            const floatx4 eb = *reinterpret_cast<const floatx4*>(bet + wc * WTN + jp * 16 + 16 + 4 * g);
-#pragma unroll
-            for (int i = 0; i < FM; ++i) {
-              floatx4 va, vb;
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                va[r] = (acc[i][jp][r] - mu[i]) * rsd[i] * ga[r] + ea[r];
-                vb[r] = (acc[i][jp + 1][r] - mu[i]) * rsd[i] * gb[r] + eb[r];
-              }
-              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, va), rc, vf(i),
-                                                     sf(jp), 0);
-              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, vb), rc, vf(i),
-                                                     sf(jp + 1), 0);
-              half4 ha, hb, la, lb;
-#pragma unroll
-              for (int r = 0; r < 4; r += 2) {
-                half2 h2, l2;
-                split16x2(va[r], va[r + 1], h2, l2);
-                ha[r] = h2[0]; ha[r + 1] = h2[1]; la[r] = l2[0]; la[r + 1] = l2[1];
-                split16x2(vb[r], vb[r + 1], h2, l2);
-                hb[r] = h2[0]; hb[r + 1] = h2[1]; lb[r] = l2[0]; lb[r + 1] = l2[1];
-              }
-              const int vo = ((wr * WTM + i * 16 + (lane & 15)) * N + wc * WTN + jp * 16 + cofs) * 2;
-              store_f16_pair(ha, hb, rh, vo);
-              if constexpr (SPLIT) store_f16_pair(la, lb, rl, vo);
-            }
-          }
-        } else
+        // stores issue fewer stores than the 8-B count S; with S unchanged the next tile's
+        // first ring stage was read before it landed: wrong dwords — round 2.)
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
           const floatx4 gj = *reinterpret_cast<const floatx4*>(gam + wc * WTN + j * 16 + 4 * g);
@@ -1347,7 +1269,7 @@ __global__ __launch_bounds__(kPipeBlock<CFG>, 1) void gemm_pipe_kernel(
           }
         }
       } else {
-        pipe_plain_epilogue<EPI, SPLIT, CFG, P_NO_STORE>(
+        pipe_plain_epilogue<EPI, SPLIT, CFG, false>(
             acc, kpart ? bias_l + kPipeBiasMax / 2 : bias_l, rc, rl, N, n0, wr, wc, lane);
       }
 #pragma unroll
@@ -1374,33 +1296,27 @@ __global__ __launch_bounds__(kPipeBlock<CFG>, 1) void gemm_pipe_kernel(
 // landed, the MFMA waves once they are done reading stage g-1 (whose slot the loaders refill
 // right after it). 12 waves: 3 per SIMD, <= 168 VGPRs each (the MFMA path needs ~145).
 // ----------------------------------------------------------------------------------------
-// PROBE 18 (the WS kernel's FULL / FREE ring): wait until an LDS counter reaches `target`
-// (bounded: a wrong count ends the wait after ~1.7 ms instead of hanging the wave)
-__device__ __forceinline__ void lds_spin_ge(uint32_t* p, uint32_t target) {
-  for (int n = 0; n < (1 << 16); ++n) {
-    const uint32_t v = __builtin_amdgcn_readfirstlane(
-        __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-    if (v >= target) return;
-    __builtin_amdgcn_s_sleep(1);
-  }
-}
-
 // block size of a gemm_ws_kernel instance: the MFMA waves plus one wave per loader
 // (launch_fixed; its __launch_bounds__)
 template <typename CFG> constexpr int kWsBlock = CFG::THREADS + 64 * CFG::LOADERS;
 
+// PROBE (diagnostic timing probes of the forward's large-batch GEMM, rag_bert_gemm variants
+// RAG_GEMM_WS_NO_STORE / _MFMA_ONLY / _DMA_ONLY; results meaningless): 6 = the epilogue without
+// its stores, 7 = no DMAs and no stores (MFMAs, LDS reads and barriers only), 8 = no MFMAs and
+// no stores (the DMA ring alone). The other round 2-4 probes and A/B forms of this kernel are
+// gone (round 5); their measurements are in DESIGN.md.
 template <int EPI, bool SPLIT, typename CFG, int PROBE = 0, int AUX = 0>
 __global__ __launch_bounds__(kWsBlock<CFG>, 1) void gemm_ws_kernel(
     const _Float16* __restrict__ A, const _Float16* __restrict__ Al,
     const _Float16* __restrict__ W, const _Float16* __restrict__ Wl,
     const float* __restrict__ bias, int M, int N, int K, void* __restrict__ Cout,
     _Float16* __restrict__ Clo, DlArgs dl) {
-  static_assert(EPI != kEpiAddLn && (CFG::PRELOAD || CFG::LOADERS < 4),
-                "plain epilogues; large tiles, or the small-tile single-loader instance");
+  static_assert(EPI != kEpiAddLn && CFG::PRELOAD, "plain / deferred-LN epilogues, large tiles");
+  static_assert(PROBE == 0 || PROBE == 6 || PROBE == 7 || PROBE == 8, "probe");
   constexpr bool DL = EPI == kEpiLnF16 || EPI == kEpiLnGeluF16 || EPI == kEpiResLn;
   static_assert(!DL || SPLIT, "deferred LayerNorm: fp16x3 only");
   constexpr int BM = CFG::BM, BN = CFG::BN, NS = CFG::NS, TH = CFG::THREADS;
-  constexpr int LTH = 64 * CFG::LOADERS;            // loader threads (4 waves; 1 for small)
+  constexpr int LTH = 64 * CFG::LOADERS;            // loader threads
   constexpr int FM = CFG::FM, FN = CFG::FN, WTM = 16 * FM, WTN = 16 * FN;
   constexpr int BK = CFG::BK ? CFG::BK : kBK<SPLIT>, CPR = BK / 8, KSN = BK / 32;
   constexpr int NPL = SPLIT ? 2 : 1;
@@ -1408,29 +1324,14 @@ __global__ __launch_bounds__(kWsBlock<CFG>, 1) void gemm_ws_kernel(
   constexpr int STAGE_H8 = NPL * (A_H8 + W_H8);
   constexpr int LA = A_H8 / LTH, LW = W_H8 / LTH;  // DMAs per loader wave per plane
   constexpr int L = NPL * (LA + LW);               // DMAs per loader wave per stage
-  constexpr bool P_NO_MFMA = PROBE == 1 || PROBE == 8 || PROBE == 23 || PROBE == 25;
-  constexpr bool P_NO_DMA = PROBE == 2 || PROBE == 7;
-  constexpr bool P_NO_STORE = PROBE == 6 || PROBE == 7 || PROBE == 8 || PROBE == 23 || PROBE == 25;
-  // PROBE 22 / 23 (round 4, A/B): the loader waves stage through registers (buffer_load to
-  // VGPRs one K step ahead, then ds_write_b128 into the ring slot) instead of LDS-DMA; 23 =
-  // the same without MFMAs and stores (the intake alone, as PROBE 8 for the DMA path)
-  constexpr bool REGST = PROBE == 22 || PROBE == 23;
-  // PROBE 24 / 25 (round 4, A/B): every loader wave also issues one 4-B-per-lane LDS-DMA per
-  // stage into a sink, touching the A panel's lines kPrefD K steps ahead (an L2 prefetch: the
-  // long-K FFN2 streams its A panel from HBM at the ring's depth); 25 = with PROBE 8's cuts
-  constexpr bool PREF = PROBE == 24 || PROBE == 25;
-  constexpr int kPrefD = 6;
-  constexpr int LP = L + (PREF ? 1 : 0);   // vector-memory ops per loader wave per stage
+  constexpr bool P_NO_MFMA = PROBE == 8;
+  constexpr bool P_NO_DMA = PROBE == 7;
+  constexpr bool P_NO_STORE = PROBE == 6 || PROBE == 7 || PROBE == 8;
   constexpr int OUT_B = EPI == kEpiF32 ? 4 : 2;
   static_assert(A_H8 % LTH == 0 && W_H8 % LTH == 0 && FN % 2 == 0, "tile shape");
   static_assert((NS - 2) * (L + 1) <= 63, "vmcnt range");
   __shared__ half8 lds[NS * STAGE_H8 + kPipeBiasMax / 4];
   float* bias_l = reinterpret_cast<float*>(lds + NS * STAGE_H8);
-  // PROBE 18: FULL[s] (loader waves' landed stages) and FREE[s] (MFMA waves' released
-  // stages) counters of ring slot s, in the last 16 floats of the bias area (the launcher
-  // keeps 3N of the staged vectors below them)
-  uint32_t* ring_cnt = reinterpret_cast<uint32_t*>(bias_l + kPipeBiasMax - 16);
-  constexpr bool FLAGS = PROBE == 18;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1457,9 +1358,10 @@ __global__ __launch_bounds__(kWsBlock<CFG>, 1) void gemm_ws_kernel(
   // as two 128-row halves on two workgroups, so the round ends after a half tile instead of a
   // full one. A half tile keeps the 256-row ring image (rows past its 128 read as zeros
   // through the A panel's extent, so no bytes move for them); the MFMA waves of the upper
-  // rows skip their MFMAs and stores. PROBE 19 = without (A/B).
+  // rows skip their MFMAs and stores (round 2: one layer at 117K tokens 1.252 / 1.247 vs
+  // 1.263 / 1.273 ms without).
   const int r_x = aligned ? t_x % stride : 0;
-  const bool halves = PROBE != 19 && aligned && r_x > 0 && 2 * r_x <= stride;
+  const bool halves = aligned && r_x > 0 && 2 * r_x <= stride;
   const int n_full = halves ? t_x / stride : l0 < t_x ? (t_x - l0 + stride - 1) / stride : 0;
   const int n_mine = n_full + (halves && lx < 2 * r_x ? 1 : 0);
   const int steps = n_mine * nk;
@@ -1488,19 +1390,10 @@ __global__ __launch_bounds__(kWsBlock<CFG>, 1) void gemm_ws_kernel(
         *reinterpret_cast<floatx4*>(bias_l + 2 * N + i) = *reinterpret_cast<const floatx4*>(dl.beta + i);
       }
   }
-  if constexpr (FLAGS)
-    if (tid < 16) ring_cnt[tid] = 0u;
   __syncthreads();
-  // Phase offset (dl.phase > 0, A/B): every CU runs the same tile sequence, so all of them
-  // reach their epilogues — the output store bursts — together, and the chip's MFMAs idle
-  // while HBM takes the writes. The odd workgroups start dl.phase x ~3.4 us late, which puts
-  // their store bursts between the even workgroups' ones.
-  if (dl.phase > 0 && (lx & 1))
-    for (int i = 0; i < dl.phase; ++i) __builtin_amdgcn_s_sleep(127);
 
   if (wid >= TH / 64) {
     // ---- loader waves: stage g+NS-1 issued after the barrier of step g ----
-    if constexpr (PROBE == 16) __builtin_amdgcn_s_setprio(3);   // A/B: loaders first in issue
     const int lw = wid - TH / 64;
     uint32_t voA[LA], voW[LW];
 #pragma unroll
@@ -1515,68 +1408,6 @@ __global__ __launch_bounds__(kWsBlock<CFG>, 1) void gemm_ws_kernel(
     }
     int it_i = 0, kt_i = 0, kr_i = 0, slot_i = 0;
     __amdgpu_buffer_rsrc_t rA0 = panel(A, 0), rA1 = rA0, rW0 = rA0, rW1 = rA0;
-    if constexpr (REGST) {
-      u32x4 rb0[L], rb1[L];
-      auto load_stage = [&](u32x4 (&r)[L]) __attribute__((always_inline)) {
-        if (it_i >= n_mine) return;
-        if (kt_i == 0) {
-          int m0, nt, m_end;
-          tile_mn(it_i, m0, nt, m_end);
-          const int n0 = nt * BN;
-          kr_i = aligned ? 0 : nt % nk;
-          const int64_t abytes = (int64_t)(m_end - m0) * K * 2, wbytes = (int64_t)BN * K * 2;
-          rA0 = panel(A + (int64_t)m0 * K, abytes);
-          rW0 = panel(W + (int64_t)n0 * K, wbytes);
-          if constexpr (SPLIT) {
-            rA1 = panel(Al + (int64_t)m0 * K, abytes);
-            rW1 = panel(Wl + (int64_t)n0 * K, wbytes);
-          }
-        }
-        const uint32_t soff = __builtin_amdgcn_readfirstlane((uint32_t)kr_i * (BK * 2));
-        if (++kr_i == nk) kr_i = 0;
-#pragma unroll
-        for (int i = 0; i < LA; ++i) {
-          r[i * NPL] = __builtin_amdgcn_raw_buffer_load_b128(rA0, voA[i], soff, 0);
-          if constexpr (SPLIT) r[i * NPL + 1] = __builtin_amdgcn_raw_buffer_load_b128(rA1, voA[i], soff, 0);
-        }
-#pragma unroll
-        for (int i = 0; i < LW; ++i) {
-          r[NPL * LA + i * NPL] = __builtin_amdgcn_raw_buffer_load_b128(rW0, voW[i], soff, 0);
-          if constexpr (SPLIT)
-            r[NPL * LA + i * NPL + 1] = __builtin_amdgcn_raw_buffer_load_b128(rW1, voW[i], soff, 0);
-        }
-        if (++kt_i == nk) { kt_i = 0; ++it_i; }
-      };
-      // stage g's registers -> ring slot g % NS, then the step's barrier. The slot was last
-      // read at step g - NS, whose reads every MFMA wave finished before barrier g - NS + 1.
-      auto write_stage = [&](const u32x4 (&r)[L]) __attribute__((always_inline)) {
-        u32x4* base = reinterpret_cast<u32x4*>(lds + slot_i * STAGE_H8);
-#pragma unroll
-        for (int i = 0; i < LA; ++i) {
-          base[(lw * LA + i) * 64 + lane] = r[i * NPL];
-          if constexpr (SPLIT) base[A_H8 + (lw * LA + i) * 64 + lane] = r[i * NPL + 1];
-        }
-#pragma unroll
-        for (int i = 0; i < LW; ++i) {
-          base[NPL * A_H8 + (lw * LW + i) * 64 + lane] = r[NPL * LA + i * NPL];
-          if constexpr (SPLIT)
-            base[NPL * A_H8 + W_H8 + (lw * LW + i) * 64 + lane] = r[NPL * LA + i * NPL + 1];
-        }
-        if (++slot_i == NS) slot_i = 0;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-      };
-      load_stage(rb0);
-      for (int g = 0; g < steps; g += 2) {
-        load_stage(rb1);                  // stage g + 1 in flight while stage g is written
-        write_stage(rb0);
-        if (g + 1 >= steps) break;
-        load_stage(rb0);
-        write_stage(rb1);
-      }
-      return;
-    }
     auto issue_next = [&]() __attribute__((always_inline)) {
       if (it_i >= n_mine) return;
       if constexpr (P_NO_DMA) {
@@ -1587,7 +1418,7 @@ __global__ __launch_bounds__(kWsBlock<CFG>, 1) void gemm_ws_kernel(
         int m0, nt, m_end;
         tile_mn(it_i, m0, nt, m_end);
         const int n0 = nt * BN;
-        kr_i = aligned || PROBE == 11 ? 0 : nt % nk;   // rotated K order unless aligned
+        kr_i = aligned ? 0 : nt % nk;   // rotated K order unless aligned
         const int64_t abytes = (int64_t)(m_end - m0) * K * 2, wbytes = (int64_t)BN * K * 2;
         rA0 = panel(A + (int64_t)m0 * K, abytes);
         rW0 = panel(W + (int64_t)n0 * K, wbytes);
@@ -1596,7 +1427,6 @@ __global__ __launch_bounds__(kWsBlock<CFG>, 1) void gemm_ws_kernel(
           rW1 = panel(Wl + (int64_t)n0 * K, wbytes);
         }
       }
-      const int kr_cur = kr_i;
       const uint32_t soff = __builtin_amdgcn_readfirstlane((uint32_t)kr_i * (BK * 2));
       if (++kr_i == nk) kr_i = 0;
       const uint32_t slot = lbase + (uint32_t)slot_i * (STAGE_H8 * 16);
@@ -1612,37 +1442,14 @@ __global__ __launch_bounds__(kWsBlock<CFG>, 1) void gemm_ws_kernel(
         blds16(rW0, voW[i], soff, d);
         if constexpr (SPLIT) blds16(rW1, voW[i], soff, d + W_H8 * 16);
       }
-      if constexpr (PREF) {
-        // rows lw*64 + lane of the panel (4 loader waves x 64 = BM rows), the 128-B line
-        // holding K steps 2m, 2m+1 of one plane: hi at even kp, lo at odd (a wrap past the
-        // tile's last step touches its first lines again: hits)
-        // (BK 64, one plane: one line per row per step)
-        static_assert(LTH == BM && (BK * 2 == 64 || BK * 2 == 128), "a line per row per 1-2 steps");
-        int kp = kr_cur + kPrefD;
-        if (kp >= nk) kp -= nk;
-        const int kl = BK * 2 == 64 ? (kp & ~1) : kp;
-        const uint32_t vo = (uint32_t)(((lw * 64 + lane) * K + kl * BK) * 2);
-        const uint32_t sink = lbase + (uint32_t)(NS * STAGE_H8 * 16 + (kPipeBiasMax - 64) * 4);
-        if (SPLIT && BK * 2 == 64 && (kp & 1)) blds4(rA1, vo, 0, sink);
-        else blds4(rA0, vo, 0, sink);
-      }
       if (++kt_i == nk) { kt_i = 0; ++it_i; }
       if (++slot_i == NS) slot_i = 0;
     };
 #pragma unroll
     for (int p = 0; p < NS - 1; ++p) issue_next();
     for (int g = 0; g < steps; ++g) {
-      wait_ring<LP, 0, NS - 2>(min(NS - 2, steps - 1 - g), false);   // stage g landed
-      if constexpr (FLAGS) {
-        // publish stage g, then take slot (g-1) % NS once all 8 MFMA waves released stage g-1
-        if (lane == 0)
-          __hip_atomic_fetch_add(&ring_cnt[g % NS], 1u, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (g >= 1 && g + NS - 1 < steps)
-          lds_spin_ge(&ring_cnt[8 + (g - 1) % NS], (uint32_t)(TH / 64) * ((g - 1) / NS + 1));
-      } else {
-        __builtin_amdgcn_s_barrier();
-      }
+      wait_ring<L, 0, NS - 2>(min(NS - 2, steps - 1 - g), false);   // stage g landed
+      __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       issue_next();                     // stage g+NS-1 -> slot (g-1) % NS
     }
@@ -1650,7 +1457,6 @@ __global__ __launch_bounds__(kWsBlock<CFG>, 1) void gemm_ws_kernel(
   }
 
   // ---- MFMA waves ----
-  if constexpr (PROBE == 17) __builtin_amdgcn_s_setprio(2);   // A/B: MFMA waves first in issue
   const int wr = wid / CFG::WAVES_N, wc = wid % CFG::WAVES_N;
   floatx4 acc[FM][FN];
 #pragma unroll
@@ -1658,10 +1464,7 @@ __global__ __launch_bounds__(kWsBlock<CFG>, 1) void gemm_ws_kernel(
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
   int kt_c = 0, it_c = 0, slot_c = 0;
-  // (declared outside the step loop only so the PROBE 14 / 15 timing probes can keep stale
-  // fragments: every production step overwrites them all before use)
   half8 af[KSN][NPL][FM], wf[KSN][NPL][FN];
-  half8 a_st[FM], w_st[FN];   // PROBE 21: the even step's lo16 fragments
   // deferred LN: the current tile's row statistics, loaded right after the previous tile's
   // epilogue (a whole tile before they are used; loaded at the tile's first K step instead, the
   // compiler's waitcnt model put a vmcnt(0) there — a wait for the previous tile's stores)
@@ -1680,22 +1483,10 @@ __global__ __launch_bounds__(kWsBlock<CFG>, 1) void gemm_ws_kernel(
   prefetch(0);
   for (int g = 0; g < steps; ++g) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // done reading stage g-1
-    if constexpr (FLAGS) {
-      // release stage g-1, wait for the 4 loader waves' stage g (no workgroup barrier: the
-      // MFMA waves drift up to the ring's depth apart)
-      if (g >= 1 && lane == 0)
-        __hip_atomic_fetch_add(&ring_cnt[8 + (g - 1) % NS], 1u, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);
-      lds_spin_ge(&ring_cnt[g % NS], (uint32_t)(LTH / 64) * (g / NS + 1));
-    } else {
-      __builtin_amdgcn_s_barrier();                      // stage g landed
-    }
+    __builtin_amdgcn_s_barrier();                        // stage g landed
     asm volatile("" ::: "memory");
     const half8* sa = lds + slot_c * STAGE_H8;
     const half8* sw = sa + NPL * A_H8;
-    // timing probes (results meaningless): 14 = A fragments read from LDS only at the first
-    // step (the DMA still streams A), 15 = the same for W
-    const bool rd_a = PROBE != 14 || g == 0, rd_w = PROBE != 15 || g == 0;
     auto read_a = [&](int i) __attribute__((always_inline)) {
 #pragma unroll
       for (int ks = 0; ks < KSN; ++ks)
@@ -1703,96 +1494,36 @@ __global__ __launch_bounds__(kWsBlock<CFG>, 1) void gemm_ws_kernel(
         for (int p = 0; p < NPL; ++p)
           af[ks][p][i] = sa[p * A_H8 + swz<CPR>(wr * WTM + i * 16 + (lane & 15), ks * 4 + (lane >> 4))];
     };
-    auto read_w = [&]() __attribute__((always_inline)) {
-#pragma unroll
-      for (int ks = 0; ks < KSN; ++ks)
-#pragma unroll
-        for (int p = 0; p < NPL; ++p)
-#pragma unroll
-          for (int j = 0; j < FN; ++j)
-            wf[ks][p][j] = sw[p * W_H8 + swz<CPR>(wc * WTN + j * 16 + (lane & 15), ks * 4 + (lane >> 4))];
-    };
-    auto mma = [&](int ks, int i, int j) __attribute__((always_inline)) {
-      if constexpr (PROBE == 20) {   // timing: the hi x hi MFMA alone (fp16x3 bytes and reads)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[ks][0][j], af[ks][0][i], acc[i][j], 0, 0, 0);
-        return;
-      }
-      if constexpr (PROBE == 21) {
-        // timing: hi x hi per step + the two correction products of 2 steps as ONE block-scaled
-        // fp8 MFMA (16x16x128: 2 K steps x [A_hi8 | A_lo8] . [W_lo8 ; W_hi8]); the lo16
-        // fragments of the even step stand in for the fp8 ones (same LDS bytes)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[ks][0][j], af[ks][0][i], acc[i][j], 0, 0, 0);
-        if (kt_c & 1) {
-          typedef int i4 __attribute__((ext_vector_type(4)));
-          typedef int i8 __attribute__((ext_vector_type(8)));
-          const i8 a8 = __builtin_shufflevector(__builtin_bit_cast(i4, a_st[i]),
-                                                __builtin_bit_cast(i4, af[ks][1][i]),
-                                                0, 1, 2, 3, 4, 5, 6, 7);
-          const i8 w8 = __builtin_shufflevector(__builtin_bit_cast(i4, w_st[j]),
-                                                __builtin_bit_cast(i4, wf[ks][1][j]),
-                                                0, 1, 2, 3, 4, 5, 6, 7);
-          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(w8, a8, acc[i][j], 0, 0,
-                                                                       0, 127, 0, 127);
-        }
-        return;
-      }
-      if constexpr (!P_NO_MFMA) {
-        if constexpr (SPLIT) {   // small terms first: W_lo A_hi + W_hi A_lo + W_hi A_hi
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[ks][1][j], af[ks][0][i], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[ks][0][j], af[ks][1][i], acc[i][j], 0, 0, 0);
-        }
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[ks][0][j], af[ks][0][i], acc[i][j], 0, 0, 0);
-      }
-    };
     // the upper-row MFMA waves of a half tile (split last round) have no rows: no reads,
     // MFMAs or stores (they still keep the ring's barriers)
     const bool idle = halves && it_c == n_full && wr >= CFG::WAVES_M / 2;
-    if (!idle) {
-      if constexpr (PROBE != 13 && !P_NO_MFMA) {
-        // interleaved order: A_0, W_0..W_{FN-1}, A_1, ... read in the order the i-major MFMAs
-        // consume them, with no barrier between the reads and the MFMAs, so the first MFMA
-        // waits for 4 reads instead of 13 (all 8 waves issue their reads together after the
-        // barrier; the LDS serves them interleaved). 123 instead of 138 VGPRs; measured
-        // (profiles/r02e_gemm_ilv.jsonl, same process, PROBE 13 = the previous all-reads-first
-        // order): 117K-token layer fp16x3 1.274 -> 1.264 ms, fp16 0.586 -> 0.581, QKV -3 to -6%,
-        // the others within +-1%.
-        if (rd_a) read_a(0);
-        if (rd_w)
-  #pragma unroll
-          for (int j = 0; j < FN; ++j)    // W_j's planes together: MFMA (0, j) needs 2 + 2j reads
-  #pragma unroll
-            for (int ks = 0; ks < KSN; ++ks)
-  #pragma unroll
-              for (int p = 0; p < NPL; ++p)
-                wf[ks][p][j] = sw[p * W_H8 + swz<CPR>(wc * WTN + j * 16 + (lane & 15), ks * 4 + (lane >> 4))];
-  #pragma unroll
-        for (int i = 0; i < FM; ++i) {
-          if (i + 1 < FM && rd_a) read_a(i + 1);
-  #pragma unroll
-          for (int ks = 0; ks < KSN; ++ks)
-  #pragma unroll
-            for (int j = 0; j < FN; ++j) mma(ks, i, j);
-        }
-        if constexpr (PROBE == 21)
-          if (!(kt_c & 1)) {
+    if (!idle && !P_NO_MFMA) {
+      // interleaved order: A_0, W_0..W_{FN-1}, A_1, ... read in the order the i-major MFMAs
+      // consume them, with no barrier between the reads and the MFMAs, so the first MFMA
+      // waits for 4 reads instead of 13 (all 8 waves issue their reads together after the
+      // barrier; the LDS serves them interleaved). Round 2: 117K-token layer fp16x3 1.274 ->
+      // 1.264 ms against all reads first (profiles/r02e_gemm_ilv.jsonl).
+      read_a(0);
 #pragma unroll
-            for (int i = 0; i < FM; ++i) a_st[i] = af[0][1][i];
+      for (int j = 0; j < FN; ++j)    // W_j's planes together: MFMA (0, j) needs 2 + 2j reads
 #pragma unroll
-            for (int j = 0; j < FN; ++j) w_st[j] = wf[0][1][j];
-          }
-      } else {
-        if constexpr (!P_NO_MFMA) {
-  #pragma unroll
-          for (int i = 0; i < FM; ++i) read_a(i);
-          read_w();
-          __builtin_amdgcn_sched_barrier(0);
-        }
-  #pragma unroll
         for (int ks = 0; ks < KSN; ++ks)
-  #pragma unroll
-          for (int i = 0; i < FM; ++i)
-  #pragma unroll
-            for (int j = 0; j < FN; ++j) mma(ks, i, j);
+#pragma unroll
+          for (int p = 0; p < NPL; ++p)
+            wf[ks][p][j] = sw[p * W_H8 + swz<CPR>(wc * WTN + j * 16 + (lane & 15), ks * 4 + (lane >> 4))];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        if (i + 1 < FM) read_a(i + 1);
+#pragma unroll
+        for (int ks = 0; ks < KSN; ++ks)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            if constexpr (SPLIT) {   // small terms first: W_lo A_hi + W_hi A_lo + W_hi A_hi
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[ks][1][j], af[ks][0][i], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[ks][0][j], af[ks][1][i], acc[i][j], 0, 0, 0);
+            }
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[ks][0][j], af[ks][0][i], acc[i][j], 0, 0, 0);
+          }
       }
     }
     if (++slot_c == NS) slot_c = 0;
@@ -1801,7 +1532,6 @@ __global__ __launch_bounds__(kWsBlock<CFG>, 1) void gemm_ws_kernel(
       int m0, nt, m_end;
       tile_mn(it_c, m0, nt, m_end);
       ++it_c;
-      if (PROBE == 9) m0 = 0;   // every tile stored over the first row band: L2-resident writes
       const int n0 = nt * BN;
       const __amdgpu_buffer_rsrc_t rc = panel(static_cast<char*>(Cout) + (int64_t)m0 * N * OUT_B,
                                               (int64_t)(m_end - m0) * N * OUT_B);
@@ -1824,484 +1554,6 @@ __global__ __launch_bounds__(kWsBlock<CFG>, 1) void gemm_ws_kernel(
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
       prefetch(it_c);
-    }
-  }
-}
-
-// ----------------------------------------------------------------------------------------
-// GEMM, ping-pong (gemm_pp_kernel; round 5): fp16x3 token-row GEMMs of large batches with
-// N % 192 == 0 (MiniLM / bge-small: Q|K|V 1152, FFN1 1536, O-proj / FFN2 384, last-layer
-// K|V 768). Same arithmetic as gemm_ws_kernel in its panel-aligned order — per output element
-// the same MFMA sequence (K steps in order; per step W_lo A_hi, W_hi A_lo, W_hi A_hi), so the
-// two kernels agree bit for bit from 64 row panels up — on a different structure:
-//  * 256 x 192 tiles (the WS kernel's 256 x 128): 448 operand rows per K step instead of 384
-//    for 1.5x the products, -22% L2 -> LDS bytes per FLOP. The WS probes put the LDS-DMA intake
-//    (~24-30 B/clk per CU) on the critical path of these GEMMs; with
-//    the hi + lo output stream that intake is what bounds a tile, not the MFMA pipe.
-//  * no loader waves: 8 waves, two per SIMD (256 registers each), each computing 32 rows x
-//    the 192 columns (three whole 64-column stats blocks, as the deferred-LN epilogue needs)
-//    and each taking a share of the DMAs. Waves 0-3 (group 0: tile rows 0-127) and 4-7
-//    (group 1: rows 128-255) sit on the same four SIMDs and run half a step apart: between two
-//    consecutive s_barriers one group issues its MFMAs (C phase: 72 MFMAs of 16x16x32, the
-//    step's fragments already in registers) while the other reads the next step's fragments
-//    from LDS, issues its half of a coming stage's DMAs and runs any tile epilogue (M phase).
-//    The matrix pipe of each SIMD alternates between the two waves it hosts instead of idling
-//    while both read (the WS kernel's MFMA waves read their fragments in lockstep after each
-//    step's barrier: 0.59 of the pipe even with no DMA and no stores).
-//  * a two-stage LDS ring (2 x 56 KB) + the staged bias area. Group 1 streams the A planes of
-//    stage s during its M phase of step s - 2 (right after its own reads of the slot), group 0
-//    the W planes during its M phase of step s - 1; each group retires its own DMAs with a
-//    counted vmcnt before the barrier that precedes the slot's first read (group 0: end of its
-//    C phase; group 1: end of its M phase, the next stage's DMAs left in flight).
-// Barriers: group 1 passes one extra barrier at the start and skips the last, so every wave
-// arrives at every barrier (2 per K step). LDS reads of a stage finish (lgkmcnt(0)) before the
-// barrier that ends the M phase, so no DMA into a slot can overtake a read of it.
-// ----------------------------------------------------------------------------------------
-using PipePP = PipeCfg<256, 192, 8, 1, 2, 32, 0>;
-constexpr int kPpBlock = 512;
-
-// the deferred-LN epilogues for wave tiles of several 64-column stats blocks (WTN % 64 == 0):
-// ws_dl_epilogue's arithmetic per element (same formulas, same order), block by block; the
-// residual planes of one row group are loaded at a time (the ping-pong kernel's register budget)
-template <int EPI, typename CFG, int AUX>
-__device__ __forceinline__ void pp_dl_epilogue(floatx4 (&acc)[CFG::FM][CFG::FN],
-                                               const float* lds_f, __amdgpu_buffer_rsrc_t rc,
-                                               __amdgpu_buffer_rsrc_t rl,
-                                               const floatx4 (&dls)[CFG::FM],
-                                               __amdgpu_buffer_rsrc_t rs_out, bool has_stats,
-                                               int N, int n0, int wr, int wc, int lane,
-                                               float eps) {
-  constexpr int FM = CFG::FM, FN = CFG::FN, WTM = 16 * FM, WTN = 16 * FN;
-  static_assert(WTN % 64 == 0 && FN % 4 == 0, "whole 64-column stats blocks per wave");
-  const int g = lane >> 4;
-  const int cofs = 8 * ((g & 1) * 2 + (g >> 1));
-  const float* bias_l = lds_f;
-  const float* c1_l = lds_f + N;                          // Ln*
-  const float *gam_l = lds_f + N, *bet_l = lds_f + 2 * N;  // ResLn
-  float mu[FM], rs[FM];
-#pragma unroll
-  for (int i = 0; i < FM; ++i) {
-    mu[i] = 0.f;
-    rs[i] = 1.f;
-    if (EPI != kEpiResLn || has_stats) dl_lane_stats(dls[i], g, eps, mu[i], rs[i]);
-  }
-  // column-block outer, row group inner: a block's staged vectors are read once for all the
-  // wave's rows and are dead after it (rows outer, the compiler kept every block's vectors
-  // live beside the accumulators and spilled)
-  if constexpr (EPI == kEpiResLn) {
-    // row group by row group: the residual z of a group's 16 rows x WTN columns in flight at
-    // once (one round trip per group; both groups' 96 registers would not fit)
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int ml = wr * WTM + i * 16 + (lane & 15);
-      u32x2 zh[FN], zl[FN];
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int vo = (ml * N + n0 + wc * WTN + j * 16 + 4 * g) * 2;
-        zh[j] = __builtin_amdgcn_raw_buffer_load_b64(rc, vo, 0, 0);
-        zl[j] = __builtin_amdgcn_raw_buffer_load_b64(rl, vo, 0, 0);
-      }
-      const floatx4 a4 = {rs[i], rs[i], rs[i], rs[i]};
-      const floatx4 b4 = {-mu[i] * rs[i], -mu[i] * rs[i], -mu[i] * rs[i], -mu[i] * rs[i]};
-#pragma unroll
-      for (int bb = 0; bb < FN / 4; ++bb) {
-        floatx4 s4 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          const int j = 4 * bb + jj;
-          const int nl = n0 + wc * WTN + j * 16 + 4 * g;
-          const floatx4 z = mix_f16x4(zh[j], zl[j]);
-          const floatx4 b = *reinterpret_cast<const floatx4*>(bias_l + nl);
-          floatx4 xr = z;
-          if (has_stats)
-            xr = __builtin_elementwise_fma(__builtin_elementwise_fma(z, a4, b4),
-                                           *reinterpret_cast<const floatx4*>(gam_l + nl),
-                                           *reinterpret_cast<const floatx4*>(bet_l + nl));
-          acc[i][j] = (acc[i][j] + b) + xr;
-          s4 += acc[i][j];
-          if (jj & 1) __builtin_amdgcn_sched_barrier(0);   // staged vectors of 2 frags live
-        }
-        float s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
-        s += __shfl_xor(s, 16, 64);
-        s += __shfl_xor(s, 32, 64);
-        const float mw = s * (1.0f / 64);
-        const floatx4 m4 = {mw, mw, mw, mw};
-        floatx4 q4 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          const floatx4 d = acc[i][4 * bb + jj] - m4;
-          q4 = __builtin_elementwise_fma(d, d, q4);
-        }
-        float q = (q4[0] + q4[1]) + (q4[2] + q4[3]);
-        q += __shfl_xor(q, 16, 64);
-        q += __shfl_xor(q, 32, 64);
-        if (g == 0) {
-          const u32x2 d = {__builtin_bit_cast(uint32_t, mw), __builtin_bit_cast(uint32_t, q)};
-          __builtin_amdgcn_raw_buffer_store_b64(
-              d, rs_out, (ml * kDlParts + (n0 + wc * WTN) / 64 + bb) * 8, 0, 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      // z planes (default policy), row group by row group (ws_dl_epilogue's order)
-#pragma unroll
-      for (int jp = 0; jp < FN; jp += 2) dl_store_pair<AUX>(acc, i, jp, ml, N, n0, wc, cofs, rc, rl);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  } else {
-#pragma unroll
-    for (int bb = 0; bb < FN / 4; ++bb) {
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        const int j = 4 * bb + jj;
-        const int nl = n0 + wc * WTN + j * 16 + 4 * g;
-        const floatx4 c1 = *reinterpret_cast<const floatx4*>(c1_l + nl);
-        const floatx4 c2 = *reinterpret_cast<const floatx4*>(bias_l + nl);
-#pragma unroll
-        for (int i = 0; i < FM; ++i) {
-          const floatx4 nm4 = {-mu[i], -mu[i], -mu[i], -mu[i]}, rs4 = {rs[i], rs[i], rs[i], rs[i]};
-          acc[i][j] = __builtin_elementwise_fma(rs4, __builtin_elementwise_fma(nm4, c1, acc[i][j]), c2);
-          if constexpr (EPI == kEpiLnGeluF16) acc[i][j] = gelu_erf4(acc[i][j]);
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    // QKV / FFN1 outputs: the plain epilogue's order (see ws_dl_epilogue)
-#pragma unroll
-    for (int jp = 0; jp < FN; jp += 2)
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-        dl_store_pair<AUX>(acc, i, jp, wr * WTM + i * 16 + (lane & 15), N, n0, wc, cofs, rc, rl);
-  }
-}
-
-// PROBE (diagnostic timing probes, results meaningless): 6 = no stores, 7 = no DMAs and no
-// stores (MFMAs, LDS reads and barriers only), 8 = no MFMAs and no stores (the DMA ring alone);
-// 31 (A/B, results valid) = s_setprio 1 around every C phase.
-template <int EPI, typename CFG, int PROBE = 0, int AUX = 0>
-__global__ __launch_bounds__(kPpBlock, 1) void gemm_pp_kernel(
-    const _Float16* __restrict__ A, const _Float16* __restrict__ Al,
-    const _Float16* __restrict__ W, const _Float16* __restrict__ Wl,
-    const float* __restrict__ bias, int M, int N, int K, void* __restrict__ Cout,
-    _Float16* __restrict__ Clo, DlArgs dl) {
-  static_assert(EPI != kEpiAddLn, "plain and deferred-LN epilogues");
-  constexpr bool DL = EPI == kEpiLnF16 || EPI == kEpiLnGeluF16 || EPI == kEpiResLn;
-  constexpr int BM = CFG::BM, BN = CFG::BN;
-  constexpr int FM = CFG::FM, FN = CFG::FN, WTM = 16 * FM;
-  static_assert(BM == 256 && CFG::WAVES_M == 8 && CFG::WAVES_N == 1 && CFG::NS == 2 &&
-                    CFG::BK == 32 && kPpBlock == 64 * CFG::WAVES_M,
-                "8 waves of 32 rows x BN, two-stage BK-32 ring");
-  constexpr int BK = 32, CPR = BK / 8, NPL = 2;
-  constexpr int A_H8 = BM * CPR, W_H8 = BN * CPR;
-  constexpr int STAGE_H8 = NPL * (A_H8 + W_H8);
-  // DMAs per wave and plane: group 1's four waves stream the A planes, group 0's the W planes
-  constexpr int LA = A_H8 / 256, LW = W_H8 / 256;
-  static_assert(A_H8 % 256 == 0 && W_H8 % 256 == 0 && FN % 2 == 0, "tile shape");
-  constexpr int OUT_B = EPI == kEpiF32 ? 4 : 2;
-  constexpr bool P_NO_MFMA = PROBE == 8, P_NO_DMA = PROBE == 7;
-  constexpr bool P_NO_STORE = PROBE == 6 || PROBE == 7 || PROBE == 8;
-  __shared__ half8 lds[2 * STAGE_H8 + kPipeBiasMax / 4];
-  float* bias_l = reinterpret_cast<float*>(lds + 2 * STAGE_H8);
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int grp = wid >> 2, lw = wid & 3;
-  const uint32_t lbase = lds_addr_of(lds);
-  const int nN = N / BN, nM = (M + BM - 1) / BM;
-  const int nk = K / BK;
-  // tile schedule: gemm_ws_kernel's (panel-aligned XCD placement from 64 row panels up, split
-  // last round), K steps always in order
-  const int G = gridDim.x, per_xcd = G >> 3;    // G: a multiple of 8 (launcher)
-  const int xcd = blockIdx.x & 7, lx = blockIdx.x >> 3;
-  const bool aligned = nM >= 64;
-  const int t_x = aligned ? (nM > xcd ? (nM - xcd + 7) >> 3 : 0) * nN : nM * nN;
-  const int l0 = aligned ? lx : xcd * per_xcd + lx, stride = aligned ? per_xcd : G;
-  const int r_x = aligned ? t_x % stride : 0;
-  const bool halves = aligned && r_x > 0 && 2 * r_x <= stride;
-  const int n_full = halves ? t_x / stride : l0 < t_x ? (t_x - l0 + stride - 1) / stride : 0;
-  const int n_mine = n_full + (halves && lx < 2 * r_x ? 1 : 0);
-  const int steps = n_mine * nk;
-  auto tile_mn = [&](int it, int& m0, int& nt, int& m_end) __attribute__((always_inline)) {
-    if (it < n_full) {
-      const int t = it * stride + l0;
-      m0 = (aligned ? xcd + 8 * (t / nN) : t / nN) * BM;
-      nt = t % nN;
-      m_end = min(M, m0 + BM);
-    } else {                                  // the half tile of the split last round
-      const int t = n_full * stride + (lx >> 1);
-      m0 = (xcd + 8 * (t / nN)) * BM + (lx & 1) * (BM / 2);
-      nt = t % nN;
-      m_end = min(M, m0 + BM / 2);
-    }
-  };
-
-  for (int i = tid * 4; i < N; i += kPpBlock * 4) {
-    *reinterpret_cast<floatx4*>(bias_l + i) = *reinterpret_cast<const floatx4*>(bias + i);
-    if constexpr (EPI == kEpiLnF16 || EPI == kEpiLnGeluF16)
-      *reinterpret_cast<floatx4*>(bias_l + N + i) = *reinterpret_cast<const floatx4*>(dl.c1 + i);
-    if constexpr (EPI == kEpiResLn)
-      if (dl.st_in) {
-        *reinterpret_cast<floatx4*>(bias_l + N + i) = *reinterpret_cast<const floatx4*>(dl.gamma + i);
-        *reinterpret_cast<floatx4*>(bias_l + 2 * N + i) = *reinterpret_cast<const floatx4*>(dl.beta + i);
-      }
-  }
-  __syncthreads();
-  // start stagger (dl.phase > 0, A/B): workgroup lx starts (lx % 4) x dl.phase x ~3.9 us late,
-  // spreading the chip's tile epilogues (each CU's output burst) over a tile's time
-  if (dl.phase > 0)
-    for (int i = 0; i < dl.phase * (lx & 3); ++i) __builtin_amdgcn_s_sleep(127);
-
-  // ---- DMA duties ----
-  // A planes: every wave streams ITS OWN 32 rows (LA2 = 2 DMAs per plane), which no other wave
-  // reads, so refilling them right after its own reads needs no barrier, and landing them needs
-  // only its own counted vmcnt. W planes (read by all 8 waves): group 0, LW = 3 DMAs per plane
-  // per wave, into the slot both groups finished reading a barrier ago. DMA i covers 16 rows:
-  // row 16 b + lane / 4, source chunk swz_chunk(row, lane % 4), which depends on the lane only
-  // (row bit 3 is lane bit 5), so one per-lane byte offset serves every DMA and the row block
-  // goes into soffset. (Round 5's first form split the A planes over group 1's waves: a wave
-  // could refill rows another wave of its group was still reading — wrong tiles under load.)
-  static_assert(CPR == 4, "64-B rows: 4 chunks per row, 16 rows per DMA");
-  constexpr int LA2 = WTM / 16;
-  const uint32_t vo = (uint32_t)(((lane >> 2) * K + swz_chunk<CPR>(lane >> 2, lane & 3) * 8) * 2);
-  struct Feed {
-    int s = 0, it = 0, kt = 0;
-    __amdgpu_buffer_rsrc_t r0, r1;
-  };
-  Feed fa, fw;
-  fa.r0 = fa.r1 = fw.r0 = fw.r1 = panel(A, 0);
-  // the next stage of feed f (A: this wave's rows; W: group 0's share) into slot s & 1; false
-  // once every stage is issued
-  auto issue = [&](Feed& f, bool is_w) __attribute__((always_inline)) -> bool {
-    if (f.it >= n_mine) return false;
-    if (f.kt == 0) {
-      int m0, nt, m_end;
-      tile_mn(f.it, m0, nt, m_end);
-      if (is_w) {
-        const int64_t wbytes = (int64_t)BN * K * 2;
-        f.r0 = panel(W + (int64_t)nt * BN * K, wbytes);
-        f.r1 = panel(Wl + (int64_t)nt * BN * K, wbytes);
-      } else {
-        const int64_t abytes = (int64_t)(m_end - m0) * K * 2;
-        f.r0 = panel(A + (int64_t)m0 * K, abytes);
-        f.r1 = panel(Al + (int64_t)m0 * K, abytes);
-      }
-    }
-    const uint32_t slot = lbase + (uint32_t)(f.s & 1) * (STAGE_H8 * 16);
-    if constexpr (!P_NO_DMA) {
-      if (is_w) {
-#pragma unroll
-        for (int i = 0; i < LW; ++i) {
-          const uint32_t d = slot + (uint32_t)((NPL * A_H8 + (lw * LW + i) * 64) * 16);
-          const uint32_t soff = __builtin_amdgcn_readfirstlane(
-              (uint32_t)f.kt * (BK * 2) + (uint32_t)((lw * LW + i) * 16 * K * 2));
-          blds16(f.r0, vo, soff, d);
-          blds16(f.r1, vo, soff, d + W_H8 * 16);
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < LA2; ++i) {
-          const uint32_t d = slot + (uint32_t)((wid * LA2 + i) * 64 * 16);
-          const uint32_t soff = __builtin_amdgcn_readfirstlane(
-              (uint32_t)f.kt * (BK * 2) + (uint32_t)((wid * LA2 + i) * 16 * K * 2));
-          blds16(f.r0, vo, soff, d);
-          blds16(f.r1, vo, soff, d + A_H8 * 16);
-        }
-      }
-    }
-    ++f.s;
-    if (++f.kt == nk) { f.kt = 0; ++f.it; }
-    return true;
-  };
-
-  // ---- compute state: rows wid * 32 .. + 31 of the tile, all BN columns ----
-  const int wr = wid, wc = 0;
-  const int lane_sw = swz<CPR>(lane & 15, lane >> 4);   // fragment read offset in a 16-row block
-  floatx4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-  floatx4 dls[FM];
-  // (the residual epilogue loads its rows' statistics itself, beside the residual planes:
-  // held through the tile, the 8 registers were spilled)
-  auto prefetch = [&](int it) __attribute__((always_inline)) {
-    if constexpr (DL && EPI != kEpiResLn) {
-      if (dl.st_in && it < n_mine) {
-        int m0, nt, m_end;
-        tile_mn(it, m0, nt, m_end);
-        const __amdgpu_buffer_rsrc_t rsi =
-            panel(dl.st_in + (int64_t)m0 * kDlParts * 2, (int64_t)(m_end - m0) * kDlParts * 8);
-        dl_prefetch_stats<FM>(dls, rsi, wr, lane);
-      }
-    }
-  };
-  // the epilogue of tile `it` (this wave's 32 rows; none in the upper half of a half tile)
-  auto epilogue = [&](int it) __attribute__((always_inline)) {
-    int m0, nt, m_end;
-    tile_mn(it, m0, nt, m_end);
-    const bool idle_t = it >= n_full && grp == 1;
-    const int n0 = nt * BN;
-    const __amdgpu_buffer_rsrc_t rc = panel(static_cast<char*>(Cout) + (int64_t)m0 * N * OUT_B,
-                                            (int64_t)(m_end - m0) * N * OUT_B);
-    __amdgpu_buffer_rsrc_t rl = rc;
-    if constexpr (EPI != kEpiF32)
-      rl = panel(Clo + (int64_t)m0 * N, (int64_t)(m_end - m0) * N * 2);
-    if (!idle_t) {
-      // the lane index laundered per call: every lane-derived address of the epilogue is then
-      // computed in the epilogue, not hoisted out of the step loop (hoisted, ~20 such values
-      // lived through the loop and the residual epilogue spilled them)
-      int ln = lane;
-      asm volatile("" : "+v"(ln));
-      if constexpr (DL) {
-        const int64_t sb = (int64_t)(m_end - m0) * kDlParts * 8;
-        const __amdgpu_buffer_rsrc_t rso =
-            panel(dl.st_out + (int64_t)m0 * kDlParts * 2, dl.st_out ? sb : 0);
-        if constexpr (EPI == kEpiResLn)
-          if (dl.st_in)
-            dl_prefetch_stats<FM>(
-                dls, panel(dl.st_in + (int64_t)m0 * kDlParts * 2, (int64_t)(m_end - m0) * kDlParts * 8),
-                wr, ln);
-        pp_dl_epilogue<EPI, CFG, AUX>(acc, bias_l, rc, rl, dls, rso, dl.st_in != nullptr, N, n0,
-                                      wr, wc, ln, dl.eps);
-      } else {
-        pipe_plain_epilogue<EPI, true, CFG, P_NO_STORE, AUX>(acc, bias_l, rc, rl, N, n0, wr, wc,
-                                                             ln);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-  };
-
-  prefetch(0);
-  issue(fa, false);                              // stages 0 and 1
-  issue(fa, false);
-  if (grp == 0) {
-    issue(fw, true);
-    issue(fw, true);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  if (grp == 1 && steps > 0) __builtin_amdgcn_s_barrier();   // half a step behind group 0
-  asm volatile("" ::: "memory");
-  int it_c = 0, kt_c = 0;
-  bool pending = false;                          // a finished tile awaits its epilogue
-  // vector-memory ops an epilogue issues (all unconditional for a wave with rows): the counted
-  // waits below leave them in flight instead of draining them with the DMAs they wait for
-  // (vmcnt is positional: "all but the N youngest done")
-  constexpr int S_EPI = FM * FN;
-  constexpr int DA = 2 * LA2;                    // own-A DMAs per stage (both planes)
-  bool prev_epi_stores = false;                  // the previous M phase ran a storing epilogue
-  for (int g = 0; g < steps; ++g) {
-    // ---------------- M phase ----------------
-    const bool epi = pending;
-    const bool epi_stores = epi && !P_NO_STORE && !(it_c - 1 >= n_full && grp == 1);
-    // own A rows of stage g (issued at the end of M phase g - 2; younger than them: the
-    // previous M phase's epilogue ops and its own-A DMAs of stage g + 1 — group 0's are also
-    // covered by its W wait at the end of the previous C phase)
-    if (grp == 1) {
-      if (prev_epi_stores) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(S_EPI + DA) : "memory");
-      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DA) : "memory");
-    }
-    prev_epi_stores = epi_stores;
-    bool w_issued = false;
-    if (grp == 0 && g >= 1) {
-      // W planes of stage g + 1 (their slot: both groups read stage g - 1 a barrier ago), before
-      // the epilogue's stores, so waiting for them does not wait for those
-      if constexpr (DL)
-        if (epi)
-#pragma unroll
-          for (int i = 0; i < FM; ++i) asm volatile("" ::"v"(dls[i]));   // (its loads done)
-      w_issued = issue(fw, true);
-    }
-    if (pending) {
-      if constexpr (P_NO_STORE) {
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j) {
-            asm volatile("" ::"v"(acc[i][j]));
-            acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-          }
-      } else {
-        epilogue(it_c - 1);
-      }
-      prefetch(it_c);
-      pending = false;
-      // (the next step's fragment reads stay below the epilogue: interleaved with it, its
-      // temporaries, the accumulators and 112 fragment registers would not fit in 256)
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    const bool idle = halves && it_c == n_full && grp == 1;
-    // (declared per step: nothing carries fragments across steps, so they are dead during
-    // the epilogue; declared outside the loop, the compiler kept all 112 registers live)
-    half8 af[NPL][FM], wf[NPL][FN];
-    if (!idle) {
-      // swz<CPR>(16 b + (lane & 15), lane >> 4) = 64 b + lane_sw for every 16-row block b:
-      // one base address per operand, the rest immediate offsets (computed per fragment, the
-      // compiler kept ~20 loop-invariant address registers, which the in-loop deferred-LN
-      // epilogues could not spare)
-      const half8* sa = lds + (g & 1) * STAGE_H8 + lane_sw + wr * (WTM * CPR);
-      const half8* sw = lds + (g & 1) * STAGE_H8 + NPL * A_H8 + lane_sw;
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int p = 0; p < NPL; ++p) af[p][i] = sa[p * A_H8 + i * 16 * CPR];
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-#pragma unroll
-        for (int p = 0; p < NPL; ++p) wf[p][j] = sw[p * W_H8 + j * 16 * CPR];
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // own reads done
-    // own A rows of stage g + 2 into the slot just read (nobody else reads them)
-    const bool a_issued = issue(fa, false);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    // ---------------- C phase ----------------
-    if constexpr (PROBE == 31) __builtin_amdgcn_s_setprio(1);
-    if (!idle && !P_NO_MFMA) {
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) {   // small terms first: W_lo A_hi + W_hi A_lo + W_hi A_hi
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[1][j], af[0][i], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[0][j], af[1][i], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[0][j], af[0][i], acc[i][j], 0, 0, 0);
-        }
-    }
-    if constexpr (P_NO_MFMA) {
-#pragma unroll
-      for (int j = 0; j < FN; ++j) asm volatile("" ::"v"(wf[0][j]), "v"(wf[1][j]));
-#pragma unroll
-      for (int i = 0; i < FM; ++i) asm volatile("" ::"v"(af[0][i]), "v"(af[1][i]));
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (PROBE == 31) __builtin_amdgcn_s_setprio(0);
-    if (w_issued) {   // W planes of stage g + 1 (younger: the epilogue ops, own-A DMAs)
-      if (epi_stores) {
-        if (a_issued) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(S_EPI + DA) : "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(S_EPI) : "memory");
-      } else {
-        if (a_issued) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DA) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-    }
-    if (++kt_c == nk) {
-      kt_c = 0;
-      ++it_c;
-      pending = true;
-    }
-    if (grp == 0 || g + 1 < steps) __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  }
-  if (pending) {
-    if constexpr (P_NO_STORE) {
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) asm volatile("" ::"v"(acc[i][j]));
-    } else {
-      epilogue(it_c - 1);
     }
   }
 }
@@ -3174,59 +2426,6 @@ __global__ __launch_bounds__(256) void ce_head_kernel(const float* __restrict__ 
   if (lane == 0) part[wid] = acc;
   __syncthreads();
   if (tid == 0) out[b] = part[0] + part[1] + part[2] + part[3] + bc[0];
-}
-
-// The same head with the pooler dot products spread over the lanes (round 3). ce_head_kernel
-// gives every thread whole W_p rows: each float4 load of a wave touches 64 different rows, and
-// the 384-long FMA chain is serial (36 us for a 480-pair batch, latency-bound). Here a wave
-// reads one W_p row coalesced (lane l holds columns 2l, 2l+1 of each 128-column slice), dots it
-// with the R CLS rows held in registers and reduces over the wave (wave_sum64), so a row is one
-// coalesced 1.5 KB read shared by R pairs. Wave w takes outputs w, w+4, ... The summation order
-// differs from ce_head_kernel's (within the 1e-3 head contract) but is the same for every slot r,
-// so a pair scores identically alone and inside a batch.
-template <int H, int R>
-__global__ __launch_bounds__(256) void ce_head_rows_kernel(const float* __restrict__ x, int B,
-                                                           const float* __restrict__ wp,
-                                                           const float* __restrict__ bp,
-                                                           const float* __restrict__ wc,
-                                                           const float* __restrict__ bc,
-                                                           float* __restrict__ out) {
-  static_assert(H % 128 == 0, "lanes own column pairs of 128-column slices");
-  constexpr int NS = H / 128;
-  __shared__ float part[R][4];
-  const int b0 = blockIdx.x * R, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int nr = min(R, B - b0);
-  float2 cl[R][NS];
-#pragma unroll
-  for (int r = 0; r < R; ++r)
-#pragma unroll
-    for (int k = 0; k < NS; ++k)
-      cl[r][k] = r < nr ? *reinterpret_cast<const float2*>(x + (int64_t)(b0 + r) * H + k * 128 +
-                                                            2 * lane)
-                        : make_float2(0.f, 0.f);
-  float acc[R];
-#pragma unroll
-  for (int r = 0; r < R; ++r) acc[r] = 0.f;
-#pragma unroll 4
-  for (int o = wid; o < H; o += 4) {
-    float2 w2[NS];
-#pragma unroll
-    for (int k = 0; k < NS; ++k)
-      w2[k] = *reinterpret_cast<const float2*>(wp + (int64_t)o * H + k * 128 + 2 * lane);
-    const float b = bp[o], w = wc[o];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      float d = 0.f;
-#pragma unroll
-      for (int k = 0; k < NS; ++k) d = fmaf(w2[k].y, cl[r][k].y, fmaf(w2[k].x, cl[r][k].x, d));
-      acc[r] = fmaf(tanhf(wave_sum64(d) + b), w, acc[r]);
-    }
-  }
-  if (lane == 0)
-#pragma unroll
-    for (int r = 0; r < R; ++r) part[r][wid] = acc[r];
-  __syncthreads();
-  if (tid < nr) out[b0 + tid] = part[tid][0] + part[tid][1] + part[tid][2] + part[tid][3] + bc[0];
 }
 
 }  // namespace bert

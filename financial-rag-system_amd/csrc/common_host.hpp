@@ -27,15 +27,24 @@ inline int fail(int code, const std::string& msg) {
 
 // ---- diagnostic A/B knobs -------------------------------------------
 // The RAGMI_* environment variables that switch kernels for A/B measurements (scan grid,
-// seed sample, rescan grid, GEMM variants, attention variant, ...) are honoured only once a
-// handle of this process was created with RAG_CREATE_DIAGNOSTIC (rag_index_create_ex's
-// storage argument, rag_encoder_create_ex's flags). Otherwise every knob reads as its
+// seed sample, rescan grid, GEMM variant, LayerNorm modes, ...) are honoured only while a
+// handle of this process created with RAG_CREATE_DIAGNOSTIC (rag_index_create_ex's storage
+// argument, rag_encoder_create_ex's flags) is alive: a successful create counts it, its
+// destroy releases it, and the first one says so on stderr. Otherwise every knob reads as its
 // production default, and a knob that is set but ignored is reported once on stderr, so a
 // stray variable in a serving process cannot change results or speed unnoticed.
-inline std::atomic<bool>& diagnostics_on() {
-  static std::atomic<bool> on{false};
-  return on;
+inline std::atomic<int>& diagnostic_handles() {
+  static std::atomic<int> n{0};
+  return n;
 }
+inline void diagnostic_acquire() {
+  static std::atomic<bool> said{false};
+  diagnostic_handles().fetch_add(1);
+  if (!said.exchange(true))
+    std::fprintf(stderr, "ragmi: diagnostic handle created: RAGMI_* A/B knobs are honoured "
+                         "while diagnostic handles live\n");
+}
+inline void diagnostic_release() { diagnostic_handles().fetch_sub(1); }
 
 class Knob {
  public:
@@ -55,7 +64,7 @@ class Knob {
  private:
   bool honoured() {
     if (!set_) return false;
-    if (diagnostics_on().load(std::memory_order_relaxed)) return true;
+    if (diagnostic_handles().load(std::memory_order_relaxed) > 0) return true;
     if (!warned_.exchange(true))
       std::fprintf(stderr,
                    "ragmi: %s=%s ignored: A/B knobs need a handle created with "

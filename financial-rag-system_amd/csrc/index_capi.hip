@@ -78,6 +78,7 @@ struct ProfPair {
 
 struct rag_index {
   int dim = 0;
+  bool diagnostic = false;   // counted in ragmi::diagnostic_handles() (common_host.hpp)
   int device = 0;
   int64_t cap_rows = 0;   // multiple of 16
   int64_t count = 0;
@@ -323,16 +324,9 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
       // ring loads non-temporal (the corpus is read once per pass): 50M x 1024, B = 128
       // 70.3% -> 71.2% of the HBM roofline, loads-only 80.1% -> 85.8%
       // (profiles/r01h_wide_nt.jsonl). The diagnostic variants run only via rag_bench_scan.
-      // RAGMI_WIDE_HALF=1 (diagnostic A/B, round 4): the half-tile ring (MODE 5)
-      static ragmi::Knob k_half("RAGMI_WIDE_HALF");
-      if (k_half.get(0) == 1)
-        launch_fixed<kWideBlock>(scan_wide_kernel<D, 5, true>, dim3(grid), 0, st, h->corpus,
-                                 w.qfrag, (int)h->count, (int)n_tiles, w.seed, w.part_s,
-                                 w.part_i, w.heads_s, w.heads_i, w.heads_n, groups);
-      else
-        launch_fixed<kWideBlock>(scan_wide_kernel<D, 0, true>, dim3(grid), 0, st, h->corpus,
-                                 w.qfrag, (int)h->count, (int)n_tiles, w.seed, w.part_s,
-                                 w.part_i, w.heads_s, w.heads_i, w.heads_n, groups);
+      launch_fixed<kWideBlock>(scan_wide_kernel<D, 0, true>, dim3(grid), 0, st, h->corpus,
+                               w.qfrag, (int)h->count, (int)n_tiles, w.seed, w.part_s,
+                               w.part_i, w.heads_s, w.heads_i, w.heads_n, groups);
     } else if (groups == 1) {
       if (filt)
         launch_fixed<kLdsBlock>(scan_lds_kernel<D, true, true>, g3, 0, st, RAG_SCAN_ARGS, groups,
@@ -837,7 +831,10 @@ int rag_index_create_ex(int dim, int64_t capacity_rows, int device, int storage,
       return ragmi::fail(RAG_ENOMEM, "workspace allocation failed");
     }
   }
-  if (diag) ragmi::diagnostics_on().store(true);
+  if (diag) {
+    h->diagnostic = true;
+    ragmi::diagnostic_acquire();
+  }
   *out = h;
   return RAG_OK;
 }
@@ -851,6 +848,7 @@ int rag_knob_probe(const char* name, int dflt) {
 int rag_index_destroy(rag_index_t* h) {
   ragmi::clear_error();
   if (!h) return RAG_OK;
+  if (h->diagnostic) ragmi::diagnostic_release();
   (void)hipSetDevice(h->device);
   (void)hipDeviceSynchronize();
   for (auto& w : h->ws) {

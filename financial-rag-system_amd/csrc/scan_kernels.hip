@@ -1215,8 +1215,8 @@ constexpr int kWidePre = 8;   // tile-fragment LDS reads in flight ahead of the 
 // MODE (diagnostic timing variants, rag_bench_scan at dim 1024): 0 production; 1 no top-k (MFMA + a
 // running max); 2 loads and barriers only; 3 production with an infinite threshold (the
 // per-tile check runs, no candidate is ever taken: results invalid); 4 loads, barriers and
-// the tile-fragment LDS reads, no MFMA; 5 production results through a half-tile ring (A/B,
-// RAGMI_WIDE_HALF). NT: ring loads with the non-temporal policy.
+// the tile-fragment LDS reads, no MFMA (round 4's half-tile ring, MODE 5, was measured no faster
+// and removed in round 5). NT: ring loads with the non-temporal policy.
 template <int D, int MODE = 0, bool NT = false>
 __global__ __launch_bounds__(kWideBlock, 1) void scan_wide_kernel(
     const half8* __restrict__ corpus, const half8* __restrict__ qfrag, int n_rows, int n_tiles,
@@ -1276,68 +1276,6 @@ __global__ __launch_bounds__(kWideBlock, 1) void scan_wide_kernel(
       }
     }
   };
-  if constexpr (MODE == 5) {
-    // Half-tile ring (round 4, A/B): 8 slots of 16 KB (k-steps 16u .. 16u + 15 of a tile),
-    // 7 in flight (112 KB instead of 96), one barrier per half; a tile's accumulator carries
-    // across its two halves, so the MFMA order and every score are those of MODE 0.
-    constexpr int HB = 8, HS = S / 2;                            // slots, k-steps per half
-    static_assert(S % 2 == 0 && HS % 8 == 0, "half tiles of whole wave slices");
-    const int n_half = 2 * n_mine;
-    auto issue_h = [&](int jh) {   // this wave's 2 KB of half jh -> slot jh % 8
-      if (jh < n_half) {
-        const int t = b + (jh >> 1) * nb, u = jh & 1;
-        const char* src = cbase + (int64_t)t * (S * 1024) + (u * HS + wid_u * (HS / 8)) * 1024 +
-                          lane * 16;
-        const uint32_t dst = ring_addr + (jh % HB) * (HS * 1024) + wid_u * (HS / 8) * 1024;
-#pragma unroll
-        for (int i = 0; i < HS / 8; ++i) glds16_nt(src + i * 1024, dst + i * 1024);
-      }
-    };
-#pragma unroll
-    for (int p = 0; p < HB - 1; ++p) issue_h(p);
-    // one tile per iteration, its two halves unrolled (compile-time query-fragment offsets)
-    for (int j = 0; j < n_mine; ++j) {
-      floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-      auto half_step = [&](auto uc) __attribute__((always_inline)) {
-        constexpr int U = decltype(uc)::value;
-        const int jh = 2 * j + U;
-        const int later = min(HB - 2, n_half - 1 - jh);          // halves issued after jh
-        switch (later) {                                         // HS / 8 DMAs per half
-          case 6: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-          case 5: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-          case 4: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-          case 3: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-          case 2: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-          case 1: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-          default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-        }
-        __builtin_amdgcn_s_barrier();   // half jh landed for all; everyone is past half jh-1
-        asm volatile("" ::: "memory");
-        issue_h(jh + HB - 1);           // slot (jh+7)%8 == (jh-1)%8
-        if (active) {
-          const half8* tb = ring + (jh % HB) * (HS * 64) + lane;
-          half8 a[HS];
-#pragma unroll
-          for (int s = 0; s < HS; ++s) a[s] = tb[s * 64];
-#pragma unroll
-          for (int s = 0; s < HS; ++s)
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[s], qf[U * HS + s], acc, 0, 0, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, kWidePre, 0);    // DS reads
-#pragma unroll
-          for (int s = 0; s < HS - kWidePre; ++s) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);         // one MFMA
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);         // one DS read
-          }
-          __builtin_amdgcn_sched_group_barrier(0x008, kWidePre, 0);
-        }
-      };
-      half_step(std::integral_constant<int, 0>{});
-      half_step(std::integral_constant<int, 1>{});
-      if (active) wtopk_tile(st, acc, b + j * nb, n_rows, lane);
-    }
-    if (active) wtopk_finish(st, lane, qt, b, nw, part_s, part_i, heads_s, heads_i, heads_n);
-    return;
-  }
   issue(0);
   issue(1);
   issue(2);

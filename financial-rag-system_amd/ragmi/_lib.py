@@ -179,10 +179,6 @@ BERT_API = {
     "rag_bert_gemm_dl": (ctypes.c_int, [ctypes.c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                         c_vp, c_vp, ctypes.c_float, ctypes.c_int, ctypes.c_int,
                                         ctypes.c_int, c_vp, c_vp, c_vp, c_vp]),
-    "rag_bert_gemm_add_ln_probe": (ctypes.c_int, [ctypes.c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
-                                                  c_vp, c_vp, ctypes.c_float, ctypes.c_int,
-                                                  ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_vp,
-                                                  c_vp]),
     "rag_bert_attention": (ctypes.c_int, [ctypes.c_int, c_vp, c_vp, c_vp, ctypes.c_int,
                                           ctypes.c_int, c_vp, c_vp, c_vp]),
 }

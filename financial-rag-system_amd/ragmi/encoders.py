@@ -163,7 +163,9 @@ def st_head_from_dir(model_dir: str) -> int:
 
 
 # ------------------------------------------------------------------ one encoder GEMM
-GEMM_AUTO, GEMM_TILE, GEMM_PIPE, GEMM_SMALL = 0, 1, 2, 5   # rag_bert_gemm variants (ragmi_bert.h)
+# rag_bert_gemm variants (ragmi_bert.h): production forms, then the WS timing probes
+GEMM_AUTO, GEMM_TILE, GEMM_SMALL, GEMM_WS = 0, 1, 5, 19
+GEMM_WS_MFMA_ONLY, GEMM_WS_NO_STORE, GEMM_WS_DMA_ONLY = 20, 21, 22
 EPI_F16, EPI_GELU_F16, EPI_F32 = 0, 1, 2            # epilogues
 
 

@@ -110,45 +110,20 @@ int rag_build_pairs(const int32_t* q_ids, const int32_t* q_cu, int B, const int6
  * BertSelfAttention/BertIntermediate/BertOutput), device pointers, async on `stream`.
  * A, W fp16 row-major; A_lo/W_lo the fp16x3 residual planes (both NULL = plain fp16).
  * epilogue: RAG_EPI_F16 (C fp16 [+ C_lo]), RAG_EPI_GELU_F16 (erf-GELU, fp16 [+ C_lo]),
- * RAG_EPI_F32 (C fp32). variant: RAG_GEMM_AUTO (what the forward uses), _TILE, _PIPE, _SMALL,
- * _WIDE (_PIPE at 256x256 (N % 256 == 0) or 256x192 (N % 192 == 0, fp16) tiles),
- * _SMALL_BK64 (_SMALL with 64-wide K steps in fp16x3; = _SMALL in fp16);
- * _BIG / _BIG128 register-blocked PIPE shapes (diagnostic); _PROBE_* are timing probes of the
- * PIPE kernel, fp16 or fp16x3, with parts removed (results meaningless): its MFMAs / its loads /
- * its loads and barriers / its epilogue stores / loads and stores (_MFMA_ONLY) / MFMAs and
- * stores (_DMA_ONLY). _WS: PIPE's tiles with the DMAs on 4 loader waves beside the 8 MFMA
- * waves; _WS_NT the same with non-temporal output stores; _WS_* probes as the PIPE ones, and
- * _WS_L2_STORE with every tile stored over the first row band (L2-resident writes);
- * _WS_NOROT rotated-K-order-off A/B; _WS_READS_FIRST the MFMA waves' previous fragment order
- * (all reads of a K step before its MFMAs) for A/B against the interleaved one. _WS_BIG128
- * (round 4, A/B): the WS ring with 4 MFMA waves of 128 x 64 (one per SIMD beside its loader
- * wave, 256 registers each) instead of 8 of 64 x 64. _WS_PROBE_HI_ONLY / _WS_PROBE_FP8_CORR
- * (round 4 timing probes, fp16x3 only, results meaningless): the hi x hi MFMA alone; hi x hi
- * plus one block-scaled fp8 16x16x128 MFMA per 2 K steps standing in for the two corrections.
- * _WS_REGSTAGE (A/B): the loader waves stage through registers (buffer_load to VGPRs, then
- * ds_write_b128) instead of LDS-DMA; _WS_REGSTAGE_INTAKE its loads alone (timing probe).
- * _WS_L2PF (A/B): the loader waves also touch the A panel's lines 6 K steps ahead (one 4-B
- * LDS-DMA per lane and stage into a sink: an L2 prefetch); _WS_L2PF_INTAKE its loads alone.
- * N % 128 == 0, K % 64 == 0 (PIPE/SMALL also N <= 4096). */
+ * RAG_EPI_F32 (C fp32). variant: RAG_GEMM_AUTO (what the forward uses: SMALL for query
+ * batches, WS once its 256x128 tiles reach half the CUs, TILE in between), _TILE (128x128
+ * tiles, 2 workgroups per CU), _SMALL (64x64 tiles, the K panel in flight), _WS (persistent
+ * 256x128 tiles, 4 loader waves feeding 8 MFMA waves through an LDS-DMA ring).
+ * Timing probes of _WS (results meaningless; scripts/bench_gemm.py): _WS_NO_STORE (the
+ * epilogue without its stores), _WS_MFMA_ONLY (no DMAs, no stores), _WS_DMA_ONLY (the DMA
+ * ring alone). The round 1-5 A/B forms (PIPE, WIDE, BIG, SMALL_BK64, WS_BIG128, the ping-pong
+ * GEMM, ...) were removed in round 5; their ids stay unassigned and are refused.
+ * N % 128 == 0, K % 64 == 0 (SMALL / WS also N <= 4096). */
 enum { RAG_EPI_F16 = 0, RAG_EPI_GELU_F16 = 1, RAG_EPI_F32 = 2 };
 /* deferred-LayerNorm epilogues (rag_bert_gemm_dl) */
 enum { RAG_EPI_LN_F16 = 4, RAG_EPI_LN_GELU_F16 = 5, RAG_EPI_RES_LN = 6 };
-enum { RAG_GEMM_AUTO = 0, RAG_GEMM_TILE = 1, RAG_GEMM_PIPE = 2, RAG_GEMM_PROBE_NO_MFMA = 3,
-       RAG_GEMM_PROBE_NO_DMA = 4, RAG_GEMM_SMALL = 5, RAG_GEMM_WIDE = 8,
-       RAG_GEMM_PROBE_NO_SYNC = 9, RAG_GEMM_SMALL_BK64 = 10, RAG_GEMM_BIG = 11,
-       RAG_GEMM_BIG128 = 12, RAG_GEMM_PROBE_NO_STORE = 13, RAG_GEMM_PROBE_MFMA_ONLY = 14,
-       RAG_GEMM_PROBE_DMA_ONLY = 15, RAG_GEMM_WS = 19, RAG_GEMM_WS_MFMA_ONLY = 20,
-       RAG_GEMM_WS_NO_STORE = 21, RAG_GEMM_WS_DMA_ONLY = 22, RAG_GEMM_WS_L2_STORE = 23,
-       RAG_GEMM_WS_NT = 24, RAG_GEMM_WS_NOROT = 26, RAG_GEMM_WS_READS_FIRST = 27,
-       RAG_GEMM_WS_PROBE_NO_A_READS = 28, RAG_GEMM_WS_PROBE_NO_W_READS = 29,
-       RAG_GEMM_WS_PRIO_LOAD = 30, RAG_GEMM_WS_PRIO_MFMA = 31, RAG_GEMM_WS_FLAGS = 32,
-       RAG_GEMM_WS_NOHALF = 33, RAG_GEMM_WS_SMALL = 34, RAG_GEMM_WS_BIG128 = 35,
-       RAG_GEMM_WS_BIG128_MFMA_ONLY = 36, RAG_GEMM_WS_BIG128_DMA_ONLY = 37,
-       RAG_GEMM_WS_BIG128_NO_STORE = 38, RAG_GEMM_WS_PROBE_HI_ONLY = 39,
-       RAG_GEMM_WS_PROBE_FP8_CORR = 40, RAG_GEMM_WS_REGSTAGE = 41,
-       RAG_GEMM_WS_REGSTAGE_INTAKE = 42, RAG_GEMM_WS_L2PF = 43, RAG_GEMM_WS_L2PF_INTAKE = 44,
-       RAG_GEMM_PP = 45, RAG_GEMM_PP_MFMA_ONLY = 46, RAG_GEMM_PP_DMA_ONLY = 47,
-       RAG_GEMM_PP_NO_STORE = 48, RAG_GEMM_PP_PRIO = 49 };
+enum { RAG_GEMM_AUTO = 0, RAG_GEMM_TILE = 1, RAG_GEMM_SMALL = 5, RAG_GEMM_WS = 19,
+       RAG_GEMM_WS_MFMA_ONLY = 20, RAG_GEMM_WS_NO_STORE = 21, RAG_GEMM_WS_DMA_ONLY = 22 };
 int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, const void* W,
                   const void* W_lo, const float* bias, int M, int N, int K, void* C,
                   void* C_lo, void* stream);
@@ -156,7 +131,7 @@ int rag_bert_gemm(int variant, int epilogue, const void* A, const void* A_lo, co
 /* Diagnostic (parity tests, GEMM benchmark): the fp32-output GEMM with the split-K the forward
  * uses for small token batches — C holds max_parts x [M][N] floats and receives `*parts`
  * partial products (part 0 carries the bias) whose sum is A . W^T + bias; the forward sums
- * them in order inside its residual + LayerNorm pass. variant: AUTO, SMALL or SMALL_BK64
+ * them in order inside its residual + LayerNorm pass. variant: AUTO or SMALL
  * (AUTO outside the small-batch regime writes one part). */
 int rag_bert_gemm_splitk(int variant, const void* A, const void* A_lo, const void* W,
                          const void* W_lo, const float* bias, int M, int N, int K, float* C,
@@ -181,14 +156,6 @@ int rag_bert_gemm_add_ln(const void* A, const void* A_lo, const void* W, const v
  * forward runs. For A/B timing and parity tests. */
 int rag_bert_attention(int variant, const void* qkv, const void* qkv_lo, const int32_t* cu,
                        int B, int max_len, void* ctx, void* ctx_lo, void* stream);
-
-/* Diagnostic (tests only): rag_bert_gemm_add_ln with the fp16 copy stored by the plain
- * epilogue's paired 16-B stores — probe 4 with the ring's post-epilogue vmcnt budget counting
- * them, probe 5 with it counting the production 8-B stores (too many: the wait passes early). */
-int rag_bert_gemm_add_ln_probe(int probe, const void* A, const void* A_lo, const void* W,
-                               const void* W_lo, const float* bias, const float* gamma,
-                               const float* beta, float eps, int M, int N, int K, float* x,
-                               void* xh, void* xl, void* stream);
 
 /* forward's use of rag_bert_gemm_add_ln: -1 auto (default; env RAGMI_FUSE_LN overrides at
  * create), 0 never (separate GEMM + add-LayerNorm kernels), 1 always where the shape allows */

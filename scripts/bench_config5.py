@@ -98,6 +98,8 @@ def main():
     ap.add_argument("--rows", type=int, default=50_000_000)
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--no-recall", action="store_true")
+    ap.add_argument("--diagnostic", action="store_true",
+                    help="create the index with RAG_CREATE_DIAGNOSTIC (RAGMI_* A/B knobs honoured)")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -110,7 +112,7 @@ def main():
     from ragmi.dist import ShardedIndex
 
     n = args.rows
-    sh = ShardedIndex(n, dim=D, device=dev, diagnostic=True)
+    sh = ShardedIndex(n, dim=D, device=dev, diagnostic=args.diagnostic)
     idx, lo, hi = sh.local, sh.lo, sh.hi
     t_build = time.perf_counter()
     build_shard(idx, lo, hi, n, dev)
@@ -177,6 +179,8 @@ def main():
                          "avg_ms": round(scan_avg, 4),
                          "algorithmic_bytes_per_launch": algo},
             "build_s": round(t_build, 2),
+            "diagnostic_knobs": ({k: v for k, v in os.environ.items() if k.startswith("RAGMI_")}
+                                 if args.diagnostic else None),
         }), flush=True)
     idx.close()
     if world > 1:

@@ -19,20 +19,8 @@ sys.path.insert(0, os.path.join(ROOT, "financial-rag-system_amd"))
 from ragmi.encoders import EPI_F16, EPI_F32, EPI_GELU_F16, linear  # noqa: E402
 
 PEAK = 2.5e15
-VNAME = {0: "auto", 1: "tile", 2: "pipe", 3: "probe_no_mfma", 4: "probe_no_dma", 5: "small",
-         8: "wide", 9: "probe_no_sync", 10: "small_bk64", 11: "big", 12: "big128",
-         13: "probe_no_store", 14: "probe_mfma_only", 15: "probe_dma_only",
-         19: "ws", 20: "ws_mfma_only",
-         21: "ws_no_store", 22: "ws_dma_only", 23: "ws_l2_store", 24: "ws_nt", 26: "ws_norot",
-         27: "ws_readsfirst",
-         28: "ws_probe_no_a_reads", 29: "ws_probe_no_w_reads", 30: "ws_prio_load",
-         31: "ws_prio_mfma", 32: "ws_flags",
-         33: "ws_nohalf", 34: "ws_small", 35: "ws_big128",
-         36: "ws_big128_mfma_only", 37: "ws_big128_dma_only", 38: "ws_big128_no_store",
-         39: "ws_probe_hi_only", 40: "ws_probe_fp8_corr", 41: "ws_regstage",
-         42: "ws_regstage_intake", 43: "ws_l2pf", 44: "ws_l2pf_intake",
-         45: "pp", 46: "pp_mfma_only", 47: "pp_dma_only",
-         48: "pp_no_store", 49: "pp_wb_stores"}
+VNAME = {0: "auto", 1: "tile", 5: "small", 19: "ws", 20: "ws_mfma_only", 21: "ws_no_store",
+         22: "ws_dma_only"}
 LAYERS = {
     "small": [("qkv", 1152, 384, EPI_F16), ("o", 384, 384, EPI_F32),
               ("ffn1", 1536, 384, EPI_GELU_F16), ("ffn2", 384, 1536, EPI_F32)],
@@ -62,10 +50,10 @@ def timeit(fn, reps=20):
 
 def main():
     Ms = [int(x) for x in os.environ.get("GEMM_M", "117000,14800,782").split(",")]
-    variants = [int(x) for x in os.environ.get("GEMM_VARIANTS", "1,2").split(",")]
+    variants = [int(x) for x in os.environ.get("GEMM_VARIANTS", "1,19").split(",")]
     for M in Ms:
         for prec in os.environ.get("GEMM_PRECS", "fp16,fp16x3").split(","):
-            vs = [v for v in variants if prec == "fp16x3" or v < 45]   # PP: fp16x3 only
+            vs = list(variants)
             tot = {v: 0.0 for v in vs}
             for name, N, K, epi in LAYERS[os.environ.get("GEMM_LAYER", "small")]:
                 g = torch.Generator(device="cuda")

@@ -104,6 +104,17 @@ def planted_queries(nb, batch, n, dim, seed0, dev, qseed):
     return qs, picks
 
 
+def _diag(args) -> bool:
+    """--diagnostic (bench.py): handles created with RAG_CREATE_DIAGNOSTIC, so the RAGMI_*
+    A/B knobs are honoured; off by default (a measurement line is the production path)."""
+    return bool(getattr(args, "diagnostic", False))
+
+
+def _knobs(args):
+    return ({k: v for k, v in os.environ.items() if k.startswith("RAGMI_")}
+            if _diag(args) else None)
+
+
 def _line(metric, value, unit, args, elapsed, world, dtype, data, config, **extra):
     d = {"metric": metric, "value": round(value, 3), "unit": unit, "n_gpus": world,
          "steps": args.steps, "warmup": args.warmup,
@@ -111,7 +122,8 @@ def _line(metric, value, unit, args, elapsed, world, dtype, data, config, **extr
          "scaling": "strong" if config.get("corpus_rows") else "weak", "vs_baseline": None,
          "dtype": dtype, "data": data, "config": config,
          "backend": dist.get_backend() if dist.is_initialized() else None,
-         "ranks_seen": dist.get_world_size() if dist.is_initialized() else 1}
+         "ranks_seen": dist.get_world_size() if dist.is_initialized() else 1,
+         "diagnostic_knobs": _knobs(args)}
     d.update(extra)
     return d
 
@@ -220,7 +232,7 @@ def run_pipeline(args, cfg_id):
     torch.cuda.set_device(dev)
     _init_dist(dev)
     n, D, prec = args.rows or 1_000_000, 384, args.precision
-    idx = FlatIndex(dim=D, capacity=n, device=dev, diagnostic=True)
+    idx = FlatIndex(dim=D, capacity=n, device=dev, diagnostic=_diag(args))
     build_shard(idx, 0, n, n, D, 1000, dev)
     g = torch.Generator(device=dev)
     g.manual_seed(77)
@@ -250,8 +262,8 @@ def run_pipeline(args, cfg_id):
     tok_ms = (time.perf_counter() - t_tok) / min(20, len(texts)) * 1e3
     q_lens = np.concatenate([np.diff(b[2]) for b in batches])
     bge_w, ce_w = R.make_weights(R.BGE_SMALL, 1), R.make_weights(R.MINILM_CE, 2)
-    bge = BertEncoder(R.BGE_SMALL, bge_w, HEAD_CLS_L2, dev, prec, diagnostic=True)
-    ce = BertEncoder(R.MINILM_CE, ce_w, HEAD_POOLER_CLS, dev, prec, diagnostic=True)
+    bge = BertEncoder(R.BGE_SMALL, bge_w, HEAD_CLS_L2, dev, prec, diagnostic=_diag(args))
+    ce = BertEncoder(R.MINILM_CE, ce_w, HEAD_POOLER_CLS, dev, prec, diagnostic=_diag(args))
     # batches in flight: config 2 four, config 3 three. Round 3 measured config 2 at 2 / 3 / 4
     # in flight 60.7K / 71.1K / 60.4K qps (profiles/r03b_small_gemm.jsonl); on the round-4
     # build (graphs captured on a private stream) 4 beat 3 in four of four pairs (70.5-72.8K
@@ -607,7 +619,7 @@ def run_search(args, mode):
     def tags_fn(rows):            # ticker code 1..16 per global row (PayloadTags code space)
         return ((rows * 2654435761) % (1 << 32) // 7 % n_tick + 1).astype(np.uint32)
 
-    sh = ShardedIndex(n, dim=D, device=dev, diagnostic=True)
+    sh = ShardedIndex(n, dim=D, device=dev, diagnostic=_diag(args))
     idx, lo, hi = sh.local, sh.lo, sh.hi
     t_b = time.perf_counter()
     build_shard(idx, lo, hi, n, D, seed0, dev, tags_fn if mode == "filtered" else None)

@@ -8,7 +8,7 @@ out=${OUT:-gpurun_out/sweep.jsonl}
 : > $out
 for rep in $(seq 1 ${REPS:-2}); do
   for v in $VALS; do
-    env $VAR=$v timeout -k 10 ${TMO:-300} python3 -u bench.py $ARGS > gpurun_out/sweep_one.log 2> gpurun_out/sweep.err \
+    env $VAR=$v timeout -k 10 ${TMO:-300} python3 -u bench.py --diagnostic $ARGS > gpurun_out/sweep_one.log 2> gpurun_out/sweep.err \
       || { rc=$?; tail -20 gpurun_out/sweep.err; exit $rc; }
     grep '^{' gpurun_out/sweep_one.log | sed "s/^{/{\"$VAR\": \"$v\", \"rep\": $rep, /" >> $out
     python3 -c "

@@ -1,0 +1,85 @@
+"""The library's diagnostic surface is the short documented list: the GEMM
+variant ids include/ragmi_bert.h exports, and the RAGMI_* A/B knobs the product sources read
+(all through ragmi::Knob, honoured only for RAG_CREATE_DIAGNOSTIC handles). The lists below
+are the ones DESIGN.md "Diagnostic surface" documents; a new variant or knob must be added
+there and here, a measured loser removed from both. CPU only: parses the header and sources,
+and calls rag_bert_gemm with removed ids (refused during argument checks, before any HIP call).
+"""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "financial-rag-system_amd", "csrc")
+
+# rag_bert_gemm variants: production forms, then the WS kernel's three timing probes
+GEMM_VARIANTS = {"RAG_GEMM_AUTO": 0, "RAG_GEMM_TILE": 1, "RAG_GEMM_SMALL": 5, "RAG_GEMM_WS": 19,
+                 "RAG_GEMM_WS_MFMA_ONLY": 20, "RAG_GEMM_WS_NO_STORE": 21,
+                 "RAG_GEMM_WS_DMA_ONLY": 22}
+# RAGMI_* knobs: index (scan grid sizes, fused query prep) and encoder (GEMM pick, split-K,
+# deferred / fused LayerNorm, graph replay, CLS-only last layer)
+KNOBS = {"RAGMI_SCAN_WGS", "RAGMI_RESCAN_WG", "RAGMI_SAMPLE_DIV", "RAGMI_WIDE_WGS",
+         "RAGMI_FUSED_PREP", "RAGMI_GEMM", "RAGMI_KSPLIT", "RAGMI_DEFER_LN", "RAGMI_FUSE_LN",
+         "RAGMI_ENC_GRAPH", "RAGMI_CLS_ATTN"}
+# removed in round 5 (measured losers / retired probes): must not come back silently
+REMOVED_KNOBS = {"RAGMI_WS_PHASE", "RAGMI_WS_BIG128", "RAGMI_GEMM_PP", "RAGMI_PP_STAGGER",
+                 "RAGMI_DL_SMALL", "RAGMI_CE_ROWS", "RAGMI_ATTN_VAR", "RAGMI_SMALL_BK",
+                 "RAGMI_SMALL_WIDE", "RAGMI_SMALL_WS", "RAGMI_WIDE_HALF", "RAGMI_ADDLN_VEC",
+                 "RAGMI_RESIDUAL_F32"}
+REMOVED_IDS = [2, 3, 4, 8, 9, 10, 11, 12, 13, 14, 15] + list(range(23, 50))
+
+
+@pytest.fixture(scope="module")
+def libpath():
+    from ragmi import _build
+    return _build.build()
+
+
+def _src(name):
+    return open(os.path.join(CSRC, name)).read()
+
+
+def test_exported_gemm_variants_are_the_documented_list():
+    hdr = open(os.path.join(ROOT, "include", "ragmi_bert.h")).read()
+    ids = {m.group(1): int(m.group(2))
+           for m in re.finditer(r"\b(RAG_GEMM_[A-Z0-9_]+)\s*=\s*(\d+)", hdr)}
+    assert ids == GEMM_VARIANTS
+
+
+def test_knobs_read_by_the_sources_are_the_documented_list():
+    found = set()
+    for f in os.listdir(CSRC):
+        if f.endswith((".hip", ".hpp", ".cpp")):
+            found |= set(re.findall(r'Knob\s+\w+\("(RAGMI_[A-Z0-9_]+)"\)', _src(f)))
+    assert found == KNOBS
+    text = "".join(_src(f) for f in os.listdir(CSRC) if f.endswith((".hip", ".hpp", ".cpp")))
+    for k in REMOVED_KNOBS:
+        assert f'"{k}"' not in text, k
+
+
+def test_design_documents_the_surface():
+    design = open(os.path.join(ROOT, "DESIGN.md")).read()
+    sec = design[design.index("### Diagnostic surface"):]
+    sec = sec[:sec.index("\n## ", 1)] if "\n## " in sec[1:] else sec
+    for k in KNOBS | set(GEMM_VARIANTS):
+        assert k in sec, f"{k} not documented in DESIGN.md 'Diagnostic surface'"
+
+
+def test_removed_variant_ids_are_refused(libpath):
+    L = ctypes.CDLL(libpath)
+    L.rag_bert_gemm.restype = ctypes.c_int
+    L.rag_bert_gemm.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 5 + \
+        [ctypes.c_int] * 3 + [ctypes.c_void_p] * 3
+    fake = ctypes.c_void_p(16)          # never dereferenced: refused before any launch
+    for v in REMOVED_IDS:
+        rc = L.rag_bert_gemm(v, 2, fake, None, fake, None, fake, 64, 128, 128, fake, None, None)
+        assert rc != 0, f"variant {v} accepted"
+
+
+@pytest.mark.parametrize("v", sorted(GEMM_VARIANTS.values()))
+def test_python_constants_match(v):
+    from ragmi import encoders as E
+    names = {n: getattr(E, n) for n in dir(E) if n.startswith("GEMM_")}
+    assert v in names.values()
