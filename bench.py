@@ -326,6 +326,11 @@ def main():
                          "A/B knobs are honoured (never for a reported line)")
     ap.add_argument("--precision", choices=["fp16x3", "fp16"], default="fp16x3",
                     help="encoder precision for --config 2/3 (fp16x3 = the 1e-3 contract)")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="default line without the config-2 / config-3 legs (profiling runs: "
+                         "their 1M-row scans share the headline scan kernel's name)")
+    ap.add_argument("--config-steps", type=int, default=50,
+                    help="timed batches of each config-2 / config-3 leg (warmup 5)")
     args = ap.parse_args()
     world = check_world(args.gpus)
     if world > 1 and "WORLD_SIZE" not in os.environ:
@@ -565,10 +570,44 @@ def main():
                          "standalone_frac": round(algo_bytes / (alone_ms * 1e-3) / HBM_PEAK, 4)},
             "cpu_baseline": cpu,
         }
-        print(json.dumps(line), flush=True)
     idx.close()
     if world > 1 or rehearsal:
         dist.destroy_process_group()
+    if rank == 0:
+        # the default run also measures the end-to-end configs 2 and 3
+        # (BASELINE configs[1] / [2]: encode + search (+ CE rerank) of 32 query strings over
+        # 1M x 384) after the headline's timed region, each with its own parity legs,
+        # rooflines and CPU baseline, as extra keys; value / ms_per_step stay the headline's.
+        # N = 1 only (at N > 1 every rank would run its own replica of them).
+        legs_on = world == 1 and not rehearsal and not args.no_configs
+        for cfg in ("2", "3"):
+            line[f"config{cfg}"] = (_config_leg(args, cfg) if legs_on else
+                                    {"skipped": "--no-configs" if args.no_configs else
+                                     "N > 1 (measured by the N = 1 run)"})
+        print(json.dumps(line), flush=True)
+
+
+def _config_leg(args, cfg: str) -> dict:
+    """One config-2 / config-3 measurement (scripts/bench_modes.run_pipeline) as a dict of the
+    keys a reader compares: qps, ms per batch, the certified parity legs, rooflines, the CPU
+    baseline. Runs after the headline's index is freed."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import bench_modes
+    a = argparse.Namespace(**vars(args))
+    a.config, a.rows, a.streams = cfg, 0, 0
+    a.steps, a.warmup = args.config_steps, 5
+    print(f"bench.py: headline done; config {cfg} leg ({a.steps} batches)", file=sys.stderr,
+          flush=True)
+    t0 = time.perf_counter()
+    full = bench_modes.run_pipeline(a, int(cfg), emit=False)
+    keep = ("metric", "value", "unit", "ms_per_step", "steps", "warmup", "dtype", "config",
+            "search_top15_exact_queries", "encode_max_abs_diff_vs_oracle",
+            "rerank_max_abs_diff_vs_oracle", "rerank_checked_queries",
+            "rerank_top5_order_matches", "checked_timed_batches", "roofline", "roofline_search",
+            "cpu_baseline", "id_input_qps", "text_vs_id_input")
+    leg = {k: full[k] for k in keep if k in full}
+    leg["wall_s"] = round(time.perf_counter() - t0, 1)
+    return leg
 
 
 if __name__ == "__main__":

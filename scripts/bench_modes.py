@@ -222,7 +222,8 @@ def _cpu_pipeline_baseline(cfg_id, budget_s, corpus16_sample, n_total, R, bge_w,
                         f"({t_ce * 1e3:.0f} ms/batch)" if cfg_id == 3 else ""))}
 
 
-def run_pipeline(args, cfg_id):
+def run_pipeline(args, cfg_id, emit=True):
+    """Config 2 / 3 line; rank 0 returns the line dict (and prints it when `emit`)."""
     from ragmi import synth as R          # model shapes, seeded weights (product-side data)
     from ragmi.encoders import HEAD_CLS_L2, HEAD_POOLER_CLS, BertEncoder
     from ragmi.index import FlatIndex
@@ -536,10 +537,14 @@ def run_pipeline(args, cfg_id):
             id_input_qps=round(B * args.steps / elapsed_ids * world, 3),
             text_vs_id_input=round(elapsed_ids / elapsed, 4), **extra)
         line["scaling"] = "weak"
-        print(json.dumps(line), flush=True)
+        if emit:
+            print(json.dumps(line), flush=True)
+    else:
+        line = None
     idx.close()
     if world > 1:
         dist.destroy_process_group()
+    return line
 
 
 # ---------------------------------------------------------------------------- search configs

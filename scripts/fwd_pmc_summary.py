@@ -15,9 +15,54 @@ import sys
 H, FF, NL = 384, 1536, 6
 
 
+def mfma_busy(d, T):
+    """MFMA-busy pass (SQ_VALU_MFMA_BUSY_CYCLES, SQ_BUSY_CYCLES, GRBM_GUI_ACTIVE): per forward
+    GEMM, the busy cycles against (a) the MFMA count the GEMM issues x 16 cycles per
+    16x16x32 MFMA (MI355X_MICROARCH.md price list: the counter's own scale) and (b) the
+    dispatch's cycles x 1024 SIMDs (GRBM_GUI_ACTIVE / 8 XCDs = the dispatch's clock cycles)."""
+    f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
+    disp = collections.OrderedDict()
+    for r in csv.DictReader(open(f)):
+        k = int(r["Dispatch_Id"])
+        e = disp.setdefault(k, {"name": r["Kernel_Name"]})
+        e[r["Counter_Name"]] = e.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    shapes = {"qkv": (3 * H, H), "o_proj": (H, H), "ffn1": (FF, H), "ffn2": (H, FF)}
+    res = collections.defaultdict(list)
+    n6 = 0
+    for e in disp.values():
+        name = e["name"]
+        if "gemm_ws_kernel" not in name:
+            continue
+        epi = name.split("gemm_ws_kernelILi")[1].split("E")[0]
+        key = {"0": "qkv", "4": "qkv", "5": "ffn1"}.get(epi)
+        if epi == "6":
+            key = "o_proj" if n6 % 2 == 0 else "ffn2"
+            n6 += 1
+        if key is None:
+            continue
+        res[key].append(e)
+    out = {"counter": "SQ_VALU_MFMA_BUSY_CYCLES", "tokens": T,
+           "note": "per GEMM (median launch): busy / (MFMAs issued x 16) is the counter's scale "
+                   "check; busy / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs) the MFMA-busy fraction"}
+    for key, es in res.items():
+        N, K = shapes[key]
+        n_mfma = 3 * T * N * K / (16 * 16 * 32)          # fp16x3: three MFMAs per product
+        es = sorted(es, key=lambda e: e.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0))
+        e = es[len(es) // 2]
+        busy = e.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0)
+        cyc = e.get("GRBM_GUI_ACTIVE", 0.0) / 8
+        out[key] = {"launches": len(es), "mfma_busy_cycles": busy,
+                    "sq_busy_cycles": e.get("SQ_BUSY_CYCLES"), "dispatch_cycles": cyc,
+                    "busy_per_mfma": round(busy / n_mfma, 3) if n_mfma else None,
+                    "mfma_busy_frac": round(busy / (cyc * 1024), 4) if cyc else None}
+    print(json.dumps(out))
+
+
 def main():
     d, T = sys.argv[1], int(sys.argv[2])
     ctr = sys.argv[3] if len(sys.argv) > 3 else "FETCH_SIZE"
+    if ctr == "MFMA":
+        return mfma_busy(d, T)
     f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
     disp = collections.OrderedDict()
     for r in csv.DictReader(open(f)):

@@ -16,3 +16,4 @@ done
 T=$(grep '^{' gpurun_out/fpmc_1.log | head -1 | python3 -c "import json,sys; print(json.loads(sys.stdin.readline())['tokens'])")
 python3 scripts/fwd_pmc_summary.py gpurun_out/fpmc_1 $T FETCH_SIZE | tee gpurun_out/fwd_pmc.jsonl
 python3 scripts/fwd_pmc_summary.py gpurun_out/fpmc_2 $T WRITE_SIZE | tee -a gpurun_out/fwd_pmc.jsonl
+python3 scripts/fwd_pmc_summary.py gpurun_out/fpmc_3 $T MFMA | tee -a gpurun_out/fwd_pmc.jsonl

@@ -26,9 +26,7 @@ def _grid(g, shape, den, kmax):
 @pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "x".join(map(str, s)))
 @pytest.mark.parametrize("epi", [0, 2], ids=["f16", "f32"])
 @pytest.mark.parametrize("split", [False, True], ids=["fp16", "fp16x3"])
-@pytest.mark.parametrize("variant", [1, 2, 5, 8, 10, 11, 12, 19, 24, 27, 34, 35, 41, 43],
-                         ids=["tile", "pipe", "small", "wide", "small64", "big", "big128", "ws", "ws_nt",
-                              "ws_reads_first", "ws_small", "ws_big128", "ws_regstage", "ws_l2pf"])
+@pytest.mark.parametrize("variant", [1, 5, 19], ids=["tile", "small", "ws"])
 def test_gemm_epilogue_bit_exact(gpu, shape, epi, split, variant):
     from ragmi.encoders import linear
     M, N, K = shape
@@ -71,9 +69,7 @@ def test_gemm_epilogue_bit_exact(gpu, shape, epi, split, variant):
 
 @pytest.mark.parametrize("shape", [(20000, 1152, 384), (3001, 384, 1536), (777, 1536, 384)],
                          ids=lambda s: "x".join(map(str, s)))
-@pytest.mark.parametrize("variant", [1, 2, 10, 19, 27, 34, 35, 41, 43],
-                         ids=["tile", "pipe", "small64", "ws", "ws_reads_first", "ws_small", "ws_big128",
-                              "ws_regstage", "ws_l2pf"])
+@pytest.mark.parametrize("variant", [1, 5, 19], ids=["tile", "small", "ws"])
 def test_split_planes_match_fp32_epilogue(gpu, shape, variant):
     """Random (non-dyadic) fp16x3 operands: the fp16 epilogue's planes are exactly
     hi = fp16(v), lo = fp16(v - hi) of the fp32 value v the same kernel's fp32 epilogue stores
