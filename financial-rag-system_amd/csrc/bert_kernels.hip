@@ -539,7 +539,12 @@ using PipeLarge = PipeCfg<256, 128, 4, 2, 3>;
 // whole 384-wide rows per tile (bge-small / MiniLM hidden size): the output projections with
 // residual + LayerNorm fused into the epilogue (kEpiAddLn); 2 x 4 waves of 64 x 96
 using PipeRow = PipeCfg<128, 384, 2, 4, 2>;
-template <bool SPLIT> using PipeSmall = PipeCfg<64, 64, 2, 2, SPLIT ? 3 : 4>;
+// (RAGMI_SMALL_NS: ring depth of the fp16x3 query-batch tiles, a build-time A/B of
+// scripts/gpu_build_ab.sh; 3 = two workgroups per CU with 16 KB of staged vectors)
+#ifndef RAGMI_SMALL_NS
+#define RAGMI_SMALL_NS 3
+#endif
+template <bool SPLIT> using PipeSmall = PipeCfg<64, 64, 2, 2, SPLIT ? RAGMI_SMALL_NS : 4>;
 // (Measured and removed in round 5 — numbers in DESIGN.md §R5: 256x256 / 256x192 PIPE tiles,
 // register-blocked BIG / BIG128 shapes, BK-64 and 64x128 query-batch tiles, the one-loader and
 // deferred-LN query-batch WS tiles, and the 256x192 ping-pong kernel.)
@@ -558,19 +563,6 @@ __device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t rs, uint32_t voff,
   asm volatile(
       "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
       "buffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(voff), "s"(rs), "s"(lds_addr), "s"(soff)
-      : "memory");
-}
-
-// 4 B per lane buffer -> LDS DMA into a sink: used only for the line fetch it causes (an L2
-// prefetch that occupies no VGPR; lane l's dword lands at lds_addr + 4 l)
-__device__ __forceinline__ void blds4(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff,
-                                      uint32_t lds_addr) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
-      "buffer_load_dword %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
       : "=&s"(keep)
       : "v"(voff), "s"(rs), "s"(lds_addr), "s"(soff)
       : "memory");

@@ -31,15 +31,21 @@ def needs_build() -> bool:
     return any(os.path.getmtime(f) > t for f in _inputs())
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not needs_build():
+def build(force: bool = False, verbose: bool = False, out: str | None = None,
+          defines: tuple = ()) -> str:
+    """Compile libragmi.so (in-tree unless `out`: an A/B build of the same sources with extra
+    `-D` defines, loaded through RAGMI_LIB_AB)."""
+    lib = out or LIB_PATH
+    if not force and not out and not needs_build():
         return LIB_PATH
     srcs = [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
     objs, procs = [], []
     for src in srcs:                     # translation units compile in parallel
-        obj = os.path.join(CSRC, os.path.basename(src) + ".o")
+        obj = (os.path.join(CSRC, os.path.basename(src) + ".o") if not out else
+               lib + "." + os.path.basename(src) + ".o")
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
-               "-fno-strict-aliasing", "-Wall", "-Wno-unused-function", "-c", src, "-o", obj]
+               "-fno-strict-aliasing", "-Wall", "-Wno-unused-function", *defines, "-c", src,
+               "-o", obj]
         if verbose:
             print(" ".join(cmd))
         procs.append((subprocess.Popen(cmd), cmd))
@@ -47,16 +53,23 @@ def build(force: bool = False, verbose: bool = False) -> str:
     failed = [cmd for p, cmd in procs if p.wait() != 0]
     if failed:
         raise subprocess.CalledProcessError(1, failed[0])
-    tmp = LIB_PATH + ".tmp"
+    tmp = lib + ".tmp"
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)
-    os.replace(tmp, LIB_PATH)
+    os.replace(tmp, lib)
     for o in objs:
         os.remove(o)
-    return LIB_PATH
+    return lib
 
 
 if __name__ == "__main__":
-    print(build(force=True, verbose=True))
+    import sys
+    # python ragmi/_build.py [OUT.so [-DNAME=V ...]]: an A/B build beside the in-tree one
+    if len(sys.argv) > 1:
+        os.makedirs(os.path.dirname(os.path.abspath(sys.argv[1])), exist_ok=True)
+        print(build(force=True, verbose=True, out=os.path.abspath(sys.argv[1]),
+                    defines=tuple(sys.argv[2:])))
+    else:
+        print(build(force=True, verbose=True))
