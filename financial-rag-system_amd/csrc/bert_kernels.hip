@@ -545,6 +545,12 @@ using PipeRow = PipeCfg<128, 384, 2, 4, 2>;
 #define RAGMI_SMALL_NS 3
 #endif
 template <bool SPLIT> using PipeSmall = PipeCfg<64, 64, 2, 2, SPLIT ? RAGMI_SMALL_NS : 4>;
+// the same tiles with a deeper ring (fp16x3, one workgroup per CU: 6 x 16 KB stages + 16 KB of
+// staged vectors) for query-batch GEMMs whose work units fit the CUs in one round
+#ifndef RAGMI_SMALL_DEEP_NS
+#define RAGMI_SMALL_DEEP_NS 6
+#endif
+using PipeSmallDeep = PipeCfg<64, 64, 2, 2, RAGMI_SMALL_DEEP_NS>;
 // (Measured and removed in round 5 — numbers in DESIGN.md §R5: 256x256 / 256x192 PIPE tiles,
 // register-blocked BIG / BIG128 shapes, BK-64 and 64x128 query-batch tiles, the one-loader and
 // deferred-LN query-batch WS tiles, and the 256x192 ping-pong kernel.)
