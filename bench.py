@@ -588,18 +588,27 @@ def main():
 
 
 def _config_leg(args, cfg: str) -> dict:
-    """One config-2 / config-3 measurement (scripts/bench_modes.run_pipeline) as a dict of the
-    keys a reader compares: qps, ms per batch, the certified parity legs, rooflines, the CPU
-    baseline. Runs after the headline's index is freed."""
-    sys.path.insert(0, os.path.join(ROOT, "scripts"))
-    import bench_modes
-    a = argparse.Namespace(**vars(args))
-    a.config, a.rows, a.streams = cfg, 0, 0
-    a.steps, a.warmup = args.config_steps, 5
-    print(f"bench.py: headline done; config {cfg} leg ({a.steps} batches)", file=sys.stderr,
-          flush=True)
+    """One config-2 / config-3 measurement (`bench.py --config 2|3`, scripts/bench_modes.py) as
+    a dict of the keys a reader compares: qps, ms per batch, the certified parity legs,
+    rooflines, the CPU baseline. Run as a child process after the headline's index is freed:
+    the configs' host-side pipelines (tokeniser thread, ~90 launches per batch) measured
+    58.5K qps in-process after the headline's CPU baseline vs 71K standalone."""
+    torch.cuda.empty_cache()
+    cmd = [sys.executable, "-u", os.path.abspath(__file__), "--config", cfg,
+           "--steps", str(args.config_steps), "--warmup", "5", "--precision", args.precision,
+           "--cpu-budget", str(args.cpu_budget)]
+    cmd += [f for f, on in (("--no-cpu", args.no_cpu), ("--no-recall", args.no_recall),
+                            ("--diagnostic", args.diagnostic)) if on]
+    print(f"bench.py: headline done; config {cfg} leg ({args.config_steps} batches)",
+          file=sys.stderr, flush=True)
     t0 = time.perf_counter()
-    full = bench_modes.run_pipeline(a, int(cfg), emit=False)
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, env=env, text=True, timeout=900)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": f"config {cfg} leg exited {r.returncode}"}
+    full = json.loads(lines[-1])
     keep = ("metric", "value", "unit", "ms_per_step", "steps", "warmup", "dtype", "config",
             "search_top15_exact_queries", "encode_max_abs_diff_vs_oracle",
             "rerank_max_abs_diff_vs_oracle", "rerank_checked_queries",
@@ -608,7 +617,6 @@ def _config_leg(args, cfg: str) -> dict:
     leg = {k: full[k] for k in keep if k in full}
     leg["wall_s"] = round(time.perf_counter() - t0, 1)
     return leg
-
 
 if __name__ == "__main__":
     main()
