@@ -591,8 +591,9 @@ def _config_leg(args, cfg: str) -> dict:
     """One config-2 / config-3 measurement (`bench.py --config 2|3`, scripts/bench_modes.py) as
     a dict of the keys a reader compares: qps, ms per batch, the certified parity legs,
     rooflines, the CPU baseline. Run as a child process after the headline's index is freed:
-    the configs' host-side pipelines (tokeniser thread, ~90 launches per batch) measured
-    58.5K qps in-process after the headline's CPU baseline vs 71K standalone."""
+    run inside this process after the headline, config 2 measured 58.5K qps against 74.5K as
+    a child (profiles/r05a_bench.json, r05b_bench_default.json; its host-side pipeline —
+    tokeniser thread, ~90 launches per batch — is what suffered)."""
     torch.cuda.empty_cache()
     cmd = [sys.executable, "-u", os.path.abspath(__file__), "--config", cfg,
            "--steps", str(args.config_steps), "--warmup", "5", "--precision", args.precision,
@@ -613,7 +614,7 @@ def _config_leg(args, cfg: str) -> dict:
             "search_top15_exact_queries", "encode_max_abs_diff_vs_oracle",
             "rerank_max_abs_diff_vs_oracle", "rerank_checked_queries",
             "rerank_top5_order_matches", "checked_timed_batches", "roofline", "roofline_search",
-            "cpu_baseline", "id_input_qps", "text_vs_id_input")
+            "cpu_baseline", "id_input_qps", "text_vs_id_input", "host_enqueue_ms_per_step")
     leg = {k: full[k] for k in keep if k in full}
     leg["wall_s"] = round(time.perf_counter() - t0, 1)
     return leg

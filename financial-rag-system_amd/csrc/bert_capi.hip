@@ -491,18 +491,6 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
     // vs 0.637 ms with BK-64 tiles at 1 per CU, and the config-2 line at 3 batches in flight
     // 71.1K vs 65.9K qps, where a 1-per-CU GEMM keeps the other batches' kernels off its CUs)
     const int ks = ks_for(Al ? kBK<true> : kBK<false>);
-#ifndef RAGMI_SMALL_DEEP
-#define RAGMI_SMALL_DEEP 0
-#endif
-    // fp16x3 GEMMs whose work units fit the CUs in one round take the deep ring (one
-    // workgroup per CU: more K steps in flight against the L2 / MALL latency that sets a
-    // query-batch K step's time)
-    if (RAGMI_SMALL_DEEP && Al && small_tiles * ks <= cu_count()) {
-      launch_pipe<EPI, true, PipeSmallDeep>(A, Al, W, Wl, bias, M, N, K, C, Clo, st, cu_count(),
-                                            LnArgs{}, ks);
-      if (ksplit_io) *ksplit_io = ks;
-      return;
-    }
     if (Al)   // 48 KB ring + 16 KB bias area: two workgroups per CU
       launch_pipe<EPI, true, PipeSmall<true>>(A, Al, W, Wl, bias, M, N, K, C, Clo, st,
                                               2 * cu_count(), LnArgs{}, ks);

@@ -539,18 +539,12 @@ using PipeLarge = PipeCfg<256, 128, 4, 2, 3>;
 // whole 384-wide rows per tile (bge-small / MiniLM hidden size): the output projections with
 // residual + LayerNorm fused into the epilogue (kEpiAddLn); 2 x 4 waves of 64 x 96
 using PipeRow = PipeCfg<128, 384, 2, 4, 2>;
-// (RAGMI_SMALL_NS: ring depth of the fp16x3 query-batch tiles, a build-time A/B of
-// scripts/gpu_build_ab.sh; 3 = two workgroups per CU with 16 KB of staged vectors)
-#ifndef RAGMI_SMALL_NS
-#define RAGMI_SMALL_NS 3
-#endif
-template <bool SPLIT> using PipeSmall = PipeCfg<64, 64, 2, 2, SPLIT ? RAGMI_SMALL_NS : 4>;
-// the same tiles with a deeper ring (fp16x3, one workgroup per CU: 6 x 16 KB stages + 16 KB of
-// staged vectors) for query-batch GEMMs whose work units fit the CUs in one round
-#ifndef RAGMI_SMALL_DEEP_NS
-#define RAGMI_SMALL_DEEP_NS 6
-#endif
-using PipeSmallDeep = PipeCfg<64, 64, 2, 2, RAGMI_SMALL_DEEP_NS>;
+// (fp16x3: a 3-stage ring, 64 KB with the staged vectors, two workgroups per CU. Round 5
+// A/B builds: 4 stages (2 per CU) and 6 / 8 stages (1 per CU, for GEMMs whose units fit the
+// CUs) each ran the 32-query bge-small forward slower, 0.69 -> 0.71 / 0.72 / 0.73 ms, and
+// config 2 at 72.6-74.5K -> 71.0-71.2K / 64.8-65.4K / 64.1K qps: a K step's time there is not
+// the ring's latency; profiles/r05b_small_ring_depth_ab.jsonl)
+template <bool SPLIT> using PipeSmall = PipeCfg<64, 64, 2, 2, SPLIT ? 3 : 4>;
 // (Measured and removed in round 5 — numbers in DESIGN.md §R5: 256x256 / 256x192 PIPE tiles,
 // register-blocked BIG / BIG128 shapes, BK-64 and 64x128 query-batch tiles, the one-loader and
 // deferred-LN query-batch WS tiles, and the 256x192 ping-pong kernel.)

@@ -345,6 +345,7 @@ def run_pipeline(args, cfg_id, emit=True):
             futs[k + depth] = pool.submit(tok.encode_packed, texts[args.warmup + k + depth])
         return t
     outs = run_seq(args.warmup, args.steps, True, toks_at)
+    enqueued = time.perf_counter() - t0      # host time to issue every batch (no sync inside)
     _sync(dev)
     elapsed = time.perf_counter() - t0
     pool.shutdown()
@@ -535,6 +536,7 @@ def run_pipeline(args, cfg_id, emit=True):
              "parallelism": f"replicas{world}" if world > 1 else "1 GPU"},
             roofline=roof, roofline_search=roof_search, cpu_baseline=cpu,
             id_input_qps=round(B * args.steps / elapsed_ids * world, 3),
+            host_enqueue_ms_per_step=round(enqueued / args.steps * 1e3, 4),
             text_vs_id_input=round(elapsed_ids / elapsed, 4), **extra)
         line["scaling"] = "weak"
         if emit:
