@@ -326,6 +326,10 @@ def main():
                          "A/B knobs are honoured (never for a reported line)")
     ap.add_argument("--precision", choices=["fp16x3", "fp16"], default="fp16x3",
                     help="encoder precision for --config 2/3 (fp16x3 = the 1e-3 contract)")
+    ap.add_argument("--partition", choices=["auto", "on", "off"], default="auto",
+                    help="batches in flight on CU-partitioned streams (rag_stream_create_cu_"
+                         "partition): auto = with free scan order and several in flight "
+                         "(shards below 4M rows per GPU)")
     ap.add_argument("--no-configs", action="store_true",
                     help="default line without the config-2 / config-3 legs (profiling runs: "
                          "their 1M-row scans share the headline scan kernel's name)")
@@ -411,8 +415,23 @@ def main():
         idx.set_scan_order(2)
     else:
         idx.set_scan_order(serial)
-    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev)
-                                                  for _ in range(n_streams - 1)]
+    # Spatial partition (round 5): with free order and several batches in
+    # flight, each batch's stream owns 1/n of the CUs and its scan one workgroup per CU of
+    # them, so the scans run side by side instead of interleaving over every CU — 1.25M rows,
+    # 4 in flight: 222-223K qps vs 206-208K (scripts/diag/cu_partition.py,
+    # profiles/r05c_cu_partition.jsonl)
+    partition = None
+    use_part = args.partition == "on" or (args.partition == "auto" and not serial
+                                          and n_streams > 1)
+    if use_part:
+        from ragmi.index import PartitionStreams
+        partition = PartitionStreams(dev, n_streams)
+        streams = list(partition.streams)
+        for s in streams:
+            s.wait_stream(torch.cuda.current_stream(dev))   # the queries were made there
+    else:
+        streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev)
+                                                      for _ in range(n_streams - 1)]
     n_step = [0]
 
     def step(q):
@@ -459,7 +478,9 @@ def main():
     # workload once more on ONE stream (after the timed region, not part of `value`). Serial
     # scan order already keeps every scan launch alone.
     alone_ms = scan_avg_ms
-    if len(streams) > 1 and not serial:
+    if partition is not None:
+        alone_ms = None        # a partition's scan alone runs on 1/n of the CUs: not comparable
+    elif len(streams) > 1 and not serial:
         torch.cuda.synchronize()
         idx.profile(True)
         for k in range(min(args.steps, 20)):
@@ -469,10 +490,11 @@ def main():
         a_ms, a_n = idx.profile_scan_ms()
         alone_ms = a_ms / max(a_n, 1)
     if world > 1:
-        t = torch.tensor([elapsed, scan_avg_ms, alone_ms, busy_ms], device=dev,
+        t = torch.tensor([elapsed, scan_avg_ms, alone_ms or 0.0, busy_ms], device=dev,
                          dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, scan_avg_ms, alone_ms, busy_ms = (float(v) for v in t.tolist())
+        alone_ms = alone_ms if partition is None else None
 
     check = None
     if not args.no_recall:
@@ -536,7 +558,8 @@ def main():
                        "rows_per_gpu": local_rows, "parallelism": f"corpus-shard{world}",
                        "batches_in_flight": n_streams, "storage": args.storage,
                        "scan_order": args.scan_order if args.scan_order == "stream" else
-                                     "serial" if serial else "free"},
+                                     "serial" if serial else "free",
+                       "cu_partition": len(streams) if partition is not None else None},
             "recall_at_5": check and check["recall_at_5"],
             "recall_at_5_min": check and check["recall_at_5_min"],
             "exact_batches": check and check["exact_batches"],
@@ -566,11 +589,14 @@ def main():
                          "step_frac": round(algo_bytes / (elapsed / args.steps) / HBM_PEAK, 4),
                          # the same launch timed alone (differs from avg_ms only when several
                          # batches are in flight and their scans overlap)
-                         "standalone_avg_ms": round(alone_ms, 4),
-                         "standalone_frac": round(algo_bytes / (alone_ms * 1e-3) / HBM_PEAK, 4)},
+                         "standalone_avg_ms": round(alone_ms, 4) if alone_ms else None,
+                         "standalone_frac": (round(algo_bytes / (alone_ms * 1e-3) / HBM_PEAK, 4)
+                                             if alone_ms else None)},
             "cpu_baseline": cpu,
         }
     idx.close()
+    if partition is not None:
+        partition.close()
     if world > 1 or rehearsal:
         dist.destroy_process_group()
     if rank == 0:

@@ -66,6 +66,7 @@ struct Workspace {
   hipEvent_t ev_in = nullptr;   // scan-stream order: caller stream -> scan stream -> caller
   hipEvent_t ev_out = nullptr;
   hipStream_t owner = nullptr;  // stream of the last pass that used this slot
+  int cus = 0;                  // CUs the owner stream may use (its CU mask; stream_cus)
   bool used = false;
   uint64_t tick = 0;            // last use (LRU rebinding)
 };
@@ -158,6 +159,22 @@ void launch_upsert(rag_index* h, const float* v, const int64_t* rows, const uint
 double store_eps(const rag_index* h) {
   if (h->storage != RAG_STORE_FP32) return 0.0;
   return (0x1p-11 * (1.0 + 0x1p-20) + 0x1p-25 * std::sqrt((double)h->dim)) * (1.0 + 0x1p-20);
+}
+
+// CUs a stream may run on: its CU mask (rag_stream_create_cu_partition gives each of the
+// batches in flight its own share of the CUs), popcounted once per workspace binding; the null
+// stream and unmasked streams -> every CU. The scan grids are sized to it (launch_search_pass).
+int stream_cus(const rag_index* h, hipStream_t st) {
+  if (!st) return h->n_cu;
+  uint32_t mask[32] = {};
+  const uint32_t words = (uint32_t)std::min(32, (h->n_cu + 31) / 32);
+  if (hipExtStreamGetCUMask(st, words, mask) != hipSuccess) {
+    (void)hipGetLastError();
+    return h->n_cu;
+  }
+  int n = 0;
+  for (uint32_t i = 0; i < words; ++i) n += __builtin_popcount(mask[i]);
+  return n > 0 && n < h->n_cu ? n : h->n_cu;
 }
 
 // sample + thresh: seed thresholds for the scan (see sample_kernel). ~0.8% of the shard's
@@ -255,8 +272,11 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
   // R workgroups per query group (R % 8 == 0: XCD pairing of the groups, scan_lds_kernel)
   constexpr bool kLdsQ = D > 384;
   int grid;
+  // a CU-partitioned stream (w.cus < n_cu): the same per-CU occupancy over its CUs only
+  const bool part = w.cus > 0 && w.cus < h->n_cu;
+  const int max_wgs = part ? 2 * w.cus : h->max_wgs;
   if constexpr (kLdsQ) {
-    const int per_group = std::max(8, (h->max_wgs / 2 / groups) & ~7);
+    const int per_group = std::max(8, (max_wgs / 2 / groups) & ~7);
     const int need = (int)std::min<int64_t>(
         per_group, ((n_tiles + kLdsWaves - 1) / kLdsWaves + 7) & ~int64_t(7));
     grid = std::max(8, std::min(need, kMaxLists / kLdsWaves));
@@ -276,8 +296,12 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
     // Filtered scans (a tag load and compare per row) keep two workgroups per CU: 10M rows,
     // per-query ticker filter, serial order: 26.8 / 27.0K qps at 512 vs 25.7 / 26.1K at 192
     // (scan 1.170 vs 1.21-1.24 ms, profiles/r03u_filtered_wgs.jsonl)
-    const int wg_cap = wg_env ? wg_env : filt ? h->max_wgs : h->scan_wgs;
-    grid = (int)std::min<int64_t>(std::min(h->max_wgs, wg_cap),
+    // On a CU-partitioned stream (the batches in flight on disjoint CU sets) one workgroup per
+    // CU of its share: 1.25M rows, 4 batches in flight on quarter-CU streams, 64 workgroups
+    // 222-223K qps vs 205K at 48, 210-218K at 128, and 206-208K for 4 unpartitioned streams at
+    // the default grid (scripts/diag/cu_partition.py, profiles/r05c_cu_partition.jsonl)
+    const int wg_cap = wg_env ? wg_env : filt ? max_wgs : part ? w.cus : h->scan_wgs;
+    grid = (int)std::min<int64_t>(std::min(max_wgs, wg_cap),
                                   std::max<int64_t>(1, (n_tiles + 3) / 4));
     grid = std::min(grid, kMaxLists / kWavesPerWG);
   }
@@ -314,7 +338,7 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
     // RAGMI_WIDE_WGS (diagnostic A/B): workgroup cap of the wide scan (default one per CU)
     static ragmi::Knob k_wide("RAGMI_WIDE_WGS");
     const int wide_env = k_wide.get(0) > 0 ? std::max(8, k_wide.get(0)) : 0;
-    const int cap = wide_env ? std::min(wide_env, h->max_wgs / 2) : h->max_wgs / 2;
+    const int cap = wide_env ? std::min(wide_env, max_wgs / 2) : max_wgs / 2;
     grid = (int)std::min<int64_t>(cap, std::max<int64_t>(1, n_tiles));
   }
   if constexpr (kLdsQ) {
@@ -389,7 +413,7 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
   // of the pass; otherwise its R workgroups stream the shard once per 16 marked queries.
   // RAGMI_RESCAN_WG (diagnostic A/B) caps R; 0 skips the launch, and mark_unanswered_kernel
   // then records the marked queries as unanswered (tier 3, rag_index_unanswered): timing only
-  const int R = rescan_grid(h);
+  const int R = std::min(rescan_grid(h), part ? w.cus : h->n_cu);
   if (R > 0) {
 #define RAG_RESCAN(F)                                                                   \
   launch_fixed<kScanBlock>(rescan_kernel<D, F>, dim3(R), 0, st, w.fb_tier, w.t2, Bq, h->corpus,  \
@@ -540,6 +564,7 @@ int search_locked(rag_index* h, const float* q, int B, int k, const uint32_t* fi
         if (s.tick < wp->tick) wp = &s;
     }
     Workspace& w = *wp;
+    if (!w.used || w.owner != st || w.cus == 0) w.cus = stream_cus(h, st);
     w.used = true;
     w.owner = st;
     w.tick = ++h->ws_tick;
@@ -1236,6 +1261,32 @@ int rag_index_set_scan_order(rag_index_t* h, int serial) {
   h->serial_scans = serial < 0 || serial > 2 ? 1 : serial;
   h->scan_last = nullptr;
   h->scan_any = false;
+  return RAG_OK;
+}
+
+int rag_stream_create_cu_partition(int device, int part, int parts, void** out) {
+  ragmi::clear_error();
+  if (!out || parts < 1 || part < 0 || part >= parts)
+    return ragmi::fail(RAG_EINVAL, "need 0 <= part < parts and an output pointer");
+  *out = nullptr;
+  RAG_HIP(hipSetDevice(device));
+  int n_cu = 0;
+  RAG_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device));
+  if (parts > n_cu) return ragmi::fail(RAG_EINVAL, "more parts than CUs");
+  // contiguous CU ids [part n / parts, (part + 1) n / parts)
+  std::vector<uint32_t> mask((size_t)(n_cu + 31) / 32, 0u);
+  const int c0 = (int)((int64_t)part * n_cu / parts), c1 = (int)((int64_t)(part + 1) * n_cu / parts);
+  for (int c = c0; c < c1; ++c) mask[(size_t)c / 32] |= 1u << (c % 32);
+  hipStream_t st = nullptr;
+  RAG_HIP(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
+  *out = st;
+  return RAG_OK;
+}
+
+int rag_stream_destroy(void* stream) {
+  ragmi::clear_error();
+  if (!stream) return RAG_OK;
+  RAG_HIP(hipStreamDestroy(static_cast<hipStream_t>(stream)));
   return RAG_OK;
 }
 

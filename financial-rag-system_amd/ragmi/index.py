@@ -300,6 +300,39 @@ class FlatIndex:
         return a[:m], b[:m]
 
 
+class PartitionStreams:
+    """`parts` HIP streams on disjoint shares of the device's CUs
+    (rag_stream_create_cu_partition) as torch streams, for `parts` batches in flight: a search
+    issued on one sizes its scan to that share, so the batches scan side by side instead of
+    interleaving over every CU. Results are the same on any stream. close() (or the end of
+    the process) destroys them; call it only after their work has finished."""
+
+    def __init__(self, device, parts: int):
+        dev = _lib.resolve_device(device)
+        self.device = torch.device("cuda", _lib.device_index(dev))
+        self._L = _lib.load()
+        self._raw, self.streams = [], []
+        for p in range(parts):
+            h = ctypes.c_void_p()
+            check(self._L.rag_stream_create_cu_partition(self.device.index, p, parts,
+                                                         ctypes.byref(h)))
+            self._raw.append(h)
+            self.streams.append(torch.cuda.ExternalStream(h.value, device=self.device))
+
+    def __len__(self):
+        return len(self.streams)
+
+    def __getitem__(self, i):
+        return self.streams[i]
+
+    def close(self) -> None:
+        if self._raw:
+            torch.cuda.synchronize(self.device)
+            for h in self._raw:
+                self._L.rag_stream_destroy(h)
+            self._raw, self.streams = [], []
+
+
 def busy_union_ms(start_ms, end_ms) -> float:
     """Length of the union of [start, end) intervals: the time at least one of the launches
     was running (overlapping launches counted once)."""

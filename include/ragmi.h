@@ -205,6 +205,14 @@ int rag_index_unanswered(rag_index_t* index, int64_t* n);
  * (main.py:232-237); this is serving-loop plumbing for main2.py:281-295's batch processor
  * with several batches in flight. */
 int rag_index_set_scan_order(rag_index_t* index, int serial);
+/* Spatial partition of the batches in flight (serving option): a HIP stream restricted to CU
+ * share `part` of `parts` (contiguous CU ids, hipExtStreamCreateWithCUMask). Searches issued
+ * on such a stream size their scan grids to the stream's CUs (one scan workgroup per CU), so
+ * `parts` batches in flight on `parts` partition streams scan side by side on disjoint CUs.
+ * Results are identical on any stream. Destroy with rag_stream_destroy. (The reference has no
+ * counterpart: Qdrant serves concurrent searches from one server process, main2.py:281-295.) */
+int rag_stream_create_cu_partition(int device, int part, int parts, void** stream);
+int rag_stream_destroy(void* stream);
 
 /* Kernel timing hook for bench.py: average device time (ms) of `rag_index_search` scan-kernel
  * launches measured with HIP events on the launch stream. enable = 0 off; enable = n > 0 records
