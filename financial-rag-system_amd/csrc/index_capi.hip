@@ -299,7 +299,8 @@ int launch_search_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k
     // On a CU-partitioned stream (the batches in flight on disjoint CU sets) one workgroup per
     // CU of its share: 1.25M rows, 4 batches in flight on quarter-CU streams, 64 workgroups
     // 222-223K qps vs 205K at 48, 210-218K at 128, and 206-208K for 4 unpartitioned streams at
-    // the default grid (scripts/diag/cu_partition.py, profiles/r05c_cu_partition.jsonl)
+    // the default grid (scripts/diag/cu_partition.py, profiles/r05c_cu_partition.jsonl; bench lines
+    // 222.7-223.3K vs 207.0-207.6K, profiles/r05d_partition_lines.jsonl)
     const int wg_cap = wg_env ? wg_env : filt ? max_wgs : part ? w.cus : h->scan_wgs;
     grid = (int)std::min<int64_t>(std::min(max_wgs, wg_cap),
                                   std::max<int64_t>(1, (n_tiles + 3) / 4));
