@@ -1057,14 +1057,19 @@ __global__ __launch_bounds__(kPipeBlock<CFG>, 1) void gemm_pipe_kernel(
     const uint32_t soff = __builtin_amdgcn_readfirstlane((uint32_t)(kb_i + kr_i) * (BK * 2));
     if (++kr_i == nk) kr_i = 0;
     const uint32_t slot = lbase + (uint32_t)slot_i * (STAGE_H8 * 16);
+#ifndef RAGMI_PIPE_PROBE
+// build-time timing probe (ragmi/_build.py OUT.so -DRAGMI_PIPE_PROBE=n; results meaningless):
+// 1 = no LDS reads / MFMAs in the query-batch tiles' K loop, 2 = no DMAs, 3 = neither
+#define RAGMI_PIPE_PROBE 0
+#endif
 #pragma unroll
-    for (int i = 0; i < LA; ++i) {
+    for (int i = 0; i < ((RAGMI_PIPE_PROBE & 2) ? 0 : LA); ++i) {
       const uint32_t d = slot + (uint32_t)((wid * LA + i) * 64 * 16);
       blds16(rA0, voA[i], soff, d);
       if constexpr (SPLIT) blds16(rA1, voA[i], soff, d + A_H8 * 16);
     }
 #pragma unroll
-    for (int i = 0; i < LW; ++i) {
+    for (int i = 0; i < ((RAGMI_PIPE_PROBE & 2) ? 0 : LW); ++i) {
       const uint32_t d = slot + (uint32_t)((NPL * A_H8 + (wid * LW + i) * 64) * 16);
       blds16(rW0, voW[i], soff, d);
       if constexpr (SPLIT) blds16(rW1, voW[i], soff, d + W_H8 * 16);
@@ -1127,7 +1132,7 @@ __global__ __launch_bounds__(kPipeBlock<CFG>, 1) void gemm_pipe_kernel(
           }
     }
 #pragma unroll
-    for (int ks = 0; ks < (CFG::PRELOAD ? 0 : BK / 32); ++ks) {
+    for (int ks = 0; ks < (CFG::PRELOAD || (RAGMI_PIPE_PROBE & 1) ? 0 : BK / 32); ++ks) {
       const int ch = ks * 4 + (lane >> 4);
       half8 af[FM], wf[FN];
 #pragma unroll

@@ -272,7 +272,14 @@ def run_pipeline(args, cfg_id, emit=True):
     # More hardware queues per process (GPU_MAX_HW_QUEUES=8) drop config 2 to 30-45K
     # (profiles/r04u_config2_streams_hwq.jsonl).
     S = args.streams or (4 if cfg_id == 2 else 3)
-    streams = [torch.cuda.Stream(dev) for _ in range(S)]
+    # --partition on: the batches in flight on CU-partitioned streams (bench.py, DESIGN R5.3)
+    part = None
+    if getattr(args, "partition", "auto") == "on":
+        from ragmi.index import PartitionStreams
+        part = PartitionStreams(dev, S)
+        streams = list(part.streams)
+    else:
+        streams = [torch.cuda.Stream(dev) for _ in range(S)]
     ev_every = 4                        # CE forward events on every 4th batch (sampled)
     evs, flops = [], []
 
@@ -533,6 +540,7 @@ def run_pipeline(args, cfg_id, emit=True):
              "tokenize_ms_per_batch": round(tok_ms, 3),
              "batch": B, "k": K_TOP, "rerank_top_k": TOPK if cfg_id == 3 else None,
              "precision": prec, "batches_in_flight": S,
+             "cu_partition": S if part is not None else None,
              "parallelism": f"replicas{world}" if world > 1 else "1 GPU"},
             roofline=roof, roofline_search=roof_search, cpu_baseline=cpu,
             id_input_qps=round(B * args.steps / elapsed_ids * world, 3),
@@ -544,6 +552,8 @@ def run_pipeline(args, cfg_id, emit=True):
     else:
         line = None
     idx.close()
+    if part is not None:
+        part.close()
     if world > 1:
         dist.destroy_process_group()
     return line

@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, os.path.join(ROOT, "financial-rag-system_amd"))
 
 from ragmi import _lib  # noqa: E402
-from ragmi.encoders import EPI_F16, GEMM_SMALL, linear  # noqa: E402
+from ragmi.encoders import EPI_F16, GEMM_SMALL  # noqa: E402
 
 
 def timeit(fn, reps=50):
@@ -49,10 +49,18 @@ def main():
     L = _lib.load()
     st = torch.cuda.current_stream().cuda_stream
     for N in (1152, 384):
-        for K in (64, 128, 256, 384, 768, 1536):
+        for K in [int(k) for k in os.environ.get("SWEEP_K", "64,128,256,384,768,1536").split(",")]:
             a, al, w, wl, b = operands(M, N, K)
-            us = timeit(lambda: linear(a, w, b, EPI_F16, al, wl, GEMM_SMALL))
-            print(json.dumps({"kind": "small_f16", "M": M, "N": N, "K": K, "us": round(us, 2)}),
+            ch = torch.empty((M, N), dtype=torch.float16, device="cuda")
+            cl = torch.empty_like(ch)
+
+            def f16():        # preallocated outputs: the device time, not linear()'s host path
+                _lib.check(L.rag_bert_gemm(GEMM_SMALL, EPI_F16, a.data_ptr(), al.data_ptr(),
+                                           w.data_ptr(), wl.data_ptr(), b.data_ptr(), M, N, K,
+                                           ch.data_ptr(), cl.data_ptr(), st))
+            us = timeit(f16)
+            tag = os.path.basename(os.environ.get("RAGMI_LIB_AB", "in-tree"))
+            print(json.dumps({"lib": tag, "kind": "small_f16", "M": M, "N": N, "K": K, "us": round(us, 2)}),
                   flush=True)
             c = torch.empty((4, M, N), device="cuda")
             parts = ctypes.c_int()
@@ -62,7 +70,7 @@ def main():
                                                   w.data_ptr(), wl.data_ptr(), b.data_ptr(), M, N,
                                                   K, c.data_ptr(), 4, ctypes.byref(parts), st))
             us = timeit(sk)
-            print(json.dumps({"kind": "splitk_f32", "M": M, "N": N, "K": K, "parts": parts.value,
+            print(json.dumps({"lib": tag, "kind": "splitk_f32", "M": M, "N": N, "K": K, "parts": parts.value,
                               "us": round(us, 2)}), flush=True)
 
 
