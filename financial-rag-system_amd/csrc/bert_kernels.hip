@@ -544,6 +544,9 @@ using PipeRow = PipeCfg<128, 384, 2, 4, 2>;
 // CUs) each ran the 32-query bge-small forward slower, 0.69 -> 0.71 / 0.72 / 0.73 ms, and
 // config 2 at 72.6-74.5K -> 71.0-71.2K / 64.8-65.4K / 64.1K qps: a K step's time there is not
 // the ring's latency; profiles/r05b_small_ring_depth_ab.jsonl)
+// (wave grid, round 5 A/B builds: 2 x 1 / 1 x 2 / 1 x 1 waves of 32 x 64 / 64 x 32 / 64 x 64
+// ran the 32-query forward in 0.757 / 0.762 / 0.99 ms vs 0.675 for 2 x 2 — fewer LDS fragment
+// reads per step, but fewer waves to issue them; profiles/r05i_small_wave_grid_ab.jsonl)
 template <bool SPLIT> using PipeSmall = PipeCfg<64, 64, 2, 2, SPLIT ? 3 : 4>;
 // (Measured and removed in round 5 — numbers in DESIGN.md §R5: 256x256 / 256x192 PIPE tiles,
 // register-blocked BIG / BIG128 shapes, BK-64 and 64x128 query-batch tiles, the one-loader and
