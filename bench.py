@@ -297,8 +297,12 @@ def check_world(gpus: int, environ=None) -> int:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default 50; --config 2 / 3: 200)")
+    ap.add_argument("--warmup", type=int, default=None,
+                    help="untimed steps (default 5; --config 2 / 3: 20 — the encoder's "
+                         "hipGraphs are captured per padded shape and per stream, so the "
+                         "pipelines need a few batches per stream to reach steady state)")
     ap.add_argument("--rows", type=int, default=10_000_000)
     ap.add_argument("--no-recall", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
@@ -333,9 +337,14 @@ def main():
     ap.add_argument("--no-configs", action="store_true",
                     help="default line without the config-2 / config-3 legs (profiling runs: "
                          "their 1M-row scans share the headline scan kernel's name)")
-    ap.add_argument("--config-steps", type=int, default=50,
-                    help="timed batches of each config-2 / config-3 leg (warmup 5)")
+    ap.add_argument("--config-steps", type=int, default=200,
+                    help="timed batches of each config-2 / config-3 leg (warmup 20)")
     args = ap.parse_args()
+    pipeline = args.config in ("2", "3")
+    if args.steps is None:
+        args.steps = 200 if pipeline else 50
+    if args.warmup is None:
+        args.warmup = 20 if pipeline else 5
     world = check_world(args.gpus)
     if world > 1 and "WORLD_SIZE" not in os.environ:
         # plain `python bench.py --gpus N`: one rank process per GPU, started before this
@@ -622,7 +631,7 @@ def _config_leg(args, cfg: str) -> dict:
     tokeniser thread, ~90 launches per batch — is what suffered)."""
     torch.cuda.empty_cache()
     cmd = [sys.executable, "-u", os.path.abspath(__file__), "--config", cfg,
-           "--steps", str(args.config_steps), "--warmup", "5", "--precision", args.precision,
+           "--steps", str(args.config_steps), "--warmup", "20", "--precision", args.precision,
            "--cpu-budget", str(args.cpu_budget)]
     cmd += [f for f, on in (("--no-cpu", args.no_cpu), ("--no-recall", args.no_recall),
                             ("--diagnostic", args.diagnostic)) if on]

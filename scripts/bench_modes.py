@@ -242,11 +242,12 @@ def run_pipeline(args, cfg_id, emit=True):
     c_lens = torch.randint(180, 261, (n,), generator=g, device=dev, dtype=torch.int32)
     # stage 1 starts from STRINGS (main2.py:170-171 encode(list[str]) tokenises every call):
     # seeded question-like texts over a synthetic 30522-entry WordPiece vocab, tokenised by
-    # the product tokenizer (ragmi.encoders.WordPiece) inside the timed region on a host
-    # worker thread pipelined ahead of the GPU; the same batches pre-tokenised are timed
+    # the product tokenizer (ragmi.encoders.WordPiece) inside the timed region, inline on the
+    # issuing thread as main2.py's encode(list[str]) does (the batches in flight keep the GPU
+    # fed: the host issues a batch in ~0.23 of the ~0.40 ms the GPU takes; a tokeniser worker
+    # thread measured 8-10% slower, round 5 §R5.2); the same batches pre-tokenised are timed
     # after it as the id-input comparison
     import tempfile
-    from concurrent.futures import ThreadPoolExecutor
 
     from ragmi.encoders import WordPiece
     vocab = R.make_vocab(30522, seed=5)
@@ -338,24 +339,13 @@ def run_pipeline(args, cfg_id, emit=True):
 
     run_seq(0, args.warmup, False)
     _sync(dev)
-    # timed region: strings in, top-5 (config 3) / top-15 (config 2) out; tokenisation of
-    # batch i+depth runs on the worker while the GPU works on batch i
-    depth = S + 1
-    pool = ThreadPoolExecutor(max_workers=1)
+    # timed region: strings in, top-5 (config 3) / top-15 (config 2) out
     t0 = time.perf_counter()
-    futs = {k: pool.submit(tok.encode_packed, texts[args.warmup + k])
-            for k in range(min(depth, args.steps))}
-
-    def toks_at(k):
-        t = futs.pop(k).result()
-        if k + depth < args.steps:
-            futs[k + depth] = pool.submit(tok.encode_packed, texts[args.warmup + k + depth])
-        return t
-    outs = run_seq(args.warmup, args.steps, True, toks_at)
+    outs = run_seq(args.warmup, args.steps, True,
+                   lambda k: tok.encode_packed(texts[args.warmup + k]))
     enqueued = time.perf_counter() - t0      # host time to issue every batch (no sync inside)
     _sync(dev)
     elapsed = time.perf_counter() - t0
-    pool.shutdown()
     ce_ms = float(np.mean([a.elapsed_time(b) for a, b in evs])) if evs else None
     # the same batches from pre-tokenised ids (the round-2 line's input), for the delta
     n_ev = len(evs)
@@ -533,7 +523,7 @@ def run_pipeline(args, cfg_id, emit=True):
             "bge-small / MiniLM-L6 architectures; seeded question-like query strings over a "
             "synthetic 30522-entry WordPiece vocab, ~21 tokens; chunk token ids 180-260)",
             {"workload": f"config {cfg_id}: 32 query STRINGS -> WordPiece tokenisation (host "
-                         f"worker thread, pipelined) -> bge-small ({prec}) -> top-15 of "
+                         f"issuing thread, inline) -> bge-small ({prec}) -> top-15 of "
                          f"{n}x384" + (" -> CE rerank 480 pairs (chunk tokens cached at "
                                        "ingest) -> top-5" if cfg_id == 3 else ""),
              "query_tokens_mean": round(float(q_lens.mean()), 1),
