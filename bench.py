@@ -542,6 +542,12 @@ def main():
         # without overlap this IS the average launch duration (avg_ms)
         achieved = algo_bytes / (busy_ms * 1e-3)
         traffic, traffic_source = scan_traffic(local_rows, args.storage)
+        if partition is not None:
+            # the PMC FETCH_SIZE of a CU-partitioned scan launch reads 0.50x its algorithmic
+            # bytes after the x2 correction (profiles/scan_pmc.json partitioned_by_rows_per_gpu)
+            # — below what the launch must read, so not a traffic measurement
+            traffic, traffic_source = None, ("not reported: PMC FETCH_SIZE under-counts the "
+                                             "CU-partitioned scan launch (DESIGN R5.3)")
         qps = B * args.steps / elapsed
         line = {
             "metric": "queries/sec + recall@5, batch=32 over 10Mx384 corpus",
