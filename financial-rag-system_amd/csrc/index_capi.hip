@@ -1270,7 +1270,6 @@ int rag_stream_create_cu_partition(int device, int part, int parts, void** out) 
   if (!out || parts < 1 || part < 0 || part >= parts)
     return ragmi::fail(RAG_EINVAL, "need 0 <= part < parts and an output pointer");
   *out = nullptr;
-  RAG_HIP(hipSetDevice(device));
   int n_cu = 0;
   RAG_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device));
   if (parts > n_cu) return ragmi::fail(RAG_EINVAL, "more parts than CUs");
@@ -1278,8 +1277,15 @@ int rag_stream_create_cu_partition(int device, int part, int parts, void** out) 
   std::vector<uint32_t> mask((size_t)(n_cu + 31) / 32, 0u);
   const int c0 = (int)((int64_t)part * n_cu / parts), c1 = (int)((int64_t)(part + 1) * n_cu / parts);
   for (int c = c0; c < c1; ++c) mask[(size_t)c / 32] |= 1u << (c % 32);
+  // (the stream belongs to the current device: switch to `device` for the call only)
+  int prev = 0;
+  RAG_HIP(hipGetDevice(&prev));
+  RAG_HIP(hipSetDevice(device));
   hipStream_t st = nullptr;
-  RAG_HIP(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
+  const hipError_t e = hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data());
+  (void)hipSetDevice(prev);
+  if (e != hipSuccess)
+    return ragmi::fail(RAG_EHIP, std::string("hipExtStreamCreateWithCUMask: ") + hipGetErrorString(e));
   *out = st;
   return RAG_OK;
 }

@@ -53,6 +53,11 @@ def test_library_loads_and_binds_without_gpu(libpath):
     h = ctypes.c_void_p()
     rc = L.rag_index_create(100, 16, 0, ctypes.byref(h))
     assert rc == -1 and b"dim" in L.rag_last_error()
+    # partition streams: argument errors before any HIP call
+    st = ctypes.c_void_p()
+    for part, parts in ((0, 0), (2, 2), (-1, 4)):
+        assert L.rag_stream_create_cu_partition(0, part, parts, ctypes.byref(st)) == -1
+    assert L.rag_stream_destroy(None) == 0
 
 
 def test_code_object_targets_gfx950(libpath):
