@@ -63,6 +63,7 @@ struct Workspace {
   int* lk_again = nullptr;
   int* lk_need = nullptr;
   int* lk_cand = nullptr;
+  float* lk_es = nullptr;       // [32][kLkCap] exact scores of the candidates (lk_rescore)
   hipEvent_t ev_in = nullptr;   // scan-stream order: caller stream -> scan stream -> caller
   hipEvent_t ev_out = nullptr;
   hipStream_t owner = nullptr;  // stream of the last pass that used this slot
@@ -446,7 +447,8 @@ int ensure_lk(Workspace& w) {
       hipMalloc(reinterpret_cast<void**>(&w.lk_cnt), Q * 4) == hipSuccess &&
       hipMalloc(reinterpret_cast<void**>(&w.lk_again), Q * 4) == hipSuccess &&
       hipMalloc(reinterpret_cast<void**>(&w.lk_need), 64) == hipSuccess &&
-      hipMalloc(reinterpret_cast<void**>(&w.lk_cand), Q * kLkCap * 4) == hipSuccess;
+      hipMalloc(reinterpret_cast<void**>(&w.lk_cand), Q * kLkCap * 4) == hipSuccess &&
+      hipMalloc(reinterpret_cast<void**>(&w.lk_es), Q * kLkCap * 4) == hipSuccess;
   if (!ok) return ragmi::fail(RAG_ENOMEM, "large-k workspace allocation failed");
   return RAG_OK;
 }
@@ -475,7 +477,9 @@ int launch_large_k_pass(rag_index* h, Workspace& w, const float* q, int Bq, int 
   }
   lk_bound_kernel<<<dim3(Bq), dim3(256), 0, st>>>(w.lk_smax, n_sample, k, w.eps, w.lk_thr,
                                                   w.lk_cnt, w.lk_again, w.lk_need);
-  const int cgrid = (int)std::max<int64_t>(1, std::min<int64_t>(4 * h->n_cu, (n_tiles + 3) / 4));
+  // collection grid: two workgroups per CU (10M rows, k = 33: 1.54-1.55 ms per pass vs
+  // 1.57-1.64 at four, 2.37 at one; k = 100 1.64 either way; profiles/r05q_large_k_grid.jsonl)
+  const int cgrid = (int)std::max<int64_t>(1, std::min<int64_t>(2 * h->n_cu, (n_tiles + 3) / 4));
   for (int r = 0; r < kLkRounds; ++r) {
     if (filt)
       lk_collect_kernel<D, true><<<dim3(cgrid), dim3(256), 0, st>>>(
@@ -485,8 +489,10 @@ int launch_large_k_pass(rag_index* h, Workspace& w, const float* q, int Bq, int 
       lk_collect_kernel<D, false><<<dim3(cgrid), dim3(256), 0, st>>>(
           h->corpus, h->tags, w.filt, w.qfrag, (int)h->count, n_tiles, Bq, w.lk_thr, w.lk_cnt,
           w.lk_cand, w.lk_again, w.lk_need, r);
+    lk_rescore_kernel<D><<<dim3(kLkCap / 256, Bq), dim3(256), 0, st>>>(
+        h->corpus, w.qn, w.lk_cnt, w.lk_cand, w.lk_again, w.lk_need, r, w.lk_es, h->rows32);
     lk_final_kernel<D><<<dim3(Bq), dim3(256), 0, st>>>(
-        h->corpus, w.qn, k, w.lk_cnt, w.lk_cand, w.eps, w.lk_thr, w.lk_again, w.lk_need, r,
+        h->corpus, w.qn, k, w.lk_cnt, w.lk_cand, w.lk_es, w.eps, w.lk_thr, w.lk_again, w.lk_need, r,
         w.fb_tier, w.fb_cnt, id_offset, out_s, out_i, out_packed, h->rows32);
   }
   RAG_HIP(hipGetLastError());
@@ -896,7 +902,7 @@ int rag_index_destroy(rag_index_t* h) {
     for (void* p : {(void*)w.t2, (void*)w.t2_s, (void*)w.t2_i, (void*)w.t2_tk})
       if (p) (void)hipFree(p);
     for (void* p : {(void*)w.lk_smax, (void*)w.lk_thr, (void*)w.lk_cnt, (void*)w.lk_again,
-                    (void*)w.lk_need, (void*)w.lk_cand})
+                    (void*)w.lk_need, (void*)w.lk_cand, (void*)w.lk_es})
       if (p) (void)hipFree(p);
     if (w.ev_in) (void)hipEventDestroy(w.ev_in);
     if (w.ev_out) (void)hipEventDestroy(w.ev_out);

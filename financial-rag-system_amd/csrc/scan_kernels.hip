@@ -2940,22 +2940,58 @@ __device__ __forceinline__ float fkey_inv(uint32_t k) {
   return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
 }
 
-// the largest key t with #{i < n : keys[i] >= t} >= k (keys in LDS; 256 threads); sets *ge
-// to that count. Requires n >= k.
-__device__ uint32_t lk_kth_key(const uint32_t* keys, int n, int k, int* red) {
-  uint32_t t = 0;
-  for (int bit = 31; bit >= 0; --bit) {
-    const uint32_t c = t | (1u << bit);
-    int m = 0;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) m += keys[i] >= c;
+// the kk-th largest of the n keys key(i), 1 <= kk <= n (multiplicity counted; 256 threads):
+// a radix select over 8-bit digits, most significant first — each pass an LDS histogram of the
+// keys that match the digits chosen so far, then wave 0 scans the 256 bins from the top (a
+// wave-wide prefix sum) for the digit where the count reaches kk. 4 passes where a bisection
+// over the 32 key bits took 32 (round 5: lk_bound 166 us for 16384 keys).
+template <typename KeyFn>
+__device__ uint32_t radix_kth_key(KeyFn key, int n, int kk, int* hist, int* sh) {
+  uint32_t prefix = 0, mask = 0;
+  int need = kk;
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) hist[i] = 0;
     __syncthreads();
-    if (threadIdx.x == 0) *red = 0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      const uint32_t v = key(i);
+      if ((v & mask) == prefix) atomicAdd(&hist[(v >> shift) & 255u], 1);
+    }
     __syncthreads();
-    atomicAdd(red, m);
+    if (threadIdx.x < 64) {
+      // lane l holds digits 255 - 4l .. 252 - 4l (descending); inclusive scan over lanes
+      const int l = threadIdx.x;
+      int bv[4], sl = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bv[j] = hist[255 - 4 * l - j];
+        sl += bv[j];
+      }
+      int incl = sl;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(incl, o, 64);
+        if (l >= o) incl += t;
+      }
+      const int excl = incl - sl;
+      if (excl < need && need <= incl) {       // exactly one lane
+        int c = excl, d = 255 - 4 * l;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          d = 255 - 4 * l - j;
+          if (c + bv[j] >= need) break;
+          c += bv[j];
+        }
+        sh[0] = d;
+        sh[1] = need - c;
+      }
+    }
     __syncthreads();
-    if (*red >= k) t = c;
+    prefix |= (uint32_t)sh[0] << shift;
+    mask |= 255u << shift;
+    need = sh[1];
+    __syncthreads();
   }
-  return t;
+  return prefix;
 }
 
 // per query q < B: thr[q] from the sample maxima smax [32][n_sample]; resets the round state
@@ -2967,7 +3003,7 @@ __global__ __launch_bounds__(256) void lk_bound_kernel(const float* __restrict__
                                                        int* __restrict__ again,
                                                        int* __restrict__ need) {
   __shared__ uint32_t keys[kLkSampleMax];
-  __shared__ int red;
+  __shared__ int red, hist[256], sh[2];
   const int q = blockIdx.x;
   int fin = 0;
   for (int i = threadIdx.x; i < n_sample; i += 256) {
@@ -2983,7 +3019,7 @@ __global__ __launch_bounds__(256) void lk_bound_kernel(const float* __restrict__
   __syncthreads();
   float th = kNegInf;
   if (n_fin >= k) {
-    const float T = fkey_inv(lk_kth_key(keys, n_sample, k, &red));
+    const float T = fkey_inv(radix_kth_key([&](int i) { return keys[i]; }, n_sample, k, hist, sh));
     const double d = (double)T - 2.0 * (double)eps[q];
     th = (float)d;
     if ((double)th > d) th = nextafterf(th, kNegInf);   // round toward -inf
@@ -3026,6 +3062,18 @@ __global__ __launch_bounds__(256) void lk_collect_kernel(const half8* __restrict
     fmb = filt[2 * qb];
     fvb = filt[2 * qb + 1];
   }
+  // D <= 384: the two query groups' fragments stay in registers for the whole launch (24
+  // half8); reloading them per tile tripled the vector-memory instructions per tile
+  // (k = 33 collect 1.34 ms vs the scan's 1.08 over the same 10M rows, round 5)
+  constexpr bool QREG = S <= 12;
+  half8 qra[QREG ? S : 1], qrb[QREG ? S : 1];
+  if constexpr (QREG) {
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      qra[s] = qfrag[s * 64 + lane];
+      qrb[s] = qfrag[(S + s) * 64 + lane];
+    }
+  }
   for (int t = w0; t < n_tiles; t += nw) {
     const half8* p = corpus + (int64_t)t * (S * 64) + lane;
     floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
@@ -3036,8 +3084,13 @@ __global__ __launch_bounds__(256) void lk_collect_kernel(const half8* __restrict
 #pragma unroll
       for (int s = 0; s < CH; ++s) {
         a[s] = __builtin_nontemporal_load(p + (c * CH + s) * 64);
-        b0[s] = qfrag[(c * CH + s) * 64 + lane];
-        b1[s] = qfrag[(S + c * CH + s) * 64 + lane];
+        if constexpr (QREG) {
+          b0[s] = qra[c * CH + s];
+          b1[s] = qrb[c * CH + s];
+        } else {
+          b0[s] = qfrag[(c * CH + s) * 64 + lane];
+          b1[s] = qfrag[(S + c * CH + s) * 64 + lane];
+        }
       }
 #pragma unroll
       for (int s = 0; s < CH; ++s) {
@@ -3072,11 +3125,46 @@ __global__ __launch_bounds__(256) void lk_collect_kernel(const half8* __restrict
 
 // per query (workgroup q < B): exact rescoring of the candidates, then the top-k by
 // (score desc, row asc) -> output; on overflow a tighter thr and another round (see above).
+// 3a. exact scores of query q's kept candidates (lk_collect's list), 256 candidates per
+// workgroup, grid (kLkCap / 256, B): the same canonical fp64 order as select / the oracle
+// (exact_scores_wave), 8 rows per wave per round trip. One workgroup per query rescored
+// ~1,300 candidates at k = 33 in ~0.6 ms of serial round trips (round 5).
+template <int D>
+__global__ __launch_bounds__(256) void lk_rescore_kernel(const half8* __restrict__ corpus,
+                                                         const float* __restrict__ qn,
+                                                         const int* __restrict__ cnt,
+                                                         const int* __restrict__ cand,
+                                                         const int* __restrict__ again,
+                                                         const int* __restrict__ need, int round,
+                                                         float* __restrict__ es_g,
+                                                         const float* __restrict__ rows32) {
+  const int q = blockIdx.y, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (!need[round] || !again[q]) return;
+  const int n = min(cnt[q], kLkCap);
+  const int c0 = blockIdx.x * 256, c1 = min(n, c0 + 256);
+  if (c0 >= c1) return;
+  const int* cq = cand + (int64_t)q * kLkCap;
+  const float* qq = qn + (int64_t)q * D;
+  constexpr int NC = 8;
+  for (int i0 = c0 + wid * NC; i0 < c1; i0 += 4 * NC) {
+    int rows[NC];
+#pragma unroll
+    for (int j = 0; j < NC; ++j) rows[j] = i0 + j < c1 ? cq[i0 + j] : -1;
+    float sc[NC];
+    exact_scores_wave<D, NC>(corpus, rows, qq, lane, sc, rows32);
+    if (lane == 0)
+#pragma unroll
+      for (int j = 0; j < NC; ++j)
+        if (i0 + j < c1) es_g[(int64_t)q * kLkCap + i0 + j] = sc[j];
+  }
+}
+
 template <int D>
 __global__ __launch_bounds__(256) void lk_final_kernel(const half8* __restrict__ corpus,
                                                        const float* __restrict__ qn, int k,
                                                        int* __restrict__ cnt,
                                                        const int* __restrict__ cand,
+                                                       const float* __restrict__ es_g,
                                                        const float* __restrict__ eps,
                                                        float* __restrict__ thr,
                                                        int* __restrict__ again,
@@ -3091,26 +3179,14 @@ __global__ __launch_bounds__(256) void lk_final_kernel(const half8* __restrict__
   __shared__ float es[kLkCap];            // exact scores of the kept candidates
   __shared__ float ss[kLkMax];            // the selected entries (sorted in place)
   __shared__ int si[kLkMax];
-  __shared__ int red, red2, verdict;
-  const int q = blockIdx.x, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  __shared__ int red, red2, verdict, hist[256], sh[2];
+  const int q = blockIdx.x;
   if (!need[round] || !again[q]) return;
   const int total = cnt[q];
   const int n = min(total, kLkCap);
   const int* cq = cand + (int64_t)q * kLkCap;
-  const float* qq = qn + (int64_t)q * D;
-  // 1. exact scores of the kept candidates, 8 rows per wave per round trip
-  constexpr int NC = 8;
-  for (int i0 = wid * NC; i0 < n; i0 += 4 * NC) {
-    int rows[NC];
-#pragma unroll
-    for (int j = 0; j < NC; ++j) rows[j] = i0 + j < n ? cq[i0 + j] : -1;
-    float sc[NC];
-    exact_scores_wave<D, NC>(corpus, rows, qq, lane, sc, rows32);
-    if (lane == 0)
-#pragma unroll
-      for (int j = 0; j < NC; ++j)
-        if (i0 + j < n) es[i0 + j] = sc[j];
-  }
+  // 1. the kept candidates' exact scores (lk_rescore_kernel, spread over many workgroups)
+  for (int i = threadIdx.x; i < n; i += 256) es[i] = es_g[(int64_t)q * kLkCap + i];
   __syncthreads();
   // block-wide count of the candidates passing pred(i)
   auto count_if = [&](auto pred) -> int {
@@ -3127,11 +3203,7 @@ __global__ __launch_bounds__(256) void lk_final_kernel(const half8* __restrict__
   // 2. tkey = the key of the kk-th best exact score among the kept candidates
   const int kk = min(k, n);
   uint32_t tkey = 0;
-  if (kk > 0)
-    for (int bit = 31; bit >= 0; --bit) {
-      const uint32_t c = tkey | (1u << bit);
-      if (count_if([&](int i) { return fkey(es[i]) >= c; }) >= kk) tkey = c;
-    }
+  if (kk > 0) tkey = radix_kth_key([&](int i) { return fkey(es[i]); }, n, kk, hist, sh);
   if (total > kLkCap) {
     // overflow: the kept candidates are real rows, so e_k >= fkey_inv(tkey) and every exact
     // top-k row has a >= that - eps: a tighter threshold for the next round
