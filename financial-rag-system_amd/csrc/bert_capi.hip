@@ -85,6 +85,7 @@ struct EncWorkspace {
            *ffcl = nullptr;
   // deferred LayerNorm: row statistics of z after the attention block (sa) / the FFN (sb)
   float *sa = nullptr, *sb = nullptr;
+
   // hipGraph replay of small-batch forwards (forward_graph): executable graphs keyed by the
   // padded shape (B, T, max_len), the padded inputs they read ([ids T | types T | cu B+1])
   // and the rows they write. A graph holds this workspace's buffer addresses: any regrowth

@@ -227,6 +227,86 @@ __device__ __forceinline__ float wave_sum64(float v) {
 // forward's residual passes (2 per layer, ~87 launches per 32-query encode) were
 // latency-bound on 2-byte accesses and 12 dependent ds_bpermute round trips.
 // Same formula, parts summed in part order; the reduction order differs from add_ln_kernel's.
+// ln384_rows: R rows t[0..R) of one wave (t < 0: none), every row's loads issued before any
+// row's reductions (add_ln384_kernel: R = 1). Round 5 also ran it with R = 4 inside the SMALL
+// split-K GEMM, the last arriving workgroup of each 64-row block finishing the block behind an
+// agent-scope release / acquire ticket: bit-identical forward, but the per-unit L2 write-back
+// of the release made the 32-query forward 0.71 -> 1.17 ms (profiles/r05r_split_ln_ab.jsonl).
+template <bool XF, int R>
+__device__ __forceinline__ void ln384_rows(float* __restrict__ x, const float* __restrict__ y,
+                                           const float* __restrict__ g,
+                                           const float* __restrict__ bt, float eps,
+                                           _Float16* __restrict__ xh, _Float16* __restrict__ xl,
+                                           const int64_t (&t)[R], int lane, int parts,
+                                           int64_t pstride) {
+  constexpr int H = 384;
+  const bool on = lane < H / 8;
+  float v[R][8];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int64_t o = (t[r] < 0 ? 0 : t[r]) * H + 8 * (on ? lane : 0);
+    if (on && t[r] >= 0) {
+      floatx4 y0 = *reinterpret_cast<const floatx4*>(y + o);
+      floatx4 y1 = *reinterpret_cast<const floatx4*>(y + o + 4);
+#pragma unroll
+      for (int p = 1; p < 4; ++p)
+        if (p < parts) {
+          y0 += *reinterpret_cast<const floatx4*>(y + p * pstride + o);
+          y1 += *reinterpret_cast<const floatx4*>(y + p * pstride + o + 4);
+        }
+      if constexpr (XF) {
+        const half8 h = *reinterpret_cast<const half8*>(xh + o);
+        const half8 l = xl ? *reinterpret_cast<const half8*>(xl + o) : half8{};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[r][e] = ((float)h[e] + (float)l[e]) + (e < 4 ? y0[e] : y1[e - 4]);
+      } else {
+        const floatx4 r0 = *reinterpret_cast<const floatx4*>(x + o);
+        const floatx4 r1 = *reinterpret_cast<const floatx4*>(x + o + 4);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[r][e] = (e < 4 ? r0[e] : r1[e - 4]) + (e < 4 ? y0[e] : y1[e - 4]);
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[r][e] = 0.f;
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    if (t[r] < 0) continue;                     // (wave-uniform)
+    const int64_t o = t[r] * H + 8 * (on ? lane : 0);
+    const float s = ((v[r][0] + v[r][1]) + (v[r][2] + v[r][3])) +
+                    ((v[r][4] + v[r][5]) + (v[r][6] + v[r][7]));
+    const float mu = wave_sum64(s) * (1.0f / H);
+    float q = 0.f;
+    if (on)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) q = fmaf(v[r][e] - mu, v[r][e] - mu, q);
+    const float rs = rsqrtf(wave_sum64(q) * (1.0f / H) + eps);
+    if (!on) continue;
+    const floatx4 g0 = *reinterpret_cast<const floatx4*>(g + 8 * lane);
+    const floatx4 g1 = *reinterpret_cast<const floatx4*>(g + 8 * lane + 4);
+    const floatx4 b0 = *reinterpret_cast<const floatx4*>(bt + 8 * lane);
+    const floatx4 b1 = *reinterpret_cast<const floatx4*>(bt + 8 * lane + 4);
+    float out[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      out[e] = (v[r][e] - mu) * rs * (e < 4 ? g0[e] : g1[e - 4]) + (e < 4 ? b0[e] : b1[e - 4]);
+    if constexpr (!XF) {
+      *reinterpret_cast<floatx4*>(x + o) = floatx4{out[0], out[1], out[2], out[3]};
+      *reinterpret_cast<floatx4*>(x + o + 4) = floatx4{out[4], out[5], out[6], out[7]};
+    }
+    half8 hh, ll;
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) {
+      half2 h2, l2;
+      split16x2(out[e], out[e + 1], h2, l2);
+      hh[e] = h2[0]; hh[e + 1] = h2[1]; ll[e] = l2[0]; ll[e + 1] = l2[1];
+    }
+    *reinterpret_cast<half8*>(xh + o) = hh;
+    if (xl) *reinterpret_cast<half8*>(xl + o) = ll;
+  }
+}
+
 template <bool XF>
 __global__ __launch_bounds__(256) void add_ln384_kernel(float* __restrict__ x,
                                                         const float* __restrict__ y,
@@ -235,66 +315,10 @@ __global__ __launch_bounds__(256) void add_ln384_kernel(float* __restrict__ x,
                                                         _Float16* __restrict__ xh,
                                                         _Float16* __restrict__ xl, int T,
                                                         int parts = 1, int64_t pstride = 0) {
-  constexpr int H = 384;
   const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
   if (t >= T) return;
-  const bool on = lane < H / 8;
-  const int64_t o = t * H + 8 * (on ? lane : 0);
-  float v[8];
-  if (on) {
-    floatx4 y0 = *reinterpret_cast<const floatx4*>(y + o);
-    floatx4 y1 = *reinterpret_cast<const floatx4*>(y + o + 4);
-#pragma unroll
-    for (int p = 1; p < 4; ++p)
-      if (p < parts) {
-        y0 += *reinterpret_cast<const floatx4*>(y + p * pstride + o);
-        y1 += *reinterpret_cast<const floatx4*>(y + p * pstride + o + 4);
-      }
-    if constexpr (XF) {
-      const half8 h = *reinterpret_cast<const half8*>(xh + o);
-      const half8 l = xl ? *reinterpret_cast<const half8*>(xl + o) : half8{};
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = ((float)h[e] + (float)l[e]) + (e < 4 ? y0[e] : y1[e - 4]);
-    } else {
-      const floatx4 r0 = *reinterpret_cast<const floatx4*>(x + o);
-      const floatx4 r1 = *reinterpret_cast<const floatx4*>(x + o + 4);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = (e < 4 ? r0[e] : r1[e - 4]) + (e < 4 ? y0[e] : y1[e - 4]);
-    }
-  } else {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = 0.f;
-  }
-  float s = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
-  const float mu = wave_sum64(s) * (1.0f / H);
-  float q = 0.f;
-  if (on)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) q = fmaf(v[e] - mu, v[e] - mu, q);
-  const float rs = rsqrtf(wave_sum64(q) * (1.0f / H) + eps);
-  if (!on) return;
-  const floatx4 g0 = *reinterpret_cast<const floatx4*>(g + 8 * lane);
-  const floatx4 g1 = *reinterpret_cast<const floatx4*>(g + 8 * lane + 4);
-  const floatx4 b0 = *reinterpret_cast<const floatx4*>(bt + 8 * lane);
-  const floatx4 b1 = *reinterpret_cast<const floatx4*>(bt + 8 * lane + 4);
-  float out[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e)
-    out[e] = (v[e] - mu) * rs * (e < 4 ? g0[e] : g1[e - 4]) + (e < 4 ? b0[e] : b1[e - 4]);
-  if constexpr (!XF) {
-    *reinterpret_cast<floatx4*>(x + o) = floatx4{out[0], out[1], out[2], out[3]};
-    *reinterpret_cast<floatx4*>(x + o + 4) = floatx4{out[4], out[5], out[6], out[7]};
-  }
-  half8 hh, ll;
-#pragma unroll
-  for (int e = 0; e < 8; e += 2) {
-    half2 h2, l2;
-    split16x2(out[e], out[e + 1], h2, l2);
-    hh[e] = h2[0]; hh[e + 1] = h2[1]; ll[e] = l2[0]; ll[e + 1] = l2[1];
-  }
-  *reinterpret_cast<half8*>(xh + o) = hh;
-  if (xl) *reinterpret_cast<half8*>(xl + o) = ll;
+  const int64_t tr[1] = {t};
+  ln384_rows<XF, 1>(x, y, g, bt, eps, xh, xl, tr, threadIdx.x & 63, parts, pstride);
 }
 
 // ----------------------------------------------------------------------------------------
