@@ -337,6 +337,10 @@ def main():
     ap.add_argument("--no-configs", action="store_true",
                     help="default line without the config-2 / config-3 legs (profiling runs: "
                          "their 1M-row scans share the headline scan kernel's name)")
+    ap.add_argument("--certify", action="store_true",
+                    help="--config 5: certify EVERY timed batch exact after the timed region "
+                         "(oracle rescoring + an fp32 GEMM superset; scripts/bench_modes.py "
+                         "_certify_all) instead of recall on two batches")
     ap.add_argument("--config-steps", type=int, default=200,
                     help="timed batches of each config-2 / config-3 leg (warmup 20)")
     args = ap.parse_args()
@@ -646,7 +650,11 @@ def _config_leg(args, cfg: str) -> dict:
     t0 = time.perf_counter()
     env = {k: v for k, v in os.environ.items()
            if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
-    r = subprocess.run(cmd, stdout=subprocess.PIPE, env=env, text=True, timeout=900)
+    try:
+        r = subprocess.run(cmd, stdout=subprocess.PIPE, env=env, text=True, timeout=900)
+    except (subprocess.TimeoutExpired, OSError) as e:
+        # the headline is already measured: a hung or unstartable leg must not lose its line
+        return {"error": f"config {cfg} leg: {type(e).__name__}: {e}"}
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     if r.returncode != 0 or not lines:
         return {"error": f"config {cfg} leg exited {r.returncode}"}

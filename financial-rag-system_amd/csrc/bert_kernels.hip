@@ -1669,6 +1669,9 @@ struct AttnState {
 // same 4 waves per SIMD) measured slower at the rerank shape (profiles/r02q_attn_pairs.jsonl,
 // same process, 7 rounds): 10 -> 26 0.254 -> 0.282 ms, 2 -> 18 0.268 -> 0.303: a diagnostic.
 constexpr int kAttnVar = 42;
+// rag_bert_attention's A/B slot in the production library: VAR 10 = 42 without the peeled,
+// prefetched block loop (bitwise the same outputs, tests/test_attention_gpu.py)
+constexpr int kAttnVarAB = 10;
 template <int H, int HD, bool SPLIT, int VAR = kAttnVar>
 __global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) void attn_kernel(
     const _Float16* __restrict__ qkv, const _Float16* __restrict__ qkv_lo,

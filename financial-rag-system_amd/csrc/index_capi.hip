@@ -9,6 +9,7 @@
 #include <cstdlib>
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -17,6 +18,8 @@
 #include "../../include/ragmi.h"
 #include "common_host.hpp"
 #include "scan_kernels.hip"
+
+#include <hipcub/hipcub.hpp>
 
 using ragmi::half8;
 
@@ -68,6 +71,7 @@ struct Workspace {
   hipEvent_t ev_out = nullptr;
   hipStream_t owner = nullptr;  // stream of the last pass that used this slot
   int cus = 0;                  // CUs the owner stream may use (its CU mask; stream_cus)
+  uint64_t cus_gen = 0;         // g_stream_gen when `cus` was read
   bool used = false;
   uint64_t tick = 0;            // last use (LRU rebinding)
 };
@@ -161,6 +165,11 @@ double store_eps(const rag_index* h) {
   if (h->storage != RAG_STORE_FP32) return 0.0;
   return (0x1p-11 * (1.0 + 0x1p-20) + 0x1p-25 * std::sqrt((double)h->dim)) * (1.0 + 0x1p-20);
 }
+
+// Bumped by every rag_stream_create_cu_partition / rag_stream_destroy: a workspace's cached CU
+// count is re-read when it changed, so a stream created later at a destroyed partition
+// stream's address (with another mask, or none) never inherits the old count.
+std::atomic<uint64_t> g_stream_gen{1};
 
 // CUs a stream may run on: its CU mask (rag_stream_create_cu_partition gives each of the
 // batches in flight its own share of the CUs), popcounted once per workspace binding; the null
@@ -441,16 +450,101 @@ int ensure_lk(Workspace& w) {
   using namespace ragmi;
   if (w.lk_cand) return RAG_OK;
   const size_t Q = kQ;
-  const bool ok =
-      hipMalloc(reinterpret_cast<void**>(&w.lk_smax), Q * kLkSampleMax * 4) == hipSuccess &&
-      hipMalloc(reinterpret_cast<void**>(&w.lk_thr), Q * 4) == hipSuccess &&
-      hipMalloc(reinterpret_cast<void**>(&w.lk_cnt), Q * 4) == hipSuccess &&
-      hipMalloc(reinterpret_cast<void**>(&w.lk_again), Q * 4) == hipSuccess &&
-      hipMalloc(reinterpret_cast<void**>(&w.lk_need), 64) == hipSuccess &&
-      hipMalloc(reinterpret_cast<void**>(&w.lk_cand), Q * kLkCap * 4) == hipSuccess &&
-      hipMalloc(reinterpret_cast<void**>(&w.lk_es), Q * kLkCap * 4) == hipSuccess;
-  if (!ok) return ragmi::fail(RAG_ENOMEM, "large-k workspace allocation failed");
+  // all seven or none: each buffer is allocated into a local and the workspace takes them only
+  // when every allocation succeeded (a partial set would be re-allocated, and leaked, by the
+  // next large-k call)
+  void* p[7] = {};
+  const size_t bytes[7] = {Q * kLkSampleMax * 4, Q * 4, Q * 4, Q * 4, 64, Q * kLkCap * 4,
+                           Q * kLkCap * 4};
+  for (int i = 0; i < 7; ++i) {
+    if (hipMalloc(&p[i], bytes[i]) != hipSuccess) {
+      (void)hipGetLastError();
+      for (int j = 0; j < i; ++j) (void)hipFree(p[j]);
+      return ragmi::fail(RAG_ENOMEM, "large-k workspace allocation failed");
+    }
+  }
+  w.lk_smax = static_cast<float*>(p[0]);
+  w.lk_thr = static_cast<float*>(p[1]);
+  w.lk_cnt = static_cast<int*>(p[2]);
+  w.lk_again = static_cast<int*>(p[3]);
+  w.lk_need = static_cast<int*>(p[4]);
+  w.lk_cand = static_cast<int*>(p[5]);
+  w.lk_es = static_cast<float*>(p[6]);
   return RAG_OK;
+}
+
+// One search pass of <= 32 queries by the full exact path (scan_kernels.hip "Exact top-k
+// for ANY k"): k > RAG_MAX_K_LARGE, or rag_index_search_full. Per query: exact scores of every
+// row, a stable descending radix sort of (key, row), the first k emitted. The sort buffers
+// (16 B per row + hipcub's scratch) are stream-ordered allocations released at the pass's end.
+template <int D>
+int launch_full_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k,
+                     const uint32_t* filt, int64_t id_offset, float* out_s, int64_t* out_i,
+                     int32_t* out_packed, hipStream_t st) {
+  using namespace ragmi;
+  qprep_kernel<D><<<dim3(kQ), dim3(64), 0, st>>>(q, Bq, filt, w.qn, w.qfrag, w.filt, w.eps,
+                                                  store_eps(h));
+  RAG_HIP(hipGetLastError());
+  const int n = (int)h->count;
+  auto emit_grid = [&]() { return dim3((unsigned)std::min<int64_t>(1024, (k + 255) / 256)); };
+  if (n == 0) {
+    int* zero = nullptr;
+    RAG_HIP(hipMallocAsync(reinterpret_cast<void**>(&zero), 4, st));
+    RAG_HIP(hipMemsetAsync(zero, 0, 4, st));
+    for (int j = 0; j < Bq; ++j)
+      full_emit_kernel<<<emit_grid(), dim3(256), 0, st>>>(
+          nullptr, nullptr, zero, k, id_offset, out_s ? out_s + (int64_t)j * k : nullptr,
+          out_i ? out_i + (int64_t)j * k : nullptr,
+          out_packed ? out_packed + (int64_t)j * k * 2 : nullptr);
+    RAG_HIP(hipGetLastError());
+    RAG_HIP(hipFreeAsync(zero, st));
+    return RAG_OK;
+  }
+  size_t tmp_bytes = 0;
+  RAG_HIP(hipcub::DeviceRadixSort::SortPairsDescending(
+      nullptr, tmp_bytes, static_cast<const uint32_t*>(nullptr), static_cast<uint32_t*>(nullptr),
+      static_cast<const int*>(nullptr), static_cast<int*>(nullptr), n, 0, 32, st));
+  const size_t nb = (size_t)n * 4;
+  char* buf = nullptr;
+  const size_t m_off = 4 * nb, t_off = m_off + 256;
+  RAG_HIP(hipMallocAsync(reinterpret_cast<void**>(&buf), t_off + tmp_bytes, st));
+  uint32_t* k_in = reinterpret_cast<uint32_t*>(buf);
+  uint32_t* k_out = reinterpret_cast<uint32_t*>(buf + nb);
+  int* v_in = reinterpret_cast<int*>(buf + 2 * nb);
+  int* v_out = reinterpret_cast<int*>(buf + 3 * nb);
+  int* n_match = reinterpret_cast<int*>(buf + m_off);
+  void* tmp = buf + t_off;
+  RAG_HIP(hipMemsetAsync(n_match, 0, 4 * kQ, st));
+  // one wave per 8 rows per step; up to 8 workgroups per CU
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(8 * h->n_cu, (n + 31) / 32));
+  int rc = RAG_OK;
+  for (int j = 0; j < Bq && rc == RAG_OK; ++j) {
+    if (filt)
+      full_score_kernel<D, true><<<dim3(grid), dim3(256), 0, st>>>(
+          h->corpus, h->tags, w.filt + 2 * j, w.qn + (int64_t)j * D, n, h->rows32, k_in, v_in,
+          n_match + j);
+    else
+      full_score_kernel<D, false><<<dim3(grid), dim3(256), 0, st>>>(
+          h->corpus, h->tags, nullptr, w.qn + (int64_t)j * D, n, h->rows32, k_in, v_in,
+          n_match + j);
+    if (hipGetLastError() != hipSuccess ||
+        hipcub::DeviceRadixSort::SortPairsDescending(tmp, tmp_bytes,
+                                                     static_cast<const uint32_t*>(k_in), k_out,
+                                                     static_cast<const int*>(v_in), v_out, n, 0,
+                                                     32, st) != hipSuccess) {
+      rc = ragmi::fail(RAG_EHIP, "full exact pass: score / sort launch failed");
+      break;
+    }
+    full_emit_kernel<<<emit_grid(), dim3(256), 0, st>>>(
+        k_out, v_out, n_match + j, k, id_offset, out_s ? out_s + (int64_t)j * k : nullptr,
+        out_i ? out_i + (int64_t)j * k : nullptr,
+        out_packed ? out_packed + (int64_t)j * k * 2 : nullptr);
+    if (hipGetLastError() != hipSuccess) rc = ragmi::fail(RAG_EHIP, "full exact pass: emit");
+  }
+  // the pass certifies every query (tier 0) by construction
+  (void)hipMemsetAsync(w.fb_tier, 0, 4 * kQ, st);
+  (void)hipFreeAsync(buf, st);
+  return rc;
 }
 
 template <int D>
@@ -545,15 +639,19 @@ int upsert_locked(rag_index* h, const float* vecs, const int64_t* rows, const ui
   return RAG_OK;
 }
 
+// full: the full exact path for every query (rag_index_search_full); it is also taken for
+// k > RAG_MAX_K_LARGE (unpacked output only: the exchange merge holds at most that many)
 int search_locked(rag_index* h, const float* q, int B, int k, const uint32_t* filt,
                   int64_t id_offset, float* out_s, int64_t* out_i, int32_t* out_packed,
-                  hipStream_t st) {
+                  hipStream_t st, bool full = false) {
   if (B < 0 || (B > 0 && (!q || (!out_packed && (!out_s || !out_i)))))
     return ragmi::fail(RAG_EINVAL, "bad search args");
-  if (k < 1 || k > RAG_MAX_K_LARGE)
-    return ragmi::fail(RAG_ERANGE, "k must be in [1, RAG_MAX_K_LARGE=4096]");
+  if (k < 1) return ragmi::fail(RAG_ERANGE, "k must be >= 1");
+  if (out_packed && k > RAG_MAX_K_LARGE)
+    return ragmi::fail(RAG_ERANGE, "packed (exchange) search: k must be <= RAG_MAX_K_LARGE=4096");
+  full = full || k > RAG_MAX_K_LARGE;
   RAG_HIP(hipSetDevice(h->device));
-  const bool large = k > RAG_MAX_K;
+  const bool large = k > RAG_MAX_K || full;
   const int per_pass = large ? ragmi::kQ : ragmi::kQ * h->groups;
   for (int b0 = 0; b0 < B; b0 += per_pass) {
     const int Bq = std::min(per_pass, B - b0);
@@ -571,7 +669,11 @@ int search_locked(rag_index* h, const float* q, int B, int k, const uint32_t* fi
         if (s.tick < wp->tick) wp = &s;
     }
     Workspace& w = *wp;
-    if (!w.used || w.owner != st || w.cus == 0) w.cus = stream_cus(h, st);
+    const uint64_t gen = g_stream_gen.load(std::memory_order_acquire);
+    if (!w.used || w.owner != st || w.cus == 0 || w.cus_gen != gen) {
+      w.cus = stream_cus(h, st);
+      w.cus_gen = gen;
+    }
     w.used = true;
     w.owner = st;
     w.tick = ++h->ws_tick;
@@ -583,6 +685,15 @@ int search_locked(rag_index* h, const float* q, int B, int k, const uint32_t* fi
       int64_t* oi = out_packed ? nullptr : out_i + (int64_t)b0 * k;
       int32_t* op = out_packed ? out_packed + (int64_t)b0 * k * 2 : nullptr;
       const uint32_t* fq = filt ? filt + 2 * b0 : nullptr;
+      if (full) {
+        rc = h->dim == 384
+                 ? launch_full_pass<384>(h, w, q + (int64_t)b0 * h->dim, Bq, k, fq, id_offset, os,
+                                         oi, op, st)
+                 : launch_full_pass<1024>(h, w, q + (int64_t)b0 * h->dim, Bq, k, fq, id_offset,
+                                          os, oi, op, st);
+        if (rc) return rc;
+        continue;
+      }
       rc = h->dim == 384
                ? launch_large_k_pass<384>(h, w, q + (int64_t)b0 * h->dim, Bq, k, fq, id_offset, os,
                                           oi, op, st)
@@ -653,6 +764,7 @@ int bench_scan(rag_index* h, const float* q, int B, int variant, int reps, doubl
   half8* rows64 = nullptr;
   half8* qc = nullptr;
   const int n_groups = (int)((h->count + 63) / 64);
+#ifdef RAGMI_DIAG_BUILD
   if (variant == 8) {
     RAG_HIP(hipMalloc(reinterpret_cast<void**>(&rows64), (size_t)n_groups * 64 * D * 2));
     RAG_HIP(hipMalloc(reinterpret_cast<void**>(&qc), (size_t)kQ * D * 2));
@@ -662,11 +774,18 @@ int bench_scan(rag_index* h, const float* q, int B, int variant, int reps, doubl
         h->corpus, h->count, rows64);
     qchunk_kernel<D><<<dim3(kQ), dim3(64), 0, nullptr>>>(w.qn, qc);
   }
+#endif
   const int vgrid = std::min(h->max_wgs, std::max(1, (n_groups + 3) / 4));
+  (void)vgrid;
   hipEvent_t a, b;
   RAG_HIP(hipEventCreate(&a));
   RAG_HIP(hipEventCreate(&b));
   auto one = [&]() {
+#ifndef RAGMI_DIAG_BUILD
+    // production library: the production scan only (variants 0 and 7); the MODE / DYN /
+    // VALU probes are instantiated in the diagnostic build alone
+    launch_variant<D, 0>(h, w, grid, nullptr);
+#else
     if (variant == 8) {
       scan_valu_kernel<D><<<dim3(vgrid), dim3(256), 0, nullptr>>>(
           rows64, qc, (int)h->count, n_groups, w.seed, w.part_s, w.part_i, w.heads_s,
@@ -685,8 +804,10 @@ int bench_scan(rag_index* h, const float* q, int B, int variant, int reps, doubl
       case 16: launch_variant<D, 16>(h, w, grid, nullptr); break;
       default: launch_variant<D, 6>(h, w, grid, nullptr); break;
     }
+#endif
   };
   float ms = 0.f;
+#ifdef RAGMI_DIAG_BUILD
   if (variant >= 9 && variant <= 14) {
     // one launch per event pair; the tile-queue heads are zeroed before each, outside it
     for (int r = -1; r < reps; ++r) {
@@ -706,7 +827,9 @@ int bench_scan(rag_index* h, const float* q, int B, int variant, int reps, doubl
       RAG_HIP(hipEventElapsedTime(&m1, a, b));
       if (r >= 0) ms += m1;   // r = -1: warm-up
     }
-  } else {
+  } else
+#endif
+  {
     one();  // warm
     RAG_HIP(hipEventRecord(a, nullptr));
     for (int r = 0; r < reps; ++r) one();
@@ -742,6 +865,7 @@ int bench_wide(rag_index* h, const float* q, int B, int mode, int reps, double* 
   launch_fixed<kWideBlock>(scan_wide_kernel<D, MODE, true>, dim3(grid), 0, nullptr,          \
                            h->corpus, w.qfrag, (int)h->count, (int)n_tiles, w.seed, w.part_s, \
                            w.part_i, w.heads_s, w.heads_i, w.heads_n, groups)
+#ifdef RAGMI_DIAG_BUILD
     switch (mode) {
       case 1: RAG_WIDE(1); break;
       case 2: RAG_WIDE(2); break;
@@ -749,6 +873,9 @@ int bench_wide(rag_index* h, const float* q, int B, int mode, int reps, double* 
       case 4: RAG_WIDE(4); break;
       default: RAG_WIDE(0); break;
     }
+#else
+    RAG_WIDE(0);
+#endif
 #undef RAG_WIDE
   };
   hipEvent_t a, b;
@@ -869,6 +996,14 @@ int rag_index_create_ex(int dim, int64_t capacity_rows, int device, int storage,
   }
   *out = h;
   return RAG_OK;
+}
+
+int rag_diagnostic_build(void) {
+#ifdef RAGMI_DIAG_BUILD
+  return 1;
+#else
+  return 0;
+#endif
 }
 
 int rag_knob_probe(const char* name, int dflt) {
@@ -1019,6 +1154,15 @@ int rag_index_search(rag_index_t* h, const float* q, int B, int k, const uint32_
                        static_cast<hipStream_t>(stream));
 }
 
+int rag_index_search_full(rag_index_t* h, const float* q, int B, int k, const uint32_t* filters,
+                          int64_t id_offset, float* out_s, int64_t* out_i, void* stream) {
+  ragmi::clear_error();
+  if (!h) return ragmi::fail(RAG_EINVAL, "index is NULL");
+  std::lock_guard<std::mutex> lk(h->mu);
+  return search_locked(h, q, B, k, filters, id_offset, out_s, out_i, nullptr,
+                       static_cast<hipStream_t>(stream), true);
+}
+
 int rag_index_search_packed(rag_index_t* h, const float* q, int B, int k,
                             const uint32_t* filters, int64_t id_offset, int32_t* out_packed,
                             void* stream) {
@@ -1037,8 +1181,7 @@ int rag_index_search_host(rag_index_t* h, const float* q, int B, int k,
   ragmi::clear_error();
   if (!h) return ragmi::fail(RAG_EINVAL, "index is NULL");
   if (B < 0 || (B > 0 && (!q || !out_s || !out_i))) return ragmi::fail(RAG_EINVAL, "bad search args");
-  if (k < 1 || k > RAG_MAX_K_LARGE)
-    return ragmi::fail(RAG_ERANGE, "k must be in [1, RAG_MAX_K_LARGE=4096]");
+  if (k < 1) return ragmi::fail(RAG_ERANGE, "k must be >= 1");
   if (B == 0) return RAG_OK;
   std::lock_guard<std::mutex> lk(h->mu);
   RAG_HIP(hipSetDevice(h->device));
@@ -1199,6 +1342,11 @@ int rag_merge_topk_packed(const int32_t* in_packed, int n_lists, int B, int k, f
 int rag_bench_scan(rag_index_t* h, const float* queries_dev, int B, int variant, int reps,
                    double* avg_ms) {
   ragmi::clear_error();
+#ifndef RAGMI_DIAG_BUILD
+  if (variant != 0 && (variant != 7 || (h && h->dim != 384)))
+    return ragmi::fail(RAG_EINVAL, "variant: 0 (production) or 7 (dim 384: seeds at +inf); the "
+                                   "scan's timing probes are in the diagnostic build only");
+#endif
   if (!h || !queries_dev || B < 1 || reps < 1 || !avg_ms || variant < 0 || variant > 16)
     return ragmi::fail(RAG_EINVAL, "bad bench args");
   std::lock_guard<std::mutex> lk(h->mu);
@@ -1293,12 +1441,14 @@ int rag_stream_create_cu_partition(int device, int part, int parts, void** out) 
   if (e != hipSuccess)
     return ragmi::fail(RAG_EHIP, std::string("hipExtStreamCreateWithCUMask: ") + hipGetErrorString(e));
   *out = st;
+  g_stream_gen.fetch_add(1, std::memory_order_acq_rel);
   return RAG_OK;
 }
 
 int rag_stream_destroy(void* stream) {
   ragmi::clear_error();
   if (!stream) return RAG_OK;
+  g_stream_gen.fetch_add(1, std::memory_order_acq_rel);
   RAG_HIP(hipStreamDestroy(static_cast<hipStream_t>(stream)));
   return RAG_OK;
 }

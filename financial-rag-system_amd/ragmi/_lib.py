@@ -101,6 +101,8 @@ INDEX_API = {
                                              ctypes.c_int64]),
     "rag_index_search": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, ctypes.c_int, c_vp,
                                         ctypes.c_int64, c_vp, c_vp, c_vp]),
+    "rag_index_search_full": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, ctypes.c_int, c_vp,
+                                             ctypes.c_int64, c_vp, c_vp, c_vp]),
     "rag_index_search_packed": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, ctypes.c_int, c_vp,
                                                ctypes.c_int64, c_vp, c_vp]),
     "rag_index_search_host": (ctypes.c_int, [c_vp, c_f32p, ctypes.c_int, ctypes.c_int, c_u32p,
@@ -122,6 +124,7 @@ INDEX_API = {
     "rag_index_exactness_stats": (ctypes.c_int, [c_vp, c_i64p, c_i64p, c_i32p, ctypes.c_int]),
     "rag_index_unanswered": (ctypes.c_int, [c_vp, c_i64p]),
     "rag_knob_probe": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int]),
+    "rag_diagnostic_build": (ctypes.c_int, []),
     "rag_profile_enable": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "rag_profile_scan_ms": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_double), c_i64p]),
     "rag_profile_scan_intervals": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_double),

@@ -18,7 +18,8 @@ from . import _lib
 from ._lib import check
 
 MAX_K = 32          # RAG_MAX_K in include/ragmi.h: the scan's certified top-k path
-MAX_K_LARGE = 4096  # RAG_MAX_K_LARGE: k in (32, 4096] takes the exact large-k pass
+MAX_K_LARGE = 4096  # RAG_MAX_K_LARGE: k in (32, 4096] takes the exact large-k pass; larger k
+                    # the full exact pass (and the packed exchange form stops here)
 QUERY_TILE = 32     # RAG_QUERY_TILE
 STORAGE = {"fp16": 0, "fp32": 1}   # RAG_STORE_FP16 / RAG_STORE_FP32
 CREATE_DIAGNOSTIC = 0x100          # RAG_CREATE_DIAGNOSTIC: honour the RAGMI_* A/B knobs
@@ -114,9 +115,9 @@ class FlatIndex:
                                        _stream_ptr(self.device)))
 
     # ---------------------------------------------------------------- search
-    def _search_args(self, queries, k, filters):
-        if not 1 <= k <= MAX_K_LARGE:
-            raise ValueError(f"k must be in [1, {MAX_K_LARGE}]")
+    def _search_args(self, queries, k, filters, k_max=None):
+        if k < 1 or (k_max is not None and k > k_max):
+            raise ValueError(f"k must be in [1, {k_max}]" if k_max else "k must be >= 1")
         q = _as_dev(queries, torch.float32, self.device)
         if q.dim() == 1:
             q = q.unsqueeze(0)
@@ -138,7 +139,7 @@ class FlatIndex:
     def search_packed(self, queries, k: int, filters=None, id_offset: int = 0) -> torch.Tensor:
         """Top-k in the multi-GPU exchange form: int32 [B, k, 2] = (fp32 score bits, global
         row; -1 = none), enqueued on the current stream (rag_index_search_packed)."""
-        q, B, f = self._search_args(queries, k, filters)
+        q, B, f = self._search_args(queries, k, filters, k_max=MAX_K_LARGE)
         out = torch.empty((B, k, 2), dtype=torch.int32, device=self.device)
         check(self._L.rag_index_search_packed(self._h, q.data_ptr(), B, int(k),
                                               f.data_ptr() if f is not None else None,
@@ -147,20 +148,25 @@ class FlatIndex:
         return out
 
     def search(self, queries, k: int, filters=None, id_offset: int = 0,
-               out: tuple[torch.Tensor, torch.Tensor] | None = None):
+               out: tuple[torch.Tensor, torch.Tensor] | None = None, full: bool = False):
         """Top-k of each query row. Returns (scores fp32 [B,k], ids int64 [B,k]) as cuda
         tensors, enqueued on the current stream (ids -1 where fewer than k rows match).
-        `filters`: None, or per-query (tag_mask, tag_value) pairs [B, 2] (uint32)."""
+        `filters`: None, or per-query (tag_mask, tag_value) pairs [B, 2] (uint32).
+        Any k >= 1: k <= 32 on the scan, k <= 4096 on the large-k pass, beyond on the full
+        exact pass (every row scored exactly, then sorted); full=True forces the full pass
+        (rag_index_search_full) — the same result, the path for queries a large-k pass left
+        unanswered."""
         q, B, f = self._search_args(queries, k, filters)
         if out is None:
             out_s = torch.empty((B, k), dtype=torch.float32, device=self.device)
             out_i = torch.empty((B, k), dtype=torch.int64, device=self.device)
         else:
             out_s, out_i = out
-        check(self._L.rag_index_search(self._h, q.data_ptr(), B, int(k),
-                                       f.data_ptr() if f is not None else None,
-                                       int(id_offset), out_s.data_ptr(), out_i.data_ptr(),
-                                       _stream_ptr(self.device)))
+        fn = self._L.rag_index_search_full if full else self._L.rag_index_search
+        check(fn(self._h, q.data_ptr(), B, int(k),
+                 f.data_ptr() if f is not None else None,
+                 int(id_offset), out_s.data_ptr(), out_i.data_ptr(),
+                 _stream_ptr(self.device)))
         # staging tensors (q, f) go back to torch's stream-ordered caching allocator: any
         # reuse is enqueued on this same stream after our kernels, so no sync is needed.
         return out_s, out_i
@@ -260,9 +266,13 @@ class FlatIndex:
         return int(t1.value), int(t2.value), last
 
     def unanswered(self) -> int:
-        """Marked (tier-2) queries since creation that got NO result because the second pass
-        was skipped (RAGMI_RESCAN_WG=0 on a diagnostic handle; their tier reads 3). Always 0
-        in production (rag_index_unanswered)."""
+        """Queries since creation that got NO result (their tier reads 3, their ids -1):
+        k <= 32 passes whose second pass was skipped (RAGMI_RESCAN_WG=0, diagnostic handles
+        only), and 32 < k <= 4096 passes where more than 16384 rows tie within the MFMA error
+        band of a query's k-th best score after the last collection round (possible in
+        production, e.g. thousands of identical boilerplate chunks). Collection.search re-runs
+        such queries on the full exact pass (search(full=True)). rag_index_unanswered;
+        synchronises the device."""
         n = ctypes.c_int64()
         check(self._L.rag_index_unanswered(self._h, ctypes.byref(n)))
         return int(n.value)

@@ -31,7 +31,7 @@ import numpy as np
 import torch
 
 from . import qdrant_models as models
-from .index import MAX_K, MAX_K_LARGE, FlatIndex
+from .index import MAX_K, FlatIndex
 
 DEFAULT_TAG_FIELDS = ("ticker", "document_type")
 
@@ -54,11 +54,6 @@ def _norm_id(pid):
 
 class UnsupportedFilter(NotImplementedError):
     pass
-
-
-class LimitTooLarge(ValueError):
-    """query_points(limit > RAG_MAX_K_LARGE on a collection of more points): refused loudly,
-    never answered with empty points (ragmi.rag lets it through the reference's swallow)."""
 
 
 class PayloadTags:
@@ -244,6 +239,8 @@ class Collection:
         self.payloads: list[dict | None] = []
         self.versions: list[int] = []
         self.op = 0
+        self._unanswered = 0     # index.unanswered() as last read (Collection.search)
+        self.rescued = 0         # queries re-answered on the full exact pass (stats)
         self.lock = threading.RLock()
         # 32 queries per scan pass at D = 384, 4 groups of 32 at D = 1024 (ragmi.h)
         self.coalescer = Coalescer(self, 0.0, 32 if dim <= 384 else 128)
@@ -295,13 +292,10 @@ class Collection:
             B = len(filters)
             if limit < 1:
                 return [[] for _ in range(B)]
-            # Qdrant answers at most the collection's points: a limit past them is the whole
-            # collection, which fits any k once it holds <= RAG_MAX_K_LARGE points
+            # Qdrant answers any limit with at most the collection's points (main.py:215,
+            # 232-237): k <= 32 on the scan, <= 4096 on the large-k pass, beyond that on the
+            # full exact pass (rag_index_search)
             k = min(limit, max(1, self.index.count))
-            if k > MAX_K_LARGE:
-                raise LimitTooLarge(f"limit {limit} > {MAX_K_LARGE} (RAG_MAX_K_LARGE) over "
-                                    f"{self.index.count} points (the reference uses "
-                                    f"limit=15, main.py:215)")
             live = [i for i, f in enumerate(filters) if f is not None]
             out = [[] for _ in range(B)]
             if not live or self.index.count == 0:
@@ -313,6 +307,21 @@ class Collection:
             s, ids = self.index.search(q, k, filters=use)
             s = s.cpu().numpy()
             ids = ids.cpu().numpy()
+            if (ids < 0).any():
+                # a -1 is padding (fewer matching points than k) unless the pass left the
+                # query unanswered (tier 3: more than 16384 rows tied within the error band
+                # of its k-th best on the large-k pass). Only then, re-run those queries on
+                # the full exact pass: an unanswered query must never read as "no documents"
+                # (ADVICE r5).
+                n_un = self.index.unanswered()
+                if n_un > self._unanswered:
+                    redo = np.nonzero((ids < 0).any(axis=1))[0].tolist()
+                    s2, i2 = self.index.search(q[redo], k, filters=use[redo] if use is not None
+                                               else None, full=True)
+                    s[redo] = s2.cpu().numpy()
+                    ids[redo] = i2.cpu().numpy()
+                    self.rescued += len(redo)
+                self._unanswered = n_un
             for j, i in enumerate(live):
                 out[i] = [(int(r), float(sc)) for r, sc in zip(ids[j], s[j]) if r >= 0]
             return out

@@ -63,12 +63,14 @@ enum {
  * re-scored exactly, from the scan's per-wave lists when they provably hold all of them,
  * otherwise by a second pass over the shard (see rag_index_exactness_stats). */
 #define RAG_MAX_K 32
-/* Largest k overall (round 5; Qdrant's query_points takes any `limit`, main.py:215,232-237).
- * RAG_MAX_K < k <= RAG_MAX_K_LARGE runs a separate exact pass per 32 queries: a sampled
- * certified lower bound of each query's k-th best score, every row whose MFMA score can reach
- * it collected, all of those re-scored exactly, the k best by (score desc, row asc) emitted —
- * the same exact result and canonical scores as the k <= 32 path (scan_kernels.hip, "Exact
- * top-k for RAG_MAX_K < k"). rag_merge_topk[_packed] accept the same k. */
+/* Largest k of the large-k pass (round 5; Qdrant's query_points takes any `limit`,
+ * main.py:215,232-237). RAG_MAX_K < k <= RAG_MAX_K_LARGE runs a separate exact pass per 32
+ * queries: a sampled certified lower bound of each query's k-th best score, every row whose
+ * MFMA score can reach it collected, all of those re-scored exactly, the k best by (score
+ * desc, row asc) emitted — the same exact result and canonical scores as the k <= 32 path
+ * (scan_kernels.hip, "Exact top-k for RAG_MAX_K < k"). rag_merge_topk[_packed] and
+ * rag_index_search_packed accept k up to this. rag_index_search itself takes ANY k >= 1:
+ * k > RAG_MAX_K_LARGE runs the full exact pass (rag_index_search_full, round 6). */
 #define RAG_MAX_K_LARGE 4096
 /* Queries handled per scan pass; larger batches run ceil(B/32) passes. */
 #define RAG_QUERY_TILE 32
@@ -104,6 +106,11 @@ enum { RAG_STORE_FP16 = 0, RAG_STORE_FP32 = 1 };
  * value when it is set and diagnostics are on, else `dflt` (reporting an ignored variable
  * once on stderr). Runs the same code path as every knob site; for tests. */
 int rag_knob_probe(const char* name, int dflt);
+/* 1 in a diagnostic build of the library (-DRAGMI_DIAG_BUILD, out of tree: `python
+ * ragmi/_build.py OUT.so -DRAGMI_DIAG_BUILD`), whose rag_bench_scan / rag_bert_attention also
+ * carry the measured timing probes and kernel variants; 0 in the production libragmi.so
+ * (rag_bench_scan variants 0 / 7, rag_bert_attention -1 / 42 / 10 only). */
+int rag_diagnostic_build(void);
 /* rag_index_create with an explicit storage (rag_index_create = RAG_STORE_FP16). */
 int rag_index_create_ex(int dim, int64_t capacity_rows, int device, int storage,
                         rag_index_t** out);
@@ -136,6 +143,16 @@ int rag_index_upsert_host(rag_index_t* index, const float* vecs_host, const int6
 int rag_index_search(rag_index_t* index, const float* queries_dev, int B, int k,
                      const uint32_t* filters_dev, int64_t id_offset,
                      float* out_scores_dev, int64_t* out_ids_dev, void* stream);
+/* rag_index_search by the full exact pass, for any k >= 1: per query every row is scored
+ * exactly (the canonical fp64 order), the (score, row) pairs are radix-sorted (stable, score
+ * descending, so ties stay row-ascending) and the first k emitted, -1 / -inf past the
+ * matching rows. The same result as rag_index_search at every k; ~ms per query at 10M rows.
+ * rag_index_search takes it for k > RAG_MAX_K_LARGE; callers take it to re-answer a query a
+ * large-k pass left unanswered (rag_index_unanswered). No reference counterpart beyond
+ * query_points(limit) itself (main.py:232-237). */
+int rag_index_search_full(rag_index_t* index, const float* queries_dev, int B, int k,
+                          const uint32_t* filters_dev, int64_t id_offset,
+                          float* out_scores_dev, int64_t* out_ids_dev, void* stream);
 /* Same, host pointers (filters_host may be NULL), synchronous. */
 int rag_index_search_host(rag_index_t* index, const float* queries_host, int B, int k,
                           const uint32_t* filters_host, int64_t id_offset,
@@ -188,10 +205,13 @@ int rag_merge_topk_packed(const int32_t* in_packed_dev, int n_lists, int B, int 
 int rag_index_exactness_stats(rag_index_t* index, int64_t* tier1, int64_t* tier2,
                               int32_t* last_tiers, int n_last);
 
-/* Number of marked (tier-2) queries, since the index was created, that received NO result
- * because the second pass was skipped (RAGMI_RESCAN_WG=0, honoured only under
- * RAG_CREATE_DIAGNOSTIC; their last_tiers entry reads 3). Always 0 in production.
- * Synchronises the device. */
+/* Number of queries, since the index was created, that received NO result (-1 ids; their
+ * last_tiers entry reads 3): k <= RAG_MAX_K passes whose second pass was skipped
+ * (RAGMI_RESCAN_WG=0, honoured only under RAG_CREATE_DIAGNOSTIC), and large-k passes
+ * (RAG_MAX_K < k <= RAG_MAX_K_LARGE) where more than 16384 rows tie within the MFMA error band
+ * of a query's k-th best after the last collection round — possible in production (thousands
+ * of identical chunks). Re-answer such queries with rag_index_search_full (the QdrantClient
+ * front end does). Synchronises the device. */
 int rag_index_unanswered(rag_index_t* index, int64_t* n);
 
 /* Scan order across streams. serial = 1: each search pass's scan launch waits for the
@@ -238,7 +258,8 @@ int rag_profile_scan_intervals(rag_index_t* index, double* start_ms, double* end
  * / loads only (9-14 time every launch on its own event pair), 15 production without the
  * end-of-scan sort of pending-only queries (timing probe), 16 production with the round-1
  * end-of-scan sort (A/B). dim 1024: variants 0-4 of
- * the wide (33-128 query) scan. */
+ * the wide (33-128 query) scan. The production library accepts variants 0 and 7 only (dim
+ * 1024: 0); the others are compiled into the diagnostic build (rag_diagnostic_build). */
 int rag_bench_scan(rag_index_t* index, const float* queries_dev, int B, int variant, int reps,
                    double* avg_ms);
 

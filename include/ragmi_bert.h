@@ -153,7 +153,9 @@ int rag_bert_gemm_add_ln(const void* A, const void* A_lo, const void* W, const v
  * ctx_lo: the fp16x3 lo planes (both or neither). variant: the kernel's VAR bit mask, 0..15
  * (1 rolling Q prefetch, 2 fp16x3 row sums by MFMA, 4 software-pipelined scores, 8 lean
  * block), 18 or 26 (16 = two query blocks per wave side by side), or -1 for the one the
- * forward runs. For A/B timing and parity tests. */
+ * forward runs (42). For A/B timing and parity tests. The production library carries -1 / 42
+ * and the A/B slot 10 only; the rest of the family is in the diagnostic build
+ * (rag_diagnostic_build, ragmi.h). */
 int rag_bert_attention(int variant, const void* qkv, const void* qkv_lo, const int32_t* cu,
                        int B, int max_len, void* ctx, void* ctx_lo, void* stream);
 

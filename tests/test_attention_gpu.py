@@ -5,14 +5,25 @@ VAR bit mask: Q prefetch, fp16x3 row sums by MFMA, software-pipelined scores) an
 precisions. Ragged lengths cover the masked tail blocks (len % 32 != 0), a 1-token sequence,
 sequences past 256 keys, and more query blocks per wave than the Q prefetch depth.
 
+The production libragmi.so carries the forward's variant (42) and one A/B slot (10) only
+(VERDICT r5 item 6); the measured family runs against a diagnostic build
+(`python financial-rag-system_amd/ragmi/_build.py OUT.so -DRAGMI_DIAG_BUILD`, loaded with
+RAGMI_LIB_AB=OUT.so and RAGMI_TEST_DIAG_BUILD=1).
+
 Tolerances: fp16x3 carries Q/K/V/P as hi + lo planes (~2^-22 relative), so its error is the
 fp32 accumulation's: 2e-5 absolute on O (|O| <= max|V| = 1); fp16 rounds P to fp16 and
 the output to fp16: 2e-3."""
+import os
+
 import numpy as np
 import pytest
 import torch
 
 pytestmark = pytest.mark.gpu
+
+DIAG = os.environ.get("RAGMI_TEST_DIAG_BUILD") == "1"
+FAMILY = list(range(16)) + [18, 26, 40, 42, 43, 44, 46, 106, 107]
+PRODUCTION = [42, 10, -1]
 
 LENS = [1, 31, 32, 33, 244, 257, 288, 64, 7, 200, 511]
 
@@ -43,7 +54,7 @@ def data():
     return x, hi, lo, cu
 
 
-@pytest.mark.parametrize("variant", list(range(16)) + [18, 26, 40, 42, 43, 44, 46, 106, 107])
+@pytest.mark.parametrize("variant", FAMILY if DIAG else PRODUCTION)
 @pytest.mark.parametrize("split", [True, False], ids=["fp16x3", "fp16"])
 def test_attention_matches_fp32(gpu, data, variant, split):
     from ragmi.encoders import attention
@@ -70,39 +81,41 @@ def test_attention_matches_fp32(gpu, data, variant, split):
                              f"got {got[t, c].item():.6f} ref {ref[t, c].item():.6f}")
 
 
-@pytest.mark.parametrize("variant", [0, 2, 4, 6])
-@pytest.mark.parametrize("split", [True, False], ids=["fp16x3", "fp16"])
-def test_lean_block_is_bitwise_identical(gpu, data, variant, split):
-    """VAR bit 8 (permlane max, split16x2 of P and O, batched V^T reads) changes how the same
-    arithmetic is issued, not the arithmetic: outputs equal the variant without it bit for
-    bit (split16x2's fp16(v - hi) by v_fma_mix equals split16's convert-subtract-convert)."""
-    from ragmi.encoders import attention
-    x, hi, lo, cu = data
-    cu_t = torch.from_numpy(cu).cuda()
-    a = attention(hi, cu_t, max(LENS), lo if split else None, variant)
-    b = attention(hi, cu_t, max(LENS), lo if split else None, variant | 8)
-    torch.cuda.synchronize()
-    for x1, x2 in (zip(a, b) if split else [(a, b)]):
-        assert torch.equal(x1.view(torch.int16), x2.view(torch.int16))
+if DIAG:   # the VAR family: diagnostic build only (no skip entries in production)
+    @pytest.mark.parametrize("variant", [0, 2, 4, 6])
+    @pytest.mark.parametrize("split", [True, False], ids=["fp16x3", "fp16"])
+    def test_lean_block_is_bitwise_identical(gpu, data, variant, split):
+        """VAR bit 8 (permlane max, split16x2 of P and O, batched V^T reads) changes how the same
+        arithmetic is issued, not the arithmetic: outputs equal the variant without it bit for
+        bit (split16x2's fp16(v - hi) by v_fma_mix equals split16's convert-subtract-convert)."""
+        from ragmi.encoders import attention
+        x, hi, lo, cu = data
+        cu_t = torch.from_numpy(cu).cuda()
+        a = attention(hi, cu_t, max(LENS), lo if split else None, variant)
+        b = attention(hi, cu_t, max(LENS), lo if split else None, variant | 8)
+        torch.cuda.synchronize()
+        for x1, x2 in (zip(a, b) if split else [(a, b)]):
+            assert torch.equal(x1.view(torch.int16), x2.view(torch.int16))
 
 
-@pytest.mark.parametrize("variant", [2, 10])
-@pytest.mark.parametrize("split", [True, False], ids=["fp16x3", "fp16"])
-def test_paired_blocks_are_bitwise_identical(gpu, data, variant, split):
-    """VAR bit 16 (two query blocks per wave side by side) only reorders whole blocks: outputs
-    equal the variant without it bit for bit, including waves left with one block and
-    sequences shorter than one block per wave."""
-    from ragmi.encoders import attention
-    x, hi, lo, cu = data
-    cu_t = torch.from_numpy(cu).cuda()
-    a = attention(hi, cu_t, max(LENS), lo if split else None, variant)
-    b = attention(hi, cu_t, max(LENS), lo if split else None, variant | 16)
-    torch.cuda.synchronize()
-    for x1, x2 in (zip(a, b) if split else [(a, b)]):
-        assert torch.equal(x1.view(torch.int16), x2.view(torch.int16))
+if DIAG:   # the VAR family: diagnostic build only (no skip entries in production)
+    @pytest.mark.parametrize("variant", [2, 10])
+    @pytest.mark.parametrize("split", [True, False], ids=["fp16x3", "fp16"])
+    def test_paired_blocks_are_bitwise_identical(gpu, data, variant, split):
+        """VAR bit 16 (two query blocks per wave side by side) only reorders whole blocks: outputs
+        equal the variant without it bit for bit, including waves left with one block and
+        sequences shorter than one block per wave."""
+        from ragmi.encoders import attention
+        x, hi, lo, cu = data
+        cu_t = torch.from_numpy(cu).cuda()
+        a = attention(hi, cu_t, max(LENS), lo if split else None, variant)
+        b = attention(hi, cu_t, max(LENS), lo if split else None, variant | 16)
+        torch.cuda.synchronize()
+        for x1, x2 in (zip(a, b) if split else [(a, b)]):
+            assert torch.equal(x1.view(torch.int16), x2.view(torch.int16))
 
 
-@pytest.mark.parametrize("variant", [8, 10, 12, 14])
+@pytest.mark.parametrize("variant", [8, 10, 12, 14] if DIAG else [10])
 @pytest.mark.parametrize("split", [True, False], ids=["fp16x3", "fp16"])
 def test_peeled_prefetch_is_bitwise_identical(gpu, data, variant, split):
     """VAR bit 32 (full key blocks without the mask, the partial tail block peeled off, the
@@ -119,16 +132,33 @@ def test_peeled_prefetch_is_bitwise_identical(gpu, data, variant, split):
         assert torch.equal(x1.view(torch.int16), x2.view(torch.int16))
 
 
-@pytest.mark.parametrize("pair", [(42, 106), (42, 43), (43, 107)], ids=lambda p: f"{p[0]}-{p[1]}")
-@pytest.mark.parametrize("split", [True, False], ids=["fp16x3", "fp16"])
-def test_staging_and_q_prefetch_are_bitwise_identical(gpu, data, pair, split):
-    """VAR bit 64 (staging loads all issued before the LDS stores) and bit 1 (rolling Q
-    prefetch) change when bytes move, not the arithmetic: outputs equal bit for bit."""
+if DIAG:   # the VAR family: diagnostic build only (no skip entries in production)
+    @pytest.mark.parametrize("pair", [(42, 106), (42, 43), (43, 107)], ids=lambda p: f"{p[0]}-{p[1]}")
+    @pytest.mark.parametrize("split", [True, False], ids=["fp16x3", "fp16"])
+    def test_staging_and_q_prefetch_are_bitwise_identical(gpu, data, pair, split):
+        """VAR bit 64 (staging loads all issued before the LDS stores) and bit 1 (rolling Q
+        prefetch) change when bytes move, not the arithmetic: outputs equal bit for bit."""
+        from ragmi.encoders import attention
+        x, hi, lo, cu = data
+        cu_t = torch.from_numpy(cu).cuda()
+        a = attention(hi, cu_t, max(LENS), lo if split else None, pair[0])
+        b = attention(hi, cu_t, max(LENS), lo if split else None, pair[1])
+        torch.cuda.synchronize()
+        for x1, x2 in (zip(a, b) if split else [(a, b)]):
+            assert torch.equal(x1.view(torch.int16), x2.view(torch.int16))
+
+
+def test_production_library_refuses_the_family(gpu):
+    """Only -1 / 42 / 10 are built into the production libragmi.so (rag_diagnostic_build 0)."""
+    from ragmi import _lib
+    L = _lib.load()
+    if L.rag_diagnostic_build():
+        pytest.skip("diagnostic build loaded")
     from ragmi.encoders import attention
-    x, hi, lo, cu = data
-    cu_t = torch.from_numpy(cu).cuda()
-    a = attention(hi, cu_t, max(LENS), lo if split else None, pair[0])
-    b = attention(hi, cu_t, max(LENS), lo if split else None, pair[1])
-    torch.cuda.synchronize()
-    for x1, x2 in (zip(a, b) if split else [(a, b)]):
-        assert torch.equal(x1.view(torch.int16), x2.view(torch.int16))
+    g = torch.Generator(device="cuda")
+    g.manual_seed(1)
+    cu_t = torch.tensor([0, 40], dtype=torch.int32, device="cuda")
+    hi = torch.randn((40, 1152), generator=g, device="cuda").half()
+    for v in (0, 2, 43, 106):
+        with pytest.raises(RuntimeError, match="diagnostic build"):
+            attention(hi, cu_t, 40, None, v)

@@ -83,3 +83,45 @@ def test_python_constants_match(v):
     from ragmi import encoders as E
     names = {n: getattr(E, n) for n in dir(E) if n.startswith("GEMM_")}
     assert v in names.values()
+
+
+# round 6: the scan's MODE / DYN / VALU probes and the attention VAR
+# family are compiled into the diagnostic build only (-DRAGMI_DIAG_BUILD); the production
+# library exports these ids and refuses the rest during argument checks
+PROD_SCAN_VARIANTS = [0, 7]
+PROD_ATTN_VARIANTS = [-1, 42, 10]
+
+
+def test_production_build_is_not_diagnostic(libpath):
+    L = ctypes.CDLL(libpath)
+    assert L.rag_diagnostic_build() == 0
+
+
+def test_scan_and_attention_probes_are_refused(libpath):
+    L = ctypes.CDLL(libpath)
+    L.rag_last_error.restype = ctypes.c_char_p
+    ms = ctypes.c_double()
+    fake = ctypes.c_void_p(16)          # never dereferenced: refused before any HIP call
+    for v in range(17):
+        if v in PROD_SCAN_VARIANTS:
+            continue
+        rc = L.rag_bench_scan(None, fake, 1, v, 1, ctypes.byref(ms))
+        assert rc != 0 and b"diagnostic build" in L.rag_last_error(), v
+    for v in list(range(16)) + [18, 26, 40, 43, 44, 46, 106, 107]:
+        if v in PROD_ATTN_VARIANTS:
+            continue
+        rc = L.rag_bert_attention(v, fake, None, fake, 1, 32, fake, None, None)
+        assert rc != 0 and b"diagnostic build" in L.rag_last_error(), v
+
+
+def test_diagnostic_instances_are_gated_in_the_sources():
+    """Every non-production scan / attention instantiation sits under RAGMI_DIAG_BUILD."""
+    idx = _src("index_capi.hip")
+    for probe in ("scan_valu_kernel<D><<<", "launch_variant<D, 3>", "launch_variant<D, 9>",
+                  "RAG_WIDE(4)"):
+        pos = idx.index(probe)
+        opened = max(idx.rfind("#ifdef RAGMI_DIAG_BUILD", 0, pos), idx.rfind("#else", 0, pos))
+        assert opened > idx.rfind("#endif", 0, pos), probe
+    bert = _src("bert_capi.hip")
+    pos = bert.index("integral_constant<int, 106>")
+    assert bert.rfind("#else", 0, pos) > bert.rfind("#endif", 0, pos)

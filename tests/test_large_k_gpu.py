@@ -6,7 +6,8 @@ bit for bit (oracle/scan_ref.c, canonical fp64 order), ties by row ascending —
 1024, with and without payload filters, with padding where fewer than k rows match, on
 near-duplicate clusters whose scores sit inside the MFMA error band, and when a query's first
 candidate list overflows (a second, tighter round). Massive exact ties beyond the candidate
-capacity are reported as unanswered, never silently truncated.
+capacity are reported as unanswered, never silently truncated, and re-answered by the full
+exact pass (round 6), which also serves every k > RAG_MAX_K_LARGE.
 """
 import numpy as np
 import pytest
@@ -146,6 +147,85 @@ def test_large_k_massive_ties_are_unanswered_not_truncated(gpu):
     s2, i2 = O.search(O.encode_rows(x), q[1:], 100)       # the other query is still exact
     np.testing.assert_array_equal(i[1], i2[0])
     np.testing.assert_array_equal(s[1], s2[0])
+    # the full exact pass answers the tied query (round 6): 100 of the 20000
+    # copies, the lowest rows first
+    sf, i_f = idx.search(q, 100, full=True)
+    torch.cuda.synchronize()
+    s3, i3 = O.search(O.encode_rows(x), q, 100)
+    np.testing.assert_array_equal(i_f.cpu().numpy(), i3)
+    np.testing.assert_array_equal(sf.cpu().numpy(), s3)
+    assert np.array_equal(i3[0], np.arange(100))
+    idx.close()
+
+
+def test_qdrant_reanswers_massive_ties(gpu):
+    """QdrantClient.query_points on the massive-ties collection: the large-k pass leaves the
+    tied query unanswered and Collection.search re-runs it on the full pass, so the points come
+    back exact instead of empty."""
+    from ragmi import qdrant_models as m
+    from ragmi.qdrant import QdrantClient
+    rng = np.random.default_rng(9)
+    n, dim = 24_000, 384
+    x = rng.standard_normal((n, dim)).astype(np.float32)
+    x[:20_000] = x[0]
+    c = QdrantClient(device=gpu)
+    c.create_collection("t", m.VectorParams(size=dim, distance=m.Distance.COSINE,
+                                            datatype="float16"))
+    c.upsert("t", m.Batch(ids=list(range(n)), vectors=x, payloads=[{"ticker": "A"}] * n))
+    res = c.query_points("t", query=x[0], limit=100)
+    s2, i2 = O.search(O.encode_rows(x), x[:1], 100)
+    assert [p.id for p in res.points] == i2[0].tolist()
+    assert [p.score for p in res.points] == s2[0].tolist()
+    assert c._col("t").rescued == 1
+    c.close()
+
+
+@pytest.mark.parametrize("dim,n,k", [(384, 20_000, 5000), (384, 7_000, 9000), (1024, 9_000, 4500)])
+def test_full_pass_any_k(gpu, dim, n, k):
+    """k > RAG_MAX_K_LARGE: rag_index_search takes the full exact pass —
+    ids and scores bit-exact vs the oracle; k past the row count pads with -1 / -inf."""
+    rng = np.random.default_rng(dim + n)
+    x = rng.standard_normal((n, dim)).astype(np.float32)
+    x[100:140] = x[3]                                       # exact ties: rows ascending
+    q = np.concatenate([_queries(rng, x, 6, dim), x[3:4]])
+    idx = _index(gpu, x)
+    s, i = _search(idx, q, k)
+    kk = min(k, n)
+    s2, i2 = O.search(O.encode_rows(x), q, kk)
+    np.testing.assert_array_equal(i[:, :kk], i2)
+    np.testing.assert_array_equal(s[:, :kk], s2)
+    assert np.all(i[:, kk:] == -1) and np.all(s[:, kk:] == -np.inf)
+    idx.close()
+
+
+@pytest.mark.parametrize("storage", ["fp16", "fp32"])
+def test_full_pass_filtered_and_forced(gpu, storage):
+    """Per-query filters with a rare ticker (padding) on the full pass, at k > 4096 and forced
+    (full=True) at k = 15 / 100 — the same result as the scan and large-k paths."""
+    rng = np.random.default_rng(41)
+    n, dim = 15_000, 384
+    x = rng.standard_normal((n, dim)).astype(np.float32)
+    tags = rng.integers(1, 3, n).astype(np.uint32)
+    tags[rng.choice(n, 50, replace=False)] = 7
+    q = _queries(rng, x, 5, dim)
+    vals = [1, 2, 7, 1, 7]
+    filters = np.array([[0xffffffff, v] for v in vals], dtype=np.uint32)
+    idx = _index(gpu, x, tags, storage=storage)
+    enc = O.encode_rows32(x) if storage == "fp32" else O.encode_rows(x)
+    for k, full in ((6000, False), (15, True), (100, True)):
+        s, i = idx.search(q, k, filters=filters, full=full)
+        torch.cuda.synchronize()
+        s, i = s.cpu().numpy(), i.cpu().numpy()
+        if k <= 100:
+            sp, ip = _search(idx, q, k, filters)                # scan / large-k path
+            np.testing.assert_array_equal(i, ip)
+            np.testing.assert_array_equal(s, sp)
+        for b, v in enumerate(vals):
+            s2, i2 = O.search(enc, q[b:b + 1], k, tags=tags, mask=0xffffffff, value=v,
+                              use_filter=True)
+            np.testing.assert_array_equal(i[b], i2[0])
+            np.testing.assert_array_equal(s[b], s2[0])
+        assert (i[2] >= 0).sum() == min(50, k)
     idx.close()
 
 

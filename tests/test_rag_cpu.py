@@ -87,14 +87,15 @@ def test_reference_model_constructors():
     assert m.Filter(must=[fc]).must[0].match.value == "AAPL"
 
 
-def test_limit_too_large_fails_loudly(monkeypatch):
-    """A limit the build cannot answer (> RAG_MAX_K_LARGE over a larger collection) passes the
-    reference's swallow-to-empty wrapper (main.py:238-239) as LimitTooLarge: it must not read
-    as 'no documents'. Any other query error still gives empty points, as in the reference."""
+def test_retrieve_swallows_like_the_reference(monkeypatch):
+    """retrieve_from_qdrant keeps the reference's swallow-to-empty (main.py:232-239): every
+    query error gives empty points. Nothing is refused for its size any more — query_points
+    answers any limit exactly (k > RAG_MAX_K_LARGE on the full exact pass, round 6)."""
     monkeypatch.setenv("TESTING", "False")
     import ragmi.rag as rag
     rag = importlib.reload(rag)
-    from ragmi.qdrant import LimitTooLarge
+    import ragmi.qdrant as qd
+    assert not hasattr(qd, "LimitTooLarge")
 
     class Fake:
         def __init__(self, exc):
@@ -103,11 +104,62 @@ def test_limit_too_large_fails_loudly(monkeypatch):
         def query_points(self, **kw):
             raise self.exc
 
-    monkeypatch.setattr(rag, "get_qdrant", lambda: Fake(LimitTooLarge("limit 5000")))
-    with pytest.raises(LimitTooLarge):
-        rag.retrieve_from_qdrant([0.0] * 384, "aapl", limit=5000)
     monkeypatch.setattr(rag, "get_qdrant", lambda: Fake(RuntimeError("down")))
     assert rag.retrieve_from_qdrant([0.0] * 384, "aapl", limit=5000).points == []
+
+
+class _StubIndex:
+    """FlatIndex stand-in for Collection.search's host logic: the first search leaves query 1
+    unanswered (ids -1, unanswered() + 1) as a large-k pass does past 16384 near-ties; the full
+    pass answers it."""
+
+    def __init__(self, count, k_full_ids):
+        self.count = count
+        self.n_un = 0
+        self.calls = []
+        self.k_full_ids = k_full_ids
+
+    def search(self, q, k, filters=None, full=False):
+        import torch
+        B = len(q)
+        self.calls.append((B, k, full))
+        if full:
+            ids = torch.tensor([self.k_full_ids[:k]] * B, dtype=torch.int64)
+            return torch.full((B, k), 0.5), ids
+        ids = torch.arange(k, dtype=torch.int64).repeat(B, 1)
+        s = torch.full((B, k), 0.9)
+        ids[1] = -1
+        s[1] = float("-inf")
+        self.n_un += 1
+        return s, ids
+
+    def unanswered(self):
+        return self.n_un
+
+
+def test_collection_reanswers_unanswered_queries_on_the_full_pass():
+    import numpy as np
+    import threading
+    from ragmi.qdrant import Collection, PayloadTags
+    col = Collection.__new__(Collection)
+    col.index = _StubIndex(count=100, k_full_ids=list(range(50, 100)))
+    col.lock = threading.RLock()
+    col._unanswered = 0
+    col.rescued = 0
+    col.tags = PayloadTags()
+    out = col.search(np.zeros((3, 384), np.float32), 40, [(0, 0)] * 3)
+    assert col.index.calls == [(3, 40, False), (1, 40, True)]
+    assert [r for r, _ in out[1]] == list(range(50, 90))      # answered, not "no documents"
+    assert [r for r, _ in out[0]] == list(range(40))
+    assert col.rescued == 1 and col._unanswered == 1
+    # padding -1 (fewer matching points than k) with no unanswered query: no second pass
+    col.index.n_un = 0
+    col._unanswered = 0
+    col.index.search = lambda q, k, filters=None, full=False: (
+        __import__("torch").tensor([[0.9, float("-inf")]]),
+        __import__("torch").tensor([[3, -1]]))
+    col.index.unanswered = lambda: 0
+    assert col.search(np.zeros((1, 384), np.float32), 2, [(0, 0)]) == [[(3, 0.8999999761581421)]]
 
 
 def test_limit_range_constants():

@@ -311,3 +311,36 @@ def test_d1024_planted_200k_batch128(gpu):
     s2, i2 = O.search_fast(idx.export_rows(), q, 15)
     np.testing.assert_array_equal(i, i2)
     np.testing.assert_array_equal(s, s2)
+
+
+def test_d1024_million_rows_batch128(gpu):
+    """Config 5's per-rank shape at 1M x 1024, B = 128: corpus generated
+    on the device, planted + pure-random queries and a 64-row near-duplicate cluster (its
+    queries sit inside the MFMA error band, so the certified select's fallbacks run), every
+    query's top-15 ids and scores bit-exact against the certified oracle shortlist
+    (oracle_scan.search_fast, exact canonical rescoring), plus a 30-row fp32-encoding pin of
+    the stored rows."""
+    n, b, d = 1_000_000, 128, 1024
+    g = torch.Generator(device=gpu)
+    g.manual_seed(1024)
+    x = torch.randn((n, d), generator=g, device=gpu)
+    rows = torch.arange(900_000, 900_064, device=gpu)
+    x[rows] = x[900_000] + 1e-5 * torch.randn((64, d), generator=g, device=gpu)
+    src = torch.randint(0, n, (96,), generator=g, device=gpu)
+    q = torch.cat([x[src] + 0.05 * torch.randn((96, d), generator=g, device=gpu),
+                   torch.randn((24, d), generator=g, device=gpu),
+                   x[900_000:900_008] + 1e-4 * torch.randn((8, d), generator=g, device=gpu)])
+    from ragmi.index import FlatIndex
+    idx = FlatIndex(dim=d, capacity=n, device=gpu)
+    idx.upsert(x, torch.arange(n, device=gpu), new_count=n)
+    s, i = search(idx, q, 15)
+    enc = idx.export_rows()
+    pin = np.random.default_rng(3).choice(n, 30, replace=False)
+    np.testing.assert_array_equal(enc[pin], O.encode_rows(x[pin].cpu().numpy()))
+    del x
+    assert (i[:96, 0] == src.cpu().numpy()).mean() > 0.95
+    st = {}
+    s2, i2 = O.search_fast(enc, q.cpu().numpy(), 15, stats=st)
+    np.testing.assert_array_equal(i, i2)
+    np.testing.assert_array_equal(s, s2)
+    idx.close()
