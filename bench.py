@@ -341,6 +341,11 @@ def main():
                     help="--config 5: certify EVERY timed batch exact after the timed region "
                          "(oracle rescoring + an fp32 GEMM superset; scripts/bench_modes.py "
                          "_certify_all) instead of recall on two batches")
+    ap.add_argument("--legs", choices=["child", "inproc"], default="child",
+                    help="where the default line's config-2 / config-3 legs run: a fresh child "
+                         "process each (default), or inside this process after the headline's "
+                         "index is freed (the serving shape: one process holding the index "
+                         "and both encoders; VERDICT r5 item 4)")
     ap.add_argument("--config-steps", type=int, default=200,
                     help="timed batches of each config-2 / config-3 leg (warmup 20)")
     args = ap.parse_args()
@@ -625,11 +630,39 @@ def main():
         # rooflines and CPU baseline, as extra keys; value / ms_per_step stay the headline's.
         # N = 1 only (at N > 1 every rank would run its own replica of them).
         legs_on = world == 1 and not rehearsal and not args.no_configs
+        leg_fn = _config_leg_inproc if args.legs == "inproc" else _config_leg
         for cfg in ("2", "3"):
-            line[f"config{cfg}"] = (_config_leg(args, cfg) if legs_on else
+            line[f"config{cfg}"] = (leg_fn(args, cfg) if legs_on else
                                     {"skipped": "--no-configs" if args.no_configs else
                                      "N > 1 (measured by the N = 1 run)"})
         print(json.dumps(line), flush=True)
+
+
+LEG_KEYS = ("metric", "value", "unit", "ms_per_step", "steps", "warmup", "dtype", "config",
+            "search_top15_exact_queries", "encode_max_abs_diff_vs_oracle",
+            "rerank_max_abs_diff_vs_oracle", "rerank_checked_queries",
+            "rerank_top5_order_matches", "checked_timed_batches", "roofline", "roofline_search",
+            "cpu_baseline", "id_input_qps", "text_vs_id_input", "host_enqueue_ms_per_step")
+
+
+def _config_leg_inproc(args, cfg: str) -> dict:
+    """The same leg inside this process (--legs inproc): bench_modes.run_pipeline builds the
+    1M-row index, bge-small and the cross-encoder here, after the headline's index was freed."""
+    import copy
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import bench_modes
+    a = copy.copy(args)
+    a.config, a.steps, a.warmup, a.rows, a.streams, a.partition = cfg, args.config_steps, 20, 0, 0, "auto"
+    torch.cuda.empty_cache()
+    t0 = time.perf_counter()
+    try:
+        full = bench_modes.run_pipeline(a, int(cfg), emit=False)
+    except Exception as e:                              # the headline line still prints
+        return {"error": f"config {cfg} leg (in process): {type(e).__name__}: {e}"}
+    leg = {k: full[k] for k in LEG_KEYS if k in full}
+    leg["wall_s"] = round(time.perf_counter() - t0, 1)
+    leg["process"] = "in-process (after the headline)"
+    return leg
 
 
 def _config_leg(args, cfg: str) -> dict:
@@ -659,13 +692,9 @@ def _config_leg(args, cfg: str) -> dict:
     if r.returncode != 0 or not lines:
         return {"error": f"config {cfg} leg exited {r.returncode}"}
     full = json.loads(lines[-1])
-    keep = ("metric", "value", "unit", "ms_per_step", "steps", "warmup", "dtype", "config",
-            "search_top15_exact_queries", "encode_max_abs_diff_vs_oracle",
-            "rerank_max_abs_diff_vs_oracle", "rerank_checked_queries",
-            "rerank_top5_order_matches", "checked_timed_batches", "roofline", "roofline_search",
-            "cpu_baseline", "id_input_qps", "text_vs_id_input", "host_enqueue_ms_per_step")
-    leg = {k: full[k] for k in keep if k in full}
+    leg = {k: full[k] for k in LEG_KEYS if k in full}
     leg["wall_s"] = round(time.perf_counter() - t0, 1)
+    leg["process"] = "child"
     return leg
 
 if __name__ == "__main__":

@@ -222,6 +222,31 @@ def _cpu_pipeline_baseline(cfg_id, budget_s, corpus16_sample, n_total, R, bge_w,
                         f"({t_ce * 1e3:.0f} ms/batch)" if cfg_id == 3 else ""))}
 
 
+def encoder_traffic(stage: str, tokens: int, path: str | None = None):
+    """HBM bytes of one encoder forward from the committed rocprofv3 --pmc FETCH_SIZE /
+    WRITE_SIZE passes (profiles/encoder_pmc.json, scripts/gpu_encoder_pmc.sh +
+    scripts/encoder_traffic.py): (read + write bytes, a dict with the read /
+    write bytes, their ratios to the algorithmic bytes and the source), scaled from the
+    profiled token count to this forward's (the traffic is linear in tokens to within the
+    weights' share). (None, None) when no pass exists."""
+    path = path or os.path.join(ROOT, "profiles", "encoder_pmc.json")
+    try:
+        e = json.load(open(path))[stage]
+    except (OSError, ValueError, KeyError):
+        return None, None
+    f = tokens / e["tokens"] if tokens else 1.0
+    rd, wr = e["read_bytes_per_forward"] * f, e["write_bytes_per_forward"] * f
+    return round(rd + wr), {
+        "read_bytes": round(rd), "write_bytes": round(wr),
+        "read_ratio_to_algorithmic": e["read_ratio"],
+        "write_ratio_to_algorithmic": e["write_ratio"],
+        "profiled_tokens": e["tokens"],
+        "source": "not measured in this run: rocprofv3 --pmc FETCH_SIZE (x2 gfx950 correction) "
+                  "and WRITE_SIZE passes of one forward, " + os.path.relpath(path, ROOT) +
+                  f" [{stage}]" + (f", scaled x{f:.3f} to this forward's tokens"
+                                   if abs(f - 1) > 1e-3 else "")}
+
+
 def run_pipeline(args, cfg_id, emit=True):
     """Config 2 / 3 line; rank 0 returns the line dict (and prints it when `emit`)."""
     from ragmi import synth as R          # model shapes, seeded weights (product-side data)
@@ -355,6 +380,7 @@ def run_pipeline(args, cfg_id, emit=True):
     _sync(dev)
     elapsed_ids = time.perf_counter() - t1
     del evs[n_ev:]
+    flops_cu = list(flops)
     flops = [_ce_flops(c.cpu().numpy(), R.MINILM_CE) for c in flops]
     # config 2's two stages re-timed alone on one stream (after the timed region; with S
     # batches in flight their kernels overlap): the query-encoder forward and the search pass
@@ -474,9 +500,13 @@ def run_pipeline(args, cfg_id, emit=True):
             fl = float(np.mean(flops))
             ach = fl / (ce_ms * 1e-3)
             pipe = 3 if prec == "fp16x3" else 1
+            tr, tr_src = (encoder_traffic("rerank", int(np.mean([c.cpu().numpy()[-1]
+                                                              for c in flops_cu])))
+                          if prec == "fp16x3" else (None, None))
             roof = {"bound": "mfma", "achieved": round(ach / 1e12, 2),
                     "peak": MFMA_PEAK_F16 / 1e12, "unit": "TFLOP/s",
-                    "frac": round(ach / MFMA_PEAK_F16, 4), "traffic": None,
+                    "frac": round(ach / MFMA_PEAK_F16, 4), "traffic": tr,
+                    "traffic_detail": tr_src,
                     "kernel": f"MiniLM-L6 cross-encoder forward (480 pairs, {prec}; GEMM + "
                               f"attention + LayerNorm kernels, one packed batch)",
                     "avg_ms": round(ce_ms, 4), "algorithmic_flops_per_launch": fl,
@@ -494,9 +524,12 @@ def run_pipeline(args, cfg_id, emit=True):
             share = enc_ms / (enc_ms + search_ms)
             ach = fl / (enc_ms * 1e-3)
             pipe = 3 if prec == "fp16x3" else 1
+            tr, tr_src = (encoder_traffic("encode_q", T0) if prec == "fp16x3"
+                          else (None, None))
             roof = {"bound": "mfma", "achieved": round(ach / 1e12, 2),
                     "peak": MFMA_PEAK_F16 / 1e12, "unit": "TFLOP/s",
-                    "frac": round(ach / MFMA_PEAK_F16, 4), "traffic": None,
+                    "frac": round(ach / MFMA_PEAK_F16, 4), "traffic": tr,
+                    "traffic_detail": tr_src,
                     "kernel": f"bge-small query-encoder forward (32 queries, {T0} tokens, "
                               f"{prec}; 12 layers of GEMM + attention + LayerNorm kernels)",
                     "avg_ms": round(enc_ms, 4), "algorithmic_flops_per_launch": fl,
