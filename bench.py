@@ -330,7 +330,7 @@ def main():
                          "A/B knobs are honoured (never for a reported line)")
     ap.add_argument("--precision", choices=["fp16x3", "fp16"], default="fp16x3",
                     help="encoder precision for --config 2/3 (fp16x3 = the 1e-3 contract)")
-    ap.add_argument("--partition", choices=["auto", "on", "off"], default="auto",
+    ap.add_argument("--partition", choices=["auto", "on", "off", "whole"], default="auto",
                     help="batches in flight on CU-partitioned streams (rag_stream_create_cu_"
                          "partition): auto = with free scan order and several in flight "
                          "(shards below 4M rows per GPU)")
@@ -438,7 +438,7 @@ def main():
     # them, so the scans run side by side instead of interleaving over every CU — 1.25M rows,
     # 4 in flight: 222-223K qps vs 206-208K (scripts/diag/cu_partition.py,
     # profiles/r05c_cu_partition.jsonl)
-    partition = None
+    partition = whole = None
     use_part = args.partition == "on" or (args.partition == "auto" and not serial
                                           and n_streams > 1)
     if use_part:
@@ -447,6 +447,13 @@ def main():
         streams = list(partition.streams)
         for s in streams:
             s.wait_stream(torch.cuda.current_stream(dev))   # the queries were made there
+    elif args.partition == "whole":
+        # every batch stream on a dedicated hardware queue (full-CU-mask streams)
+        from ragmi.index import PartitionStreams
+        whole = PartitionStreams(dev, n_streams, whole=True)
+        streams = list(whole.streams)
+        for s in streams:
+            s.wait_stream(torch.cuda.current_stream(dev))
     else:
         streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev)
                                                       for _ in range(n_streams - 1)]
@@ -583,7 +590,10 @@ def main():
                        "batches_in_flight": n_streams, "storage": args.storage,
                        "scan_order": args.scan_order if args.scan_order == "stream" else
                                      "serial" if serial else "free",
-                       "cu_partition": len(streams) if partition is not None else None},
+                       "cu_partition": len(streams) if partition is not None else None,
+                       "stream_queues": ("CU partitions" if partition is not None else
+                                         "dedicated (whole-CU-mask streams)" if whole is not None
+                                         else "torch streams")},
             "recall_at_5": check and check["recall_at_5"],
             "recall_at_5_min": check and check["recall_at_5_min"],
             "exact_batches": check and check["exact_batches"],
@@ -619,8 +629,9 @@ def main():
             "cpu_baseline": cpu,
         }
     idx.close()
-    if partition is not None:
-        partition.close()
+    for ps in (partition, whole):
+        if ps is not None:
+            ps.close()
     if world > 1 or rehearsal:
         dist.destroy_process_group()
     if rank == 0:

@@ -139,6 +139,8 @@ struct rag_encoder {
   int fuse_ln = -1;
   // deferred LayerNorm on the token rows (fp16x3, hidden 384): -1 auto, 0 off, 1 on
   int defer_ln = -1;
+  // the deferred-LN FFN as one fused launch (ffn_fused_kernel): -1 auto, 0 off, 1 on
+  int ffn_fused = -1;
   // hipGraph replay of small-batch forwards: -1 auto, 0 off, 1 on. A call on the null stream
   // replays on the encoder's own stream, ordered by two events (gstream, gev_*)
   int graphs = -1;
@@ -375,6 +377,44 @@ bool dl_gemm_ok(int epi, int M, int N, int K) {
   if (epi == kEpiResLn) return N == kDlH;
   return K == kDlH && 2 * N <= kPipeBiasMax;
 }
+
+#ifdef RAGMI_DIAG_BUILD
+// the fused deferred-LN FFN (ffn_fused_kernel): hidden 384, intermediate 1536 (bge-small,
+// MiniLM-L6), inside the deferred-LayerNorm forward. Auto: once the 128-row tiles fill every
+// CU at least twice (round 6 measurements)
+bool ffn_fused_for(const rag_encoder* e, int T, int FF) {
+  if (FF != kFfnFF || e->ffn_fused == 0) return false;
+  if (e->ffn_fused > 0) return true;
+  return false;
+}
+// chunk width of the fused FFN (FfnRing): mode 1 -> V 0 (128 columns of H per pass), mode 2
+// -> V 1 (256)
+// (A/B modes 3 / 4 / 5: chunk 256 + the next stage's DMA issued mid-step / + s_setprio 1 on
+// waves 4-7 / both)
+int ffn_ring(const rag_encoder* e) {
+  switch (e->ffn_fused) {
+    case 2: return 1;
+    case 3: return 3;
+    case 4: return 5;
+    case 5: return 7;
+    default: return 0;
+  }
+}
+
+void launch_ffn_fused(_Float16* zh, _Float16* zl, int M, const FfnArgs& a, hipStream_t st,
+                      int ring) {
+  const int tiles = (M + kFfnBM - 1) / kFfnBM;
+  const dim3 grid((unsigned)std::max(1, std::min(cu_count(), tiles)));   // one per CU
+  switch (ring) {
+    case 1: launch_fixed<kFfnThreads>(ffn_fused_kernel<1>, grid, 0, st, zh, zl, M, a); break;
+    case 3: launch_fixed<kFfnThreads>(ffn_fused_kernel<3>, grid, 0, st, zh, zl, M, a); break;
+    case 5: launch_fixed<kFfnThreads>(ffn_fused_kernel<5>, grid, 0, st, zh, zl, M, a); break;
+    case 7: launch_fixed<kFfnThreads>(ffn_fused_kernel<7>, grid, 0, st, zh, zl, M, a); break;
+    default: launch_fixed<kFfnThreads>(ffn_fused_kernel<0>, grid, 0, st, zh, zl, M, a); break;
+  }
+}
+
+#endif
 
 // deferred-LayerNorm mode of the forward: -1 auto, 0 off, 1 on (where the shapes allow)
 int defer_ln_default() {
@@ -639,6 +679,26 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
       o.eps = c.layer_norm_eps;
       launch_ws_large<kEpiResLn, true>(w->ctx, w->ctx_l, L.wo, L.wo_l, L.bo, T, H, H, w->xh,
                                  w->xl, st, o);
+#ifdef RAGMI_DIAG_BUILD
+      if (ffn_fused_for(e, T, FF)) {
+        // FFN1 + GELU + FFN2 + residual + LN statistics in one launch, H kept on the CU
+        FfnArgs fa;
+        fa.w1 = L.w1_f;
+        fa.w1l = L.w1_fl;
+        fa.c1 = L.w1_c1;
+        fa.c2 = L.w1_c2;
+        fa.w2 = L.w2;
+        fa.w2l = L.w2_l;
+        fa.b2 = L.bi2;
+        fa.gamma = L.g1;
+        fa.beta = L.be1;
+        fa.st_in = w->sa;
+        fa.st_out = w->sb;
+        fa.eps = c.layer_norm_eps;
+        launch_ffn_fused(w->xh, w->xl, T, fa, st, ffn_ring(e));
+        continue;
+      }
+#endif
       DlArgs f;
       f.st_in = w->sa;
       f.c1 = L.w1_c1;
@@ -1269,6 +1329,22 @@ int rag_encoder_set_graphs(rag_encoder_t* e, int mode) {
   if (!e || mode < -1 || mode > 1) return ragmi::fail(RAG_EINVAL, "mode: -1 auto, 0 off, 1 on");
   std::lock_guard<std::mutex> lk(e->mu);
   e->graphs = mode;
+  return RAG_OK;
+}
+
+int rag_encoder_set_ffn_fused(rag_encoder_t* e, int mode) {
+  ragmi::clear_error();
+#ifdef RAGMI_DIAG_BUILD
+  if (!e || mode < -1 || mode > 5)
+    return ragmi::fail(RAG_EINVAL, "mode: -1 auto, 0 off, 1 on (2-5: A/B shapes)");
+#else
+  if (!e || mode < -1 || mode > 0)
+    return ragmi::fail(RAG_EINVAL, "mode: -1 auto or 0 off; the fused FFN (measured slower) is "
+                                   "in the diagnostic build only");
+#endif
+  std::lock_guard<std::mutex> lk(e->mu);
+  e->ffn_fused = mode;
+  for (auto& w : e->ws) w.drop_graphs();
   return RAG_OK;
 }
 

@@ -1582,6 +1582,377 @@ __global__ __launch_bounds__(kWsBlock<CFG>, 1) void gemm_ws_kernel(
   }
 }
 
+#ifdef RAGMI_DIAG_BUILD
+// ----------------------------------------------------------------------------------------
+// Fused FFN of the deferred-LayerNorm forward (round 6): one launch for
+//   H  = GELU(LN1(z) W1^T + b1)        (FFN1, kEpiLnGeluF16 with LN1 folded: W1' = W1 diag(g1))
+//   z' = LN1(z) + (H W2^T + b2)        (FFN2, kEpiResLn; row statistics of z' out)
+// (modeling_bert.py BertIntermediate + BertOutput) over 128-row tiles of the token rows,
+// with the 1536-wide intermediate H never leaving the CU: per tile, for each 128-column chunk
+// c of H, (1) 12 K-steps of z x W1'[c]^T into H_c (128 x 128 accumulators), (2) the LnGelu
+// epilogue in registers, split into fp16 hi + lo, re-laid lane to lane into MFMA operand
+// fragments (v_permlane32/16_swap, no LDS), (3) 4 K-steps of H_c x W2[:, c]^T accumulated into
+// the tile's 128 x 384 output; after the 12 chunks, the ResLn epilogue writes z' in place.
+// The two-kernel path writes H (T x 1536, hi + lo: 725 MB at 118K tokens) to HBM and reads it
+// back (1.19x, FFN2's A streamed from HBM); its FFN1 epilogue's store bursts stall the MFMA
+// waves. Arithmetic: every output element is computed by the same MFMA sequence
+// (K steps in natural order, the three fp16x3 terms W_lo A_hi, W_hi A_lo, W_hi A_hi), the same
+// epilogue operations and the same operand-to-lane mapping as gemm_ws_kernel's FFN1 / FFN2 at
+// aligned (>= 64 row panels) token counts, so the forward's outputs are bitwise those of the
+// two-kernel path there (tests/test_ffn_fused_gpu.py).
+// MEASURED SLOWER: 1.08 ms per launch against 0.90 ms for the two WS GEMMs at
+// 118K tokens (rerank forward 9.2-9.9 vs 8.9-9.1 ms over five shapes), MFMA busy 0.35, waves
+// waiting 43% — so it is compiled into the diagnostic build only (-DRAGMI_DIAG_BUILD).
+// Layout: 8 waves, wave w owns rows 16w .. 16w+15 of the tile and ALL columns (H_c: 8 16x16
+// fragments = 32 VGPRs; the output: 24 fragments = 96), so a wave's H_c rows are exactly the
+// A operand rows its phase (3) needs. The waves issue their own LDS-DMA (no loader waves: the
+// register budget needs two waves per SIMD); a 3-slot ring of 48 KB stages (phase 1: z hi/lo
+// 128 rows x 32 K + W1'[c] hi/lo 128 rows x 32 K = 32 KB; phase 3: W2[:, c] hi/lo 384 rows x
+// 32 K = 48 KB), one barrier per K step; c1 | c2 (LN1 fold vectors) staged in LDS.
+// ----------------------------------------------------------------------------------------
+constexpr int kFfnBM = 128, kFfnFF = 1536;
+constexpr int kFfnWaves = 8, kFfnThreads = 64 * kFfnWaves;
+constexpr int kFfnS1 = kDlH / 32;                       // phase-1 K steps per chunk (12)
+// timing probes of a diagnostic build (-DRAGMI_FFN_PROBE=n; results meaningless): 1 no MFMAs,
+// 2 no DMAs, 3 no W fragment LDS reads (A fragments stand in), 4 no LnGelu epilogue math
+#ifndef RAGMI_FFN_PROBE
+#define RAGMI_FFN_PROBE 0
+#endif
+constexpr int kFfnProbe = RAGMI_FFN_PROBE;
+
+// chunk width CH of the intermediate per pass (V): 0 -> 128 (12 chunks; a phase-1 stage is
+// 32 KB in a 48 KB slot), 1 -> 256 (6 chunks: every stage 48 KB, half the z re-reads, 24 MFMAs
+// -> 48 per wave in a phase-1 K step). A 3-slot ring of 48 KB slots either way.
+template <int V> struct FfnRing {
+  static constexpr int CH = (V & 1) ? 256 : 128;
+  static constexpr bool LATE_DMA = (V & 2) != 0;          // next stage issued mid-step
+  static constexpr bool PRIO = (V & 4) != 0;              // s_setprio 1 on waves 4-7
+  static constexpr int CHUNKS = kFfnFF / CH;
+  static constexpr int S3 = CH / 32;                      // phase-3 K steps per chunk
+  static constexpr int PER_CHUNK = kFfnS1 + S3;
+  static constexpr int PER_TILE = CHUNKS * PER_CHUNK;
+  static constexpr int SLOTS = 3, SLOT_H8 = 3072;         // 48 KB in 16-B units
+  static constexpr int P1 = (kFfnBM + CH) * 2 / 16 / kFfnWaves;  // phase-1 pieces per wave
+  static constexpr int P3 = 6;                            // phase-3 pieces per wave
+  static constexpr int FN1 = CH / 16;                     // H_c fragments per wave
+  static constexpr int AHEAD = SLOTS - 1;
+};
+
+struct FfnArgs {
+  const _Float16 *w1, *w1l;     // W1' = W1 diag(g_prev) [1536][384] (folded), hi / lo
+  const float *c1, *c2;         // [1536]: column sums of W1' and b1 + W1 beta_prev
+  const _Float16 *w2, *w2l;     // [384][1536]
+  const float *b2, *gamma, *beta;   // FFN2 bias; the LayerNorm pending on z (LN1)
+  const float* st_in;           // [M][6] x {mean, M2} of z (the attention block's ResLn)
+  float* st_out;                // [M][6] of z'
+  float eps;
+};
+
+// lane-to-lane re-lay of two adjacent 16-column accumulator fragments (f0 = columns 0..15, f1
+// = 16..31 of a 32-deep K step; lane group g holds columns 4g..4g+3 of each, one dword per two
+// fp16) into the MFMA A-operand fragment of that K step (lane group g: columns 8g .. 8g+7):
+// permlane32_swap then permlane16_swap (derivation in DESIGN §R6.1)
+__device__ __forceinline__ half8 ffn_relay(u32x2 f0, u32x2 f1) {
+  u32x4 o;
+#pragma unroll
+  for (int d = 0; d < 2; ++d) {
+    const auto x = __builtin_amdgcn_permlane32_swap(f0[d], f1[d], false, false);
+    const auto y = __builtin_amdgcn_permlane16_swap(x[0], x[1], false, false);
+    o[d] = y[0];         // columns 8g + 2d, +1
+    o[2 + d] = y[1];     // columns 8g + 4 + 2d, +1
+  }
+  return __builtin_bit_cast(half8, o);
+}
+
+// s_waitcnt vmcnt(n) for a runtime n in [0, N] (the immediate is compile-time)
+template <int N>
+__device__ __forceinline__ void wait_vm(int n) {
+  if (n >= N) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+    return;
+  }
+  if constexpr (N > 0) wait_vm<N - 1>(n);
+}
+
+template <int V = 0>
+__global__ __launch_bounds__(kFfnThreads, 1) void ffn_fused_kernel(
+    _Float16* __restrict__ zh, _Float16* __restrict__ zl, int M, FfnArgs a) {
+  using R = FfnRing<V>;
+  constexpr int H = kDlH, FF = kFfnFF, CPR = 4, CH = R::CH;
+  constexpr int A_H8 = kFfnBM * CPR;                    // 512: one plane of a 128-row stage
+  constexpr int W1_H8 = CH * CPR;                       // one plane of W1'[c] in a stage
+  constexpr int W3_H8 = H * CPR;                        // one plane of a phase-3 stage
+  __shared__ half8 lds[R::SLOTS * R::SLOT_H8];
+  __shared__ float cvec[2 * FF];                        // c1 | c2
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t lbase = lds_addr_of(lds);
+  const int nT = (M + kFfnBM - 1) / kFfnBM;
+  const int G = gridDim.x, b = blockIdx.x;
+  const int n_mine = b < nT ? (nT - b + G - 1) / G : 0;
+  const int steps = n_mine * R::PER_TILE;
+
+  for (int i = tid * 4; i < FF; i += kFfnThreads * 4) {
+    *reinterpret_cast<floatx4*>(cvec + i) = *reinterpret_cast<const floatx4*>(a.c1 + i);
+    *reinterpret_cast<floatx4*>(cvec + FF + i) = *reinterpret_cast<const floatx4*>(a.c2 + i);
+  }
+
+  // ---- this wave's share of each stage's DMA pieces (1 KB = 64 lanes x 16 B) ----
+  // phase 1: the stage's pieces in image order — z hi (8), z lo (8), W1'[c] hi (CH / 16),
+  // W1'[c] lo — wave w takes pieces P1 w .. P1 w + P1 - 1; every operand row is 384 K long, so
+  // a piece's lane offsets depend only on its index inside its region
+  uint32_t vo1[R::P1], vo3[R::P3];
+  int reg1[R::P1];
+#pragma unroll
+  for (int i = 0; i < R::P1; ++i) {
+    const int p = R::P1 * w + i;
+    const int region = p < 8 ? 0 : p < 16 ? 1 : p < 16 + CH / 16 ? 2 : 3;
+    const int q = region < 2 ? p - 8 * region : p - 16 - (region - 2) * (CH / 16);
+    const int r = q * 16 + (lane >> 2), cs = lane & 3;
+    reg1[i] = region;
+    vo1[i] = (uint32_t)(r * H + swz_chunk<CPR>(r, cs) * 8) * 2u;
+  }
+  // phase 3: region w / 4 (0 W2 hi, 1 W2 lo), pieces (w & 3) * P3 + i of the stage's rows
+#pragma unroll
+  for (int i = 0; i < R::P3; ++i) {
+    const int q = (w & 3) * R::P3 + i, r = q * 16 + (lane >> 2), cs = lane & 3;
+    vo3[i] = (uint32_t)(r * FF + swz_chunk<CPR>(r, cs) * 8) * 2u;
+  }
+  const __amdgpu_buffer_rsrc_t rW2 = panel((w >> 2) ? a.w2l : a.w2, (int64_t)H * FF * 2);
+  // stage gi of this workgroup's sequence -> slot gi % SLOTS
+  auto issue = [&](int gi) __attribute__((always_inline)) {
+    if (gi >= steps || kFfnProbe == 2) return;
+    const int it = gi / R::PER_TILE, loc = gi % R::PER_TILE;
+    const int c = loc / R::PER_CHUNK, s = loc % R::PER_CHUNK;
+    const uint32_t slot = lbase + (uint32_t)(gi % R::SLOTS) * (R::SLOT_H8 * 16);
+    if (s < kFfnS1) {
+      const int m0 = (it * G + b) * kFfnBM, rows = min(M - m0, kFfnBM);
+      const __amdgpu_buffer_rsrc_t rz0 = panel(zh + (int64_t)m0 * H, (int64_t)rows * H * 2);
+      const __amdgpu_buffer_rsrc_t rz1 = panel(zl + (int64_t)m0 * H, (int64_t)rows * H * 2);
+      const __amdgpu_buffer_rsrc_t rw0 = panel(a.w1 + (int64_t)c * CH * H, (int64_t)CH * H * 2);
+      const __amdgpu_buffer_rsrc_t rw1 = panel(a.w1l + (int64_t)c * CH * H, (int64_t)CH * H * 2);
+      const uint32_t soff = __builtin_amdgcn_readfirstlane((uint32_t)(s * 64));
+#pragma unroll
+      for (int i = 0; i < R::P1; ++i) {
+        // (image position of piece P1 w + i: pieces are laid out in their global order)
+        const uint32_t d = slot + (uint32_t)((R::P1 * w + i) * 64 * 16);
+        const int rg = reg1[i];
+        blds16(rg == 0 ? rz0 : rg == 1 ? rz1 : rg == 2 ? rw0 : rw1, vo1[i], soff, d);
+      }
+    } else {
+      const int k = s - kFfnS1;
+      const uint32_t soff = __builtin_amdgcn_readfirstlane((uint32_t)((c * CH + k * 32) * 2));
+#pragma unroll
+      for (int i = 0; i < R::P3; ++i)
+        blds16(rW2, vo3[i], soff,
+               slot + (uint32_t)(((w >> 2) * W3_H8 + ((w & 3) * R::P3 + i) * 64) * 16));
+    }
+  };
+  auto pieces = [&](int gi) -> int {
+    if (gi >= steps || kFfnProbe == 2) return 0;
+    return (gi % R::PER_TILE) % R::PER_CHUNK < kFfnS1 ? R::P1 : R::P3;
+  };
+
+  // the tile's row statistics (one 16-row group per wave), loaded a tile ahead of use
+  floatx4 dls[1];
+  auto prefetch = [&](int it) __attribute__((always_inline)) {
+    if (it < n_mine) {
+      const int m0 = (it * G + b) * kFfnBM, rows = min(M - m0, kFfnBM);
+      dl_prefetch_stats<1>(dls, panel(a.st_in + (int64_t)m0 * kDlParts * 2,
+                                      (int64_t)rows * kDlParts * 8), w, lane);
+    }
+  };
+  prefetch(0);
+#pragma unroll
+  for (int p = 0; p < R::AHEAD; ++p) issue(p);
+  __syncthreads();                                       // cvec staged
+
+  // one ring step: stage gi landed (this wave's pieces: everything older than the AHEAD - 1
+  // stages issued after it), every wave done reading stage gi - 1 (its slot is refilled next)
+  auto step_begin = [&](int gi) __attribute__((always_inline)) -> const half8* {
+    int younger = 0;
+#pragma unroll
+    for (int p = 1; p < R::AHEAD; ++p) younger += pieces(gi + p);
+    wait_vm<(R::AHEAD - 1) * 6>(younger);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if constexpr (!R::LATE_DMA) issue(gi + R::AHEAD);
+    return lds + (gi % R::SLOTS) * R::SLOT_H8;
+  };
+  if constexpr (R::PRIO)
+    if (w >= 4) __builtin_amdgcn_s_setprio(1);
+
+  int gi = 0;
+  for (int it = 0; it < n_mine; ++it) {
+    floatx4 y[24];
+#pragma unroll
+    for (int j = 0; j < 24; ++j) y[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    float mu, rs;
+    dl_lane_stats(dls[0], g, a.eps, mu, rs);             // the tile's rows
+    for (int c = 0; c < R::CHUNKS; ++c) {
+      // ---- phase 1: H_c = z W1'[c]^T, 12 K steps ----
+      floatx4 hacc[R::FN1];
+#pragma unroll
+      for (int j = 0; j < R::FN1; ++j) hacc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+      for (int s = 0; s < kFfnS1; ++s, ++gi) {
+        const half8* sl = step_begin(gi);
+        const int ar = swz<CPR>(16 * w + (lane & 15), g);
+        const half8 a0 = sl[ar], a1 = sl[A_H8 + ar];
+#pragma unroll
+        for (int j = 0; j < R::FN1; ++j) {
+          if constexpr (R::LATE_DMA)
+            if (j == R::FN1 / 2) issue(gi + R::AHEAD);
+          const int wrw = swz<CPR>(16 * j + (lane & 15), g);
+          half8 w0, w1;
+          if constexpr (kFfnProbe == 3) {
+            w0 = a1;
+            w1 = a0;
+          } else {
+            w0 = sl[2 * A_H8 + wrw];
+            w1 = sl[2 * A_H8 + W1_H8 + wrw];
+          }
+          if constexpr (kFfnProbe == 1) {
+            hacc[j][0] += (float)w0[0] + (float)w1[1];
+            continue;
+          }
+          hacc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1, a0, hacc[j], 0, 0, 0);
+          hacc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0, a1, hacc[j], 0, 0, 0);
+          hacc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0, a0, hacc[j], 0, 0, 0);
+        }
+      }
+      // ---- phase 2: the LnGelu epilogue of H_c in registers (ws_dl_epilogue's arithmetic)
+      // -> fp16 hi / lo -> the A operand fragments of phase 3's four K steps ----
+      half8 ah[R::S3], al[R::S3];
+      {
+        const floatx4 nm4 = {-mu, -mu, -mu, -mu}, rs4 = {rs, rs, rs, rs};
+        u32x2 hh[R::FN1], hl[R::FN1];
+#pragma unroll
+        for (int j = 0; j < R::FN1; ++j) {
+          const int nl = c * CH + 16 * j + 4 * g;
+          const floatx4 c1 = *reinterpret_cast<const floatx4*>(cvec + nl);
+          const floatx4 c2 = *reinterpret_cast<const floatx4*>(cvec + FF + nl);
+          floatx4 v = hacc[j];
+          if constexpr (kFfnProbe != 4) {
+            v = __builtin_elementwise_fma(rs4, __builtin_elementwise_fma(nm4, c1, hacc[j]), c2);
+            v = gelu_erf4(v);
+          }
+          half2 h0, l0, h1, l1;
+          split16x2(v[0], v[1], h0, l0);
+          split16x2(v[2], v[3], h1, l1);
+          hh[j] = u32x2{__builtin_bit_cast(uint32_t, h0), __builtin_bit_cast(uint32_t, h1)};
+          hl[j] = u32x2{__builtin_bit_cast(uint32_t, l0), __builtin_bit_cast(uint32_t, l1)};
+        }
+#pragma unroll
+        for (int k = 0; k < R::S3; ++k) {
+          ah[k] = ffn_relay(hh[2 * k], hh[2 * k + 1]);
+          al[k] = ffn_relay(hl[2 * k], hl[2 * k + 1]);
+        }
+      }
+      // ---- phase 3: out += H_c W2[:, c]^T, CH / 32 K steps ----
+#pragma unroll
+      for (int k = 0; k < R::S3; ++k, ++gi) {
+        const half8* sl = step_begin(gi);
+        constexpr int NJ = H / 16;
+        const int j0 = 0;
+#pragma unroll
+        for (int jj = 0; jj < NJ; ++jj) {
+          if constexpr (R::LATE_DMA)
+            if (jj == NJ / 4) issue(gi + R::AHEAD);
+          const int wrw = swz<CPR>(16 * jj + (lane & 15), g);
+          half8 w0, w1;
+          if constexpr (kFfnProbe == 3) {
+            w0 = al[k];
+            w1 = ah[k];
+          } else {
+            w0 = sl[wrw];
+            w1 = sl[W3_H8 + wrw];
+          }
+          floatx4& yy = y[j0 + jj];
+          if constexpr (kFfnProbe == 1) {
+            yy[0] += (float)w0[0] + (float)w1[1];
+            continue;
+          }
+          yy = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1, ah[k], yy, 0, 0, 0);
+          yy = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0, al[k], yy, 0, 0, 0);
+          yy = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0, ah[k], yy, 0, 0, 0);
+        }
+      }
+    }
+    // ---- the tile's ResLn epilogue (ws_dl_epilogue<kEpiResLn>'s arithmetic): x = LN1(z)
+    // from the planes + statistics, z' = x + (out + b2) in place, z' row statistics ----
+    const int m0 = (it * G + b) * kFfnBM, rows = min(M - m0, kFfnBM);
+    const __amdgpu_buffer_rsrc_t rc = panel(zh + (int64_t)m0 * H, (int64_t)rows * H * 2);
+    const __amdgpu_buffer_rsrc_t rl = panel(zl + (int64_t)m0 * H, (int64_t)rows * H * 2);
+    const __amdgpu_buffer_rsrc_t rso =
+        panel(a.st_out + (int64_t)m0 * kDlParts * 2, (int64_t)rows * kDlParts * 8);
+    const int ml = 16 * w + (lane & 15);
+    const int cofs = 8 * ((g & 1) * 2 + (g >> 1));
+    const floatx4 a4 = {rs, rs, rs, rs}, b4 = {-mu * rs, -mu * rs, -mu * rs, -mu * rs};
+#pragma unroll
+    for (int blk = 0; blk < kDlParts; ++blk) {
+      u32x2 zhv[4], zlv[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int vo = (ml * H + 64 * blk + 16 * j + 4 * g) * 2;
+        zhv[j] = __builtin_amdgcn_raw_buffer_load_b64(rc, vo, 0, 0);
+        zlv[j] = __builtin_amdgcn_raw_buffer_load_b64(rl, vo, 0, 0);
+      }
+      floatx4 s4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int nl = 64 * blk + 16 * j + 4 * g;
+        const floatx4 z = mix_f16x4(zhv[j], zlv[j]);
+        const floatx4 bv = *reinterpret_cast<const floatx4*>(a.b2 + nl);
+        const floatx4 xr = __builtin_elementwise_fma(
+            __builtin_elementwise_fma(z, a4, b4), *reinterpret_cast<const floatx4*>(a.gamma + nl),
+            *reinterpret_cast<const floatx4*>(a.beta + nl));
+        y[4 * blk + j] = (y[4 * blk + j] + bv) + xr;
+        s4 += y[4 * blk + j];
+      }
+      float sm = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+      sm += __shfl_xor(sm, 16, 64);
+      sm += __shfl_xor(sm, 32, 64);
+      const float mw = sm * (1.0f / 64);
+      const floatx4 m4 = {mw, mw, mw, mw};
+      floatx4 q4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const floatx4 d = y[4 * blk + j] - m4;
+        q4 = __builtin_elementwise_fma(d, d, q4);
+      }
+      float q = (q4[0] + q4[1]) + (q4[2] + q4[3]);
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      if (g == 0) {
+        const u32x2 d = {__builtin_bit_cast(uint32_t, mw), __builtin_bit_cast(uint32_t, q)};
+        __builtin_amdgcn_raw_buffer_store_b64(d, rso, (ml * kDlParts + blk) * 8, 0, 0);
+      }
+#pragma unroll
+      for (int jp = 0; jp < 4; jp += 2) {
+        const int vo = (ml * H + 64 * blk + 16 * jp + cofs) * 2;
+        half4 ha, hb, la, lb;
+#pragma unroll
+        for (int r = 0; r < 4; r += 2) {
+          half2 h2, l2;
+          split16x2(y[4 * blk + jp][r], y[4 * blk + jp][r + 1], h2, l2);
+          ha[r] = h2[0]; ha[r + 1] = h2[1]; la[r] = l2[0]; la[r + 1] = l2[1];
+          split16x2(y[4 * blk + jp + 1][r], y[4 * blk + jp + 1][r + 1], h2, l2);
+          hb[r] = h2[0]; hb[r + 1] = h2[1]; lb[r] = l2[0]; lb[r + 1] = l2[1];
+        }
+        store_f16_pair<0>(ha, hb, rc, vo);
+        store_f16_pair<0>(la, lb, rl, vo);
+      }
+    }
+    // this tile's stores and the DMAs in flight drained before the next tile's first ring
+    // wait (its vmcnt counts assume no stores in between), then the next tile's statistics
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    prefetch(it + 1);
+  }
+}
+
+#endif  // RAGMI_DIAG_BUILD
+
 // ----------------------------------------------------------------------------------------
 // attention (varlen, one workgroup per (head, sequence), 8 waves (fp16) / 16 (fp16x3)).
 // K and V of the sequence's keys are staged into LDS (all of them when they fit — always for

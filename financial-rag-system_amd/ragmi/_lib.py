@@ -176,6 +176,7 @@ BERT_API = {
     "rag_encoder_set_fusion": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "rag_encoder_set_graphs": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "rag_encoder_set_defer_ln": (ctypes.c_int, [c_vp, ctypes.c_int]),
+    "rag_encoder_set_ffn_fused": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "rag_encoder_range_bounds": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_double),
                                                 ctypes.POINTER(ctypes.c_double)]),
     "rag_encoder_weight_bounds": (ctypes.c_int, [ctypes.POINTER(RagBertConfig),

@@ -334,6 +334,11 @@ class BertEncoder:
         rag_encoder_set_defer_ln): -1 auto, 0 off, 1 on where the model allows."""
         check(self._L.rag_encoder_set_defer_ln(self._h, int(mode)))
 
+    def set_ffn_fused(self, mode: int) -> None:
+        """The deferred-LayerNorm forward's FFN as one fused launch per layer (intermediate
+        kept on the CU; rag_encoder_set_ffn_fused): -1 auto, 0 off, 1 on."""
+        check(self._L.rag_encoder_set_ffn_fused(self._h, int(mode)))
+
     def range_bounds(self) -> tuple[float, float]:
         """(plain, deferred) static fp16 range bounds of this model (rag_encoder_range_bounds)."""
         p, d = ctypes.c_double(), ctypes.c_double()

@@ -317,14 +317,19 @@ class PartitionStreams:
     interleaving over every CU. Results are the same on any stream. close() (or the end of
     the process) destroys them; call it only after their work has finished."""
 
-    def __init__(self, device, parts: int):
+    def __init__(self, device, parts: int, whole: bool = False):
+        """whole=True: `parts` streams that each may use EVERY CU (a full CU mask): still one
+        dedicated hardware queue per stream (a CU-masked queue is never shared), so batches in
+        flight cannot land on one queue whatever streams the process created before (the
+        serving-shape fix of DESIGN §R6.4)."""
         dev = _lib.resolve_device(device)
         self.device = torch.device("cuda", _lib.device_index(dev))
         self._L = _lib.load()
         self._raw, self.streams = [], []
         for p in range(parts):
             h = ctypes.c_void_p()
-            check(self._L.rag_stream_create_cu_partition(self.device.index, p, parts,
+            check(self._L.rag_stream_create_cu_partition(self.device.index,
+                                                         0 if whole else p, 1 if whole else parts,
                                                          ctypes.byref(h)))
             self._raw.append(h)
             self.streams.append(torch.cuda.ExternalStream(h.value, device=self.device))

@@ -186,6 +186,16 @@ int rag_encoder_set_graphs(rag_encoder_t* e, int mode);
  * the model allows (fp16x3, hidden 384). */
 int rag_encoder_set_defer_ln(rag_encoder_t* e, int mode);
 
+/* The deferred-LayerNorm forward's FFN (modeling_bert.py BertIntermediate + BertOutput) as ONE
+ * launch per layer (round 6): FFN1 + GELU + FFN2 + residual + LayerNorm statistics over
+ * 128-row tiles, the 1536-wide intermediate kept on the CU instead of written to and re-read
+ * from HBM. Every output bit equals the two-GEMM form's at >= 16,384 tokens (the WS GEMMs'
+ * natural K order). Measured 8-21% slower than the two GEMMs, so only the
+ * diagnostic build (rag_diagnostic_build) carries it: there -1 auto (= off), 0 never, 1 / 2
+ * on with 128- / 256-column chunks of the intermediate, 3-5 further A/B shapes; the
+ * production library accepts -1 and 0. */
+int rag_encoder_set_ffn_fused(rag_encoder_t* e, int mode);
+
 /* fp16 range guard (no reference counterpart: the reference's torch forward is fp32). Every
  * activation the forward keeps as an fp16 plane is bounded by the weights alone, for any input
  * (interval arithmetic over the layer: |LN_i| <= |gamma_i| sqrt(H-1) + |beta_i|,

@@ -299,10 +299,18 @@ def run_pipeline(args, cfg_id, emit=True):
     # (profiles/r04u_config2_streams_hwq.jsonl).
     S = args.streams or (4 if cfg_id == 2 else 3)
     # --partition on: the batches in flight on CU-partitioned streams (bench.py, DESIGN R5.3)
+    # The batches in flight go on streams with a dedicated hardware queue each: full-CU-mask
+    # streams (PartitionStreams(whole=True); a CU-masked HSA queue is never shared). Plain torch
+    # streams share the process's 4 hardware queues (GPU_MAX_HW_QUEUES) by creation history:
+    # after ONE extra stream had been created in the process, config 2's four streams ran at
+    # 62K qps against 80K in a fresh process; whole-mask streams 79.7K / 78.8K after the same
+    # history and 80.5K fresh (scripts/diag/inproc_legs.py, profiles/r06h_inproc_stream_queue_
+    # diag.jsonl). --partition on: quarter-CU partitions; off: torch streams.
     part = None
-    if getattr(args, "partition", "auto") == "on":
+    mode = getattr(args, "partition", "auto")
+    if mode in ("on", "whole", "auto"):
         from ragmi.index import PartitionStreams
-        part = PartitionStreams(dev, S)
+        part = PartitionStreams(dev, S, whole=mode != "on")
         streams = list(part.streams)
     else:
         streams = [torch.cuda.Stream(dev) for _ in range(S)]
@@ -563,7 +571,9 @@ def run_pipeline(args, cfg_id, emit=True):
              "tokenize_ms_per_batch": round(tok_ms, 3),
              "batch": B, "k": K_TOP, "rerank_top_k": TOPK if cfg_id == 3 else None,
              "precision": prec, "batches_in_flight": S,
-             "cu_partition": S if part is not None else None,
+             "cu_partition": (S if mode == "on" else None) if part is not None else None,
+             "stream_queues": "dedicated (whole-CU-mask streams)" if part is not None and mode != "on"
+                              else "shared (torch streams)" if part is None else "CU partitions",
              "parallelism": f"replicas{world}" if world > 1 else "1 GPU"},
             roofline=roof, roofline_search=roof_search, cpu_baseline=cpu,
             id_input_qps=round(B * args.steps / elapsed_ids * world, 3),

@@ -115,11 +115,15 @@ def main():
             # DEFERS=-1,0: the deferred LayerNorm (rag_encoder_set_defer_ln) auto, then off
             for defer in [int(v) for v in os.environ.get("DEFERS", "-1").split(",")]:
                 enc.set_defer_ln(defer)
-                stage_line(enc, name, prec, cfg, head, w, ids, tt, cu, B, reps, do_cpu, defer)
+                # FFNS=0,1: the fused deferred-LN FFN (rag_encoder_set_ffn_fused) off / on
+                for ffn in [int(v) for v in os.environ.get("FFNS", "-1").split(",")]:
+                    enc.set_ffn_fused(ffn)
+                    stage_line(enc, name, prec, cfg, head, w, ids, tt, cu, B, reps, do_cpu,
+                               defer, ffn)
             enc.close()
 
 
-def stage_line(enc, name, prec, cfg, head, w, ids, tt, cu, B, reps, do_cpu, defer):
+def stage_line(enc, name, prec, cfg, head, w, ids, tt, cu, B, reps, do_cpu, defer, ffn=-1):
     ms = run(enc, ids, tt, cu, reps)
     T = int(cu[-1])
     S = float(np.mean(np.diff(cu)))
@@ -129,7 +133,7 @@ def stage_line(enc, name, prec, cfg, head, w, ids, tt, cu, B, reps, do_cpu, defe
             "ms": round(ms, 4), "tokens_per_s": round(T / ms * 1e3, 1),
             "algo_TFLOPs": round(fl / ms / 1e9, 1),
             "mfma_pipe_frac_of_2.5PF": round(fl * mult / (ms * 1e-3) / PEAK_F16, 4),
-            "defer_ln": defer}
+            "defer_ln": defer, "ffn_fused": ffn}
     if do_cpu and prec == "fp16":
         cms, thr = cpu_torch_baseline(cfg, w, ids, tt, cu, head,
                                       budget=float(os.environ.get("CPU_BUDGET", "5")))

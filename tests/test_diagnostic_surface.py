@@ -114,14 +114,32 @@ def test_scan_and_attention_probes_are_refused(libpath):
         assert rc != 0 and b"diagnostic build" in L.rag_last_error(), v
 
 
+def _inside_diag(src, pos):
+    """True when offset pos of src sits inside the diagnostic side of a RAGMI_DIAG_BUILD
+    conditional (#ifdef's body or #ifndef's #else), nested conditionals tracked."""
+    stack = []
+    for line in src[:pos].splitlines():
+        t = line.strip()
+        if t.startswith("#if"):
+            stack.append("diag" if t.startswith("#ifdef RAGMI_DIAG_BUILD") else
+                         "prod" if t.startswith("#ifndef RAGMI_DIAG_BUILD") else "other")
+        elif t.startswith("#else") and stack:
+            stack[-1] = {"diag": "prod", "prod": "diag"}.get(stack[-1], stack[-1])
+        elif t.startswith("#endif") and stack:
+            stack.pop()
+    return "diag" in stack
+
+
 def test_diagnostic_instances_are_gated_in_the_sources():
     """Every non-production scan / attention instantiation sits under RAGMI_DIAG_BUILD."""
     idx = _src("index_capi.hip")
     for probe in ("scan_valu_kernel<D><<<", "launch_variant<D, 3>", "launch_variant<D, 9>",
                   "RAG_WIDE(4)"):
-        pos = idx.index(probe)
-        opened = max(idx.rfind("#ifdef RAGMI_DIAG_BUILD", 0, pos), idx.rfind("#else", 0, pos))
-        assert opened > idx.rfind("#endif", 0, pos), probe
+        assert _inside_diag(idx, idx.index(probe)), probe
+    assert not _inside_diag(idx, idx.index("launch_variant<D, 0>(h, w, grid, nullptr);"))
     bert = _src("bert_capi.hip")
-    pos = bert.index("integral_constant<int, 106>")
-    assert bert.rfind("#else", 0, pos) > bert.rfind("#endif", 0, pos)
+    assert _inside_diag(bert, bert.index("integral_constant<int, 106>"))
+    # round 6: the fused FFN (measured slower) is diagnostic-build only, kernel and launch
+    kern = _src("bert_kernels.hip")
+    for src, probe in ((kern, "void ffn_fused_kernel("), (bert, "launch_ffn_fused(w->xh")):
+        assert _inside_diag(src, src.index(probe)), probe
