@@ -341,11 +341,13 @@ def main():
                     help="--config 5: certify EVERY timed batch exact after the timed region "
                          "(oracle rescoring + an fp32 GEMM superset; scripts/bench_modes.py "
                          "_certify_all) instead of recall on two batches")
-    ap.add_argument("--legs", choices=["child", "inproc"], default="child",
-                    help="where the default line's config-2 / config-3 legs run: a fresh child "
-                         "process each (default), or inside this process after the headline's "
-                         "index is freed (the serving shape: one process holding the index "
-                         "and both encoders; VERDICT r5 item 4)")
+    ap.add_argument("--legs", choices=["child", "inproc"], default="inproc",
+                    help="where the default line's config-2 / config-3 legs run: inside this "
+                         "process after the headline's index is freed (default: the serving "
+                         "shape, one process holding the index and both encoders; VERDICT r5 "
+                         "item 4), or a fresh child process each. With the pipelines' batch "
+                         "streams on dedicated hardware queues the two agree within 1% "
+                         "(profiles/r06_legs/)")
     ap.add_argument("--config-steps", type=int, default=200,
                     help="timed batches of each config-2 / config-3 leg (warmup 20)")
     args = ap.parse_args()
@@ -679,10 +681,10 @@ def _config_leg_inproc(args, cfg: str) -> dict:
 def _config_leg(args, cfg: str) -> dict:
     """One config-2 / config-3 measurement (`bench.py --config 2|3`, scripts/bench_modes.py) as
     a dict of the keys a reader compares: qps, ms per batch, the certified parity legs,
-    rooflines, the CPU baseline. Run as a child process after the headline's index is freed:
-    run inside this process after the headline, config 2 measured 58.5K qps against 74.5K as
-    a child (profiles/r05a_bench.json, r05b_bench_default.json; its host-side pipeline —
-    tokeniser thread, ~90 launches per batch — is what suffered)."""
+    rooflines, the CPU baseline — in a child process (--legs child). Round 5 ran the legs this
+    way because config 2 lost ~21% inside the headline's process; round 6 traced that to the
+    batch streams sharing hardware queues and gave them dedicated queues, so
+    the default is now in process (_config_leg_inproc)."""
     torch.cuda.empty_cache()
     cmd = [sys.executable, "-u", os.path.abspath(__file__), "--config", cfg,
            "--steps", str(args.config_steps), "--warmup", "20", "--precision", args.precision,

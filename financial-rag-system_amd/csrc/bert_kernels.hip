@@ -2080,6 +2080,20 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) 
   // ---- stage keys [k0, k0 + n) (n multiple of 32; zeros past len): K and V row-major,
   // 16-B chunks (swizzled: swz_chunk for K's row reads, attn_vsw for V's transposed reads)
   auto stage = [&](int k0, int n) {
+    // timing probes (diagnostic build, round 6; results meaningless): VAR bit 256 = no staging
+    // at all (LDS left as it is), bit 128 = zeros stored instead of the loaded K / V
+    if constexpr ((VAR & 256) != 0) return;
+    if constexpr ((VAR & 128) != 0) {
+      for (int c = tid; c < n * (HD / 8); c += kAttnThreads<SPLIT>) {
+        const int kl = c / (HD / 8), ch = c % (HD / 8);
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+          *reinterpret_cast<half8*>(kls[p] + kl * KROW + 8 * swz_chunk<KCPR>(kl, ch)) = half8{};
+          *reinterpret_cast<half8*>(vls[p] + kl * HD + 8 * (ch ^ attn_vsw<HD>(kl))) = half8{};
+        }
+      }
+      return;
+    }
     if constexpr ((VAR & 64) != 0) {
       // VAR bit 64 (round 4): every staging load of up to SU passes issued before any LDS
       // store (one memory round trip per SU passes instead of one per pass); same bytes to

@@ -17,3 +17,8 @@ timeout -k 10 300 python -u bench.py --no-configs --no-cpu --partition whole > g
     || { rc=$?; tail -5 gpurun_out/r06i_whole.err; exit $rc; }
 python3 -c "
 import json; d=json.loads(open('gpurun_out/r06i_whole.json').read().strip().splitlines()[-1]); print('whole headline', d['value'], d['roofline']['frac'], d['exact_batches'])"
+# attention staging probes (diagnostic build): 42 vs 42+128 (zeros stored, no loads) vs 42+256
+RAGMI_LIB_AB=$PWD/ab/diag.so VARIANTS=42,170,298 PRECS=fp16x3 ROUNDS=3 REPS=10 timeout -k 10 200 \
+    python -u scripts/bench_attn.py > gpurun_out/r06i_attn_probes.jsonl 2> gpurun_out/r06i_attn.err \
+    || { rc=$?; tail -5 gpurun_out/r06i_attn.err; exit $rc; }
+cat gpurun_out/r06i_attn_probes.jsonl
