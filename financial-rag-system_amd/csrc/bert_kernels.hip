@@ -1482,6 +1482,9 @@ __global__ __launch_bounds__(kWsBlock<CFG>, 1) void gemm_ws_kernel(
 
   // ---- MFMA waves ----
   const int wr = wid / CFG::WAVES_N, wc = wid % CFG::WAVES_N;
+  // (round 6 A/B builds, removed: static s_setprio 1 on MFMA waves 4-7, and s_setprio 1
+  // around each step's MFMA chain — rerank forward 9.01-9.06 / 9.00-9.07 vs 8.98-9.04 ms,
+  // chunk encode 3.16-3.17 / 3.16-3.18 vs 3.15-3.18: neutral; profiles/r06_ws_prio/)
   floatx4 acc[FM][FN];
 #pragma unroll
   for (int i = 0; i < FM; ++i)
