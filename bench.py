@@ -300,7 +300,8 @@ def main():
     ap.add_argument("--steps", type=int, default=None,
                     help="timed steps (default 50; --config 2 / 3: 200)")
     ap.add_argument("--warmup", type=int, default=None,
-                    help="untimed steps (default 5; --config 2 / 3: 20 — the encoder's "
+                    help="untimed steps (default 20 — 30 vs 5 measured +0.2-0.3%% on the headline, "
+                         "profiles/r06k_warmup_ab.jsonl; --config 2 / 3: 20 — the encoder's "
                          "hipGraphs are captured per padded shape and per stream, so the "
                          "pipelines need a few batches per stream to reach steady state)")
     ap.add_argument("--rows", type=int, default=10_000_000)
@@ -346,7 +347,7 @@ def main():
                          "process after the headline's index is freed (default: the serving "
                          "shape, one process holding the index and both encoders; VERDICT r5 "
                          "item 4), or a fresh child process each. With the pipelines' batch "
-                         "streams on dedicated hardware queues the two agree within 1% "
+                         "streams on dedicated hardware queues the two agree within 1%% "
                          "(profiles/r06_legs/)")
     ap.add_argument("--config-steps", type=int, default=200,
                     help="timed batches of each config-2 / config-3 leg (warmup 20)")
@@ -355,7 +356,7 @@ def main():
     if args.steps is None:
         args.steps = 200 if pipeline else 50
     if args.warmup is None:
-        args.warmup = 20 if pipeline else 5
+        args.warmup = 20
     world = check_world(args.gpus)
     if world > 1 and "WORLD_SIZE" not in os.environ:
         # plain `python bench.py --gpus N`: one rank process per GPU, started before this

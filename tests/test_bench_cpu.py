@@ -232,3 +232,12 @@ def test_scan_traffic_table(tmp_path):
     assert bench.scan_traffic(2_500_000, path=str(p)) == (None, None)
     assert bench.scan_traffic(10_000_000, "fp32", path=str(p)) == (None, None)
     assert bench.scan_traffic(10_000_000, path=str(tmp_path / "missing.json")) == (None, None)
+
+
+def test_bench_py_help_renders():
+    """every option's help text formats (argparse %-expands help strings)"""
+    import subprocess
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--help"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "--legs" in r.stdout and "--certify" in r.stdout
