@@ -1484,7 +1484,11 @@ __global__ __launch_bounds__(kWsBlock<CFG>, 1) void gemm_ws_kernel(
   const int wr = wid / CFG::WAVES_N, wc = wid % CFG::WAVES_N;
   // (round 6 A/B builds, removed: static s_setprio 1 on MFMA waves 4-7, and s_setprio 1
   // around each step's MFMA chain — rerank forward 9.01-9.06 / 9.00-9.07 vs 8.98-9.04 ms,
-  // chunk encode 3.16-3.17 / 3.16-3.18 vs 3.15-3.18: neutral; profiles/r06_ws_prio/)
+  // chunk encode 3.16-3.17 / 3.16-3.18 vs 3.15-3.18: neutral; profiles/r06_ws_prio/. A
+  // stagger — the odd workgroups owning a half tile ran it first, so their epilogue bursts
+  // alternated with the others' MFMA phases — gave bitwise the same forward but 9.06-9.11 vs
+  // 8.91-8.97 ms, chunk encode unchanged: a panel's n-tiles no longer ran on one XCD at the
+  // same time to share its A slices in L2; profiles/r06_ws_stagger/)
   floatx4 acc[FM][FN];
 #pragma unroll
   for (int i = 0; i < FM; ++i)

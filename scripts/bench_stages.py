@@ -134,6 +134,11 @@ def stage_line(enc, name, prec, cfg, head, w, ids, tt, cu, B, reps, do_cpu, defe
             "algo_TFLOPs": round(fl / ms / 1e9, 1),
             "mfma_pipe_frac_of_2.5PF": round(fl * mult / (ms * 1e-3) / PEAK_F16, 4),
             "defer_ln": defer, "ffn_fused": ffn}
+    save = os.environ.get("SAVE_OUT")         # digest of the forward's output bytes (A/B
+    if save:                                  # builds / knobs must agree bit for bit)
+        import hashlib
+        o = enc.forward_packed(ids, tt, cu).cpu().numpy()
+        line["out_sha1"] = hashlib.sha1(o.tobytes()).hexdigest()[:16]
     if do_cpu and prec == "fp16":
         cms, thr = cpu_torch_baseline(cfg, w, ids, tt, cu, head,
                                       budget=float(os.environ.get("CPU_BUDGET", "5")))
