@@ -2030,6 +2030,10 @@ struct AttnState {
   float m;
 };
 
+// VAR bit 512 (round 6, diagnostic build): the P scalings as scalar v_fma_f32 (fma_scalar)
+// instead of the packed v_pk_fma_f32 of VPRE; bitwise the same values, measured neutral at the
+// rerank shape (554: 0.2427-0.2436 ms vs 42: 0.2414-0.2428, profiles/r06_attn/): the loop is
+// not bound by its vector issue.
 // VAR (bit mask; rag_bert_attention A/Bs them): 1 = rolling Q prefetch, 2 = fp16x3 row sums
 // by MFMA (else v_dot2), 4 = software-pipelined scores (block kb+1's K.Q^T MFMAs issued
 // before block kb's softmax, so they run in the matrix pipe under its vector work), 8 = lean
@@ -2283,7 +2287,10 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) 
 #pragma unroll
           for (int r = 0; r < 4; r += 2) {
             float e0, e1;
-            if constexpr (VPRE) {   // the two scalings as one packed fp32 FMA (v_pk_fma_f32)
+            if constexpr ((VAR & 512) != 0) {   // two scalar FMAs, never paired into a
+              e0 = __builtin_amdgcn_exp2f(fma_scalar(sc[j][r], c2, nm));   // v_pk_fma_f32
+              e1 = __builtin_amdgcn_exp2f(fma_scalar(sc[j][r + 1], c2, nm));
+            } else if constexpr (VPRE) {   // the two scalings as one packed fp32 FMA (v_pk_fma_f32)
               typedef float f2 __attribute__((ext_vector_type(2)));
               const f2 t = __builtin_elementwise_fma(f2{sc[j][r], sc[j][r + 1]}, f2{c2, c2},
                                                      f2{nm, nm});
