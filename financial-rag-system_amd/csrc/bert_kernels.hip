@@ -2528,7 +2528,10 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) 
     // rolling Q prefetch: a wave's first QPF query blocks are loaded before the K/V staging
     // (their latency hides behind it), and each later one while the block QPF ahead computes
     // (fp16 at head_dim 32 runs 8 waves per SIMD in 64 VGPRs: one block ahead fits)
-    constexpr int QPF = (VAR & 1) == 0 ? 0 : SPLIT || HD > 32 ? 3 : 1;
+    // (VAR bit 1024, round 6, diagnostic build: one block ahead in fp16x3 too — 8 VGPRs instead
+    // of bit 1's 24, still 112 in all; bitwise 42's outputs, timing neutral: 1066 0.2486-0.2519
+    // vs 42 0.2485-0.2507 ms, profiles/r06_attn/r06n2_*: the Q loads' latency is not exposed)
+    constexpr int QPF = (VAR & 1) == 0 ? ((VAR & 1024) != 0 ? 1 : 0) : SPLIT || HD > 32 ? 3 : 1;
     half8 qpre[QPF > 0 ? QPF : 1][KS][NP];
 #pragma unroll
     for (int i = 0; i < QPF; ++i)
