@@ -547,6 +547,62 @@ int launch_full_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k,
   return rc;
 }
 
+// k > RAG_MAX_K_LARGE: per query, three stable radix sorts over the n_lists * k entries
+// (scan_kernels.hip merge_any_*; the full pass's SortPairsDescending<uint32, int>, no other
+// hipcub instantiation); stream-ordered scratch released at the end
+template <bool PACKED>
+int merge_any_k(const float* in_s, const int64_t* in_i, int n_lists, int B, int k, float* out_s,
+                int64_t* out_i, hipStream_t st) {
+  const int64_t n64 = (int64_t)n_lists * k;
+  if (n64 > 0x7fffffff) return ragmi::fail(RAG_ERANGE, "merge: n_lists * k too large");
+  const int n = (int)n64;
+  size_t tmp = 0;
+  RAG_HIP(hipcub::DeviceRadixSort::SortPairsDescending(
+      nullptr, tmp, static_cast<const uint32_t*>(nullptr), static_cast<uint32_t*>(nullptr),
+      static_cast<const int*>(nullptr), static_cast<int*>(nullptr), n, 0, 32, st));
+  // keys in/out + positions in/out: 16 B per entry, + scratch (256-B aligned)
+  const size_t nb = (size_t)n;
+  char* buf = nullptr;
+  const size_t t_off = (nb * 16 + 255) & ~(size_t)255;
+  RAG_HIP(hipMallocAsync(reinterpret_cast<void**>(&buf), t_off + tmp, st));
+  uint32_t* ka = reinterpret_cast<uint32_t*>(buf);
+  uint32_t* kb = ka + nb;
+  int* pa = reinterpret_cast<int*>(kb + nb);
+  int* pb = pa + nb;
+  void* scratch = buf + t_off;
+  const dim3 g((unsigned)std::min<int64_t>(1024, (n64 + 255) / 256));
+  const dim3 ge((unsigned)std::min<int64_t>(1024, ((int64_t)k + 255) / 256));
+  auto sort = [&]() {   // (ka, pa) -> (kb, pb), stable, keys descending
+    size_t t = tmp;
+    return hipcub::DeviceRadixSort::SortPairsDescending(scratch, t,
+                                                        static_cast<const uint32_t*>(ka), kb,
+                                                        static_cast<const int*>(pa), pb, n, 0, 32,
+                                                        st) == hipSuccess;
+  };
+  int rc = RAG_OK;
+  for (int b = 0; b < B && rc == RAG_OK; ++b) {
+    bool ok = true;
+    for (int word = 0; word < 2 && ok; ++word) {   // id ascending: low word, then high word
+      ragmi::merge_any_ids_kernel<PACKED><<<g, dim3(256), 0, st>>>(
+          in_s, in_i, n_lists, B, k, b, word ? pb : nullptr, word, ka, pa);
+      ok = hipGetLastError() == hipSuccess && sort();
+    }
+    if (ok) {
+      ragmi::merge_any_scores_kernel<PACKED><<<g, dim3(256), 0, st>>>(in_s, in_i, n_lists, B, k,
+                                                                      b, pb, ka, pa);
+      ok = hipGetLastError() == hipSuccess && sort();
+    }
+    if (ok) {
+      ragmi::merge_any_emit_kernel<PACKED><<<ge, dim3(256), 0, st>>>(in_s, in_i, B, k, b, kb, pb,
+                                                                     out_s, out_i);
+      ok = hipGetLastError() == hipSuccess;
+    }
+    if (!ok) rc = ragmi::fail(RAG_EHIP, "merge: sort / launch failed");
+  }
+  (void)hipFreeAsync(buf, st);
+  return rc;
+}
+
 template <int D>
 int launch_large_k_pass(rag_index* h, Workspace& w, const float* q, int Bq, int k,
                         const uint32_t* filt, int64_t id_offset, float* out_s, int64_t* out_i,
@@ -1310,9 +1366,12 @@ int rag_index_export_tags(rag_index_t* h, int64_t row0, int64_t n, uint32_t* out
 int rag_merge_topk(const float* in_s, const int64_t* in_i, int n_lists, int B, int k,
                    float* out_s, int64_t* out_i, void* stream) {
   ragmi::clear_error();
-  if (n_lists < 1 || B < 0 || k < 1 || k > RAG_MAX_K_LARGE)
+  if (n_lists < 1 || B < 0 || k < 1)
     return ragmi::fail(RAG_EINVAL, "bad merge args");
   if (B == 0) return RAG_OK;
+  if (k > RAG_MAX_K_LARGE)
+    return merge_any_k<false>(in_s, in_i, n_lists, B, k, out_s, out_i,
+                              static_cast<hipStream_t>(stream));
   if (k > RAG_MAX_K)
     ragmi::merge_large_kernel<false><<<dim3(B), dim3(256), 0, static_cast<hipStream_t>(stream)>>>(
         in_s, in_i, n_lists, B, k, out_s, out_i);
@@ -1326,9 +1385,12 @@ int rag_merge_topk(const float* in_s, const int64_t* in_i, int n_lists, int B, i
 int rag_merge_topk_packed(const int32_t* in_packed, int n_lists, int B, int k, float* out_s,
                           int64_t* out_i, void* stream) {
   ragmi::clear_error();
-  if (n_lists < 1 || B < 0 || k < 1 || k > RAG_MAX_K_LARGE || (B > 0 && !in_packed))
+  if (n_lists < 1 || B < 0 || k < 1 || (B > 0 && !in_packed))
     return ragmi::fail(RAG_EINVAL, "bad merge args");
   if (B == 0) return RAG_OK;
+  if (k > RAG_MAX_K_LARGE)
+    return merge_any_k<true>(reinterpret_cast<const float*>(in_packed), nullptr, n_lists, B, k,
+                             out_s, out_i, static_cast<hipStream_t>(stream));
   if (k > RAG_MAX_K)
     ragmi::merge_large_kernel<true><<<dim3(B), dim3(256), 0, static_cast<hipStream_t>(stream)>>>(
         reinterpret_cast<const float*>(in_packed), nullptr, n_lists, B, k, out_s, out_i);

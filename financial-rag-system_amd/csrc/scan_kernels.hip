@@ -3398,4 +3398,87 @@ __global__ __launch_bounds__(256) void full_emit_kernel(const uint32_t* __restri
   }
 }
 
+// Merge for k > kLkMerge (round 6: the sharded search of a `limit` past the large-k pass's
+// exchange, ragmi.dist.ShardedIndex): per query, the n_lists * k entries (padding: id < 0) are
+// ordered by three stable radix sorts (hipcub, one instantiation: 32-bit keys descending) —
+// by the complement of the id's low word, then of its high word (so: id ascending), then by
+// the order-preserving score key — so ties stay id-ascending: the (score desc, id asc) order
+// of merge_exact_kernel / merge_large_kernel for any k. Padding gets key 0 in every pass, below
+// every id and every score.
+template <bool PACKED>
+__global__ __launch_bounds__(256) void merge_any_ids_kernel(const float* __restrict__ in_s,
+                                                            const int64_t* __restrict__ in_i,
+                                                            int n_lists, int B, int k, int b,
+                                                            const int* __restrict__ pos_in,
+                                                            int word,
+                                                            uint32_t* __restrict__ key,
+                                                            int* __restrict__ pos) {
+  const int64_t n = (int64_t)n_lists * k;
+  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < n; j += (int64_t)gridDim.x * 256) {
+    const int p = pos_in ? pos_in[j] : (int)j;
+    const int64_t off = ((int64_t)(p / k) * B + b) * k + p % k;
+    int64_t id;
+    if constexpr (PACKED) id = reinterpret_cast<const int2*>(in_s)[off].y;
+    else id = in_i[off];
+    const uint32_t w = (uint32_t)((uint64_t)id >> (32 * word));
+    key[j] = id >= 0 ? ~w : 0u;
+    pos[j] = p;
+  }
+}
+
+template <bool PACKED>
+__global__ __launch_bounds__(256) void merge_any_scores_kernel(const float* __restrict__ in_s,
+                                                               const int64_t* __restrict__ in_i,
+                                                               int n_lists, int B, int k, int b,
+                                                               const int* __restrict__ pos_in,
+                                                               uint32_t* __restrict__ key,
+                                                               int* __restrict__ pos) {
+  const int64_t n = (int64_t)n_lists * k;
+  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < n; j += (int64_t)gridDim.x * 256) {
+    const int p = pos_in[j];
+    const int64_t off = ((int64_t)(p / k) * B + b) * k + p % k;
+    float sc;
+    int64_t id;
+    if constexpr (PACKED) {
+      const int2 pv = reinterpret_cast<const int2*>(in_s)[off];
+      sc = __int_as_float(pv.x);
+      id = pv.y;
+    } else {
+      sc = in_s[off];
+      id = in_i[off];
+    }
+    if (sc == 0.0f) sc = 0.0f;                  // -0 and +0: one key
+    key[j] = id >= 0 ? fkey(sc) : 0u;
+    pos[j] = p;
+  }
+}
+
+template <bool PACKED>
+__global__ __launch_bounds__(256) void merge_any_emit_kernel(const float* __restrict__ in_s,
+                                                             const int64_t* __restrict__ in_i,
+                                                             int B, int k, int b,
+                                                             const uint32_t* __restrict__ key,
+                                                             const int* __restrict__ pos,
+                                                             float* __restrict__ out_s,
+                                                             int64_t* __restrict__ out_i) {
+  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < k; j += (int64_t)gridDim.x * 256) {
+    const int p = pos[j];
+    const int64_t off = ((int64_t)(p / k) * B + b) * k + p % k;
+    float sc = kNegInf;
+    int64_t id = -1;
+    if (key[j] != 0u) {
+      if constexpr (PACKED) {
+        const int2 pv = reinterpret_cast<const int2*>(in_s)[off];
+        sc = __int_as_float(pv.x);
+        id = pv.y;
+      } else {
+        sc = in_s[off];
+        id = in_i[off];
+      }
+    }
+    out_s[(int64_t)b * k + j] = sc;
+    out_i[(int64_t)b * k + j] = id;
+  }
+}
+
 }  // namespace ragmi

@@ -135,7 +135,10 @@ class ShardedIndex:
             self.local.upsert(vectors[m], rows, t, new_count=cnt)
 
     def search(self, queries, k: int, filters=None):
-        if (self.world > 1 or self.force_exchange) and self.packed:
+        from .index import MAX_K_LARGE
+        # the packed exchange carries k <= MAX_K_LARGE; a larger `limit` (answered by each
+        # shard's full exact pass) goes through the unpacked lists and the any-k merge
+        if (self.world > 1 or self.force_exchange) and self.packed and k <= MAX_K_LARGE:
             # one all-gather of the packed (score bits, int32 row) lists instead of two
             p = self.local.search_packed(queries, k, filters=filters, id_offset=self.lo)
             return self.merge_packed(all_gather_packed(p, self.group), k)

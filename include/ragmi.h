@@ -68,9 +68,10 @@ enum {
  * queries: a sampled certified lower bound of each query's k-th best score, every row whose
  * MFMA score can reach it collected, all of those re-scored exactly, the k best by (score
  * desc, row asc) emitted — the same exact result and canonical scores as the k <= 32 path
- * (scan_kernels.hip, "Exact top-k for RAG_MAX_K < k"). rag_merge_topk[_packed] and
- * rag_index_search_packed accept k up to this. rag_index_search itself takes ANY k >= 1:
- * k > RAG_MAX_K_LARGE runs the full exact pass (rag_index_search_full, round 6). */
+ * (scan_kernels.hip, "Exact top-k for RAG_MAX_K < k"). rag_index_search_packed accepts k
+ * up to this. rag_index_search itself takes ANY k >= 1: k > RAG_MAX_K_LARGE runs the full
+ * exact pass (rag_index_search_full, round 6), and rag_merge_topk[_packed] merge any k (past
+ * this by three stable radix sorts per query). */
 #define RAG_MAX_K_LARGE 4096
 /* Queries handled per scan pass; larger batches run ceil(B/32) passes. */
 #define RAG_QUERY_TILE 32
@@ -183,8 +184,10 @@ int rag_index_import_rows32(rag_index_t* index, int64_t row0, int64_t n, const f
 int rag_index_export_tags(rag_index_t* index, int64_t row0, int64_t n, uint32_t* out_host);
 
 /* Merge n_lists per-shard result lists (each [B][k] sorted by (score desc, id asc), device;
- * laid out [n_lists][B][k]) into the global top-k [B][k] (device). Used after the RCCL
- * all-gather of per-shard results. */
+ * laid out [n_lists][B][k]; padding: id -1) into the global top-k [B][k] (device) by (score
+ * desc, id asc), padding -inf / -1 past the valid entries. Any k >= 1 (k > RAG_MAX_K_LARGE:
+ * stream-ordered scratch of ~36 B per entry). Used after the RCCL all-gather of per-shard
+ * results. */
 int rag_merge_topk(const float* in_scores_dev, const int64_t* in_ids_dev, int n_lists, int B,
                    int k, float* out_scores_dev, int64_t* out_ids_dev, void* stream);
 /* Same merge over the packed exchange form ([n_lists][B][k][2] int32, see

@@ -162,3 +162,55 @@ def test_shard_bounds_cover_and_owner():
                 if 0 <= row < n:
                     r = owner_of(row, n, world)
                     assert b[r][0] <= row < b[r][1]
+
+
+def _worker_big_k(rank, world, port, n, q, x, k, result_q):
+    _paths()
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle_scan as O
+        from ragmi.dist import ShardedIndex, shard_bounds
+
+        class NoPacked(OracleShard):
+            def search_packed(self, *a, **kw):
+                raise AssertionError("k > MAX_K_LARGE must not use the packed exchange")
+
+        lo, hi = shard_bounds(n, rank, world)
+        sh = ShardedIndex(n, local=NoPacked(O.encode_rows(x[lo:hi])), merge=np_merge,
+                          merge_packed=np_merge_packed)
+        assert sh.packed
+        s, i = sh.search(torch.from_numpy(q), k)
+        if rank == 0:
+            result_q.put((s.numpy(), i.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_search_any_limit_uses_the_list_exchange_gloo():
+    """A `limit` past RAG_MAX_K_LARGE (the packed exchange's bound) goes through the unpacked
+    per-shard lists and the any-k merge (rag_merge_topk, stable radix sorts on the GPU;
+    its numpy restatement here): the unsharded oracle's result, padded past the row count."""
+    _paths()
+    import oracle_scan as O
+    from ragmi.index import MAX_K_LARGE
+    rng = np.random.default_rng(5)
+    n, world, k = 4500, 2, MAX_K_LARGE + 500
+    x = rng.standard_normal((n, 384)).astype(np.float32)
+    x[10:20] = x[0]                                           # exact ties across the shards
+    x[3000:3010] = x[0]
+    q = np.concatenate([x[:1], rng.standard_normal((2, 384)).astype(np.float32)])
+    ctx = mp.get_context("spawn")
+    result_q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_big_k, args=(r, world, port, n, q, x, k, result_q))
+             for r in range(world)]
+    [p.start() for p in procs]
+    s, i = result_q.get(timeout=300)
+    [p.join(timeout=60) for p in procs]
+    assert all(p.exitcode == 0 for p in procs)
+    s2, i2 = O.search(O.encode_rows(x), q, n)
+    np.testing.assert_array_equal(i[:, :n], i2)
+    np.testing.assert_array_equal(s[:, :n], s2)
+    assert (i[:, n:] == -1).all() and (s[:, n:] == -np.inf).all()

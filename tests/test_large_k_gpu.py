@@ -257,3 +257,84 @@ def test_large_k_packed_exchange_and_merge(gpu):
     torch.cuda.synchronize()
     np.testing.assert_array_equal(i3.cpu().numpy(), i2)
     np.testing.assert_array_equal(s3.cpu().numpy(), s2)
+
+
+def _np_merge(s, i, k):
+    """(score desc, id asc) over the valid entries (id >= 0) of [n_lists, B, k] lists"""
+    L, B, _ = s.shape
+    out_s = np.full((B, k), -np.inf, np.float32)
+    out_i = np.full((B, k), -1, np.int64)
+    for b in range(B):
+        ss, ii = s[:, b].ravel(), i[:, b].ravel()
+        keep = ii >= 0
+        ss, ii = ss[keep], ii[keep]
+        o = np.lexsort((ii, -ss.astype(np.float64)))[:k]
+        out_s[b, :len(o)], out_i[b, :len(o)] = ss[o], ii[o]
+    return out_s, out_i
+
+
+def test_merge_any_k_random_lists(gpu):
+    """rag_merge_topk[_packed] past RAG_MAX_K_LARGE (round 6: three stable radix sorts): random
+    per-list-sorted inputs whose id ranges interleave across lists, equal scores within and
+    across lists, +0 / -0, and padding — equal to the (score desc, id asc) merge."""
+    from ragmi.index import MAX_K_LARGE, merge_topk, merge_topk_packed
+    rng = np.random.default_rng(17)
+    L, B, k = 3, 3, MAX_K_LARGE + 904
+    s = np.round(rng.standard_normal((L, B, k)), 2).astype(np.float32)   # many exact ties
+    s[0, 0, :50] = 0.0
+    s[1, 0, :50] = -0.0
+    ids = np.stack([rng.permutation(10 * k)[:k] for _ in range(L * B)]).reshape(L, B, k)
+    ids = ids.astype(np.int64)
+    ids[2, 1, k // 2:] = -1                                  # a short list (padding)
+    s[2, 1, k // 2:] = -np.inf
+    for l in range(L):                                       # each list (score desc, id asc)
+        for b in range(B):
+            v = ids[l, b] >= 0
+            o = np.lexsort((ids[l, b][v], -s[l, b][v].astype(np.float64)))
+            s[l, b, :v.sum()] = s[l, b][v][o]
+            ids[l, b, :v.sum()] = ids[l, b][v][o]
+    want_s, want_i = _np_merge(s, ids, k)
+    ts, ti = torch.from_numpy(s).to(gpu), torch.from_numpy(ids).to(gpu)
+    gs, gi = merge_topk(ts, ti, k)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(gi.cpu().numpy(), want_i)
+    np.testing.assert_array_equal(gs.cpu().numpy().view(np.int32), want_s.view(np.int32))
+    p = torch.stack([ts.view(torch.int32), torch.where(ti >= 0, ti, -1).to(torch.int32)], -1)
+    ps, pi = merge_topk_packed(p.contiguous(), k)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(pi.cpu().numpy(), want_i)
+    np.testing.assert_array_equal(ps.cpu().numpy().view(np.int32), want_s.view(np.int32))
+    # 64-bit ids (the unpacked form): list 1's ids past 2^33 — the high-word pass orders them
+    ids64 = ids.copy()
+    ids64[1] = np.where(ids64[1] >= 0, ids64[1] + (1 << 33), -1)
+    want_s, want_i = _np_merge(s, ids64, k)
+    gs, gi = merge_topk(ts, torch.from_numpy(ids64).to(gpu), k)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(gi.cpu().numpy(), want_i)
+    np.testing.assert_array_equal(gs.cpu().numpy().view(np.int32), want_s.view(np.int32))
+
+
+def test_full_pass_sharded_any_k(gpu):
+    """The multi-GPU form past RAG_MAX_K_LARGE: per logical shard the full exact pass with a
+    global id offset, then rag_merge_topk's any-k merge equals the unsharded oracle."""
+    from ragmi.index import merge_topk
+    rng = np.random.default_rng(23)
+    n, dim, k = 16_000, 384, 5_500
+    x = rng.standard_normal((n, dim)).astype(np.float32)
+    x[4_990:5_010] = x[7]                                    # ties straddling a shard bound
+    q = np.concatenate([_queries(rng, x, 5, dim), x[7:8]])
+    bounds = [0, 5_000, 11_000, n]
+    lists_s, lists_i = [], []
+    for r in range(3):
+        lo, hi = bounds[r], bounds[r + 1]
+        idx = _index(gpu, x[lo:hi])
+        s, i = idx.search(q, k, id_offset=lo)
+        torch.cuda.synchronize()
+        lists_s.append(s)
+        lists_i.append(i)
+        idx.close()
+    s, i = merge_topk(torch.stack(lists_s), torch.stack(lists_i), k)
+    torch.cuda.synchronize()
+    s2, i2 = O.search(O.encode_rows(x), q, k)
+    np.testing.assert_array_equal(i.cpu().numpy(), i2)
+    np.testing.assert_array_equal(s.cpu().numpy(), s2)
