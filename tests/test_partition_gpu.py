@@ -18,8 +18,11 @@ def _index(gpu, x, tags=None):
     return idx
 
 
+@pytest.mark.parametrize("whole", [False, True], ids=["quarters", "whole"])
 @pytest.mark.parametrize("dim,n,k", [(384, 200_000, 15), (384, 60_000, 100), (1024, 40_000, 15)])
-def test_partition_streams_match_default_stream(gpu, dim, n, k):
+def test_partition_streams_match_default_stream(gpu, dim, n, k, whole):
+    """whole=True: full-CU-mask streams (each on a dedicated hardware queue; the config-2/3
+    pipelines' batch streams, round 6)"""
     from ragmi.index import PartitionStreams
     rng = np.random.default_rng(dim + k)
     x = rng.standard_normal((n, dim)).astype(np.float32)
@@ -28,7 +31,7 @@ def test_partition_streams_match_default_stream(gpu, dim, n, k):
                            .astype(np.float32)).to(gpu) for _ in range(8)]
     ref = [idx.search(q, k) for q in qs]
     torch.cuda.synchronize()
-    parts = PartitionStreams(gpu, 4)
+    parts = PartitionStreams(gpu, 4, whole=whole)
     try:
         cur = torch.cuda.current_stream(gpu)
         for s in parts.streams:
@@ -76,3 +79,34 @@ def test_partition_argument_checks(gpu):
     from ragmi.index import PartitionStreams
     with pytest.raises(RagmiError):
         PartitionStreams(gpu, 100_000)                  # more parts than CUs
+
+
+def test_streams_recreated_at_reused_addresses(gpu):
+    """Partition streams closed and new streams created (possibly at the same handles): the
+    index re-reads each workspace's CU share (stream generation counter), and the
+    results stay the default stream's."""
+    from ragmi.index import PartitionStreams
+    rng = np.random.default_rng(9)
+    n, dim, k = 120_000, 384, 15
+    x = rng.standard_normal((n, dim)).astype(np.float32)
+    idx = _index(gpu, x)
+    q = torch.from_numpy(x[rng.choice(n, 32)]).to(gpu)
+    s0, i0 = idx.search(q, k)
+    torch.cuda.synchronize()
+    try:
+        for parts_n, whole in ((4, False), (2, True), (8, False), (4, True)):
+            parts = PartitionStreams(gpu, parts_n, whole=whole)
+            try:
+                for st in parts.streams:
+                    st.wait_stream(torch.cuda.current_stream(gpu))
+                outs = []
+                for st in parts.streams:
+                    with torch.cuda.stream(st):
+                        outs.append(idx.search(q, k))
+                torch.cuda.synchronize()
+                for s1, i1 in outs:
+                    assert torch.equal(i0, i1) and torch.equal(s0, s1)
+            finally:
+                parts.close()
+    finally:
+        idx.close()
