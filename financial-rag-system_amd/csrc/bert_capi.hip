@@ -532,6 +532,16 @@ void gemm(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float
     // vs 0.637 ms with BK-64 tiles at 1 per CU, and the config-2 line at 3 batches in flight
     // 71.1K vs 65.9K qps, where a 1-per-CU GEMM keeps the other batches' kernels off its CUs)
     const int ks = ks_for(Al ? kBK<true> : kBK<false>);
+    // fp16x3 up to N = 2048: the 40 KB form, four workgroups per CU (PipeSmallR2; RAGMI_
+    // SMALL_RING=3 on a diagnostic handle keeps the 3-stage one for A/Bs)
+    static ragmi::Knob ring_knob("RAGMI_SMALL_RING");
+    if (Al && ring_knob.get(2) == 2 && N <= PipeSmallR2::BIAS &&
+        (ks == 1 || N <= PipeSmallR2::BIAS / 2)) {
+      launch_pipe<EPI, true, PipeSmallR2>(A, Al, W, Wl, bias, M, N, K, C, Clo, st,
+                                          4 * cu_count(), LnArgs{}, ks);
+      if (ksplit_io) *ksplit_io = ks;
+      return;
+    }
     if (Al)   // 48 KB ring + 16 KB bias area: two workgroups per CU
       launch_pipe<EPI, true, PipeSmall<true>>(A, Al, W, Wl, bias, M, N, K, C, Clo, st,
                                               2 * cu_count(), LnArgs{}, ks);

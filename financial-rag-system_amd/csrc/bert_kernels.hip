@@ -549,9 +549,12 @@ __global__ __launch_bounds__(256) void gemm_kernel(const _Float16* __restrict__ 
 // 64x64 tiles, 4 waves of 32x32, a 4-stage ring (fp16: the whole K = 384 of a tile in
 // flight after the prologue), for query batches of a few hundred to a few thousand tokens,
 // where a GEMM is a handful of tiles per CU and latency, not MFMA rate, sets its time.
-template <int BM_, int BN_, int WAVES_M_, int WAVES_N_, int NS_, int BK_ = 0, int LOADERS_ = 4>
+constexpr int kPipeBiasMax = 4096;            // floats of bias staged in LDS (N <= 4096)
+template <int BM_, int BN_, int WAVES_M_, int WAVES_N_, int NS_, int BK_ = 0, int LOADERS_ = 4,
+          int BIAS_ = kPipeBiasMax>
 struct PipeCfg {
   static constexpr int BM = BM_, BN = BN_, WAVES_M = WAVES_M_, WAVES_N = WAVES_N_, NS = NS_;
+  static constexpr int BIAS = BIAS_;   // gemm_pipe_kernel's staged-vector area (floats)
   static constexpr int BK = BK_;   // K step; 0 = kBK<SPLIT> (64 fp16 / 32 fp16x3)
   static constexpr int LOADERS = LOADERS_;   // gemm_ws_kernel's loader waves
   static constexpr int THREADS = 64 * WAVES_M * WAVES_N;
@@ -575,9 +578,15 @@ template <bool SPLIT> using PipeSmall = PipeCfg<64, 64, 2, 2, SPLIT ? 3 : 4>;
 // (Measured and removed in round 5 — numbers in DESIGN.md §R5: 256x256 / 256x192 PIPE tiles,
 // register-blocked BIG / BIG128 shapes, BK-64 and 64x128 query-batch tiles, the one-loader and
 // deferred-LN query-batch WS tiles, and the 256x192 ping-pong kernel.)
+// fp16x3 query-batch GEMMs with N <= 2048 (round 6): a 2-stage ring and an 8 KB staged-vector
+// area, 40 KB of LDS — four workgroups per CU instead of two, room for the config-2
+// pipeline's concurrent batches. Bitwise the same outputs (same tiles, K order and epilogue);
+// the 32-query forward alone 0.694 -> 0.704 ms, config 2 77.4-80.6K -> 80.0-81.5K qps over
+// five interleaved pairs, config 3 unchanged (profiles/r06_small_ring/). Wider N (bge-large's
+// 3072 / 4096) keeps PipeSmall<true>.
+using PipeSmallR2 = PipeCfg<64, 64, 2, 2, 2, 0, 4, 2048>;
 constexpr int PBM = PipeLarge::BM, PBN = PipeLarge::BN;
 constexpr int kPipeThreads = PipeLarge::THREADS;
-constexpr int kPipeBiasMax = 4096;            // floats of bias staged in LDS (N <= 4096)
 
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -976,18 +985,18 @@ __global__ __launch_bounds__(kPipeBlock<CFG>, 1) void gemm_pipe_kernel(
   static_assert(A_H8 % TH == 0 && W_H8 % TH == 0 && FN % 2 == 0, "tile shape");
   static_assert((NS - 2) * L + S <= 63, "vmcnt range");
   // kEpiAddLn keeps bias | gamma | beta | two [WAVES_N][BM] row-sum tables in the bias area
-  static_assert(EPI != kEpiAddLn || 3 * BN + 2 * CFG::WAVES_N * BM <= kPipeBiasMax,
+  static_assert(EPI != kEpiAddLn || 3 * BN + 2 * CFG::WAVES_N * BM <= CFG::BIAS,
                 "LN staging");
   // one LDS object (ring | bias): a second __shared__ object beside a DMA target can make
   // hipcc drain vmcnt before every ds_read
-  __shared__ half8 lds[NS * STAGE_H8 + kPipeBiasMax / 4];
+  __shared__ half8 lds[NS * STAGE_H8 + CFG::BIAS / 4];
   float* bias_l = reinterpret_cast<float*>(lds + NS * STAGE_H8);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wid / CFG::WAVES_N, wc = wid % CFG::WAVES_N;
   const uint32_t lbase = lds_addr_of(lds);
-  // split-K (kEpiF32 only; the launcher checks K / BK % ksplit == 0 and N <= kPipeBiasMax / 2):
+  // split-K (kEpiF32 only; the launcher checks K / BK % ksplit == 0 and N <= CFG::BIAS / 2):
   // work unit u = (tile u % n_tiles, K part u / n_tiles) over nk = K / BK / ksplit K steps;
   // part p writes its fp32 partial product to Cout + p M N, the bias only in part 0 (the
   // other parts read zeros staged in the upper half of the bias area); add_ln_kernel sums
@@ -1002,14 +1011,14 @@ __global__ __launch_bounds__(kPipeBlock<CFG>, 1) void gemm_pipe_kernel(
 
   if (ksplit > 1)
     for (int i = tid * 4; i < N; i += TH * 4)
-      *reinterpret_cast<floatx4*>(bias_l + kPipeBiasMax / 2 + i) = floatx4{0.f, 0.f, 0.f, 0.f};
+      *reinterpret_cast<floatx4*>(bias_l + CFG::BIAS / 2 + i) = floatx4{0.f, 0.f, 0.f, 0.f};
   // The staged vectors (bias [| gamma | beta]) are loaded into registers here and written to
   // LDS only after the ring prologue's DMAs are issued (below), so their load latency and the
   // first stages' run concurrently instead of back to back — a query-batch GEMM is one or two
   // tiles per workgroup, where that serial latency was a visible part of the launch.
-  constexpr int NBV = kPipeBiasMax / (TH * 4) > 0 ? kPipeBiasMax / (TH * 4) : 1;
+  constexpr int NBV = CFG::BIAS / (TH * 4) > 0 ? CFG::BIAS / (TH * 4) : 1;
   constexpr int NLN = EPI == kEpiAddLn ? (BN + TH * 4 - 1) / (TH * 4) : 0;
-  static_assert(NBV * TH * 4 >= kPipeBiasMax, "every staged bias float has a register slot");
+  static_assert(NBV * TH * 4 >= CFG::BIAS, "every staged bias float has a register slot");
   floatx4 bv[NBV], gv[NLN > 0 ? NLN : 1], ev[NLN > 0 ? NLN : 1];
 #pragma unroll
   for (int u = 0; u < NBV; ++u) {
@@ -1294,7 +1303,7 @@ __global__ __launch_bounds__(kPipeBlock<CFG>, 1) void gemm_pipe_kernel(
         }
       } else {
         pipe_plain_epilogue<EPI, SPLIT, CFG, false>(
-            acc, kpart ? bias_l + kPipeBiasMax / 2 : bias_l, rc, rl, N, n0, wr, wc, lane);
+            acc, kpart ? bias_l + CFG::BIAS / 2 : bias_l, rc, rl, N, n0, wr, wc, lane);
       }
 #pragma unroll
       for (int i = 0; i < FM; ++i)
