@@ -104,8 +104,9 @@ struct EncWorkspace {
   // record any other thread's launches on that stream into the graph
   hipStream_t cstream = nullptr;
 
-  void drop_graphs() {   // (a replay may still run on the workspace's stream: wait for it)
-    if (!graphs.empty() && stream) (void)hipStreamSynchronize(stream);
+  void drop_graphs() {   // (a replay may still run on the workspace's stream: wait for it —
+    // device-wide, since the caller may have destroyed that stream since its last forward)
+    if (!graphs.empty()) (void)hipDeviceSynchronize();
     for (auto& g : graphs)
       if (g.exec) (void)hipGraphExecDestroy(g.exec);
     graphs.clear();
@@ -344,12 +345,31 @@ int small_ksplit(int K, int BK) {
   return s;
 }
 
+// CUs a stream may use (its CU mask, rag_stream_create_cu_mask / _partition), rounded down to
+// a multiple of 8 (the WS kernel's XCD-aware tile order assumes G % 8 == 0); the null stream,
+// unmasked streams and a failed query -> every CU. The persistent WS grid is one workgroup per
+// allowed CU: sized to the device, a masked stream would queue the extra workgroups behind
+// the first ones and run a second round.
+int stream_cus_enc(hipStream_t st) {
+  if (!st) return cu_count();
+  uint32_t mask[32] = {};
+  const int words = std::min(32, (cu_count() + 31) / 32);
+  if (hipExtStreamGetCUMask(st, (uint32_t)words, mask) != hipSuccess) {
+    (void)hipGetLastError();
+    return cu_count();
+  }
+  int n = 0;
+  for (int i = 0; i < words; ++i) n += __builtin_popcount(mask[i]);
+  n = n / 8 * 8;
+  return n >= 8 && n < cu_count() ? n : cu_count();
+}
+
 template <int EPI, bool SPLIT, typename CFG, int PROBE = 0, int AUX = 0>
 void launch_ws(const _Float16* A, const _Float16* Al, const _Float16* W, const _Float16* Wl,
                const float* bias, int M, int N, int K, void* C, _Float16* Clo, hipStream_t st,
                const DlArgs& dl = DlArgs{}) {
   const int tiles = (N / CFG::BN) * ((M + CFG::BM - 1) / CFG::BM);
-  const dim3 grid((unsigned)std::min(cu_count(), (tiles + 7) / 8 * 8));   // one per CU
+  const dim3 grid((unsigned)std::min(stream_cus_enc(st), (tiles + 7) / 8 * 8));   // one per CU
   launch_fixed<kWsBlock<CFG>>(gemm_ws_kernel<EPI, SPLIT, CFG, PROBE, AUX>, grid, 0, st, A, Al, W,
                               Wl, bias, M, N, K, C, Clo, dl);
 }

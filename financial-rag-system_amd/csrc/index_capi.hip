@@ -1507,6 +1507,58 @@ int rag_stream_create_cu_partition(int device, int part, int parts, void** out) 
   return RAG_OK;
 }
 
+int rag_stream_create_cu_mask(int device, const uint32_t* mask, int words, void** out) {
+  ragmi::clear_error();
+  if (!out || !mask || words < 1 || words > 32)
+    return ragmi::fail(RAG_EINVAL, "need a mask of 1..32 words and an output pointer");
+  *out = nullptr;
+  int n = 0;
+  for (int i = 0; i < words; ++i) n += __builtin_popcount(mask[i]);
+  if (n == 0) return ragmi::fail(RAG_EINVAL, "empty CU mask");
+  int prev = 0;
+  RAG_HIP(hipGetDevice(&prev));
+  RAG_HIP(hipSetDevice(device));
+  hipStream_t st = nullptr;
+  const hipError_t e = hipExtStreamCreateWithCUMask(&st, (uint32_t)words, mask);
+  (void)hipSetDevice(prev);
+  if (e != hipSuccess)
+    return ragmi::fail(RAG_EHIP, std::string("hipExtStreamCreateWithCUMask: ") + hipGetErrorString(e));
+  *out = st;
+  g_stream_gen.fetch_add(1, std::memory_order_acq_rel);
+  return RAG_OK;
+}
+
+#ifdef RAGMI_DIAG_BUILD
+// where a stream's workgroups run (diagnostic): per workgroup (XCC_ID, HW_ID) hardware
+// registers, for mapping CU-mask bits to XCDs / shader engines / CUs
+__global__ void cu_probe_kernel(int32_t* out) {
+  uint32_t x, hw;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+  // hold the CU a little so later workgroups spread over the allowed CUs
+  const long long t0 = clock64();
+  while (clock64() - t0 < 20000) {
+  }
+  if (threadIdx.x == 0) {
+    out[2 * blockIdx.x] = (int32_t)x;
+    out[2 * blockIdx.x + 1] = (int32_t)hw;
+  }
+}
+#endif
+
+int rag_diag_cu_probe(void* stream, int n_wg, int32_t* out_dev) {
+  ragmi::clear_error();
+#ifdef RAGMI_DIAG_BUILD
+  if (n_wg < 1 || !out_dev) return ragmi::fail(RAG_EINVAL, "n_wg >= 1 and an output buffer");
+  cu_probe_kernel<<<dim3(n_wg), dim3(64), 0, static_cast<hipStream_t>(stream)>>>(out_dev);
+  RAG_HIP(hipGetLastError());
+  return RAG_OK;
+#else
+  (void)stream; (void)n_wg; (void)out_dev;
+  return ragmi::fail(RAG_EINVAL, "rag_diag_cu_probe: diagnostic build only");
+#endif
+}
+
 int rag_stream_destroy(void* stream) {
   ragmi::clear_error();
   if (!stream) return RAG_OK;

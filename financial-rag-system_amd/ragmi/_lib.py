@@ -120,6 +120,9 @@ INDEX_API = {
     "rag_index_set_scan_order": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "rag_stream_create_cu_partition": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                       ctypes.POINTER(c_vp)]),
+    "rag_stream_create_cu_mask": (ctypes.c_int, [ctypes.c_int, c_u32p, ctypes.c_int,
+                                                 ctypes.POINTER(c_vp)]),
+    "rag_diag_cu_probe": (ctypes.c_int, [c_vp, ctypes.c_int, c_vp]),
     "rag_stream_destroy": (ctypes.c_int, [c_vp]),
     "rag_index_exactness_stats": (ctypes.c_int, [c_vp, c_i64p, c_i64p, c_i32p, ctypes.c_int]),
     "rag_index_unanswered": (ctypes.c_int, [c_vp, c_i64p]),

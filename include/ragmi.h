@@ -235,7 +235,14 @@ int rag_index_set_scan_order(rag_index_t* index, int serial);
  * Results are identical on any stream. Destroy with rag_stream_destroy. (The reference has no
  * counterpart: Qdrant serves concurrent searches from one server process, main2.py:281-295.) */
 int rag_stream_create_cu_partition(int device, int part, int parts, void** stream);
+/* The same with an explicit CU mask (`words` 32-bit words, bit i = CU id i as
+ * hipExtStreamCreateWithCUMask numbers them; at least one bit set). Round 6. */
+int rag_stream_create_cu_mask(int device, const uint32_t* mask, int words, void** stream);
 int rag_stream_destroy(void* stream);
+/* Diagnostic build only (else RAG_EINVAL): n_wg one-wave workgroups on `stream`, each writing
+ * its (XCC_ID, HW_ID) hardware registers to out_dev[2 * wg .. +1] — where a CU mask's
+ * workgroups actually run. */
+int rag_diag_cu_probe(void* stream, int n_wg, int32_t* out_dev);
 
 /* Kernel timing hook for bench.py: average device time (ms) of `rag_index_search` scan-kernel
  * launches measured with HIP events on the launch stream. enable = 0 off; enable = n > 0 records

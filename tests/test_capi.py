@@ -57,6 +57,12 @@ def test_library_loads_and_binds_without_gpu(libpath):
     st = ctypes.c_void_p()
     for part, parts in ((0, 0), (2, 2), (-1, 4)):
         assert L.rag_stream_create_cu_partition(0, part, parts, ctypes.byref(st)) == -1
+    zero = (ctypes.c_uint32 * 8)()
+    assert L.rag_stream_create_cu_mask(0, zero, 8, ctypes.byref(st)) == -1      # empty mask
+    assert L.rag_stream_create_cu_mask(0, zero, 0, ctypes.byref(st)) == -1      # no words
+    assert L.rag_stream_create_cu_mask(0, None, 8, ctypes.byref(st)) == -1
+    if not L.rag_diagnostic_build():
+        assert L.rag_diag_cu_probe(None, 1, None) == -1 and b"diagnostic" in L.rag_last_error()
     assert L.rag_stream_destroy(None) == 0
 
 
