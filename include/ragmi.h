@@ -236,7 +236,10 @@ int rag_index_set_scan_order(rag_index_t* index, int serial);
  * counterpart: Qdrant serves concurrent searches from one server process, main2.py:281-295.) */
 int rag_stream_create_cu_partition(int device, int part, int parts, void** stream);
 /* The same with an explicit CU mask (`words` 32-bit words, bit i = CU id i as
- * hipExtStreamCreateWithCUMask numbers them; at least one bit set). Round 6. */
+ * hipExtStreamCreateWithCUMask numbers them). On MI355X bit i is a CU of XCD i % 8, and an
+ * XCD whose bits are all clear runs on ALL its CUs, so the mask must enable at least one CU
+ * of every XCD (else RAG_EINVAL); likewise rag_stream_create_cu_partition takes at most
+ * n_cu / 8 parts. Round 6. */
 int rag_stream_create_cu_mask(int device, const uint32_t* mask, int words, void** stream);
 int rag_stream_destroy(void* stream);
 /* Diagnostic build only (else RAG_EINVAL): n_wg one-wave workgroups on `stream`, each writing

@@ -61,6 +61,9 @@ def test_library_loads_and_binds_without_gpu(libpath):
     assert L.rag_stream_create_cu_mask(0, zero, 8, ctypes.byref(st)) == -1      # empty mask
     assert L.rag_stream_create_cu_mask(0, zero, 0, ctypes.byref(st)) == -1      # no words
     assert L.rag_stream_create_cu_mask(0, None, 8, ctypes.byref(st)) == -1
+    seven = (ctypes.c_uint32 * 8)(0x7f)                                           # XCD 7 empty
+    assert L.rag_stream_create_cu_mask(0, seven, 8, ctypes.byref(st)) == -1
+    assert b"every XCD" in L.rag_last_error()
     if not L.rag_diagnostic_build():
         assert L.rag_diag_cu_probe(None, 1, None) == -1 and b"diagnostic" in L.rag_last_error()
     assert L.rag_stream_destroy(None) == 0

@@ -79,6 +79,10 @@ def test_partition_argument_checks(gpu):
     from ragmi.index import PartitionStreams
     with pytest.raises(RagmiError):
         PartitionStreams(gpu, 100_000)                  # more parts than CUs
+    with pytest.raises(RagmiError):
+        PartitionStreams(gpu, 64)       # 4 CUs a part: XCDs without a CU would run on all
+    p = PartitionStreams(gpu, 32)       # 8 consecutive CU ids: one CU of every XCD
+    p.close()
 
 
 def test_streams_recreated_at_reused_addresses(gpu):
