@@ -1275,9 +1275,9 @@ int rag_bert_attention(int variant, const void* qkv, const void* qkv_lo, const i
   if ((variant < 0 || variant > 15) && variant != 18 && variant != 26 &&
       (variant < 40 || variant > 46 || variant % 2) && variant != 43 && variant != 106 &&
       variant != 107 && variant != 170 && variant != 298 && variant != 554 &&
-      variant != 1066)
+      variant != 1066 && variant != 2090)
     return ragmi::fail(RAG_EINVAL,
-                       "variant: -1, 0..15, 18, 26, 40, 42, 43, 44, 46, 106, 107, 170, 298, 554 or 1066");
+                       "variant: -1, 0..15, 18, 26, 40, 42, 43, 44, 46, 106, 107, 170, 298, 554, 1066 or 2090");
 #else
   // the production library carries the forward's variant and one A/B slot (round 6, VERDICT
   // r5 item 6); the measured family lives in the diagnostic build (-DRAGMI_DIAG_BUILD)
@@ -1345,6 +1345,7 @@ int rag_bert_attention(int variant, const void* qkv, const void* qkv_lo, const i
     case 42 + 256: return go(std::integral_constant<int, 42 + 256>{});
     case 42 + 512: return go(std::integral_constant<int, 42 + 512>{});   // scalar P scaling
     case 42 + 1024: return go(std::integral_constant<int, 42 + 1024>{});  // Q one block ahead
+    case 42 + 2048: return go(std::integral_constant<int, 42 + 2048>{});  // LDS-DMA staging
     default: return go(std::integral_constant<int, 15>{});
   }
 #endif

@@ -2103,6 +2103,35 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) 
     // timing probes (diagnostic build, round 6; results meaningless): VAR bit 256 = no staging
     // at all (LDS left as it is), bit 128 = zeros stored instead of the loaded K / V
     if constexpr ((VAR & 256) != 0) return;
+    if constexpr ((VAR & 2048) != 0) {
+      // VAR bit 2048 (round 6): the K / V images filled by LDS-DMA (buffer_load ... lds): one
+      // wave-instruction writes 1 KB = 64 / KCPR whole rows, lane l to LDS chunk position
+      // (row l / KCPR, chunk l % KCPR); the swizzles are XORs, so that position's source chunk
+      // is the swizzle of the position. Rows past len read as zeros through the sequence's
+      // buffer extent. No VGPR round trip, no ds_write; same bytes in the same LDS places.
+      // Diagnostic build: bitwise 42's outputs but 0.342 vs 0.242 ms per rerank-shape launch
+      // (profiles/r06_attn/r06n3_*) — each piece gathers 16 rows' 64-B segments 2,304 B apart.
+      constexpr int RPP = 64 / KCPR;
+      const int pieces = n / RPP, tot = NP * 2 * pieces;
+      const int rl = lane / KCPR, q = lane % KCPR;
+      __amdgpu_buffer_rsrc_t rs[NP];
+#pragma unroll
+      for (int p = 0; p < NP; ++p)
+        rs[p] = panel(planes[p] + (int64_t)base * (3 * H), (int64_t)len * (3 * H) * 2);
+      const int wu = __builtin_amdgcn_readfirstlane(wid);   // piece indices wave-uniform
+      for (int j = wu; j < tot; j += NW) {
+        const int p = j / (2 * pieces), kv = (j / pieces) & 1, pc = j % pieces;
+        const int r = pc * RPP + rl;
+        const int ch = kv ? (q ^ attn_vsw<HD>(r)) : swz_chunk<KCPR>(r, q);
+        const uint32_t voff =
+            (uint32_t)((k0 + r) * (3 * H) + (kv ? 2 * H : H) + h * HD + 8 * ch) * 2u;
+        const _Float16* dst = (kv ? vls[p] : kls[p]) + pc * RPP * KROW;
+        blds16(p ? rs[NP - 1] : rs[0], voff, 0u,
+               __builtin_amdgcn_readfirstlane(lds_addr_of(dst)));
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      return;
+    }
     if constexpr ((VAR & 128) != 0) {
       for (int c = tid; c < n * (HD / 8); c += kAttnThreads<SPLIT>) {
         const int kl = c / (HD / 8), ch = c % (HD / 8);
