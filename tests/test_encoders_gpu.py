@@ -266,3 +266,25 @@ def test_concurrent_streams_bitwise(ce):
     torch.cuda.synchronize()
     for o, r in zip(outs, ref):
         np.testing.assert_array_equal(o.cpu().numpy(), r)
+
+
+def test_shortest_sequences(bge, ce, prec):
+    """Sequences of 1, 2 and 3 tokens beside longer ones in one batch (an empty query is
+    [CLS] [SEP]; a 1-token row exercises the one-key softmax): both heads vs the oracle."""
+    rng = np.random.default_rng(11)
+    lens = np.array([1, 2, 3, 16, 5, 2, 31])
+    L = int(lens.max())
+    ids = np.zeros((len(lens), L), np.int64)
+    tt = np.zeros_like(ids)
+    m = np.zeros_like(ids)
+    for b, n in enumerate(lens):
+        ids[b, :n] = np.r_[101, rng.integers(1000, 30000, max(n - 2, 0)), 102][:n]
+        m[b, :n] = 1
+        tt[b, n // 2:n] = 1 if n > 2 else 0
+    (eb, wb), (ec, wc) = bge, ce
+    out = eb.forward_padded(ids, np.zeros_like(tt), m).cpu().numpy()
+    ref = R.bge_embed(wb, R.BGE_SMALL, ids, np.zeros_like(tt), m)
+    assert _report(f"[{prec}] bge short", out, ref) <= TOL[prec]["bge"]
+    out = ec.forward_padded(ids, tt, m).cpu().numpy()
+    ref = R.ce_logits(wc, R.MINILM_CE, ids, tt, m)
+    assert _report(f"[{prec}] ce short", out, ref) <= TOL[prec]["ce"]

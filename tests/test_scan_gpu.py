@@ -344,3 +344,23 @@ def test_d1024_million_rows_batch128(gpu):
     np.testing.assert_array_equal(i, i2)
     np.testing.assert_array_equal(s, s2)
     idx.close()
+
+
+@pytest.mark.parametrize("dim", [384, 1024])
+def test_zero_vectors(gpu, dim):
+    """Zero rows and zero queries (COSINE normalisation leaves a zero vector zero, every score
+    against it 0): bit-exact vs the oracle, ties by row ascending — for a zero query that is
+    the first k rows with the largest score 0 (i.e. every row scoring exactly 0 or above)."""
+    rng = np.random.default_rng(dim)
+    n = 3000
+    x = rng.standard_normal((n, dim)).astype(np.float32)
+    x[[0, 7, 100, 2999]] = 0.0
+    q = np.concatenate([np.zeros((2, dim), np.float32), rng.standard_normal((3, dim))
+                        .astype(np.float32)])
+    idx = make_index(gpu, x)
+    s, i = search(idx, q, 15)
+    s2, i2 = O.search(O.encode_rows(x), q, 15)
+    np.testing.assert_array_equal(i, i2)
+    np.testing.assert_array_equal(s, s2)
+    np.testing.assert_array_equal(i[0], np.arange(15))
+    assert (s[0] == 0).all()
