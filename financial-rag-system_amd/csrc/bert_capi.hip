@@ -382,6 +382,13 @@ void launch_ws_large(const _Float16* A, const _Float16* Al, const _Float16* W, c
   launch_ws<EPI, SPLIT, PipeLarge, 0, AUX>(A, Al, W, Wl, bias, M, N, K, C, Clo, st, dl);
 }
 
+// the 2-wave attention workgroups for query batches of sequences <= 32 tokens (attn_kernel
+// THREADS = 128); RAGMI_ATTN_SHORT=0 (diagnostic A/B) keeps the 8-wave ones
+bool attn_short(int hd, int max_len) {
+  static ragmi::Knob k("RAGMI_ATTN_SHORT");
+  return hd == 32 && max_len <= 32 && k.get(1) != 0;
+}
+
 // RAGMI_CLS_ATTN=0 (diagnostic A/B): the last layer's all-token QKV + attention instead of
 // the K|V projection + CLS-only attention (round 4: rerank forward 9.17-9.19 vs 9.30-9.32 ms,
 // profiles/r04aa_cls_attention_ab.jsonl)
@@ -692,9 +699,15 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
     const int max_qb = last ? 1 : 1 << 20;
     if (cls_done) {
       // (the CLS context is in w->cc / w->ccl already)
-    } else if (w->xl)
+    } else if (w->xl && attn_short(HD, max_len))
+      launch_fixed<128>(attn_kernel<H, HD, true, kAttnVar, 128>, agrid, alds, st,
+          w->qkv, w->qkv_l, cu, max_len, kc, scale, w->ctx, w->ctx_l, max_qb);
+    else if (w->xl)
       launch_fixed<kAttnThreads<true>>(attn_kernel<H, HD, true>, agrid, alds, st,
           w->qkv, w->qkv_l, cu, max_len, kc, scale, w->ctx, w->ctx_l, max_qb);
+    else if (attn_short(HD, max_len))
+      launch_fixed<128>(attn_kernel<H, HD, false, kAttnVar, 128>, agrid, alds, st,
+          w->qkv, nullptr, cu, max_len, kc, scale, w->ctx, nullptr, max_qb);
     else
       launch_fixed<kAttnThreads<false>>(attn_kernel<H, HD, false>, agrid, alds, st,
           w->qkv, nullptr, cu, max_len, kc, scale, w->ctx, nullptr, max_qb);
@@ -1006,6 +1019,10 @@ int set_attn_lds_attr() {
   RAG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_kernel<H, HD, true>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, kAttnLdsMax));
   RAG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_kernel<H, HD, false>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kAttnLdsMax));
+  RAG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_kernel<H, HD, true, kAttnVar, 128>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kAttnLdsMax));
+  RAG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_kernel<H, HD, false, kAttnVar, 128>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, kAttnLdsMax));
   return RAG_OK;
 }

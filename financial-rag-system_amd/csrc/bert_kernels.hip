@@ -2063,14 +2063,18 @@ constexpr int kAttnVar = 42;
 // rag_bert_attention's A/B slot in the production library: VAR 10 = 42 without the peeled,
 // prefetched block loop (bitwise the same outputs, tests/test_attention_gpu.py)
 constexpr int kAttnVarAB = 10;
-template <int H, int HD, bool SPLIT, int VAR = kAttnVar>
-__global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) void attn_kernel(
+// THREADS (round 6): 512 (8 waves) in general; 128 (2 waves) for query batches whose
+// sequences are at most 32 tokens (2 query blocks, so 6 of 8 waves would only stage), which
+// leaves the CUs' wave slots to the other batches in flight. A query block's arithmetic does
+// not depend on which wave runs it: the outputs are bitwise the same.
+template <int H, int HD, bool SPLIT, int VAR = kAttnVar, int THREADS = kAttnThreads<SPLIT>>
+__global__ __launch_bounds__(THREADS, (kAttnWavesPerEU<HD, SPLIT>)) void attn_kernel(
     const _Float16* __restrict__ qkv, const _Float16* __restrict__ qkv_lo,
     const int* __restrict__ cu, int max_len, int kc, float scale, _Float16* __restrict__ ctx,
     _Float16* __restrict__ ctx_lo, int max_qb) {
   using St = AttnState<HD, SPLIT>;
   constexpr int NP = St::NP, KS = St::KS, DT = St::DT, KROW = HD, KCPR = HD / 8;
-  constexpr int NW = kAttnThreads<SPLIT> / 64;
+  constexpr int NW = THREADS / 64;
   extern __shared__ _Float16 alds[];
   // XCD-aware (sequence, head) order: blocks are dealt round-robin over the 8 XCDs, so give
   // XCD x a contiguous range of (sequence, head) pairs: the heads of one sequence run on one
@@ -2133,7 +2137,7 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) 
       return;
     }
     if constexpr ((VAR & 128) != 0) {
-      for (int c = tid; c < n * (HD / 8); c += kAttnThreads<SPLIT>) {
+      for (int c = tid; c < n * (HD / 8); c += THREADS) {
         const int kl = c / (HD / 8), ch = c % (HD / 8);
 #pragma unroll
         for (int p = 0; p < NP; ++p) {
@@ -2148,7 +2152,7 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) 
       // store (one memory round trip per SU passes instead of one per pass); same bytes to
       // the same LDS places
       constexpr int SU = 2;
-      constexpr int T = kAttnThreads<SPLIT>;
+      constexpr int T = THREADS;
       const int total = n * (HD / 8);
       for (int c0 = tid; c0 < total; c0 += SU * T) {
         half8 kv[SU][NP], vv[SU][NP];
@@ -2180,7 +2184,7 @@ __global__ __launch_bounds__(kAttnThreads<SPLIT>, (kAttnWavesPerEU<HD, SPLIT>)) 
       }
       return;
     }
-    for (int c = tid; c < n * (HD / 8); c += kAttnThreads<SPLIT>) {
+    for (int c = tid; c < n * (HD / 8); c += THREADS) {
       const int kl = c / (HD / 8), ch = c % (HD / 8), key = k0 + kl;
 #pragma unroll
       for (int p = 0; p < NP; ++p) {

@@ -22,7 +22,8 @@ GEMM_VARIANTS = {"RAG_GEMM_AUTO": 0, "RAG_GEMM_TILE": 1, "RAG_GEMM_SMALL": 5, "R
 # deferred / fused LayerNorm, graph replay, CLS-only last layer)
 KNOBS = {"RAGMI_SCAN_WGS", "RAGMI_RESCAN_WG", "RAGMI_SAMPLE_DIV", "RAGMI_WIDE_WGS",
          "RAGMI_FUSED_PREP", "RAGMI_GEMM", "RAGMI_KSPLIT", "RAGMI_DEFER_LN", "RAGMI_FUSE_LN",
-         "RAGMI_ENC_GRAPH", "RAGMI_CLS_ATTN", "RAGMI_SMALL_RING"}
+         "RAGMI_ENC_GRAPH", "RAGMI_CLS_ATTN", "RAGMI_SMALL_RING",
+         "RAGMI_ATTN_SHORT"}
 # removed in round 5 (measured losers / retired probes): must not come back silently
 REMOVED_KNOBS = {"RAGMI_WS_PHASE", "RAGMI_WS_BIG128", "RAGMI_GEMM_PP", "RAGMI_PP_STAGGER",
                  "RAGMI_DL_SMALL", "RAGMI_CE_ROWS", "RAGMI_ATTN_VAR", "RAGMI_SMALL_BK",
