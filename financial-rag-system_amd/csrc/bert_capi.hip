@@ -604,6 +604,10 @@ bool use_graphs(const rag_encoder* e, hipStream_t st, int T, bool null_ok = fals
   return mode > 0 || T <= kGraphMaxT;
 }
 
+#ifdef RAGMI_DIAG_BUILD
+__global__ void empty_probe_kernel() {}
+#endif
+
 template <int H, int HD>
 int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const int32_t* cu,
               int B, int T, int max_len, float* out, hipStream_t st, bool capturing = false,
@@ -618,6 +622,13 @@ int forward_t(rag_encoder* e, const int32_t* ids, const int32_t* types, const in
   if (rc) return rc;
   rc = ensure_cls(c, w, B);
   if (rc) return rc;
+#ifdef RAGMI_DIAG_BUILD
+  {   // dispatch-cost probe (diagnostic build, round 6): RAGMI_PROBE_EXTRA=n empty kernels
+      // per forward (captured into the graphs like the rest), results unchanged
+    static const int n_extra = std::getenv("RAGMI_PROBE_EXTRA") ? std::atoi(std::getenv("RAGMI_PROBE_EXTRA")) : 0;
+    for (int i = 0; i < n_extra; ++i) empty_probe_kernel<<<dim3(1), dim3(64), 0, st>>>();
+  }
+#endif
   // fused: the output projections' epilogue adds the residual and normalises whole 384-wide
   // rows (saves the fp32 y round trip and add_ln's extra pass). Auto: fp16 mode once the
   // 128-row bands fill the CUs (rerank batch, 117K tokens: 5.25 -> 4.92 ms). In fp16x3 the
