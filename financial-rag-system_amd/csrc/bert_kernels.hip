@@ -307,18 +307,48 @@ __device__ __forceinline__ void ln384_rows(float* __restrict__ x, const float* _
   }
 }
 
-template <bool XF>
+template <bool XF, bool L2 = false>
 __global__ __launch_bounds__(256) void add_ln384_kernel(float* __restrict__ x,
                                                         const float* __restrict__ y,
                                                         const float* __restrict__ g,
                                                         const float* __restrict__ bt, float eps,
                                                         _Float16* __restrict__ xh,
                                                         _Float16* __restrict__ xl, int T,
-                                                        int parts = 1, int64_t pstride = 0) {
+                                                        int parts = 1, int64_t pstride = 0,
+                                                        float* __restrict__ l2out = nullptr) {
   const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (t >= T) return;
   const int64_t tr[1] = {t};
-  ln384_rows<XF, 1>(x, y, g, bt, eps, xh, xl, tr, threadIdx.x & 63, parts, pstride);
+  const int lane = threadIdx.x & 63;
+  ln384_rows<XF, 1>(x, y, g, bt, eps, xh, xl, tr, lane, parts, pstride);
+  if constexpr (L2 && !XF) {
+  // (round 6) the bge head fused into the last layer's residual + LayerNorm of the CLS rows:
+  // out[t] = x[t] / max(||x[t]||, 1e-12) with cls_normalize_kernel's exact arithmetic — its
+  // lane m holds columns m + 64 j, so the row just written goes through this wave's LDS
+  // slice into that layout (one dispatch fewer per query-batch forward)
+  __shared__ float rowbuf[4][384];
+  float* rb = rowbuf[threadIdx.x >> 6];
+  if (lane < 48) {
+    const floatx4 a = *reinterpret_cast<const floatx4*>(x + t * 384 + 8 * lane);
+    const floatx4 b = *reinterpret_cast<const floatx4*>(x + t * 384 + 8 * lane + 4);
+    *reinterpret_cast<floatx4*>(rb + 8 * lane) = a;
+    *reinterpret_cast<floatx4*>(rb + 8 * lane + 4) = b;
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  float v[6];
+  float sq = 0.f;
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    v[j] = rb[lane + 64 * j];
+    sq += v[j] * v[j];
+  }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) sq += __shfl_xor(sq, d, 64);
+  const float inv = 1.0f / fmaxf(sqrtf(sq), 1e-12f);
+#pragma unroll
+  for (int j = 0; j < 6; ++j) l2out[t * 384 + lane + 64 * j] = v[j] * inv;
+  }
 }
 
 // ----------------------------------------------------------------------------------------
