@@ -202,6 +202,11 @@ bool fused_prep() {
 // other streams' scans. Round 4 sweep (profiles/r04m_rescan_grid.jsonl), 1.25M rows, 4 in
 // flight, qps / 4 marked queries' added ms at 1.25M / 10M rows: 512 workgroups (two per CU)
 // 209.3K / 0.45 / 1.36, 256: 210.4K / 0.53 / 1.21, 128: 210.7K / 0.80 / 2.18.
+// Round 6 A/B (profiles/r06_legs/r06af_*, r06ag_*): capped at the 64 CUs the 10M-row scan
+// leaves free, the idle launch no longer waits beside the other batch's scan — 10M rows 29.03
+// / 29.03K qps vs 28.93 / 28.21K — but the 1.25M-row line (partitioned streams) lost 0.7%
+// (222.5 / 224.4K vs 223.1 / 226.9K) and a marked pass took 1.45 / 4.37 ms instead of 0.51 /
+// 1.23 ms at 1.25M / 10M rows: the default stays.
 // RAGMI_RESCAN_WG (diagnostic A/B) caps it; 0 = skip (queries left tier 3, unanswered).
 int rescan_grid(const rag_index* h) {
   static ragmi::Knob k("RAGMI_RESCAN_WG");
